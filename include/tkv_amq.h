@@ -1,0 +1,151 @@
+/*
+ * tkv_amq.h -- C ABI of the MI355X-native AMQ filter engine for TurtleKV (libtkv_amq.so).
+ *
+ * This is the drop-in boundary for TurtleKV's per-leaf filter build/probe path.  Each
+ * entry point names the reference interface it replaces (paths relative to the
+ * mathworks/turtle_kv source tree):
+ *
+ *   tkv_amq_plan            build_{bloom,quotient}_filter_for_leaf sizing
+ *                           (src/turtle_kv/tree/filter_builder.hpp:121-135, 241-290) and
+ *                           TreeOptions::filter_bits_per_key (tree/tree_options.hpp:155-164)
+ *   tkv_amq_build           build_filter_for_leaf_in_job (tree/filter_builder.hpp:307-331),
+ *                           batched over every leaf of one TreeSerializeContext::build_all_pages
+ *                           queue (tree/tree_serialize_context.cpp:62-115); per leaf it does what
+ *                           build_bloom_filter_for_leaf (:109-152) or build_vqf_filter<T> (:176-217)
+ *                           writes into the filter page payload
+ *   tkv_amq_probe           KeyQuery::reject_page filter test (tree/key_query.hpp:149-247):
+ *                           PackedBloomFilter::query (:216-219) / PackedVqfFilter::is_present
+ *                           (vqf_filter_page_view.hpp:113-125); result 0 == "reject" (kTrue)
+ *   tkv_amq_vqf_hash        vqf_hash_val (vqf_filter_page_view.hpp:32-35), hash-once per query
+ *                           (tree/key_query.hpp:82)
+ *   tkv_amq_vqf_probe_hashed PackedVqfFilter::is_present(hash_val) for pre-hashed queries
+ *   tkv_amq_vqf_*sizing     vqf_filter_load_factor<T> (vqf_filter_page_view.hpp:39-59),
+ *                           vqf_required_size<T> / vqf_nslots_for_size (vqf 0.2.4, used at
+ *                           tree/filter_builder.hpp:243-244,270,274)
+ *
+ * Conventions
+ *  - Plain pointers and sizes only.  Pointers documented "device" are HIP device pointers
+ *    (hipMalloc / framework-owned HBM); `stream` is a hipStream_t passed as void* (NULL =
+ *    the default stream).  Launch functions never allocate, copy synchronously or
+ *    synchronise, so they can be captured into a hipGraph.
+ *  - The caller owns every buffer (the reference writes into a PageCache page buffer it
+ *    does not own, tree/filter_builder.hpp:76-84,189-193).
+ *  - Return values are status codes numbered like batt::StatusCode / absl::StatusCode.
+ *    On error the output is undefined and must not be committed (reference: a failed build
+ *    leaves the leaf without a filter, tree/filter_builder.hpp:323-325).
+ *  - Thread-safe: no global mutable state; concurrent calls on different streams are fine.
+ *  - Filter bit layouts follow the frozen "tkv-amq v1" spec.
+ */
+#ifndef TKV_AMQ_H
+#define TKV_AMQ_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TKV_AMQ_ABI_VERSION 1
+
+/* status codes (batt::StatusCode values) */
+#define TKV_AMQ_OK 0
+#define TKV_AMQ_INVALID_ARGUMENT 3
+#define TKV_AMQ_RESOURCE_EXHAUSTED 8
+#define TKV_AMQ_INTERNAL 13
+#define TKV_AMQ_UNAVAILABLE 14
+
+/* filter kinds (config.hpp:20-24 compile-time switch, made a runtime argument) */
+#define TKV_AMQ_BLOOM 0
+#define TKV_AMQ_VQF 1
+
+/* One leaf's filter ("segment"), produced on the host by tkv_amq_plan and read by the
+ * device kernels.  64 bytes, little-endian, no padding. */
+typedef struct tkv_amq_segment {
+  uint64_t key_begin;     /* first key index of this leaf's (sorted) item range */
+  uint64_t out_offset;    /* byte offset of the filter page payload in the output array */
+  uint64_t src_page_id;   /* leaf PageId stored in the filter header (reject_page check) */
+  uint64_t mod_magic;     /* VQF: floor((2^64-1) / (n_blocks * buckets_per_block)); Bloom: 0 */
+  uint64_t block_base;    /* prefix sum of n_blocks (VQF workspace addressing) */
+  uint32_t n_keys;        /* items in the leaf (tombstones included) */
+  uint32_t n_blocks;      /* Bloom: 512-bit blocks; VQF: 64-byte vqf blocks */
+  uint32_t payload_bytes; /* bytes of payload the build writes (header + filter) */
+  uint16_t hash_count;    /* Bloom k; VQF 0 */
+  uint8_t tag_bits;       /* VQF 8 | 16; Bloom 0 */
+  uint8_t hash_val_shift; /* VQF hash truncation (filter_builder.hpp:280-283) */
+  uint32_t bits_per_key;  /* effective bits/key after the TreeOptions clamp */
+  uint32_t reserved;
+} tkv_amq_segment;
+
+const char* tkv_amq_version(void);
+const char* tkv_amq_status_string(int status);
+/* number of visible HIP devices; 0 => every device entry point returns TKV_AMQ_UNAVAILABLE */
+int tkv_amq_device_count(void);
+
+/* TreeOptions::filter_bits_per_key(): VQF clamps any nonzero bpk to >= 12 */
+uint64_t tkv_amq_filter_bits_per_key(int kind, uint64_t requested_bits_per_key);
+
+double tkv_amq_vqf_load_factor(int tag_bits, uint64_t bits_per_key);
+uint64_t tkv_amq_vqf_required_size(int tag_bits, uint64_t nslots);
+uint64_t tkv_amq_vqf_nslots_for_size(int tag_bits, uint64_t bytes);
+
+/* Host-side plan for a batch of n_segs leaves.
+ *  seg_key_counts[n_segs]  items per leaf (keys are laid out leaf after leaf)
+ *  src_page_ids[n_segs]    leaf page ids (NULL => segment index)
+ *  bits_per_key            as passed to build_filter_for_leaf_in_job (0 => no filters)
+ *  payload_capacity        filter page payload bytes (page size - page header); 0 => unlimited
+ *                          (VQF needs a capacity: it drives vqf_nslots_for_size)
+ *  out_stride              0 => payloads packed back to back (64-byte aligned); otherwise each
+ *                          segment s starts at s * out_stride (e.g. the filter page size)
+ *  segs[n_segs]            (out) plan; upload it to the device before tkv_amq_build
+ *  total_out_bytes         (out) size of the output array
+ *  workspace_bytes         (out) device workspace tkv_amq_build needs (0 for Bloom)
+ *  max_seg_blocks          (out) largest n_blocks of any segment (launch geometry) */
+int tkv_amq_plan(int kind, const uint64_t* seg_key_counts, const uint64_t* src_page_ids,
+                 uint32_t n_segs, uint32_t bits_per_key, uint64_t payload_capacity,
+                 uint64_t out_stride, tkv_amq_segment* segs, uint64_t* total_out_bytes,
+                 uint64_t* workspace_bytes, uint32_t* max_seg_blocks);
+
+/* Device build of every planned filter.
+ *  keys         device; fixed-length keys (key_offsets == NULL: key i at keys + i*key_stride,
+ *               length key_stride) or variable-length (key_offsets[n_keys+1], device)
+ *  d_segs       device copy of the plan; max_seg_blocks as returned by tkv_amq_plan
+ *  d_out        device output array (total_out_bytes)
+ *  d_workspace  device workspace (workspace_bytes, 16-byte aligned)
+ * Asynchronous on `stream`.  VQF insert failures (the reference BATT_CHECKs,
+ * filter_builder.hpp:211) are recorded in the workspace; read them with
+ * tkv_amq_build_check after the stream completes. */
+int tkv_amq_build(int kind, const uint8_t* keys, const uint64_t* key_offsets,
+                  uint32_t key_stride, uint64_t n_keys, const tkv_amq_segment* d_segs,
+                  uint32_t n_segs, uint32_t max_seg_blocks, uint8_t* d_out,
+                  void* d_workspace, uint64_t workspace_bytes, void* stream);
+
+/* Synchronises `stream`; returns TKV_AMQ_OK or TKV_AMQ_INTERNAL (a VQF block overflowed).
+ * Bloom builds cannot fail on the device. */
+int tkv_amq_build_check(int kind, const void* d_workspace, uint64_t workspace_bytes,
+                        void* stream);
+
+/* Batched probe: query i tests the filter of segment d_query_seg[i].  d_result[i] = 1 if
+ * the key may be present, 0 if the filter rejects it (reject_page == kTrue). */
+int tkv_amq_probe(int kind, const uint8_t* d_filters, const tkv_amq_segment* d_segs,
+                  uint32_t n_segs, const uint8_t* queries, const uint64_t* query_offsets,
+                  uint32_t query_stride, uint64_t n_queries, const uint32_t* d_query_seg,
+                  uint8_t* d_result, void* stream);
+
+/* vqf_hash_val for n keys -> d_hash[n] (device) */
+int tkv_amq_vqf_hash(const uint8_t* keys, const uint64_t* key_offsets, uint32_t key_stride,
+                     uint64_t n_keys, uint64_t* d_hash, void* stream);
+
+/* PackedVqfFilter::is_present(hash_val) for pre-hashed queries (hash once, probe many) */
+int tkv_amq_vqf_probe_hashed(const uint8_t* d_filters, const tkv_amq_segment* d_segs,
+                             uint32_t n_segs, const uint64_t* d_hash, uint64_t n_queries,
+                             const uint32_t* d_query_seg, uint8_t* d_result, void* stream);
+
+/* Synthetic 16-byte keys on the device: key i = (splitmix64_at(seed, 2(first+i)+1),
+ * splitmix64_at(seed, 2(first+i)+2)), little-endian (the bench input). */
+int tkv_amq_gen_keys16(uint64_t seed, uint64_t first, uint64_t n_keys, uint8_t* d_keys,
+                       void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TKV_AMQ_H */

@@ -1,0 +1,252 @@
+"""GPU parity: filters and probe answers from libtkv_amq (HIP, gfx950) must be byte-identical
+to the CPU oracle (tkv-amq v1 spec) on the same seeded inputs; at full BASELINE sizes the
+checks are size-independent properties (no false negatives, determinism, FPR equality).
+Every call goes through the C ABI (include/tkv_amq.h) via ctypes."""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+S = 16384
+VQF_SEED = 0x9D0924DC03E79A75
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch as t
+    assert t.cuda.is_available(), "GPU tests need a visible MI355X"
+    return t
+
+
+def seg_bounds(counts):
+    return np.concatenate([[0], np.cumsum(counts)]).astype(np.uint64)
+
+
+def oracle_per_segment(oracle, kind, keys_np, counts, bpk, cap=32704, src=None, stride=16,
+                       offsets=None):
+    """oracle payloads, one bytes object per segment"""
+    out = []
+    sb = seg_bounds(counts)
+    for s, c in enumerate(counts):
+        b = int(sb[s])
+        sid = s if src is None else int(src[s])
+        if offsets is not None:
+            o = (offsets[b:b + c + 1] - offsets[b]).astype(np.uint64)
+            kp = keys_np[int(offsets[b]):]
+        else:
+            o, kp = None, keys_np[b:]
+        if kind == 0:
+            st, pl = oracle.bloom_build(kp, c, bpk, src_page_id=sid, offsets=o, stride=stride)
+            assert st == 0
+            out.append(pl.tobytes() if bpk else b"")
+        else:
+            st, pl, plan = oracle.vqf_build(kp, c, bpk, cap, src_page_id=sid, offsets=o,
+                                            stride=stride)
+            assert st == 0, st
+            out.append(pl[:plan.payload_used].tobytes() if bpk else b"")
+    return out
+
+
+def gpu_build(amq, torch, kind, keys_t, counts, bpk, cap=32704, src=None, offsets_t=None):
+    plan = amq.plan_filters(kind, counts, bpk, payload_capacity=cap if kind == 1 else 0,
+                            src_page_ids=src)
+    kb = amq.KeyBatch.fixed(keys_t) if offsets_t is None else amq.KeyBatch.variable(keys_t, offsets_t)
+    out = amq.build_all_filters(plan, kb)
+    torch.cuda.synchronize()
+    return plan, out.cpu().numpy()
+
+
+def segment_bytes(plan, out_np, s):
+    seg = plan.segs[s]
+    o, n = int(seg["out_offset"]), int(seg["payload_bytes"])
+    return out_np[o:o + n].tobytes()
+
+
+def assert_same(plan, out_np, ref):
+    for s, r in enumerate(ref):
+        got = segment_bytes(plan, out_np, s)
+        if got != r:
+            a = np.frombuffer(got, np.uint8)
+            b = np.frombuffer(r, np.uint8)
+            n = min(len(a), len(b))
+            diff = np.nonzero(a[:n] != b[:n])[0]
+            raise AssertionError(f"segment {s}: len {len(a)} vs {len(b)}, first diff at "
+                                 f"{diff[:8].tolist()}")
+
+
+RAGGED = [16384, 1, 0, 777, 16384, 8448, 64, 63, 65, 2, 5000]
+
+
+@pytest.mark.parametrize("bpk", [10, 12, 1, 5, 20, 33])
+def test_bloom16_parity(oracle, amq, torch, bpk):
+    counts = RAGGED
+    keys = oracle.gen_keys16(42, 0, sum(counts))
+    src = [1000 + i for i in range(len(counts))]
+    ref = oracle_per_segment(oracle, 0, keys, counts, bpk, src=src)
+    plan, out = gpu_build(amq, torch, 0, torch.from_numpy(keys).cuda(), counts, bpk, src=src)
+    assert_same(plan, out, ref)
+
+
+def test_bloom_config1_sha256(oracle, amq, torch):
+    """BASELINE config 1 on the GPU: 1M x 16B keys @10 bpk, S = 16384 -> the golden SHA."""
+    g = json.load(open(os.path.join(GOLDEN, "filters.json")))["config1_bloom10_1M"]
+    n = g["n_keys"]
+    counts = [S] * (n // S) + [n % S]
+    keys = amq.gen_keys16(42, 0, n)
+    plan = amq.plan_filters(0, counts, 10)
+    out = amq.build_all_filters(plan, amq.KeyBatch.fixed(keys))
+    assert plan.total_out_bytes == g["bytes"]
+    assert hashlib.sha256(out.cpu().numpy().tobytes()).hexdigest() == g["sha256"]
+
+
+def test_gen_keys_match_oracle(oracle, amq, torch):
+    k = amq.gen_keys16(42, 123456, 5000).cpu().numpy()
+    assert np.array_equal(k, oracle.gen_keys16(42, 123456, 5000))
+
+
+def test_bloom_fixed24_workload_keys(oracle, amq, torch):
+    keys = [ln.strip().encode() for ln in open(os.path.join(GOLDEN, "workload_e_keys.txt")) if ln.strip()]
+    blob = np.frombuffer(b"".join(keys), dtype=np.uint8).reshape(len(keys), 24).copy()
+    plan, out = gpu_build(amq, torch, 0, torch.from_numpy(blob).cuda(), [len(keys)], 10, src=[7])
+    assert segment_bytes(plan, out, 0) == open(os.path.join(GOLDEN, "workload_e_bloom10.bin"), "rb").read()
+    plan, out = gpu_build(amq, torch, 1, torch.from_numpy(blob).cuda(), [len(keys)], 12, src=[7])
+    assert segment_bytes(plan, out, 0) == open(os.path.join(GOLDEN, "workload_e_vqf12.bin"), "rb").read()
+
+
+@pytest.mark.parametrize("kind", [0, 1])
+def test_variable_length_keys(oracle, amq, torch, kind):
+    rng = np.random.default_rng(11)
+    counts = [3000, 0, 17, 4096]
+    lens = rng.integers(0, 72, sum(counts))
+    blob = rng.integers(0, 256, int(lens.sum()), dtype=np.uint8)
+    offs = np.zeros(len(lens) + 1, np.int64)
+    offs[1:] = np.cumsum(lens)
+    bpk = 10 if kind == 0 else 13
+    ref = oracle_per_segment(oracle, kind, blob, counts, bpk, offsets=offs.astype(np.uint64))
+    plan, out = gpu_build(amq, torch, kind, torch.from_numpy(blob).cuda(), counts, bpk,
+                          offsets_t=torch.from_numpy(offs).cuda())
+    assert_same(plan, out, ref)
+
+
+def sorted_keys(oracle, seed, counts):
+    keys = oracle.gen_keys16(seed, 0, sum(counts))
+    oracle.sort_segments(keys, seg_bounds(counts))
+    return keys
+
+
+@pytest.mark.parametrize("bpk,cap", [(12, 32704), (13, 32704), (16, 32704), (22, 65472),
+                                     (24, 65472), (32, 65472), (12, 16320), (12, 8128)])
+def test_vqf_parity(oracle, amq, torch, bpk, cap):
+    counts = RAGGED
+    keys = sorted_keys(oracle, 42, counts)
+    src = [500 + i for i in range(len(counts))]
+    ref = oracle_per_segment(oracle, 1, keys, counts, bpk, cap=cap, src=src)
+    plan, out = gpu_build(amq, torch, 1, torch.from_numpy(keys).cuda(), counts, bpk, cap=cap,
+                          src=src)
+    assert_same(plan, out, ref)
+
+
+def test_vqf_config1_sha256(oracle, amq, torch):
+    g = json.load(open(os.path.join(GOLDEN, "filters.json")))["config1_vqf12_1M"]
+    n = g["n_keys"]
+    counts = [S] * (n // S) + [n % S]
+    keys = sorted_keys(oracle, 42, counts)
+    plan = amq.plan_filters(1, counts, 12, payload_capacity=32704, out_stride=32704)
+    out = amq.build_all_filters(plan, amq.KeyBatch.fixed(torch.from_numpy(keys).cuda()))
+    o = out.cpu().numpy()
+    # the golden buffer has zero tails after each payload; the GPU writes payloads only
+    for s in range(plan.n_segs):
+        seg = plan.segs[s]
+        o[int(seg["out_offset"]) + int(seg["payload_bytes"]):int(seg["out_offset"]) + 32704] = 0
+    assert hashlib.sha256(o.tobytes()).hexdigest() == g["sha256"]
+
+
+def test_vqf_unsorted_and_duplicate_keys(oracle, amq, torch):
+    # insertion order matters for VQF: unsorted input and duplicate keys must still match
+    counts = [16384, 9000]
+    keys = oracle.gen_keys16(77, 0, sum(counts))
+    keys[100:200] = keys[0:100]
+    ref = oracle_per_segment(oracle, 1, keys, counts, 12)
+    plan, out = gpu_build(amq, torch, 1, torch.from_numpy(keys).cuda(), counts, 12)
+    assert_same(plan, out, ref)
+
+
+def probe_inputs(oracle, n_keys, counts, n_miss):
+    hits = np.arange(n_keys)
+    seg_of = np.repeat(np.arange(len(counts)), counts)
+    miss = oracle.gen_keys16(43, 0, n_miss)
+    rng = np.random.default_rng(44)
+    miss_seg = rng.integers(0, len(counts), n_miss)
+    return hits, seg_of, miss, miss_seg
+
+
+@pytest.mark.parametrize("kind,bpk", [(0, 10), (0, 12), (1, 12), (1, 24)])
+def test_probe_parity(oracle, amq, torch, kind, bpk):
+    counts = [S] * 8 + [8448, 0, 5]
+    keys = sorted_keys(oracle, 42, counts) if kind else oracle.gen_keys16(42, 0, sum(counts))
+    cap = 65472
+    plan = amq.plan_filters(kind, counts, bpk, payload_capacity=cap if kind else 0)
+    filt = amq.build_all_filters(plan, amq.KeyBatch.fixed(torch.from_numpy(keys).cuda()))
+    n = sum(counts)
+    _, seg_of, miss, miss_seg = probe_inputs(oracle, n, counts, 200000)
+    q = np.concatenate([keys, miss])
+    qs = np.concatenate([seg_of, miss_seg]).astype(np.uint32)
+    res = amq.probe_filters(plan, filt, amq.KeyBatch.fixed(torch.from_numpy(q).cuda()),
+                            torch.from_numpy(qs.astype(np.int32)).cuda()).cpu().numpy()
+    # oracle probe over the GPU-built filter bytes (which equal the oracle's, tested above)
+    st, ref = oracle.probe_segments(kind, filt.cpu().numpy(), plan.segs["out_offset"], q, qs)
+    assert st == 0
+    assert np.array_equal(res, ref)
+    assert res[:n].all(), "false negative"
+    fpr = res[n:].mean()
+    assert fpr < (0.02 if kind == 0 else 0.01)
+    if kind == 1:
+        hv = amq.vqf_hash_val(amq.KeyBatch.fixed(torch.from_numpy(q).cuda()))
+        res2 = amq.vqf_probe_hashed(plan, filt, hv, torch.from_numpy(qs.astype(np.int32)).cuda())
+        assert np.array_equal(res2.cpu().numpy(), ref)
+
+
+def test_vqf_hash_matches_xxhash(amq, torch):
+    import xxhash
+    keys = [ln.strip().encode() for ln in open(os.path.join(GOLDEN, "workload_e_keys.txt")) if ln.strip()]
+    kb = amq.KeyBatch.from_host(keys[:1000])
+    h = amq.vqf_hash_val(kb).cpu().numpy().view(np.uint64)
+    assert [int(x) for x in h] == [xxhash.xxh64_intdigest(k, VQF_SEED) for k in keys[:1000]]
+    h16 = amq.vqf_hash_val(amq.KeyBatch.fixed(amq.gen_keys16(1, 0, 1000))).cpu().numpy().view(np.uint64)
+    k16 = amq.gen_keys16(1, 0, 1000).cpu().numpy()
+    assert [int(x) for x in h16] == [xxhash.xxh64_intdigest(k.tobytes(), VQF_SEED) for k in k16]
+
+
+def test_bloom_monolithic_global_path(oracle, amq, torch):
+    # one filter larger than the LDS image budget (64 KiB) -> global-atomic build kernel
+    n = 120000
+    keys = oracle.gen_keys16(8, 0, n)
+    ref = oracle_per_segment(oracle, 0, keys, [n], 10)
+    plan, out = gpu_build(amq, torch, 0, torch.from_numpy(keys).cuda(), [n], 10)
+    assert plan.max_seg_blocks * 64 > 64 * 1024
+    assert_same(plan, out, ref)
+
+
+def test_reference_api_mirror(oracle, amq, torch):
+    keys = sorted_keys(oracle, 3, [4000])
+    kb = amq.KeyBatch.fixed(torch.from_numpy(keys).cuda())
+    page = amq.build_filter_for_leaf_in_job(12, 4242, kb)          # default kind: VQF (config.hpp)
+    assert page is not None and page.kind == amq.VQF
+    vf = amq.PackedVqfFilter(page)
+    vf.check_magic()
+    assert vf.src_page_id == 4242 and vf.key_remainder_bits == 8
+    q = amq.KeyQuery(kb)
+    assert all(r == amq.BoolStatus.kFalse for r in q.reject_page(4242, page))
+    assert all(r == amq.BoolStatus.kUnknown for r in q.reject_page(1, page))   # page id mismatch
+    assert all(r == amq.BoolStatus.kUnknown for r in q.reject_page(4242, None))
+    miss = amq.KeyBatch.fixed(torch.from_numpy(oracle.gen_keys16(99, 0, 4000)).cuda())
+    rej = amq.KeyQuery(miss).reject_page(4242, page)
+    assert sum(r == amq.BoolStatus.kTrue for r in rej) > 3900
+    assert amq.build_filter_for_leaf_in_job(0, 1, kb) is None        # bpk 0: no filter
+    bp = amq.build_bloom_filter_for_leaf(10, 9, kb)
+    assert all(r == amq.BoolStatus.kFalse for r in q.reject_page(9, bp))

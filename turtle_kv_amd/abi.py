@@ -1,0 +1,128 @@
+"""ctypes binding of the C ABI declared in include/tkv_amq.h (libtkv_amq.so).
+
+This is the only way the Python host side reaches the filter kernels.  There is no CPU
+fallback: if the library is missing or no GPU is visible, device entry points raise.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+from . import _build
+
+OK = 0
+INVALID_ARGUMENT = 3
+RESOURCE_EXHAUSTED = 8
+INTERNAL = 13
+UNAVAILABLE = 14
+
+BLOOM = 0
+VQF = 1
+
+STATUS_NAMES = {OK: "OK", INVALID_ARGUMENT: "InvalidArgument",
+                RESOURCE_EXHAUSTED: "ResourceExhausted", INTERNAL: "Internal",
+                UNAVAILABLE: "Unavailable"}
+
+
+class TkvAmqError(RuntimeError):
+    """A non-OK status from libtkv_amq (mirrors batt::Status propagation)."""
+
+    def __init__(self, status: int, what: str):
+        super().__init__(f"{what}: {STATUS_NAMES.get(status, status)}")
+        self.status = status
+
+
+class Segment(ctypes.Structure):
+    """tkv_amq_segment (64 bytes)."""
+    _fields_ = [
+        ("key_begin", ctypes.c_uint64),
+        ("out_offset", ctypes.c_uint64),
+        ("src_page_id", ctypes.c_uint64),
+        ("mod_magic", ctypes.c_uint64),
+        ("block_base", ctypes.c_uint64),
+        ("n_keys", ctypes.c_uint32),
+        ("n_blocks", ctypes.c_uint32),
+        ("payload_bytes", ctypes.c_uint32),
+        ("hash_count", ctypes.c_uint16),
+        ("tag_bits", ctypes.c_uint8),
+        ("hash_val_shift", ctypes.c_uint8),
+        ("bits_per_key", ctypes.c_uint32),
+        ("reserved", ctypes.c_uint32),
+    ]
+
+
+assert ctypes.sizeof(Segment) == 64
+
+SEGMENT_DTYPE = np.dtype([
+    ("key_begin", "<u8"), ("out_offset", "<u8"), ("src_page_id", "<u8"),
+    ("mod_magic", "<u8"), ("block_base", "<u8"), ("n_keys", "<u4"), ("n_blocks", "<u4"),
+    ("payload_bytes", "<u4"), ("hash_count", "<u2"), ("tag_bits", "u1"),
+    ("hash_val_shift", "u1"), ("bits_per_key", "<u4"), ("reserved", "<u4")])
+assert SEGMENT_DTYPE.itemsize == 64
+
+# every symbol include/tkv_amq.h declares
+EXPORTS = [
+    "tkv_amq_version", "tkv_amq_status_string", "tkv_amq_device_count",
+    "tkv_amq_filter_bits_per_key", "tkv_amq_vqf_load_factor", "tkv_amq_vqf_required_size",
+    "tkv_amq_vqf_nslots_for_size", "tkv_amq_plan", "tkv_amq_build", "tkv_amq_build_check",
+    "tkv_amq_probe", "tkv_amq_vqf_hash", "tkv_amq_vqf_probe_hashed", "tkv_amq_gen_keys16",
+]
+
+_lib = None
+
+
+def lib(build_if_missing: bool = True):
+    """Load libtkv_amq.so (building it in-tree if absent and hipcc is available)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = _build.LIB
+    if not os.path.exists(path):
+        if not build_if_missing:
+            raise RuntimeError(f"libtkv_amq.so not built ({path}); run __graft_entry__.build()")
+        _build.build()
+    L = ctypes.CDLL(path)
+    u64, u32, i32, vp, dbl = (ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p,
+                              ctypes.c_double)
+    L.tkv_amq_version.restype = ctypes.c_char_p
+    L.tkv_amq_version.argtypes = []
+    L.tkv_amq_status_string.restype = ctypes.c_char_p
+    L.tkv_amq_status_string.argtypes = [i32]
+    L.tkv_amq_device_count.restype = i32
+    L.tkv_amq_device_count.argtypes = []
+    L.tkv_amq_filter_bits_per_key.restype = u64
+    L.tkv_amq_filter_bits_per_key.argtypes = [i32, u64]
+    L.tkv_amq_vqf_load_factor.restype = dbl
+    L.tkv_amq_vqf_load_factor.argtypes = [i32, u64]
+    L.tkv_amq_vqf_required_size.restype = u64
+    L.tkv_amq_vqf_required_size.argtypes = [i32, u64]
+    L.tkv_amq_vqf_nslots_for_size.restype = u64
+    L.tkv_amq_vqf_nslots_for_size.argtypes = [i32, u64]
+    L.tkv_amq_plan.restype = i32
+    L.tkv_amq_plan.argtypes = [i32, vp, vp, u32, u32, u64, u64, vp,
+                               ctypes.POINTER(u64), ctypes.POINTER(u64), ctypes.POINTER(u32)]
+    L.tkv_amq_build.restype = i32
+    L.tkv_amq_build.argtypes = [i32, vp, vp, u32, u64, vp, u32, u32, vp, vp, u64, vp]
+    L.tkv_amq_build_check.restype = i32
+    L.tkv_amq_build_check.argtypes = [i32, vp, u64, vp]
+    L.tkv_amq_probe.restype = i32
+    L.tkv_amq_probe.argtypes = [i32, vp, vp, u32, vp, vp, u32, u64, vp, vp, vp]
+    L.tkv_amq_vqf_hash.restype = i32
+    L.tkv_amq_vqf_hash.argtypes = [vp, vp, u32, u64, vp, vp]
+    L.tkv_amq_vqf_probe_hashed.restype = i32
+    L.tkv_amq_vqf_probe_hashed.argtypes = [vp, vp, u32, vp, u64, vp, vp, vp]
+    L.tkv_amq_gen_keys16.restype = i32
+    L.tkv_amq_gen_keys16.argtypes = [u64, u64, u64, vp, vp]
+    _lib = L
+    return L
+
+
+def check(status: int, what: str) -> None:
+    if status != OK:
+        raise TkvAmqError(status, what)
+
+
+def version() -> str:
+    return lib().tkv_amq_version().decode()

@@ -1,0 +1,192 @@
+// tkv_amq_device.h -- gfx950 device helpers for the tkv-amq v1 filter kernels.
+//
+// XXH64 (xxHash spec; the reference hashes every key with it: vqf_hash_val,
+// src/turtle_kv/vqf_filter_page_view.hpp:32-35, and llfs's Bloom hashes).  Three forms:
+//   xxh64_bytes        any length / alignment (variable-length keys)
+//   Xxh16              16-byte keys, split so that k seeds share the seed-independent work:
+//                      for len < 32 the two 8-byte lane rounds do not depend on the seed,
+//                      so a k-hash Bloom key costs 4 + 4k 64-bit multiplies instead of 8k.
+// All arithmetic is u64 wrap-around, bit-identical to the CPU oracle.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace tkv {
+
+constexpr uint64_t kP1 = 0x9E3779B185EBCA87ULL;
+constexpr uint64_t kP2 = 0xC2B2AE3D27D4EB4FULL;
+constexpr uint64_t kP3 = 0x165667B19E3779F9ULL;
+constexpr uint64_t kP4 = 0x85EBCA77C2B2AE63ULL;
+constexpr uint64_t kP5 = 0x27D4EB2F165667C5ULL;
+
+constexpr uint64_t kVqfHashSeed = 0x9d0924dc03e79a75ULL;  // vqf_filter_page_view.hpp:26
+constexpr uint64_t kVqfMagic = 0x16015305e0f43a7dULL;     // vqf_filter_page_view.hpp:66
+constexpr uint64_t kBloomMagic = 0xca6f49a0f3f8a4b0ULL;   // tkv-amq v1 PackedBloomFilterPage
+constexpr uint64_t kVqfAltMul = 0x5bd1e995ULL;
+constexpr uint32_t kBloomHeader = 64;
+constexpr uint32_t kVqfHeader = 32;   // sizeof(PackedVqfFilter) - sizeof(vqf_metadata)
+constexpr uint32_t kVqfMetadata = 48; // sizeof(vqf_metadata)
+constexpr uint32_t kMaxBloomHashes = 32;
+
+__host__ __device__ constexpr inline uint64_t rotl64(uint64_t x, int r)
+{
+  return (x << r) | (x >> (64 - r));
+}
+
+__host__ __device__ inline uint64_t xxh_round(uint64_t acc, uint64_t in)
+{
+  acc += in * kP2;
+  acc = rotl64(acc, 31);
+  return acc * kP1;
+}
+
+__host__ __device__ inline uint64_t xxh_merge(uint64_t acc, uint64_t v)
+{
+  acc ^= xxh_round(0, v);
+  return acc * kP1 + kP4;
+}
+
+__host__ __device__ inline uint64_t xxh_avalanche(uint64_t h)
+{
+  h ^= h >> 33;
+  h *= kP2;
+  h ^= h >> 29;
+  h *= kP3;
+  h ^= h >> 32;
+  return h;
+}
+
+__host__ __device__ constexpr inline uint64_t sm64_mix(uint64_t z)
+{
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  return z ^ (z >> 31);
+}
+
+__host__ __device__ constexpr inline uint64_t splitmix64_at(uint64_t seed, uint64_t n)
+{
+  return sm64_mix(seed + n * 0x9E3779B97F4A7C15ULL);
+}
+
+// tkv-amq v1 Bloom seed table entry i
+__host__ __device__ constexpr inline uint64_t bloom_seed(uint32_t i)
+{
+  return sm64_mix(0x243F6A8885A308D3ULL + (uint64_t)i * 0x9E3779B97F4A7C15ULL);
+}
+
+// 16-byte key, seed-independent part precomputed once per key.
+struct Xxh16 {
+  uint64_t k1, k2;
+  __device__ inline Xxh16(uint64_t lo, uint64_t hi) : k1{xxh_round(0, lo)}, k2{xxh_round(0, hi)} {}
+  // `hinit` = seed + P5 + 16
+  __device__ inline uint64_t finish(uint64_t hinit) const
+  {
+    uint64_t h = hinit ^ k1;
+    h = rotl64(h, 27) * kP1 + kP4;
+    h ^= k2;
+    h = rotl64(h, 27) * kP1 + kP4;
+    return xxh_avalanche(h);
+  }
+};
+
+__device__ inline uint64_t ld64_unaligned(const uint8_t* p)
+{
+  uint64_t v = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v |= (uint64_t)p[i] << (8 * i);
+  return v;
+}
+
+__device__ inline uint32_t ld32_unaligned(const uint8_t* p)
+{
+  uint32_t v = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) v |= (uint32_t)p[i] << (8 * i);
+  return v;
+}
+
+// XXH64 of an arbitrary byte string in device memory.
+__device__ inline uint64_t xxh64_bytes(const uint8_t* p, uint64_t len, uint64_t seed)
+{
+  const uint8_t* end = p + len;
+  uint64_t h;
+  if (len >= 32) {
+    uint64_t v1 = seed + kP1 + kP2, v2 = seed + kP2, v3 = seed, v4 = seed - kP1;
+    const uint8_t* limit = end - 32;
+    do {
+      v1 = xxh_round(v1, ld64_unaligned(p));
+      v2 = xxh_round(v2, ld64_unaligned(p + 8));
+      v3 = xxh_round(v3, ld64_unaligned(p + 16));
+      v4 = xxh_round(v4, ld64_unaligned(p + 24));
+      p += 32;
+    } while (p <= limit);
+    h = rotl64(v1, 1) + rotl64(v2, 7) + rotl64(v3, 12) + rotl64(v4, 18);
+    h = xxh_merge(h, v1);
+    h = xxh_merge(h, v2);
+    h = xxh_merge(h, v3);
+    h = xxh_merge(h, v4);
+  } else {
+    h = seed + kP5;
+  }
+  h += len;
+  while (p + 8 <= end) {
+    h ^= xxh_round(0, ld64_unaligned(p));
+    h = rotl64(h, 27) * kP1 + kP4;
+    p += 8;
+  }
+  if (p + 4 <= end) {
+    h ^= (uint64_t)ld32_unaligned(p) * kP1;
+    h = rotl64(h, 23) * kP2 + kP3;
+    p += 4;
+  }
+  while (p < end) {
+    h ^= (uint64_t)(*p) * kP5;
+    h = rotl64(h, 11) * kP1;
+    ++p;
+  }
+  return xxh_avalanche(h);
+}
+
+// floor(x / d) for x < 2^64, d < 2^32, given m = floor((2^64 - 1) / d): one umulhi + fix-up.
+__device__ inline uint64_t mod_by_magic(uint64_t x, uint64_t d, uint64_t m)
+{
+  uint64_t q = __umul64hi(x, m);
+  uint64_t r = x - q * d;
+  while (r >= d) r -= d;
+  return r;
+}
+
+// 64-lane wave helpers
+__device__ inline uint64_t lanemask_lt()
+{
+  const uint32_t lane = __lane_id();
+  return lane == 0 ? 0ull : (~0ull >> (64 - lane));
+}
+
+// position of the r-th (0-based) set bit of x; x must have > r set bits
+__device__ inline int select64(uint64_t x, int r)
+{
+  int pos = 0;
+  int c = __popcll(x & 0xffffffffull);
+  if (r >= c) { r -= c; x >>= 32; pos += 32; }
+  c = __popc((uint32_t)(x & 0xffffu));
+  if (r >= c) { r -= c; x >>= 16; pos += 16; }
+  c = __popc((uint32_t)(x & 0xffu));
+  if (r >= c) { r -= c; x >>= 8; pos += 8; }
+  c = __popc((uint32_t)(x & 0xfu));
+  if (r >= c) { r -= c; x >>= 4; pos += 4; }
+  c = __popc((uint32_t)(x & 0x3u));
+  if (r >= c) { r -= c; x >>= 2; pos += 2; }
+  c = (int)(x & 1u);
+  if (r >= c) { pos += 1; }
+  return pos;
+}
+
+__device__ inline int select128(uint64_t lo, uint64_t hi, int r)
+{
+  const int c0 = __popcll(lo);
+  return r < c0 ? select64(lo, r) : 64 + select64(hi, r - c0);
+}
+
+}  // namespace tkv

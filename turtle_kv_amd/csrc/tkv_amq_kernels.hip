@@ -1,0 +1,994 @@
+// tkv_amq_kernels.hip -- CDNA4 (gfx950) kernels for TurtleKV's per-leaf AMQ filters.
+//
+// Hot path:
+//   bloom_build_lds      one workgroup per leaf filter ("segment"); 16-byte keys streamed with
+//                        global_load_dwordx4, k XXH64 hashes in registers, bits set in an LDS
+//                        image of the whole filter with ds_or_b32, image written out with
+//                        16-byte coalesced stores.  No MFMA: this is hashing and bit-set.
+//   vqf_decide           one wave per segment replays the reference's insert order exactly
+//                        (power-of-two-choice decisions depend only on per-block counts);
+//                        per 64-key chunk the dependency is resolved with bit-sliced ballots,
+//                        only keys whose primary block may be near the CHECK_ALT threshold
+//                        run the serial scan.  Emits (block, rank) -> (bucket, tag) records.
+//   vqf_place            one wave per 64-byte VQF block: stable rank by bucket offset with
+//                        ballots, metadata zeros at rank+offset, block image in LDS, 16-byte
+//                        stores.
+//   *_probe              one lane per (query, segment) test.
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdint.h>
+#include <string.h>
+
+#include "tkv_amq.h"
+#include "tkv_amq_device.h"
+
+namespace tkv {
+
+// ---------------------------------------------------------------------------------------
+// constant tables
+// ---------------------------------------------------------------------------------------
+struct BloomSeeds {
+  uint64_t seed[kMaxBloomHashes];
+  uint64_t hinit16[kMaxBloomHashes];  // seed + P5 + 16 : XXH64 state after the len add
+};
+
+constexpr BloomSeeds make_bloom_seeds()
+{
+  BloomSeeds t{};
+  for (uint32_t i = 0; i < kMaxBloomHashes; ++i) {
+    t.seed[i] = bloom_seed(i);
+    t.hinit16[i] = t.seed[i] + kP5 + 16;
+  }
+  return t;
+}
+
+// constant-initialised at load: no host upload, so every entry point is graph-capturable
+__constant__ BloomSeeds c_bloom = make_bloom_seeds();
+
+// ---------------------------------------------------------------------------------------
+// key access
+// ---------------------------------------------------------------------------------------
+enum KeyMode : int { kKey16 = 0, kKeyFixed = 1, kKeyVar = 2 };
+
+template <int MODE>
+__device__ inline uint64_t hash_key(const uint8_t* keys, const uint64_t* offs, uint32_t stride,
+                                    uint64_t i, uint64_t seed)
+{
+  if constexpr (MODE == kKeyFixed) {
+    return xxh64_bytes(keys + i * stride, stride, seed);
+  } else {
+    const uint64_t b = offs[i];
+    return xxh64_bytes(keys + b, offs[i + 1] - b, seed);
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Bloom build (LDS image per segment)
+// ---------------------------------------------------------------------------------------
+__device__ inline void lds_set_bit(uint32_t* blk, uint32_t bit)
+{
+  atomicOr(blk + (bit >> 5), 1u << (bit & 31));
+}
+
+__device__ inline void write_bloom_header(uint8_t* payload, const tkv_amq_segment& sg, int part)
+{
+  // 64-byte PackedBloomFilterPage header, written as 4 x 16 bytes
+  uint64_t w0, w1;
+  const uint64_t nb = sg.n_blocks;
+  switch (part) {
+    case 0: w0 = kBloomMagic; w1 = 512ull * nb; break;
+    case 1: w0 = sg.src_page_id; w1 = 0; break;
+    case 2: w0 = 8ull * nb; w1 = nb | ((uint64_t)sg.hash_count << 32) | (2ull << 48); break;
+    default: w0 = sg.n_keys; w1 = 0; break;
+  }
+  ulonglong2 v;
+  v.x = w0;
+  v.y = w1;
+  reinterpret_cast<ulonglong2*>(payload)[part] = v;
+}
+
+template <int K>
+__device__ inline void bloom_insert16(uint32_t* s_bits, uint32_t nb, uint32_t k, const uint4& kv)
+{
+  const Xxh16 x((uint64_t)kv.x | ((uint64_t)kv.y << 32), (uint64_t)kv.z | ((uint64_t)kv.w << 32));
+  const uint64_t h0 = x.finish(c_bloom.hinit16[0]);
+  uint32_t* blk = s_bits + 16 * (uint32_t)__umul64hi(h0, (uint64_t)nb);
+  lds_set_bit(blk, (uint32_t)h0 & 511u);
+  if constexpr (K != 0) {
+#pragma unroll
+    for (uint32_t j = 1; j < (uint32_t)K; ++j)
+      lds_set_bit(blk, (uint32_t)x.finish(c_bloom.hinit16[j]) & 511u);
+  } else {
+    for (uint32_t j = 1; j < k; ++j) lds_set_bit(blk, (uint32_t)x.finish(c_bloom.hinit16[j]) & 511u);
+  }
+}
+
+template <int K>
+__device__ inline void bloom_keys16_lds(const uint4* __restrict__ kp, uint32_t n, uint32_t nb,
+                                        uint32_t k, uint32_t* s_bits)
+{
+  const uint32_t tid = threadIdx.x;
+  constexpr int U = 4;  // 4 x 16-byte loads in flight per lane
+  for (uint32_t base = 0; base < n; base += 256 * U) {
+    uint4 kv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t i = base + u * 256 + tid;
+      if (i < n) kv[u] = kp[i];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t i = base + u * 256 + tid;
+      if (i < n) bloom_insert16<K>(s_bits, nb, k, kv[u]);
+    }
+  }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256) void bloom_build_lds(const uint8_t* __restrict__ keys,
+                                                       const uint64_t* __restrict__ offs,
+                                                       uint32_t stride,
+                                                       const tkv_amq_segment* __restrict__ segs,
+                                                       uint8_t* __restrict__ out)
+{
+  extern __shared__ uint32_t s_bits[];
+  const tkv_amq_segment sg = segs[blockIdx.x];
+  const uint32_t n = sg.n_keys, nb = sg.n_blocks, k = sg.hash_count;
+  if (k == 0) return;  // bits_per_key == 0: no filter (filter_builder.hpp:115-117)
+  const uint32_t tid = threadIdx.x;
+  const uint32_t nwords = nb * 16;
+
+  for (uint32_t w = tid; w < nwords; w += 256) s_bits[w] = 0;
+  __syncthreads();
+
+  if constexpr (MODE == kKey16) {
+    const uint4* kp = reinterpret_cast<const uint4*>(keys) + sg.key_begin;
+    // k = 7 / 8 are the hash counts at 10 / 12 bits per key: fully unrolled variants
+    if (k == 7) bloom_keys16_lds<7>(kp, n, nb, k, s_bits);
+    else if (k == 8) bloom_keys16_lds<8>(kp, n, nb, k, s_bits);
+    else bloom_keys16_lds<0>(kp, n, nb, k, s_bits);
+  } else {
+    for (uint32_t i = tid; i < n; i += 256) {
+      const uint64_t gi = sg.key_begin + i;
+      const uint64_t h0 = hash_key<MODE>(keys, offs, stride, gi, c_bloom.seed[0]);
+      uint32_t* blk = s_bits + 16 * (uint32_t)__umul64hi(h0, (uint64_t)nb);
+      lds_set_bit(blk, (uint32_t)h0 & 511u);
+      for (uint32_t j = 1; j < k; ++j)
+        lds_set_bit(blk, (uint32_t)hash_key<MODE>(keys, offs, stride, gi, c_bloom.seed[j]) & 511u);
+    }
+  }
+  __syncthreads();
+
+  uint8_t* payload = out + sg.out_offset;
+  if (tid < 4) write_bloom_header(payload, sg, tid);
+  uint4* dst = reinterpret_cast<uint4*>(payload + kBloomHeader);
+  const uint4* src = reinterpret_cast<const uint4*>(s_bits);
+  for (uint32_t q = tid; q < nb * 4; q += 256) dst[q] = src[q];
+}
+
+// ---------------------------------------------------------------------------------------
+// Bloom build, global-memory fallback for segments whose image exceeds the LDS budget
+// (monolithic filters).  Pass 1 zeroes + headers, pass 2 sets bits with device atomics.
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void bloom_global_init(const tkv_amq_segment* __restrict__ segs,
+                                                         uint8_t* __restrict__ out)
+{
+  const tkv_amq_segment sg = segs[blockIdx.x];
+  if (sg.hash_count == 0) return;
+  uint8_t* payload = out + sg.out_offset;
+  const uint32_t tid = threadIdx.x;
+  if (tid < 4) write_bloom_header(payload, sg, tid);
+  uint4* dst = reinterpret_cast<uint4*>(payload + kBloomHeader);
+  const uint4 z = {0, 0, 0, 0};
+  for (uint64_t q = tid; q < 4ull * sg.n_blocks; q += 256) dst[q] = z;
+}
+
+__device__ inline uint32_t find_segment(const tkv_amq_segment* segs, uint32_t n_segs,
+                                        uint64_t key)
+{
+  uint32_t lo = 0, hi = n_segs;  // last s with key_begin <= key
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (segs[mid].key_begin <= key) lo = mid;
+    else hi = mid;
+  }
+  return lo;
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256) void bloom_global_set(const uint8_t* __restrict__ keys,
+                                                        const uint64_t* __restrict__ offs,
+                                                        uint32_t stride,
+                                                        const tkv_amq_segment* __restrict__ segs,
+                                                        uint32_t n_segs, uint64_t n_keys,
+                                                        uint8_t* __restrict__ out)
+{
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n_keys;
+       i += (uint64_t)gridDim.x * 256) {
+    const uint32_t s = find_segment(segs, n_segs, i);
+    const tkv_amq_segment& sg = segs[s];
+    if (sg.hash_count == 0 || i >= sg.key_begin + sg.n_keys) continue;
+    uint32_t* words = reinterpret_cast<uint32_t*>(out + sg.out_offset + kBloomHeader);
+    uint64_t h0;
+    if constexpr (MODE == kKey16) {
+      const uint4 kv = reinterpret_cast<const uint4*>(keys)[i];
+      const Xxh16 x((uint64_t)kv.x | ((uint64_t)kv.y << 32), (uint64_t)kv.z | ((uint64_t)kv.w << 32));
+      h0 = x.finish(c_bloom.hinit16[0]);
+      uint32_t* blk = words + 16 * (uint64_t)__umul64hi(h0, (uint64_t)sg.n_blocks);
+      const uint32_t b0 = (uint32_t)h0 & 511u;
+      atomicOr(blk + (b0 >> 5), 1u << (b0 & 31));
+      for (uint32_t j = 1; j < sg.hash_count; ++j) {
+        const uint32_t b = (uint32_t)x.finish(c_bloom.hinit16[j]) & 511u;
+        atomicOr(blk + (b >> 5), 1u << (b & 31));
+      }
+    } else {
+      h0 = hash_key<MODE>(keys, offs, stride, i, c_bloom.seed[0]);
+      uint32_t* blk = words + 16 * (uint64_t)__umul64hi(h0, (uint64_t)sg.n_blocks);
+      const uint32_t b0 = (uint32_t)h0 & 511u;
+      atomicOr(blk + (b0 >> 5), 1u << (b0 & 31));
+      for (uint32_t j = 1; j < sg.hash_count; ++j) {
+        const uint32_t b = (uint32_t)hash_key<MODE>(keys, offs, stride, i, c_bloom.seed[j]) & 511u;
+        atomicOr(blk + (b >> 5), 1u << (b & 31));
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Bloom probe
+// ---------------------------------------------------------------------------------------
+template <int MODE>
+__global__ __launch_bounds__(256) void bloom_probe(const uint8_t* __restrict__ filters,
+                                                   const tkv_amq_segment* __restrict__ segs,
+                                                   const uint8_t* __restrict__ q,
+                                                   const uint64_t* __restrict__ qoffs,
+                                                   uint32_t stride, uint64_t n,
+                                                   const uint32_t* __restrict__ qseg,
+                                                   uint8_t* __restrict__ result)
+{
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const tkv_amq_segment& sg = segs[qseg[i]];
+  const uint32_t k = sg.hash_count;
+  if (k == 0) {  // no filter page: reject_page returns kUnknown => cannot reject
+    result[i] = 1;
+    return;
+  }
+  const uint64_t* words = reinterpret_cast<const uint64_t*>(filters + sg.out_offset + kBloomHeader);
+  uint32_t ok = 1;
+  if constexpr (MODE == kKey16) {
+    const uint4 kv = reinterpret_cast<const uint4*>(q)[i];
+    const Xxh16 x((uint64_t)kv.x | ((uint64_t)kv.y << 32), (uint64_t)kv.z | ((uint64_t)kv.w << 32));
+    const uint64_t h0 = x.finish(c_bloom.hinit16[0]);
+    const uint64_t* blk = words + 8 * __umul64hi(h0, (uint64_t)sg.n_blocks);
+    uint32_t b = (uint32_t)h0 & 511u;
+    ok &= (uint32_t)(blk[b >> 6] >> (b & 63));
+    for (uint32_t j = 1; j < k; ++j) {
+      b = (uint32_t)x.finish(c_bloom.hinit16[j]) & 511u;
+      ok &= (uint32_t)(blk[b >> 6] >> (b & 63));
+    }
+  } else {
+    const uint64_t h0 = hash_key<MODE>(q, qoffs, stride, i, c_bloom.seed[0]);
+    const uint64_t* blk = words + 8 * __umul64hi(h0, (uint64_t)sg.n_blocks);
+    uint32_t b = (uint32_t)h0 & 511u;
+    ok &= (uint32_t)(blk[b >> 6] >> (b & 63));
+    for (uint32_t j = 1; j < k; ++j) {
+      b = (uint32_t)hash_key<MODE>(q, qoffs, stride, i, c_bloom.seed[j]) & 511u;
+      ok &= (uint32_t)(blk[b >> 6] >> (b & 63));
+    }
+  }
+  result[i] = (uint8_t)(ok & 1u);
+}
+
+// ---------------------------------------------------------------------------------------
+// VQF constants (tkv-amq v1)
+// ---------------------------------------------------------------------------------------
+template <int T>
+struct Vqf;
+template <>
+struct Vqf<8> {
+  static constexpr uint32_t kSlots = 48, kBuckets = 80, kThreshold = 37, kMdBytes = 16;
+  static constexpr uint32_t kOffsetBits = 7;
+  using Entry = uint16_t;  // (bucket offset << 8) | tag
+};
+template <>
+struct Vqf<16> {
+  static constexpr uint32_t kSlots = 28, kBuckets = 36, kThreshold = 22, kMdBytes = 8;
+  static constexpr uint32_t kOffsetBits = 6;
+  using Entry = uint32_t;  // (bucket offset << 16) | tag
+};
+// kThreshold: the reference-side vqf consults the alternate block only when the primary's
+// metadata popcount is below CHECK_ALT (92 / 43), i.e. when its count >= kThreshold.
+
+constexpr uint32_t kVqfTempStride = 128;  // workspace bytes per block (>= slots * entry)
+constexpr uint32_t kVqfMaxLdsBlocks = 16384;
+
+// workspace: [status u32 x16][nelts u32 x n_segs][pad to 256][128-byte record per block]
+// record = slots x Entry (insertion order) ... u32 final count at byte 124
+struct VqfWorkspace {
+  uint32_t* status;
+  uint32_t* nelts;
+  uint8_t* temp;
+};
+constexpr uint32_t kVqfCountByte = 124;
+
+__host__ __device__ inline uint64_t vqf_temp_offset(uint32_t n_segs)
+{
+  return (64 + 4ull * n_segs + 255) & ~255ull;
+}
+
+__host__ __device__ inline VqfWorkspace vqf_workspace(void* base, uint32_t n_segs)
+{
+  uint8_t* p = static_cast<uint8_t*>(base);
+  VqfWorkspace w;
+  w.status = reinterpret_cast<uint32_t*>(p);
+  w.nelts = reinterpret_cast<uint32_t*>(p + 64);
+  w.temp = p + vqf_temp_offset(n_segs);
+  return w;
+}
+
+__device__ inline uint32_t& vqf_count(VqfWorkspace ws, uint64_t block)
+{
+  return *reinterpret_cast<uint32_t*>(ws.temp + block * kVqfTempStride + kVqfCountByte);
+}
+
+// bit-sliced "which lanes hold the same value": returns the lanes j (within `valid`) with
+// value_j == mine, using one ballot per bit of the value.
+__device__ inline uint64_t match_lanes(uint32_t mine, uint32_t value, bool active, uint64_t valid,
+                                       int nbits)
+{
+  uint64_t m = valid;
+  for (int j = 0; j < nbits; ++j) {
+    const uint64_t b = __ballot(active && ((value >> j) & 1u));
+    m &= ((mine >> j) & 1u) ? b : ~b;
+  }
+  return m;
+}
+
+template <int T, int MODE>
+__device__ void vqf_decide_body(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs,
+                                uint32_t stride, const tkv_amq_segment& sg, uint32_t seg_index,
+                                VqfWorkspace ws, uint32_t* cnt)
+{
+  using C = Vqf<T>;
+  const uint32_t lane = threadIdx.x;
+  const uint32_t n = sg.n_keys, nb = sg.n_blocks;
+  const uint64_t R = (uint64_t)nb * C::kBuckets;
+  const uint64_t magic = sg.mod_magic;
+  const uint64_t mask = ~0ull << sg.hash_val_shift;  // filter_builder.hpp:187
+  const uint64_t tmask = (1ull << T) - 1;
+  const int nbits = nb <= 1 ? 0 : 32 - __clz(nb - 1);
+  const uint64_t lt = lanemask_lt();
+  typename C::Entry* temp =
+      reinterpret_cast<typename C::Entry*>(ws.temp + sg.block_base * kVqfTempStride);
+
+  for (uint32_t b = lane; b < nb; b += 64) cnt[b] = 0;
+  __syncthreads();
+
+  uint32_t nelts = 0;
+  uint32_t fail = 0;
+  for (uint32_t base = 0; base < n; base += 64) {
+    const uint32_t i = base + lane;
+    const bool valid = i < n;
+    uint64_t h = 0;
+    if (valid) {
+      const uint64_t gi = sg.key_begin + i;
+      if constexpr (MODE == kKey16) {
+        const uint4 kv = reinterpret_cast<const uint4*>(keys)[gi];
+        const Xxh16 x((uint64_t)kv.x | ((uint64_t)kv.y << 32), (uint64_t)kv.z | ((uint64_t)kv.w << 32));
+        h = x.finish(kVqfHashSeed + kP5 + 16);
+      } else {
+        h = hash_key<MODE>(keys, offs, stride, gi, kVqfHashSeed);
+      }
+    }
+    const bool kept = valid && ((h & mask) == h);  // filter_builder.hpp:210
+    const uint64_t keptmask = __ballot(kept);
+    nelts += __popcll(keptmask);
+
+    const uint32_t tag = (uint32_t)(h & tmask);
+    const uint32_t pi = (uint32_t)mod_by_magic(h >> T, R, magic);
+    const uint32_t ai = (uint32_t)mod_by_magic((h ^ ((uint64_t)tag * kVqfAltMul)) >> T, R, magic);
+    const uint32_t pb = pi / C::kBuckets, po = pi - pb * C::kBuckets;
+    const uint32_t ab = ai / C::kBuckets, ao = ai - ab * C::kBuckets;
+
+    const uint64_t Mpp = match_lanes(pb, pb, kept, keptmask, nbits);
+    const uint64_t Map = match_lanes(pb, ab, kept, keptmask, nbits);
+    const uint64_t Mpa = match_lanes(ab, pb, kept, keptmask, nbits);
+
+    const uint32_t cbp = kept ? cnt[pb] : 0;
+    const uint32_t cba = kept ? cnt[ab] : 0;
+    // upper bound of the primary block's count when this key is inserted
+    const uint32_t U = cbp + __popcll((Mpp | Map) & lt);
+    const uint64_t NT = __ballot(kept && U >= C::kThreshold);
+
+    bool alt = false;
+    if (NT != 0) {
+      uint32_t cp = cbp + __popcll(Mpp & lt & ~NT);
+      uint32_t ca = cba + __popcll(Mpa & lt & ~NT);
+      uint64_t rem = NT;
+      while (rem != 0) {
+        const uint32_t k = (uint32_t)__ffsll((long long)rem) - 1;
+        rem &= rem - 1;
+        // decision of lane k (vqf_insert): consult the alternate block only when the
+        // primary is past CHECK_ALT; move iff the alternate is strictly emptier.
+        const bool my_alt = (cp >= C::kThreshold) && (pb != ab) && (ca < cp);
+        const bool my_full = my_alt ? (ca >= C::kSlots) : (cp >= C::kSlots);
+        const uint32_t my_ch = my_alt ? ab : pb;
+        const uint32_t ch_k = __builtin_amdgcn_readlane(my_ch, k);
+        fail |= (uint32_t)__builtin_amdgcn_readlane((int)my_full, k);
+        if (lane == k) alt = my_alt;
+        if (lane > k) {
+          cp += (pb == ch_k);
+          ca += (ab == ch_k);
+        }
+      }
+    }
+    const uint32_t chosen = alt ? ab : pb;
+    const uint32_t cho = alt ? ao : po;
+    const uint64_t Mcc = match_lanes(chosen, chosen, kept, keptmask, nbits);
+    const uint32_t r = (alt ? cba : cbp) + __popcll(Mcc & lt);
+    if (kept) {
+      if (r < C::kSlots)
+        temp[(uint64_t)chosen * (kVqfTempStride / sizeof(typename C::Entry)) + r] =
+            (typename C::Entry)((cho << T) | tag);
+      atomicAdd(cnt + chosen, 1u);
+    }
+  }
+  __syncthreads();
+  for (uint32_t b = lane; b < nb; b += 64) {
+    const uint32_t c = cnt[b];
+    vqf_count(ws, sg.block_base + b) = c < C::kSlots ? c : C::kSlots;
+  }
+  if (lane == 0) {
+    ws.nelts[seg_index] = nelts;
+    if (fail) atomicOr(ws.status, 1u);
+  }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(64) void vqf_decide(const uint8_t* __restrict__ keys,
+                                                 const uint64_t* __restrict__ offs, uint32_t stride,
+                                                 const tkv_amq_segment* __restrict__ segs,
+                                                 void* ws_base, uint32_t n_segs)
+{
+  extern __shared__ uint32_t s_cnt[];
+  const tkv_amq_segment sg = segs[blockIdx.x];
+  const VqfWorkspace ws = vqf_workspace(ws_base, n_segs);
+  if (sg.tag_bits == 8) vqf_decide_body<8, MODE>(keys, offs, stride, sg, blockIdx.x, ws, s_cnt);
+  else if (sg.tag_bits == 16) vqf_decide_body<16, MODE>(keys, offs, stride, sg, blockIdx.x, ws, s_cnt);
+}
+
+template <int T>
+__device__ void vqf_place_body(const tkv_amq_segment& sg, uint32_t seg_index, VqfWorkspace ws,
+                               uint8_t* __restrict__ out, uint32_t* img)
+{
+  using C = Vqf<T>;
+  const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const uint32_t nb = sg.n_blocks;
+  uint8_t* payload = out + sg.out_offset;
+
+  if (tid < 5) {
+    // PackedVqfFilter header (vqf_filter_page_view.hpp:79-94) + vqf_metadata
+    uint64_t w0, w1;
+    switch (tid) {
+      case 0: w0 = kVqfMagic; w1 = sg.src_page_id; break;
+      case 1: w0 = kVqfHashSeed; w1 = ~0ull << sg.hash_val_shift; break;
+      case 2: w0 = 64ull * nb; w1 = T; break;
+      case 3: w0 = (uint64_t)nb * C::kBuckets << T; w1 = nb; break;
+      default: w0 = ws.nelts[seg_index]; w1 = (uint64_t)nb * C::kSlots; break;
+    }
+    ulonglong2 v;
+    v.x = w0;
+    v.y = w1;
+    reinterpret_cast<ulonglong2*>(payload)[tid] = v;
+  }
+
+  const typename C::Entry* temp =
+      reinterpret_cast<const typename C::Entry*>(ws.temp + sg.block_base * kVqfTempStride);
+  uint32_t* my_img = img + 16 * wave;
+  uint4* dst_blocks = reinterpret_cast<uint4*>(payload + kVqfHeader + kVqfMetadata);
+  const uint64_t lt = lanemask_lt();
+
+  for (uint32_t b = wave; b < nb; b += 4) {
+    const uint32_t c = vqf_count(ws, sg.block_base + b);
+    const bool has = lane < c;
+    uint32_t e = 0;
+    if (has) e = temp[(uint64_t)b * (kVqfTempStride / sizeof(typename C::Entry)) + lane];
+    const uint32_t o = e >> T, tag = e & ((1u << T) - 1);
+    // stable rank by bucket offset (insertion order breaks ties): tags of bucket o are
+    // appended at its end by vqf_insert, so the final layout is a stable sort by offset.
+    const uint64_t V = __ballot(has);
+    uint64_t less = 0, eq = V;
+    for (int bit = (int)C::kOffsetBits - 1; bit >= 0; --bit) {
+      const uint64_t bb = __ballot(has && ((o >> bit) & 1u));
+      if ((o >> bit) & 1u) {
+        less |= eq & ~bb;
+        eq &= bb;
+      } else {
+        eq &= ~bb;
+      }
+    }
+    const uint32_t rank = __popcll(less) + __popcll(eq & lt);
+
+    // block image: metadata all ones (top bit clear while empty), tags zero
+    if (lane < 16) {
+      uint32_t v = 0;
+      if (lane * 4 < C::kMdBytes) {
+        v = 0xffffffffu;
+        if (c == 0 && lane * 4 + 4 == C::kMdBytes) v = 0x7fffffffu;
+      }
+      my_img[lane] = v;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    if (has) {
+      const uint32_t z = rank + o;  // the metadata zero for this tag
+      atomicAnd(my_img + (z >> 5), ~(1u << (z & 31)));
+      const uint32_t byte = C::kMdBytes + rank * (T / 8);
+      atomicOr(my_img + (byte >> 2), tag << (8 * (byte & 3)));
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    if (lane < 4) {
+      const uint4 v = reinterpret_cast<const uint4*>(my_img)[lane];
+      dst_blocks[(uint64_t)b * 4 + lane] = v;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+__global__ __launch_bounds__(256) void vqf_place(const tkv_amq_segment* __restrict__ segs,
+                                                 void* ws_base, uint32_t n_segs,
+                                                 uint8_t* __restrict__ out)
+{
+  __shared__ uint32_t s_img[4 * 16];
+  const tkv_amq_segment sg = segs[blockIdx.x];
+  const VqfWorkspace ws = vqf_workspace(ws_base, n_segs);
+  if (sg.tag_bits == 8) vqf_place_body<8>(sg, blockIdx.x, ws, out, s_img);
+  else if (sg.tag_bits == 16) vqf_place_body<16>(sg, blockIdx.x, ws, out, s_img);
+}
+
+// ---------------------------------------------------------------------------------------
+// VQF probe (PackedVqfFilter::is_present, vqf_filter_page_view.hpp:113-125)
+// ---------------------------------------------------------------------------------------
+template <int T>
+__device__ inline bool vqf_bucket_has(const uint8_t* blocks, uint32_t idx, uint32_t tag)
+{
+  using C = Vqf<T>;
+  const uint32_t blk = idx / C::kBuckets, o = idx - blk * C::kBuckets;
+  const uint8_t* bp = blocks + (uint64_t)blk * 64;
+  uint64_t lo, hi = 0;
+  if constexpr (T == 8) {
+    const ulonglong2 md = *reinterpret_cast<const ulonglong2*>(bp);
+    lo = md.x;
+    hi = md.y;
+  } else {
+    lo = *reinterpret_cast<const uint64_t*>(bp);
+  }
+  const int start = o == 0 ? 0 : select128(lo, hi, (int)o - 1) - ((int)o - 1);
+  const int end = select128(lo, hi, (int)o) - (int)o;
+  for (int p = start; p < end; ++p) {
+    uint32_t tv;
+    if constexpr (T == 8) tv = bp[C::kMdBytes + p];
+    else tv = *reinterpret_cast<const uint16_t*>(bp + C::kMdBytes + 2 * p);
+    if (tv == tag) return true;
+  }
+  return false;
+}
+
+template <int T>
+__device__ inline bool vqf_present(const uint8_t* payload, const tkv_amq_segment& sg, uint64_t h)
+{
+  using C = Vqf<T>;
+  const uint64_t R = (uint64_t)sg.n_blocks * C::kBuckets;
+  const uint32_t tag = (uint32_t)(h & ((1ull << T) - 1));
+  const uint32_t pi = (uint32_t)mod_by_magic(h >> T, R, sg.mod_magic);
+  const uint32_t ai = (uint32_t)mod_by_magic((h ^ ((uint64_t)tag * kVqfAltMul)) >> T, R, sg.mod_magic);
+  const uint8_t* blocks = payload + kVqfHeader + kVqfMetadata;
+  return vqf_bucket_has<T>(blocks, pi, tag) || vqf_bucket_has<T>(blocks, ai, tag);
+}
+
+__device__ inline uint8_t vqf_probe_one(const uint8_t* filters, const tkv_amq_segment& sg, uint64_t h)
+{
+  if (sg.tag_bits == 0) return 1;  // no filter: cannot reject
+  const uint8_t* payload = filters + sg.out_offset;
+  const uint64_t mask = *reinterpret_cast<const uint64_t*>(payload + 24);
+  if ((h & mask) != h) return 1;  // dropped hash values are always "maybe"
+  return sg.tag_bits == 8 ? (uint8_t)vqf_present<8>(payload, sg, h)
+                          : (uint8_t)vqf_present<16>(payload, sg, h);
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256) void vqf_probe(const uint8_t* __restrict__ filters,
+                                                 const tkv_amq_segment* __restrict__ segs,
+                                                 const uint8_t* __restrict__ q,
+                                                 const uint64_t* __restrict__ qoffs, uint32_t stride,
+                                                 uint64_t n, const uint32_t* __restrict__ qseg,
+                                                 uint8_t* __restrict__ result)
+{
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  uint64_t h;
+  if constexpr (MODE == kKey16) {
+    const uint4 kv = reinterpret_cast<const uint4*>(q)[i];
+    const Xxh16 x((uint64_t)kv.x | ((uint64_t)kv.y << 32), (uint64_t)kv.z | ((uint64_t)kv.w << 32));
+    h = x.finish(kVqfHashSeed + kP5 + 16);
+  } else {
+    h = hash_key<MODE>(q, qoffs, stride, i, kVqfHashSeed);
+  }
+  result[i] = vqf_probe_one(filters, segs[qseg[i]], h);
+}
+
+__global__ __launch_bounds__(256) void vqf_probe_hashed(const uint8_t* __restrict__ filters,
+                                                        const tkv_amq_segment* __restrict__ segs,
+                                                        const uint64_t* __restrict__ hashes,
+                                                        uint64_t n, const uint32_t* __restrict__ qseg,
+                                                        uint8_t* __restrict__ result)
+{
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  result[i] = vqf_probe_one(filters, segs[qseg[i]], hashes[i]);
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256) void vqf_hash_kernel(const uint8_t* __restrict__ q,
+                                                       const uint64_t* __restrict__ qoffs,
+                                                       uint32_t stride, uint64_t n,
+                                                       uint64_t* __restrict__ out)
+{
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  if constexpr (MODE == kKey16) {
+    const uint4 kv = reinterpret_cast<const uint4*>(q)[i];
+    const Xxh16 x((uint64_t)kv.x | ((uint64_t)kv.y << 32), (uint64_t)kv.z | ((uint64_t)kv.w << 32));
+    out[i] = x.finish(kVqfHashSeed + kP5 + 16);
+  } else {
+    out[i] = hash_key<MODE>(q, qoffs, stride, i, kVqfHashSeed);
+  }
+}
+
+__global__ __launch_bounds__(256) void gen_keys16_kernel(uint64_t seed, uint64_t first, uint64_t n,
+                                                         ulonglong2* __restrict__ out)
+{
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * 256) {
+    const uint64_t g = first + i;
+    ulonglong2 v;
+    v.x = splitmix64_at(seed, 2 * g + 1);
+    v.y = splitmix64_at(seed, 2 * g + 2);
+    out[i] = v;
+  }
+}
+
+}  // namespace tkv
+
+// =======================================================================================
+// host side: planning (sizing restated from the reference) and the C ABI
+// =======================================================================================
+using namespace tkv;
+
+namespace {
+
+constexpr uint32_t kBloomLdsBudget = 64 * 1024;
+
+inline uint32_t vqf_slots(int t) { return t == 8 ? 48u : 28u; }
+inline uint32_t vqf_buckets(int t) { return t == 8 ? 80u : 36u; }
+
+uint32_t bloom_hash_count(uint32_t bpk)
+{
+  uint32_t k = (uint32_t)((double)bpk * 0.69314718055994530942 + 0.5);
+  return k < 1 ? 1 : (k > kMaxBloomHashes ? kMaxBloomHashes : k);
+}
+
+inline int key_mode(const uint64_t* offs, uint32_t stride)
+{
+  if (offs) return kKeyVar;
+  return stride == 16 ? kKey16 : kKeyFixed;
+}
+
+inline hipStream_t as_stream(void* s) { return static_cast<hipStream_t>(s); }
+
+inline uint64_t div_up(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
+
+}  // namespace
+
+extern "C" {
+
+const char* tkv_amq_version(void) { return "tkv-amq 0.1.0 (spec tkv-amq-v1, gfx950)"; }
+
+const char* tkv_amq_status_string(int s)
+{
+  switch (s) {
+    case TKV_AMQ_OK: return "OK";
+    case TKV_AMQ_INVALID_ARGUMENT: return "InvalidArgument";
+    case TKV_AMQ_RESOURCE_EXHAUSTED: return "ResourceExhausted";
+    case TKV_AMQ_INTERNAL: return "Internal";
+    case TKV_AMQ_UNAVAILABLE: return "Unavailable";
+    default: return "Unknown";
+  }
+}
+
+int tkv_amq_device_count(void)
+{
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+uint64_t tkv_amq_filter_bits_per_key(int kind, uint64_t bpk)
+{
+  // tree/tree_options.hpp:155-164
+  if (kind != TKV_AMQ_VQF) return bpk;
+  return bpk == 0 ? 0 : (bpk < 12 ? 12 : bpk);
+}
+
+double tkv_amq_vqf_load_factor(int tag_bits, uint64_t bpk)
+{
+  // vqf_filter_page_view.hpp:39-59
+  if (bpk == 0) return 0;
+  const double b = (double)bpk;
+  return tag_bits == 8 ? 10.2 / b : 18.0 / b;
+}
+
+uint64_t tkv_amq_vqf_required_size(int tag_bits, uint64_t nslots)
+{
+  const uint64_t s = vqf_slots(tag_bits);
+  return kVqfMetadata + 64ull * ((nslots + s) / s);
+}
+
+uint64_t tkv_amq_vqf_nslots_for_size(int tag_bits, uint64_t bytes)
+{
+  if (bytes < kVqfMetadata + 64) return 0;
+  return (bytes - kVqfMetadata) / 64 * vqf_slots(tag_bits) - 1;
+}
+
+int tkv_amq_plan(int kind, const uint64_t* counts, const uint64_t* src_ids, uint32_t n_segs,
+                 uint32_t bpk, uint64_t cap, uint64_t stride, tkv_amq_segment* segs,
+                 uint64_t* total_out, uint64_t* ws_bytes, uint32_t* max_blocks_out)
+{
+  if ((kind != TKV_AMQ_BLOOM && kind != TKV_AMQ_VQF) || (n_segs && (!counts || !segs)))
+    return TKV_AMQ_INVALID_ARGUMENT;
+  if (kind == TKV_AMQ_BLOOM && bpk > 64) return TKV_AMQ_INVALID_ARGUMENT;
+  if (kind == TKV_AMQ_VQF && bpk != 0 && bpk < 12) return TKV_AMQ_INVALID_ARGUMENT;  // :46
+  if (stride && (stride % 64)) return TKV_AMQ_INVALID_ARGUMENT;
+  if (kind == TKV_AMQ_VQF && bpk != 0 && cap == 0) return TKV_AMQ_INVALID_ARGUMENT;
+
+  uint64_t off = 0, key_begin = 0, block_base = 0;
+  uint32_t max_blocks = 0;
+  for (uint32_t s = 0; s < n_segs; ++s) {
+    tkv_amq_segment& g = segs[s];
+    memset(&g, 0, sizeof(g));
+    const uint64_t n = counts[s];
+    if (n > 0xffffffffull) return TKV_AMQ_INVALID_ARGUMENT;
+    g.key_begin = key_begin;
+    g.src_page_id = src_ids ? src_ids[s] : s;
+    g.n_keys = (uint32_t)n;
+    g.bits_per_key = bpk;
+    key_begin += n;
+    uint64_t payload = 0;
+    if (bpk != 0 && kind == TKV_AMQ_BLOOM) {
+      // build_bloom_filter_for_leaf, filter_builder.hpp:126-135 (kBlocked512, k = None)
+      const uint64_t nb = div_up(n * bpk, 512) == 0 ? 1 : div_up(n * bpk, 512);
+      if (nb > 0xffffffffull) return TKV_AMQ_RESOURCE_EXHAUSTED;
+      g.n_blocks = (uint32_t)nb;
+      g.hash_count = (uint16_t)bloom_hash_count(bpk);
+      payload = kBloomHeader + 64 * nb;
+      if (cap && payload > cap) return TKV_AMQ_RESOURCE_EXHAUSTED;
+    } else if (bpk != 0) {
+      // build_quotient_filter_for_leaf sizing, filter_builder.hpp:241-290
+      if (cap < kVqfHeader + kVqfMetadata + 64) return TKV_AMQ_RESOURCE_EXHAUSTED;
+      const uint64_t max8 = tkv_amq_vqf_nslots_for_size(8, cap - kVqfHeader);
+      const uint64_t max16 = tkv_amq_vqf_nslots_for_size(16, cap - kVqfHeader);
+      const double n_keys = (double)n;
+      const double lf8 = tkv_amq_vqf_load_factor(8, bpk);
+      const double lf16 = tkv_amq_vqf_load_factor(16, bpk);
+      const uint64_t n8 = (uint64_t)floor(n_keys / lf8);
+      const uint64_t n16 = (uint64_t)floor(n_keys / lf16);
+      if (!(lf8 <= 0.85)) return TKV_AMQ_INVALID_ARGUMENT;  // :265
+      int t;
+      uint64_t nslots;
+      uint32_t shift = 0;
+      if (lf16 <= 0.85 && n16 <= max16) {
+        t = 16;
+        nslots = n16;
+      } else if (n8 <= max8) {
+        t = 8;
+        nslots = n8;
+      } else {
+        if (!(max8 > max16)) return TKV_AMQ_INTERNAL;  // :278
+        shift = 1;
+        while ((double)(n >> shift) / lf8 > (double)max8) ++shift;
+        t = 8;
+        nslots = max8;
+      }
+      const uint64_t sl = vqf_slots(t);
+      const uint64_t nb = (nslots + sl) / sl;
+      if (nb > kVqfMaxLdsBlocks) return TKV_AMQ_RESOURCE_EXHAUSTED;
+      g.n_blocks = (uint32_t)nb;
+      g.tag_bits = (uint8_t)t;
+      g.hash_val_shift = (uint8_t)shift;
+      g.block_base = block_base;
+      g.mod_magic = ~0ull / (nb * vqf_buckets(t));
+      block_base += nb;
+      payload = kVqfHeader + tkv_amq_vqf_required_size(t, nslots);
+    }
+    if (g.n_blocks > max_blocks) max_blocks = g.n_blocks;
+    g.payload_bytes = (uint32_t)payload;
+    if (stride) {
+      if (payload > stride) return TKV_AMQ_RESOURCE_EXHAUSTED;
+      g.out_offset = (uint64_t)s * stride;
+    } else {
+      g.out_offset = off;
+      off += (payload + 63) & ~63ull;
+    }
+  }
+  if (total_out) *total_out = stride ? stride * n_segs : off;
+  if (ws_bytes) {
+    *ws_bytes = 0;
+    if (kind == TKV_AMQ_VQF && bpk != 0)
+      *ws_bytes = vqf_temp_offset(n_segs) + kVqfTempStride * block_base;
+  }
+  if (max_blocks_out) *max_blocks_out = max_blocks;
+  return TKV_AMQ_OK;
+}
+
+int tkv_amq_build(int kind, const uint8_t* keys, const uint64_t* offs, uint32_t stride,
+                  uint64_t n_keys, const tkv_amq_segment* d_segs, uint32_t n_segs,
+                  uint32_t max_blocks, uint8_t* d_out, void* d_ws, uint64_t ws_bytes, void* stream)
+{
+  if (tkv_amq_device_count() == 0) return TKV_AMQ_UNAVAILABLE;
+  if (n_segs == 0) return TKV_AMQ_OK;
+  if (!d_segs || !d_out || (n_keys && !keys) || (!offs && stride == 0))
+    return TKV_AMQ_INVALID_ARGUMENT;
+  const hipStream_t s = as_stream(stream);
+  const int mode = key_mode(offs, stride);
+  if (mode == kKey16 && (reinterpret_cast<uintptr_t>(keys) & 15)) return TKV_AMQ_INVALID_ARGUMENT;
+
+  if (kind == TKV_AMQ_BLOOM) {
+    const uint64_t lds = 64ull * max_blocks;
+    if (max_blocks == 0) return TKV_AMQ_OK;
+    if (lds <= kBloomLdsBudget) {
+      const dim3 grid(n_segs), block(256);
+      if (mode == kKey16)
+        hipLaunchKernelGGL(bloom_build_lds<kKey16>, grid, block, lds, s, keys, offs, stride, d_segs,
+                           d_out);
+      else if (mode == kKeyFixed)
+        hipLaunchKernelGGL(bloom_build_lds<kKeyFixed>, grid, block, lds, s, keys, offs, stride,
+                           d_segs, d_out);
+      else
+        hipLaunchKernelGGL(bloom_build_lds<kKeyVar>, grid, block, lds, s, keys, offs, stride, d_segs,
+                           d_out);
+    } else {
+      const dim3 g1(n_segs), b(256);
+      hipLaunchKernelGGL(bloom_global_init, g1, b, 0, s, d_segs, d_out);
+      const uint32_t g2 = (uint32_t)(div_up(n_keys, 256) < 8192 ? div_up(n_keys, 256) : 8192);
+      if (g2) {
+        if (mode == kKey16)
+          hipLaunchKernelGGL(bloom_global_set<kKey16>, dim3(g2), b, 0, s, keys, offs, stride,
+                             d_segs, n_segs, n_keys, d_out);
+        else if (mode == kKeyFixed)
+          hipLaunchKernelGGL(bloom_global_set<kKeyFixed>, dim3(g2), b, 0, s, keys, offs, stride,
+                             d_segs, n_segs, n_keys, d_out);
+        else
+          hipLaunchKernelGGL(bloom_global_set<kKeyVar>, dim3(g2), b, 0, s, keys, offs, stride,
+                             d_segs, n_segs, n_keys, d_out);
+      }
+    }
+    return hipGetLastError() == hipSuccess ? TKV_AMQ_OK : TKV_AMQ_INTERNAL;
+  }
+
+  if (kind != TKV_AMQ_VQF) return TKV_AMQ_INVALID_ARGUMENT;
+  if (max_blocks == 0) return TKV_AMQ_OK;
+  if (max_blocks > kVqfMaxLdsBlocks) return TKV_AMQ_RESOURCE_EXHAUSTED;
+  if (!d_ws) return TKV_AMQ_INVALID_ARGUMENT;
+  if (ws_bytes < vqf_temp_offset(n_segs)) return TKV_AMQ_INVALID_ARGUMENT;
+  if (hipMemsetAsync(d_ws, 0, 64, s) != hipSuccess) return TKV_AMQ_INTERNAL;
+  const size_t lds = 4ull * max_blocks;
+  if (mode == kKey16)
+    hipLaunchKernelGGL(vqf_decide<kKey16>, dim3(n_segs), dim3(64), lds, s, keys, offs, stride,
+                       d_segs, d_ws, n_segs);
+  else if (mode == kKeyFixed)
+    hipLaunchKernelGGL(vqf_decide<kKeyFixed>, dim3(n_segs), dim3(64), lds, s, keys, offs, stride,
+                       d_segs, d_ws, n_segs);
+  else
+    hipLaunchKernelGGL(vqf_decide<kKeyVar>, dim3(n_segs), dim3(64), lds, s, keys, offs, stride,
+                       d_segs, d_ws, n_segs);
+  hipLaunchKernelGGL(vqf_place, dim3(n_segs), dim3(256), 0, s, d_segs, d_ws, n_segs, d_out);
+  return hipGetLastError() == hipSuccess ? TKV_AMQ_OK : TKV_AMQ_INTERNAL;
+}
+
+int tkv_amq_build_check(int kind, const void* d_ws, uint64_t ws_bytes, void* stream)
+{
+  if (tkv_amq_device_count() == 0) return TKV_AMQ_UNAVAILABLE;
+  const hipStream_t s = as_stream(stream);
+  if (hipStreamSynchronize(s) != hipSuccess) return TKV_AMQ_INTERNAL;
+  if (kind != TKV_AMQ_VQF || !d_ws || ws_bytes < 64) return TKV_AMQ_OK;
+  uint32_t status = 0;
+  if (hipMemcpy(&status, d_ws, 4, hipMemcpyDeviceToHost) != hipSuccess) return TKV_AMQ_INTERNAL;
+  return status ? TKV_AMQ_INTERNAL : TKV_AMQ_OK;
+}
+
+int tkv_amq_probe(int kind, const uint8_t* d_filters, const tkv_amq_segment* d_segs,
+                  uint32_t n_segs, const uint8_t* q, const uint64_t* qoffs, uint32_t stride,
+                  uint64_t n, const uint32_t* d_qseg, uint8_t* d_result, void* stream)
+{
+  if (tkv_amq_device_count() == 0) return TKV_AMQ_UNAVAILABLE;
+  if (n == 0) return TKV_AMQ_OK;
+  if (!d_filters || !d_segs || !q || !d_qseg || !d_result || n_segs == 0 || (!qoffs && !stride))
+    return TKV_AMQ_INVALID_ARGUMENT;
+  const hipStream_t s = as_stream(stream);
+  const int mode = key_mode(qoffs, stride);
+  if (mode == kKey16 && (reinterpret_cast<uintptr_t>(q) & 15)) return TKV_AMQ_INVALID_ARGUMENT;
+  const dim3 grid((uint32_t)div_up(n, 256)), block(256);
+  if (kind == TKV_AMQ_BLOOM) {
+    if (mode == kKey16)
+      hipLaunchKernelGGL(bloom_probe<kKey16>, grid, block, 0, s, d_filters, d_segs, q, qoffs,
+                         stride, n, d_qseg, d_result);
+    else if (mode == kKeyFixed)
+      hipLaunchKernelGGL(bloom_probe<kKeyFixed>, grid, block, 0, s, d_filters, d_segs, q, qoffs,
+                         stride, n, d_qseg, d_result);
+    else
+      hipLaunchKernelGGL(bloom_probe<kKeyVar>, grid, block, 0, s, d_filters, d_segs, q, qoffs,
+                         stride, n, d_qseg, d_result);
+  } else if (kind == TKV_AMQ_VQF) {
+    if (mode == kKey16)
+      hipLaunchKernelGGL(vqf_probe<kKey16>, grid, block, 0, s, d_filters, d_segs, q, qoffs, stride,
+                         n, d_qseg, d_result);
+    else if (mode == kKeyFixed)
+      hipLaunchKernelGGL(vqf_probe<kKeyFixed>, grid, block, 0, s, d_filters, d_segs, q, qoffs,
+                         stride, n, d_qseg, d_result);
+    else
+      hipLaunchKernelGGL(vqf_probe<kKeyVar>, grid, block, 0, s, d_filters, d_segs, q, qoffs, stride,
+                         n, d_qseg, d_result);
+  } else {
+    return TKV_AMQ_INVALID_ARGUMENT;
+  }
+  return hipGetLastError() == hipSuccess ? TKV_AMQ_OK : TKV_AMQ_INTERNAL;
+}
+
+int tkv_amq_vqf_hash(const uint8_t* q, const uint64_t* qoffs, uint32_t stride, uint64_t n,
+                     uint64_t* d_hash, void* stream)
+{
+  if (tkv_amq_device_count() == 0) return TKV_AMQ_UNAVAILABLE;
+  if (n == 0) return TKV_AMQ_OK;
+  if (!q || !d_hash || (!qoffs && !stride)) return TKV_AMQ_INVALID_ARGUMENT;
+  const hipStream_t s = as_stream(stream);
+  const int mode = key_mode(qoffs, stride);
+  if (mode == kKey16 && (reinterpret_cast<uintptr_t>(q) & 15)) return TKV_AMQ_INVALID_ARGUMENT;
+  const dim3 grid((uint32_t)div_up(n, 256)), block(256);
+  if (mode == kKey16)
+    hipLaunchKernelGGL(vqf_hash_kernel<kKey16>, grid, block, 0, s, q, qoffs, stride, n, d_hash);
+  else if (mode == kKeyFixed)
+    hipLaunchKernelGGL(vqf_hash_kernel<kKeyFixed>, grid, block, 0, s, q, qoffs, stride, n, d_hash);
+  else
+    hipLaunchKernelGGL(vqf_hash_kernel<kKeyVar>, grid, block, 0, s, q, qoffs, stride, n, d_hash);
+  return hipGetLastError() == hipSuccess ? TKV_AMQ_OK : TKV_AMQ_INTERNAL;
+}
+
+int tkv_amq_vqf_probe_hashed(const uint8_t* d_filters, const tkv_amq_segment* d_segs,
+                             uint32_t n_segs, const uint64_t* d_hash, uint64_t n,
+                             const uint32_t* d_qseg, uint8_t* d_result, void* stream)
+{
+  if (tkv_amq_device_count() == 0) return TKV_AMQ_UNAVAILABLE;
+  if (n == 0) return TKV_AMQ_OK;
+  if (!d_filters || !d_segs || !d_hash || !d_qseg || !d_result || n_segs == 0)
+    return TKV_AMQ_INVALID_ARGUMENT;
+  hipLaunchKernelGGL(vqf_probe_hashed, dim3((uint32_t)div_up(n, 256)), dim3(256), 0,
+                     as_stream(stream), d_filters, d_segs, d_hash, n, d_qseg, d_result);
+  return hipGetLastError() == hipSuccess ? TKV_AMQ_OK : TKV_AMQ_INTERNAL;
+}
+
+int tkv_amq_gen_keys16(uint64_t seed, uint64_t first, uint64_t n, uint8_t* d_keys, void* stream)
+{
+  if (tkv_amq_device_count() == 0) return TKV_AMQ_UNAVAILABLE;
+  if (n == 0) return TKV_AMQ_OK;
+  if (!d_keys || (reinterpret_cast<uintptr_t>(d_keys) & 15)) return TKV_AMQ_INVALID_ARGUMENT;
+  const uint32_t g = (uint32_t)(div_up(n, 256) < 16384 ? div_up(n, 256) : 16384);
+  hipLaunchKernelGGL(gen_keys16_kernel, dim3(g), dim3(256), 0, as_stream(stream), seed, first, n,
+                     reinterpret_cast<ulonglong2*>(d_keys));
+  return hipGetLastError() == hipSuccess ? TKV_AMQ_OK : TKV_AMQ_INTERNAL;
+}
+
+}  // extern "C"

@@ -1,0 +1,378 @@
+"""Host-side mirror of TurtleKV's filter build/probe API over libtkv_amq (HIP, gfx950).
+
+Reference interface (mathworks/turtle_kv, src/turtle_kv/...) and the function here that
+replaces it:
+
+  TreeOptions::filter_bits_per_key        tree/tree_options.hpp:155-164  -> filter_bits_per_key
+  vqf_hash_val                            vqf_filter_page_view.hpp:32-35 -> vqf_hash_val
+  vqf_filter_load_factor<T>               vqf_filter_page_view.hpp:39-59 -> vqf_filter_load_factor
+  build_bloom_filter_for_leaf             tree/filter_builder.hpp:109-152 -> build_bloom_filter_for_leaf
+  build_quotient_filter_for_leaf          tree/filter_builder.hpp:221-301 -> build_quotient_filter_for_leaf
+  build_filter_for_leaf_in_job            tree/filter_builder.hpp:307-331 -> build_filter_for_leaf_in_job
+  TreeSerializeContext::build_all_pages   tree/tree_serialize_context.cpp:62-115 (the filter
+                                          half of it)                     -> build_all_filters
+  PackedVqfFilter::is_present             vqf_filter_page_view.hpp:113-125 -> PackedVqfFilter.is_present
+  KeyQuery::reject_page                   tree/key_query.hpp:149-247      -> KeyQuery.reject_page
+
+Device memory, streams and multi-GPU plumbing come from PyTorch-ROCm; every filter
+computation runs in the HIP kernels of libtkv_amq.so.  There is no CPU fallback: with no
+GPU visible the device entry points raise TkvAmqError(Unavailable).
+"""
+from __future__ import annotations
+
+import ctypes
+import enum
+import logging
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import abi
+from .abi import BLOOM, VQF, TkvAmqError
+
+log = logging.getLogger("turtle_kv_amd")
+
+# config.hpp:20-24 -- the reference compiles VQF in by default
+TURTLE_KV_USE_BLOOM_FILTER = 0
+TURTLE_KV_USE_QUOTIENT_FILTER = 1
+DEFAULT_FILTER_KIND = VQF if TURTLE_KV_USE_QUOTIENT_FILTER else BLOOM
+
+K_VQF_HASH_SEED = 0x9D0924DC03E79A75          # vqf_filter_page_view.hpp:26
+K_MIN_QUOTIENT_FILTER_BITS_PER_KEY = 12       # vqf_filter_page_view.hpp:27
+K_MAX_QUOTIENT_FILTER_LOAD_FACTOR = 0.85      # vqf_filter_page_view.hpp:28
+K_DEFAULT_FILTER_BITS_PER_KEY = 12            # tree/tree_options.hpp:57
+PACKED_PAGE_HEADER_BYTES = 64                 # llfs::PackedPageHeader (page payload offset)
+VQF_MAGIC = 0x16015305E0F43A7D
+BLOOM_MAGIC = 0xCA6F49A0F3F8A4B0
+
+
+class BoolStatus(enum.Enum):
+    """turtle_kv/import/bool_status.hpp: reject_page's tri-state result."""
+    kFalse = 0
+    kTrue = 1
+    kUnknown = 2
+
+
+def _torch():
+    import torch
+    return torch
+
+
+def _stream_handle(stream=None):
+    torch = _torch()
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+def _ptr(t) -> ctypes.c_void_p | None:
+    if t is None:
+        return None
+    if isinstance(t, np.ndarray):
+        return ctypes.c_void_p(t.ctypes.data)
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def _require_device():
+    if abi.lib().tkv_amq_device_count() == 0:
+        raise TkvAmqError(abi.UNAVAILABLE, "no HIP device visible")
+
+
+# ---------------------------------------------------------------------------------------
+# sizing
+# ---------------------------------------------------------------------------------------
+def filter_bits_per_key(requested: int | None, kind: int = DEFAULT_FILTER_KIND) -> int:
+    """TreeOptions::filter_bits_per_key(): default 12; VQF clamps nonzero values to >= 12."""
+    bpk = K_DEFAULT_FILTER_BITS_PER_KEY if requested is None else int(requested)
+    return int(abi.lib().tkv_amq_filter_bits_per_key(kind, bpk))
+
+
+def vqf_filter_load_factor(tag_bits: int, bits_per_key: int) -> float:
+    if bits_per_key != 0 and bits_per_key < K_MIN_QUOTIENT_FILTER_BITS_PER_KEY:
+        raise TkvAmqError(abi.INVALID_ARGUMENT, "vqf_filter_load_factor: bits_per_key < 12")
+    if tag_bits not in (8, 16):
+        raise TkvAmqError(abi.INVALID_ARGUMENT, "TAG_BITS must be 8 or 16")
+    return float(abi.lib().tkv_amq_vqf_load_factor(tag_bits, bits_per_key))
+
+
+def vqf_required_size(tag_bits: int, nslots: int) -> int:
+    return int(abi.lib().tkv_amq_vqf_required_size(tag_bits, nslots))
+
+
+def vqf_nslots_for_size(tag_bits: int, nbytes: int) -> int:
+    return int(abi.lib().tkv_amq_vqf_nslots_for_size(tag_bits, nbytes))
+
+
+@dataclass
+class FilterPlan:
+    """Host plan of one batch of leaf filters (one build_all_pages queue)."""
+    kind: int
+    bits_per_key: int
+    segs: np.ndarray                     # SEGMENT_DTYPE[n_segs]
+    total_out_bytes: int
+    workspace_bytes: int
+    max_seg_blocks: int
+    n_keys: int
+    _device: dict = field(default_factory=dict, repr=False)
+
+    @property
+    def n_segs(self) -> int:
+        return len(self.segs)
+
+    def device_segs(self, device=None):
+        """The plan uploaded to the device (cached per device)."""
+        torch = _torch()
+        dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+        key = str(dev)
+        if key not in self._device:
+            host = torch.from_numpy(self.segs.view(np.uint8).reshape(-1).copy())
+            self._device[key] = host.to(dev, non_blocking=False)
+        return self._device[key]
+
+
+def plan_filters(kind: int, seg_key_counts, bits_per_key: int, payload_capacity: int = 0,
+                 out_stride: int = 0, src_page_ids=None) -> FilterPlan:
+    """Restated build_{bloom,quotient}_filter_for_leaf sizing for every leaf of a batch."""
+    counts = np.ascontiguousarray(np.asarray(seg_key_counts, dtype=np.uint64))
+    n = len(counts)
+    segs = np.zeros(n, dtype=abi.SEGMENT_DTYPE)
+    src = None if src_page_ids is None else np.ascontiguousarray(np.asarray(src_page_ids, dtype=np.uint64))
+    tot, ws, mb = ctypes.c_uint64(0), ctypes.c_uint64(0), ctypes.c_uint32(0)
+    st = abi.lib().tkv_amq_plan(kind, _ptr(counts), _ptr(src), n, int(bits_per_key),
+                                int(payload_capacity), int(out_stride), _ptr(segs),
+                                ctypes.byref(tot), ctypes.byref(ws), ctypes.byref(mb))
+    abi.check(st, "tkv_amq_plan")
+    return FilterPlan(kind, int(bits_per_key), segs, int(tot.value), int(ws.value), int(mb.value),
+                      int(counts.sum()) if n else 0)
+
+
+# ---------------------------------------------------------------------------------------
+# keys
+# ---------------------------------------------------------------------------------------
+@dataclass
+class KeyBatch:
+    """Device-resident keys: fixed-length rows (`data` [n, L]) or variable-length bytes
+    (`data` [total] + `offsets` int64 [n+1]), the flattened EditView key range the reference
+    passes as `items` (core/merge_compactor.hpp:108-139)."""
+    data: object
+    n: int
+    stride: int = 16
+    offsets: object = None
+
+    @staticmethod
+    def fixed(t) -> "KeyBatch":
+        assert t.dim() == 2 and t.dtype == _torch().uint8 and t.is_cuda and t.is_contiguous()
+        return KeyBatch(t, t.shape[0], t.shape[1], None)
+
+    @staticmethod
+    def variable(data, offsets) -> "KeyBatch":
+        torch = _torch()
+        assert data.dtype == torch.uint8 and offsets.dtype == torch.int64
+        return KeyBatch(data, offsets.numel() - 1, 0, offsets)
+
+    @staticmethod
+    def from_host(keys, device=None) -> "KeyBatch":
+        """bytes-like list or [n, L] uint8 array -> device KeyBatch (H2D copy)."""
+        torch = _torch()
+        dev = device or "cuda"
+        if isinstance(keys, np.ndarray) and keys.ndim == 2:
+            return KeyBatch.fixed(torch.from_numpy(np.ascontiguousarray(keys)).to(dev))
+        ks = [bytes(k) for k in keys]
+        lens = {len(k) for k in ks}
+        if len(lens) == 1 and ks:
+            arr = np.frombuffer(b"".join(ks), dtype=np.uint8).reshape(len(ks), -1)
+            return KeyBatch.fixed(torch.from_numpy(arr.copy()).to(dev))
+        offs = np.zeros(len(ks) + 1, dtype=np.int64)
+        np.cumsum([len(k) for k in ks], out=offs[1:])
+        blob = np.frombuffer(b"".join(ks), dtype=np.uint8) if ks else np.zeros(0, np.uint8)
+        data = torch.from_numpy(blob.copy() if len(blob) else np.zeros(1, np.uint8)).to(dev)
+        return KeyBatch.variable(data, torch.from_numpy(offs).to(dev))
+
+
+def gen_keys16(seed: int, first: int, n: int, device=None, stream=None):
+    """Synthetic bench keys on the device (splitmix64 stream)."""
+    torch = _torch()
+    _require_device()
+    out = torch.empty((n, 16), dtype=torch.uint8, device=device or "cuda")
+    abi.check(abi.lib().tkv_amq_gen_keys16(seed, first, n, _ptr(out), _stream_handle(stream)),
+              "tkv_amq_gen_keys16")
+    return out
+
+
+# ---------------------------------------------------------------------------------------
+# build
+# ---------------------------------------------------------------------------------------
+def build_all_filters(plan: FilterPlan, keys: KeyBatch, out=None, workspace=None, stream=None,
+                      check: bool = True):
+    """Build every planned filter into one device array (the filter half of
+    TreeSerializeContext::build_all_pages).  Returns the output uint8 tensor."""
+    torch = _torch()
+    _require_device()
+    if keys.n != plan.n_keys:
+        raise TkvAmqError(abi.INVALID_ARGUMENT, f"plan covers {plan.n_keys} keys, got {keys.n}")
+    dev = keys.data.device
+    if out is None:
+        out = torch.empty(max(plan.total_out_bytes, 1), dtype=torch.uint8, device=dev)
+    if plan.workspace_bytes and workspace is None:
+        workspace = torch.empty(plan.workspace_bytes, dtype=torch.uint8, device=dev)
+    sh = _stream_handle(stream)
+    st = abi.lib().tkv_amq_build(plan.kind, _ptr(keys.data), _ptr(keys.offsets), keys.stride,
+                                 keys.n, _ptr(plan.device_segs(dev)), plan.n_segs,
+                                 plan.max_seg_blocks, _ptr(out), _ptr(workspace),
+                                 plan.workspace_bytes, sh)
+    abi.check(st, "tkv_amq_build")
+    if check:
+        abi.check(abi.lib().tkv_amq_build_check(plan.kind, _ptr(workspace), plan.workspace_bytes,
+                                                sh), "vqf_insert (filter_builder.hpp:211)")
+    return out
+
+
+def probe_filters(plan: FilterPlan, filters, queries: KeyBatch, query_seg, out=None, stream=None):
+    """Batched KeyQuery filter test: result[i] = 0 iff the filter of segment query_seg[i]
+    rejects queries[i] (reject_page == kTrue)."""
+    torch = _torch()
+    _require_device()
+    dev = filters.device
+    if out is None:
+        out = torch.empty(queries.n, dtype=torch.uint8, device=dev)
+    qs = query_seg.to(dtype=torch.int32)
+    st = abi.lib().tkv_amq_probe(plan.kind, _ptr(filters), _ptr(plan.device_segs(dev)),
+                                 plan.n_segs, _ptr(queries.data), _ptr(queries.offsets),
+                                 queries.stride, queries.n, _ptr(qs), _ptr(out),
+                                 _stream_handle(stream))
+    abi.check(st, "tkv_amq_probe")
+    return out
+
+
+def vqf_hash_val(keys: KeyBatch, stream=None):
+    """vqf_hash_val for every key -> int64 tensor holding the u64 XXH64 bit patterns."""
+    torch = _torch()
+    _require_device()
+    out = torch.empty(keys.n, dtype=torch.int64, device=keys.data.device)
+    abi.check(abi.lib().tkv_amq_vqf_hash(_ptr(keys.data), _ptr(keys.offsets), keys.stride, keys.n,
+                                         _ptr(out), _stream_handle(stream)), "tkv_amq_vqf_hash")
+    return out
+
+
+def vqf_probe_hashed(plan: FilterPlan, filters, hash_vals, query_seg, out=None, stream=None):
+    torch = _torch()
+    _require_device()
+    dev = filters.device
+    if out is None:
+        out = torch.empty(hash_vals.numel(), dtype=torch.uint8, device=dev)
+    qs = query_seg.to(dtype=torch.int32)
+    abi.check(abi.lib().tkv_amq_vqf_probe_hashed(_ptr(filters), _ptr(plan.device_segs(dev)),
+                                                 plan.n_segs, _ptr(hash_vals), hash_vals.numel(),
+                                                 _ptr(qs), _ptr(out), _stream_handle(stream)),
+              "tkv_amq_vqf_probe_hashed")
+    return out
+
+
+# ---------------------------------------------------------------------------------------
+# single-leaf API (the reference's per-leaf entry points)
+# ---------------------------------------------------------------------------------------
+@dataclass
+class FilterPage:
+    """A built filter page payload on the device plus its one-segment plan."""
+    kind: int
+    payload: object          # device uint8 tensor (page payload bytes)
+    plan: FilterPlan
+    leaf_page_id: int
+
+    @property
+    def filter_size(self) -> int:
+        return int(self.plan.segs[0]["payload_bytes"])
+
+    def unused_begin(self) -> int:
+        """filter_page_header->unused_begin (filter_builder.hpp:293-294)."""
+        return PACKED_PAGE_HEADER_BYTES + self.filter_size
+
+
+def _build_one(kind: int, bpk: int, leaf_page_id: int, keys: KeyBatch,
+               page_payload_bytes: int) -> FilterPage | None:
+    if bpk == 0:
+        return None  # filter_builder.hpp:115-117 / :227-229
+    plan = plan_filters(kind, [keys.n], bpk, payload_capacity=page_payload_bytes,
+                        src_page_ids=[leaf_page_id])
+    out = build_all_filters(plan, keys)
+    return FilterPage(kind, out, plan, leaf_page_id)
+
+
+def build_bloom_filter_for_leaf(filter_bits_per_key: int, leaf_page_id: int, keys: KeyBatch,
+                                page_payload_bytes: int = 0) -> FilterPage | None:
+    return _build_one(BLOOM, filter_bits_per_key, leaf_page_id, keys, page_payload_bytes)
+
+
+def build_quotient_filter_for_leaf(filter_bits_per_key: int, leaf_page_id: int, keys: KeyBatch,
+                                   page_payload_bytes: int) -> FilterPage | None:
+    return _build_one(VQF, filter_bits_per_key, leaf_page_id, keys, page_payload_bytes)
+
+
+def build_filter_for_leaf_in_job(filter_bits_per_key: int, leaf_page_id: int, keys: KeyBatch,
+                                 page_payload_bytes: int = 32768 - PACKED_PAGE_HEADER_BYTES,
+                                 kind: int = DEFAULT_FILTER_KIND) -> FilterPage | None:
+    """Like the reference: a failed build is logged and the leaf gets no filter
+    (filter_builder.hpp:323-325)."""
+    try:
+        if kind == BLOOM:
+            return build_bloom_filter_for_leaf(filter_bits_per_key, leaf_page_id, keys,
+                                               page_payload_bytes)
+        return build_quotient_filter_for_leaf(filter_bits_per_key, leaf_page_id, keys,
+                                              page_payload_bytes)
+    except TkvAmqError as e:
+        if e.status == abi.UNAVAILABLE:
+            raise
+        log.warning("Failed to build filter: %s", e)
+        return None
+
+
+class PackedVqfFilter:
+    """View of a VQF filter page payload in device memory (vqf_filter_page_view.hpp:63-126)."""
+
+    def __init__(self, page: FilterPage):
+        if page.kind != VQF:
+            raise TkvAmqError(abi.INVALID_ARGUMENT, "not a VQF filter page")
+        self.page = page
+        hdr = page.payload[:80].cpu().numpy().view("<u8")
+        self.magic, self.src_page_id, self.hash_seed, self.hash_mask = (int(x) for x in hdr[:4])
+        self.key_remainder_bits = int(hdr[5])
+
+    def check_magic(self) -> None:
+        if self.magic != VQF_MAGIC:
+            raise TkvAmqError(abi.INTERNAL, "PackedVqfFilter magic mismatch")
+
+    def is_present(self, hash_vals):
+        """Batched is_present(hash_val): uint8 tensor, 1 = maybe present."""
+        torch = _torch()
+        hv = hash_vals if hasattr(hash_vals, "data_ptr") else torch.tensor(
+            np.asarray(hash_vals, dtype=np.uint64).view(np.int64), device=self.page.payload.device)
+        qs = torch.zeros(hv.numel(), dtype=torch.int32, device=hv.device)
+        return vqf_probe_hashed(self.page.plan, self.page.payload, hv, qs)
+
+
+class KeyQuery:
+    """KeyQuery (tree/key_query.hpp:33-253) for a batch of point-query keys: the VQF hash is
+    computed once (key_query.hpp:82) and reused for every filter probed."""
+
+    def __init__(self, keys: KeyBatch):
+        self.keys = keys
+        self.hash_val = vqf_hash_val(keys)
+
+    def reject_page(self, page_id_to_reject: int, filter_page: FilterPage | None) -> list:
+        """Per key: kTrue = filter says definitely absent; kFalse = maybe present;
+        kUnknown = no filter page or it belongs to another leaf (key_query.hpp:156-159,207-232)."""
+        torch = _torch()
+        if filter_page is None:
+            return [BoolStatus.kUnknown] * self.keys.n
+        hdr = filter_page.payload[:32].cpu().numpy().view("<u8")
+        magic = int(hdr[0])
+        src = int(hdr[2]) if filter_page.kind == BLOOM else int(hdr[1])
+        if magic not in (VQF_MAGIC, BLOOM_MAGIC):
+            raise TkvAmqError(abi.INTERNAL, "filter page magic mismatch")
+        if src != page_id_to_reject:
+            return [BoolStatus.kUnknown] * self.keys.n
+        qs = torch.zeros(self.keys.n, dtype=torch.int32, device=filter_page.payload.device)
+        if filter_page.kind == VQF:
+            present = vqf_probe_hashed(filter_page.plan, filter_page.payload, self.hash_val, qs)
+        else:
+            present = probe_filters(filter_page.plan, filter_page.payload, self.keys, qs)
+        return [BoolStatus.kFalse if p else BoolStatus.kTrue for p in present.cpu().tolist()]
