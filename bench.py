@@ -1,0 +1,312 @@
+"""Filter-build benchmark (BASELINE.json metric: filter-build Mkeys/s, device-resident,
+16-byte keys @ 10 bits/key, bit-exact).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload bloom10|bloom12|vqf12|probe10]
+
+One step = one pass of the hot path over one batch: build every leaf filter of
+`--keys-per-gpu` (default 100M, BASELINE config 2) 16-byte keys held in HBM, S = 16,384 keys
+per leaf (6,103 full leaves + 8,448), into one device filter array.  Multi-GPU: one process
+per GPU (torch.distributed, RCCL); each rank builds its own contiguous range of leaves (weak
+scaling, no data-path collective).  The RCCL all-gather of the filter array (north star) is
+timed separately after the timed region and reported as `allgather_ms` (`--allgather` puts
+it inside the timed step instead).
+
+The printed JSON line carries `roofline` (dominant kernel, HIP events on the build stream,
+algorithmic bytes) and `cpu_baseline` (the C oracle -- a restatement of the reference's CPU
+path -- timed on this host's cores on rank 0, N = 1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+SEG_KEYS = 16384
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s peak (spec)
+
+WORKLOADS = {
+    # name: (kind, bits_per_key, payload_capacity, metric label)
+    "bloom10": (0, 10, 0, "Bloom @10 bits/key"),
+    "bloom12": (0, 12, 0, "Bloom @12 bits/key"),
+    "vqf12": (1, 12, 32704, "VQF @12 bits/key (reference clamp of 10 -> 12)"),
+    "probe10": (0, 10, 0, "Bloom @10 probe, 50% hits"),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="bloom10", choices=sorted(WORKLOADS))
+    ap.add_argument("--keys-per-gpu", type=int, default=100_000_000)
+    ap.add_argument("--allgather", action="store_true", help="time the RCCL all-gather in-step")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    return ap.parse_args()
+
+
+def segment_counts(n_keys):
+    full, rem = divmod(n_keys, SEG_KEYS)
+    return [SEG_KEYS] * full + ([rem] if rem else [])
+
+
+def cpu_baseline(kind, bpk, cap, keys_host, counts, threads):
+    """Oracle (C, -O3, one filter per thread at a time, leaves spread over `threads` workers
+    like TreeSerializeContext::build_all_pages) over the same keys; bounded to <= ~20 s."""
+    from oracle import oracle as O
+    O.build_oracle()
+    n_segs = len(counts)
+    # bound the sample: estimate from a small run, then size to ~10 s wall
+    probe_segs = min(n_segs, 4 * threads)
+    def run(ns):
+        c = counts[:ns]
+        sb = np.concatenate([[0], np.cumsum(c)]).astype(np.uint64)
+        if kind == 0:
+            sizes = np.array([O.lib().tkvo_bloom_payload_size(int(x), bpk) for x in c], np.uint64)
+        else:
+            sizes = np.full(ns, cap, np.uint64)
+        offs = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.uint64)
+        out = np.empty(int(sizes.sum()), np.uint8)
+        t0 = time.perf_counter()
+        st, _ = O.build_segments(kind, keys_host, sb, bpk, offs, sizes, 0, n_threads=threads,
+                                 out=out)
+        dt = time.perf_counter() - t0
+        assert st == 0, st
+        return int(sb[-1]), dt
+    n0, t0 = run(probe_segs)
+    rate = n0 / max(t0, 1e-9)
+    target_keys = min(int(sum(counts)), int(rate * 10.0))
+    ns = n_segs if target_keys >= sum(counts) else max(probe_segs, target_keys // SEG_KEYS)
+    nk, dt = run(ns)
+    return {"value": round(nk / dt / 1e6, 2), "unit": "Mkeys/s", "cores": threads,
+            "kind": "port",
+            "sample": f"{ns} leaves x {SEG_KEYS} keys ({nk} keys) of the same workload, C oracle "
+                      f"(oracle/tkv_amq_oracle.c, -O3 -march=x86-64-v3), {threads} threads, "
+                      f"{dt:.2f} s wall"}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    import turtle_kv_amd as amq
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    kind, bpk, cap, label = WORKLOADS[args.workload]
+    n = args.keys_per_gpu
+    counts = segment_counts(n)
+    # weak scaling: the checkpoint has `world` x (this GPU's leaves); rank r builds the
+    # contiguous leaf range turtle_kv_amd.dist.shard_leaves gives it, at a fixed per-leaf
+    # stride so leaf s sits at s * stride in the all-gathered array
+    from turtle_kv_amd import dist as tdist
+    shard = tdist.shard_leaves(counts * world, world, rank)
+    stride = tdist.leaf_stride(kind, bpk, SEG_KEYS, cap)
+    plan = tdist.plan_shard(kind, counts * world, bpk, shard, stride, payload_capacity=cap)
+    assert shard.key_end - shard.key_begin == n
+    keys = amq.gen_keys16(42, shard.key_begin, n, device=dev)
+    if kind == 1:
+        # VQF inserts in leaf key order: sort each leaf's keys (memcmp order) on the device
+        keys = sort_segments_device(torch, keys, counts)
+    kb = amq.KeyBatch.fixed(keys)
+    out = torch.empty(plan.total_out_bytes, dtype=torch.uint8, device=dev)
+    ws = torch.empty(max(plan.workspace_bytes, 1), dtype=torch.uint8, device=dev)
+    gathered = (torch.empty(plan.total_out_bytes * world, dtype=torch.uint8, device=dev)
+                if world > 1 else None)
+
+    probe = args.workload.startswith("probe")
+    if probe:
+        amq.build_all_filters(plan, kb, out=out, workspace=ws)
+        q, qseg = make_probe_queries(torch, amq, n, counts, dev, rank)
+        qb = amq.KeyBatch.fixed(q)
+        res = torch.empty(q.shape[0], dtype=torch.uint8, device=dev)
+
+    stream = torch.cuda.current_stream()
+
+    def step():
+        if probe:
+            amq.probe_filters(plan, out, qb, qseg, out=res)
+        else:
+            amq.build_all_filters(plan, kb, out=out, workspace=ws, check=False)
+        if args.allgather and world > 1:
+            tdist.allgather_filters(out, gathered)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if not probe and kind == 1:
+        amq.abi.check(amq.abi.lib().tkv_amq_build_check(kind, amq.filters._ptr(ws),
+                                                        plan.workspace_bytes,
+                                                        amq.filters._stream_handle()), "vqf build")
+
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ev[i][0].record(stream)
+        step()
+        ev[i][1].record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([wall], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall = float(t.item())
+    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+
+    units = (q.shape[0] if probe else n) * world
+    ms_per_step = wall / args.steps * 1e3
+    value = units * args.steps / wall / 1e6
+
+    # algorithmic bytes per launch: build = 16 B/key in + filter payload out;
+    # probe = 16 B key + 4 B leaf id + 1 B result per lookup
+    if probe:
+        alg_bytes = q.shape[0] * (16 + 4 + 1)
+    else:
+        alg_bytes = n * 16 + int(plan.segs["payload_bytes"].astype(np.int64).sum())
+    achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
+    traffic = load_traffic(args.workload)
+
+    allgather_ms = None
+    if world > 1 and not args.allgather:
+        torch.cuda.synchronize()
+        dist.barrier()
+        g0 = time.perf_counter()
+        for _ in range(3):
+            tdist.allgather_filters(out, gathered)
+        torch.cuda.synchronize()
+        allgather_ms = (time.perf_counter() - g0) / 3 * 1e3
+
+    e2e = None
+    if rank == 0 and world == 1 and not args.no_e2e and not probe:
+        e2e = end_to_end(torch, amq, plan, keys, out, ws)
+
+    if world > 1:
+        dist.barrier()
+    if rank != 0:
+        dist.destroy_process_group()
+        return
+
+    base = None
+    if world == 1 and not args.no_cpu_baseline:
+        if probe:
+            base = None
+        else:
+            base = cpu_baseline(kind, bpk, cap, keys.cpu().numpy(), counts, args.cpu_threads)
+
+    line = {
+        "metric": f"filter-build Mkeys/s (device-resident), 16B keys @10 bits/key; bit-exact"
+        if args.workload == "bloom10" else f"{label} Mkeys/s (device-resident)",
+        "value": round(value, 2),
+        "unit": "Mkeys/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u64",
+        "data": "synthetic (splitmix64 seed 42 keys generated on the device)",
+        "config": {"workload": f"{label}: {n} x 16B keys per GPU, {SEG_KEYS}-key leaves "
+                               f"({len(counts)} filters per GPU)",
+                   "keys_per_gpu": n, "leaf_keys": SEG_KEYS, "bits_per_key": bpk,
+                   "filter": "bloom-blocked512" if kind == 0 else "vqf",
+                   "parallelism": f"leaf-sharded x{world}"},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": traffic, "kernel_ms": round(kernel_ms, 4),
+                     "alg_bytes_per_launch": alg_bytes},
+        "cpu_baseline": base,
+    }
+    if allgather_ms is not None:
+        line["allgather_ms"] = round(allgather_ms, 3)
+        line["build_plus_allgather_mkeys_s"] = round(units / ((ms_per_step + allgather_ms) * 1e-3) / 1e6, 2)
+    if e2e is not None:
+        line["e2e_pcie_inclusive"] = e2e
+    print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def sort_segments_device(torch, keys, counts):
+    """memcmp order within each leaf: lexicographic on the big-endian view of the two
+    8-byte words, via two stable sorts (low word, then high word) and a stable leaf sort."""
+    n = keys.shape[0]
+    w = keys.view(torch.int64).reshape(n, 2)
+    def be(x):  # byte-swap to big-endian order, map unsigned -> signed order
+        b = x.view(torch.uint8).reshape(-1, 8).flip(1).contiguous().view(torch.int64).reshape(-1)
+        return b ^ torch.iinfo(torch.int64).min
+    hi, lo = be(w[:, 0].contiguous()), be(w[:, 1].contiguous())
+    seg = torch.repeat_interleave(torch.arange(len(counts), device=keys.device),
+                                  torch.tensor(counts, device=keys.device))
+    idx = torch.argsort(lo, stable=True)
+    idx = idx[torch.argsort(hi[idx], stable=True)]
+    idx = idx[torch.argsort(seg[idx], stable=True)]
+    return keys[idx].contiguous()
+
+
+def make_probe_queries(torch, amq, n, counts, dev, rank):
+    """BASELINE config 4: n hits (the inserted keys, each probing its own leaf) + n misses
+    (seed 43 keys, probing a seed-44 random leaf), interleaved."""
+    hits = amq.gen_keys16(42, rank * n, n, device=dev)
+    miss = amq.gen_keys16(43, rank * n, n, device=dev)
+    q = torch.stack([hits, miss], dim=1).reshape(2 * n, 16).contiguous()
+    seg_hit = torch.repeat_interleave(torch.arange(len(counts), device=dev, dtype=torch.int32),
+                                      torch.tensor(counts, device=dev))
+    g = torch.Generator(device=dev)
+    g.manual_seed(44)
+    seg_miss = torch.randint(0, len(counts), (n,), device=dev, dtype=torch.int32, generator=g)
+    qs = torch.stack([seg_hit, seg_miss], dim=1).reshape(-1).contiguous()
+    return q, qs
+
+
+def end_to_end(torch, amq, plan, keys, out, ws, iters=3):
+    """Keys from pinned host memory -> H2D -> build -> D2H into pinned host pages."""
+    h_keys = torch.empty(keys.shape, dtype=torch.uint8, pin_memory=True)
+    h_keys.copy_(keys)
+    h_out = torch.empty(out.shape, dtype=torch.uint8, pin_memory=True)
+    d_keys = torch.empty_like(keys)
+    kb = amq.KeyBatch.fixed(d_keys)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        d_keys.copy_(h_keys, non_blocking=True)
+        amq.build_all_filters(plan, kb, out=out, workspace=ws, check=False)
+        h_out.copy_(out, non_blocking=True)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / iters
+    return {"mkeys_s": round(keys.shape[0] / dt / 1e6, 2), "ms_per_batch": round(dt * 1e3, 3),
+            "note": "pinned host keys -> H2D -> build -> D2H filters, serial on one stream"}
+
+
+def load_traffic(workload):
+    p = os.path.join(ROOT, "profiles", f"traffic_{workload}.json")
+    if os.path.exists(p):
+        with open(p) as f:
+            return json.load(f).get("hbm_bytes_per_launch")
+    return None
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,88 @@
+"""CPU, world_size 2 (gloo): the leaf-sharded multi-GPU layout.  Each rank builds its own
+leaf range (here with the CPU oracle standing in for the GPU build, since the property
+under test is the sharding/layout/all-gather logic), all-gathers its fixed-size slice, and
+the gathered array must equal a single-process build of every leaf at the same stride."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def oracle_build(O, kind, keys, counts, bpk, cap, stride, leaf_ids, n_slots):
+    counts = np.asarray(counts, dtype=np.int64)
+    sb = np.concatenate([[0], np.cumsum(counts)]).astype(np.uint64)
+    offs = (np.arange(len(counts)) * stride).astype(np.uint64)
+    caps = np.full(len(counts), stride if kind == 0 else cap, np.uint64)
+    out = np.zeros(n_slots * stride, np.uint8)
+    st, out = O.build_segments(kind, keys, sb, bpk, offs, caps, 0,
+                               src_page_id=np.asarray(leaf_ids, np.uint64), out=out)
+    assert st == 0
+    return out
+
+
+def worker(rank, world, port, kind, result_q):
+    import sys
+    sys.path.insert(0, ROOT)
+    from oracle import oracle as O
+    from turtle_kv_amd import dist as tdist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    counts = [4096] * 9 + [1000]
+    bpk, cap = (10, 0) if kind == 0 else (12, 16320)
+    keys = O.gen_keys16(42, 0, sum(counts))
+    if kind == 1:
+        O.sort_segments(keys, np.concatenate([[0], np.cumsum(counts)]).astype(np.uint64))
+    stride = tdist.leaf_stride(kind, bpk, max(counts), cap)
+    sh = tdist.shard_leaves(counts, world, rank)
+    plan = tdist.plan_shard(kind, counts, bpk, sh, stride, payload_capacity=cap)
+    assert list(plan.segs["src_page_id"]) == list(range(sh.leaf_begin, sh.leaf_end))
+    assert int(plan.segs["key_begin"][0]) == 0
+    local = oracle_build(O, kind, keys[sh.key_begin:sh.key_end], counts[sh.leaf_begin:sh.leaf_end],
+                         bpk, cap, stride, range(sh.leaf_begin, sh.leaf_end), sh.leaves_per_rank)
+    g = tdist.allgather_filters(torch.from_numpy(local))
+    if rank == 0:
+        full = oracle_build(O, kind, keys, counts, bpk, cap, stride, range(len(counts)),
+                            sh.leaves_per_rank * world)
+        result_q.put(bool(np.array_equal(g.numpy(), full)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("kind", [0, 1])
+def test_sharded_allgather_world2(kind):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=worker, args=(r, 2, port, kind, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    assert q.get(timeout=5) is True
+
+
+def test_shard_ranges_cover_all_leaves():
+    from turtle_kv_amd import dist as tdist
+    counts = [16384] * 6103 + [8448]
+    for world in (1, 2, 3, 4, 8):
+        shards = [tdist.shard_leaves(counts, world, r) for r in range(world)]
+        assert shards[0].leaf_begin == 0 and shards[-1].leaf_end == len(counts)
+        for a, b in zip(shards, shards[1:]):
+            assert a.leaf_end == b.leaf_begin and a.key_end == b.key_begin
+        assert shards[-1].key_end == sum(counts)
+        assert all(s.n_leaves <= s.leaves_per_rank for s in shards)

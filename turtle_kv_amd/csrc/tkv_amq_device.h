@@ -75,19 +75,88 @@ __host__ __device__ constexpr inline uint64_t bloom_seed(uint32_t i)
   return sm64_mix(0x243F6A8885A308D3ULL + (uint64_t)i * 0x9E3779B97F4A7C15ULL);
 }
 
+// ---- 64-bit ops spelled as 32-bit halves (gfx950 has no 64-bit rotate; the compiler
+// otherwise emits v_lshlrev_b64 + v_lshrrev_b64 + 2 v_or per rotate) ----
+__device__ inline uint32_t lo32(uint64_t x) { return (uint32_t)x; }
+__device__ inline uint32_t hi32(uint64_t x) { return (uint32_t)(x >> 32); }
+__device__ inline uint64_t mk64(uint32_t lo, uint32_t hi) { return ((uint64_t)hi << 32) | lo; }
+
+template <int R>
+__device__ inline uint64_t drotl(uint64_t x)
+{
+  static_assert(R > 0 && R < 32, "rotate amount");
+  const uint32_t l = lo32(x), h = hi32(x);
+  return mk64(__builtin_amdgcn_alignbit(l, h, 32 - R), __builtin_amdgcn_alignbit(h, l, 32 - R));
+}
+
+template <int S>
+__device__ inline uint64_t dshr(uint64_t x)
+{
+  if constexpr (S >= 32) {
+    return (uint64_t)(hi32(x) >> (S - 32));
+  } else {
+    return mk64(__builtin_amdgcn_alignbit(hi32(x), lo32(x), S), hi32(x) >> S);
+  }
+}
+
+__device__ inline uint64_t dround(uint64_t acc, uint64_t in)
+{
+  acc += in * kP2;
+  acc = drotl<31>(acc);
+  return acc * kP1;
+}
+
+__device__ inline uint64_t davalanche(uint64_t h)
+{
+  h ^= dshr<33>(h);
+  h *= kP2;
+  h ^= dshr<29>(h);
+  h *= kP3;
+  h ^= dshr<32>(h);
+  return h;
+}
+
+// v_mul_u32_u24 (full rate).  Inline asm because LLVM's demanded-bits folding turns a
+// masked 24-bit multiply whose result is later masked to 9 bits back into v_mul_lo_u32
+// (quarter rate).
+__device__ inline uint32_t mul_u24(uint32_t konst, uint32_t x)
+{
+  uint32_t r;
+  asm("v_mul_u32_u24 %0, %1, %2" : "=v"(r) : "s"(konst), "v"(x));
+  return r;
+}
+
+// low 9 bits of davalanche(h) with the last multiply narrowed: bits 0..8 and 32..40 of
+// y * P3 only need hi32(y_lo * P3_lo) and the low 9 bits of the two cross products, which
+// 24-bit multiplies (full rate) give exactly.
+__device__ inline uint32_t davalanche_lo9(uint64_t h)
+{
+  h ^= dshr<33>(h);
+  h *= kP2;
+  h ^= dshr<29>(h);
+  const uint32_t yl = lo32(h), yh = hi32(h);
+  constexpr uint32_t cl = (uint32_t)kP3, ch = (uint32_t)(kP3 >> 32);
+  const uint32_t p_hi = __umulhi(yl, cl);
+  const uint32_t p_lo9 = mul_u24(cl, yl);
+  const uint32_t h3_hi = p_hi + mul_u24(ch, yl) + mul_u24(cl, yh);
+  return (p_lo9 ^ h3_hi) & 511u;
+}
+
 // 16-byte key, seed-independent part precomputed once per key.
 struct Xxh16 {
   uint64_t k1, k2;
-  __device__ inline Xxh16(uint64_t lo, uint64_t hi) : k1{xxh_round(0, lo)}, k2{xxh_round(0, hi)} {}
-  // `hinit` = seed + P5 + 16
-  __device__ inline uint64_t finish(uint64_t hinit) const
+  __device__ inline Xxh16(uint64_t lo, uint64_t hi) : k1{dround(0, lo)}, k2{dround(0, hi)} {}
+  // state before the avalanche; `hinit` = seed + P5 + 16
+  __device__ inline uint64_t pre(uint64_t hinit) const
   {
     uint64_t h = hinit ^ k1;
-    h = rotl64(h, 27) * kP1 + kP4;
+    h = drotl<27>(h) * kP1 + kP4;
     h ^= k2;
-    h = rotl64(h, 27) * kP1 + kP4;
-    return xxh_avalanche(h);
+    return drotl<27>(h) * kP1 + kP4;
   }
+  __device__ inline uint64_t finish(uint64_t hinit) const { return davalanche(pre(hinit)); }
+  // low 9 bits only (Bloom bit index inside a 512-bit block)
+  __device__ inline uint32_t finish_lo9(uint64_t hinit) const { return davalanche_lo9(pre(hinit)); }
 };
 
 __device__ inline uint64_t ld64_unaligned(const uint8_t* p)
@@ -115,37 +184,37 @@ __device__ inline uint64_t xxh64_bytes(const uint8_t* p, uint64_t len, uint64_t 
     uint64_t v1 = seed + kP1 + kP2, v2 = seed + kP2, v3 = seed, v4 = seed - kP1;
     const uint8_t* limit = end - 32;
     do {
-      v1 = xxh_round(v1, ld64_unaligned(p));
-      v2 = xxh_round(v2, ld64_unaligned(p + 8));
-      v3 = xxh_round(v3, ld64_unaligned(p + 16));
-      v4 = xxh_round(v4, ld64_unaligned(p + 24));
+      v1 = dround(v1, ld64_unaligned(p));
+      v2 = dround(v2, ld64_unaligned(p + 8));
+      v3 = dround(v3, ld64_unaligned(p + 16));
+      v4 = dround(v4, ld64_unaligned(p + 24));
       p += 32;
     } while (p <= limit);
-    h = rotl64(v1, 1) + rotl64(v2, 7) + rotl64(v3, 12) + rotl64(v4, 18);
-    h = xxh_merge(h, v1);
-    h = xxh_merge(h, v2);
-    h = xxh_merge(h, v3);
-    h = xxh_merge(h, v4);
+    h = drotl<1>(v1) + drotl<7>(v2) + drotl<12>(v3) + drotl<18>(v4);
+    h = (h ^ dround(0, v1)) * kP1 + kP4;
+    h = (h ^ dround(0, v2)) * kP1 + kP4;
+    h = (h ^ dround(0, v3)) * kP1 + kP4;
+    h = (h ^ dround(0, v4)) * kP1 + kP4;
   } else {
     h = seed + kP5;
   }
   h += len;
   while (p + 8 <= end) {
-    h ^= xxh_round(0, ld64_unaligned(p));
-    h = rotl64(h, 27) * kP1 + kP4;
+    h ^= dround(0, ld64_unaligned(p));
+    h = drotl<27>(h) * kP1 + kP4;
     p += 8;
   }
   if (p + 4 <= end) {
     h ^= (uint64_t)ld32_unaligned(p) * kP1;
-    h = rotl64(h, 23) * kP2 + kP3;
+    h = drotl<23>(h) * kP2 + kP3;
     p += 4;
   }
   while (p < end) {
     h ^= (uint64_t)(*p) * kP5;
-    h = rotl64(h, 11) * kP1;
+    h = drotl<11>(h) * kP1;
     ++p;
   }
-  return xxh_avalanche(h);
+  return davalanche(h);
 }
 
 // floor(x / d) for x < 2^64, d < 2^32, given m = floor((2^64 - 1) / d): one umulhi + fix-up.

@@ -97,10 +97,9 @@ __device__ inline void bloom_insert16(uint32_t* s_bits, uint32_t nb, uint32_t k,
   lds_set_bit(blk, (uint32_t)h0 & 511u);
   if constexpr (K != 0) {
 #pragma unroll
-    for (uint32_t j = 1; j < (uint32_t)K; ++j)
-      lds_set_bit(blk, (uint32_t)x.finish(c_bloom.hinit16[j]) & 511u);
+    for (uint32_t j = 1; j < (uint32_t)K; ++j) lds_set_bit(blk, x.finish_lo9(c_bloom.hinit16[j]));
   } else {
-    for (uint32_t j = 1; j < k; ++j) lds_set_bit(blk, (uint32_t)x.finish(c_bloom.hinit16[j]) & 511u);
+    for (uint32_t j = 1; j < k; ++j) lds_set_bit(blk, x.finish_lo9(c_bloom.hinit16[j]));
   }
 }
 
@@ -219,7 +218,7 @@ __global__ __launch_bounds__(256) void bloom_global_set(const uint8_t* __restric
       const uint32_t b0 = (uint32_t)h0 & 511u;
       atomicOr(blk + (b0 >> 5), 1u << (b0 & 31));
       for (uint32_t j = 1; j < sg.hash_count; ++j) {
-        const uint32_t b = (uint32_t)x.finish(c_bloom.hinit16[j]) & 511u;
+        const uint32_t b = x.finish_lo9(c_bloom.hinit16[j]);
         atomicOr(blk + (b >> 5), 1u << (b & 31));
       }
     } else {
@@ -265,7 +264,7 @@ __global__ __launch_bounds__(256) void bloom_probe(const uint8_t* __restrict__ f
     uint32_t b = (uint32_t)h0 & 511u;
     ok &= (uint32_t)(blk[b >> 6] >> (b & 63));
     for (uint32_t j = 1; j < k; ++j) {
-      b = (uint32_t)x.finish(c_bloom.hinit16[j]) & 511u;
+      b = x.finish_lo9(c_bloom.hinit16[j]);
       ok &= (uint32_t)(blk[b >> 6] >> (b & 63));
     }
   } else {
