@@ -1,0 +1,397 @@
+// turtle_kv_amd/filter_builder.hpp -- C++ host mirror of TurtleKV's filter API over the
+// tkv_amq C ABI (libtkv_amq.so, HIP/gfx950).  Header-only, C++17.
+//
+// Reference interface (mathworks/turtle_kv, src/turtle_kv/...) -> this header:
+//   vqf_hash_val                          vqf_filter_page_view.hpp:32-35   (device: vqf_hash_val_batch)
+//   vqf_filter_load_factor<TAG_BITS>      vqf_filter_page_view.hpp:39-59   vqf_filter_load_factor<T>
+//   PackedVqfFilter                       vqf_filter_page_view.hpp:63-131  PackedVqfFilter (layout)
+//   TreeOptions::filter_bits_per_key      tree/tree_options.hpp:155-164    filter_bits_per_key
+//   build_bloom_filter_for_leaf           tree/filter_builder.hpp:109-152  build_bloom_filter_for_leaf
+//   build_quotient_filter_for_leaf        tree/filter_builder.hpp:221-301  build_quotient_filter_for_leaf
+//   build_filter_for_leaf_in_job          tree/filter_builder.hpp:307-331  build_filter_for_leaf_in_job
+//   TreeSerializeContext::build_all_pages tree/tree_serialize_context.cpp:62-115 (filter half)
+//                                                                          FilterBatchBuilder
+//   KeyQuery::reject_page                 tree/key_query.hpp:149-247       KeyQuery::reject_page
+//
+// The single-leaf functions take the leaf's keys as host string views (the reference's
+// `items` range of EditView keys, tombstones included) and fill a host page payload
+// buffer, staging through the device.  The batched FilterBatchBuilder works on
+// device-resident keys and is the fast path.  There is no CPU implementation here: every
+// filter byte is computed by the HIP kernels.
+#pragma once
+
+#include <hip/hip_runtime_api.h>
+
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <optional>
+#include <string>
+#include <string_view>
+#include <vector>
+
+#include "../tkv_amq.h"
+
+namespace turtle_kv_amd {
+
+using u8 = std::uint8_t;
+using u16 = std::uint16_t;
+using u32 = std::uint32_t;
+using u64 = std::uint64_t;
+using usize = std::size_t;
+
+// ---------------------------------------------------------------------------------------
+// Status (batt::Status numbering)
+// ---------------------------------------------------------------------------------------
+struct Status {
+  int code = TKV_AMQ_OK;
+  std::string what;
+  bool ok() const { return code == TKV_AMQ_OK; }
+  static Status from(int c, const char* w) { return Status{c, c == TKV_AMQ_OK ? "" : w}; }
+  std::string to_string() const
+  {
+    return std::string(tkv_amq_status_string(code)) + (what.empty() ? "" : ": " + what);
+  }
+};
+inline Status OkStatus() { return Status{}; }
+
+#define TKV_AMQ_REQUIRE_OK(expr)          \
+  do {                                    \
+    ::turtle_kv_amd::Status s_ = (expr);  \
+    if (!s_.ok()) return s_;              \
+  } while (0)
+
+// ---------------------------------------------------------------------------------------
+// constants and sizing (config.hpp:20-24, vqf_filter_page_view.hpp:26-28)
+// ---------------------------------------------------------------------------------------
+enum class FilterKind : int { kBloom = TKV_AMQ_BLOOM, kQuotient = TKV_AMQ_VQF };
+inline constexpr FilterKind kDefaultFilterKind = FilterKind::kQuotient;  // TURTLE_KV_USE_QUOTIENT_FILTER 1
+inline constexpr u64 kVqfHashSeed = 0x9d0924dc03e79a75ull;
+inline constexpr usize kMinQuotientFilterBitsPerKey = 12;
+inline constexpr double kMaxQuotientFilterLoadFactor = 0.85;
+inline constexpr u16 kDefaultFilterBitsPerKey = 12;
+inline constexpr usize kPackedPageHeaderSize = 64;
+
+template <int TAG_BITS>
+inline double vqf_filter_load_factor(usize bits_per_key)
+{
+  static_assert(TAG_BITS == 8 || TAG_BITS == 16, "TAG_BITS must be 8 or 16");
+  return tkv_amq_vqf_load_factor(TAG_BITS, bits_per_key);
+}
+
+inline usize filter_bits_per_key(std::optional<u16> requested,
+                                 FilterKind kind = kDefaultFilterKind)
+{
+  return (usize)tkv_amq_filter_bits_per_key((int)kind, requested.value_or(kDefaultFilterBitsPerKey));
+}
+
+// vqf_metadata + PackedVqfFilter on-page layout (little-endian)
+struct VqfMetadata {
+  u64 total_size_in_bytes;
+  u64 key_remainder_bits;
+  u64 range;
+  u64 nblocks;
+  u64 nelts;
+  u64 nslots;
+};
+struct PackedVqfFilter {
+  static constexpr u64 kMagic = 0x16015305e0f43a7dull;
+  u64 magic;
+  u64 src_page_id;
+  u64 hash_seed;
+  u64 hash_mask;
+  VqfMetadata metadata;
+};
+static_assert(sizeof(PackedVqfFilter) == 32 + sizeof(VqfMetadata), "vqf_filter_page_view.hpp:128");
+
+struct PackedBloomFilterPage {
+  static constexpr u64 kMagic = 0xca6f49a0f3f8a4b0ull;
+  u64 magic;
+  u64 bit_count;
+  u64 src_page_id;
+  u64 xxh3_checksum;
+  u64 word_count;
+  u32 block_count;
+  u16 hash_count;
+  u8 layout;  // 2 = kBlocked512
+  u8 reserved0;
+  u64 item_count;
+  u64 reserved1;
+};
+static_assert(sizeof(PackedBloomFilterPage) == 64, "tkv-amq v1 Bloom header");
+
+// ---------------------------------------------------------------------------------------
+// device buffer helper (RAII)
+// ---------------------------------------------------------------------------------------
+class DeviceBuffer
+{
+ public:
+  DeviceBuffer() = default;
+  explicit DeviceBuffer(usize n) { resize(n); }
+  ~DeviceBuffer() { reset(); }
+  DeviceBuffer(const DeviceBuffer&) = delete;
+  DeviceBuffer& operator=(const DeviceBuffer&) = delete;
+  DeviceBuffer(DeviceBuffer&& o) noexcept : p_{o.p_}, n_{o.n_} { o.p_ = nullptr; o.n_ = 0; }
+
+  bool resize(usize n)
+  {
+    if (n <= n_) return true;
+    reset();
+    if (hipMalloc(&p_, n ? n : 1) != hipSuccess) { p_ = nullptr; return false; }
+    n_ = n;
+    return true;
+  }
+  void reset()
+  {
+    if (p_) (void)hipFree(p_);
+    p_ = nullptr;
+    n_ = 0;
+  }
+  template <typename T = u8>
+  T* get() const { return static_cast<T*>(p_); }
+  usize size() const { return n_; }
+
+ private:
+  void* p_ = nullptr;
+  usize n_ = 0;
+};
+
+// ---------------------------------------------------------------------------------------
+// FilterBatchBuilder: every leaf filter of one build_all_pages queue in one device call
+// ---------------------------------------------------------------------------------------
+class FilterBatchBuilder
+{
+ public:
+  FilterBatchBuilder(FilterKind kind, usize bits_per_key, u64 page_payload_bytes,
+                     u64 out_stride = 0)
+      : kind_{kind}, bpk_{bits_per_key}, cap_{page_payload_bytes}, stride_{out_stride}
+  {
+  }
+
+  // Queue one leaf whose keys occupy the next n_keys slots of the device key array.
+  u32 add_leaf(u64 leaf_page_id, u64 n_keys)
+  {
+    counts_.push_back(n_keys);
+    page_ids_.push_back(leaf_page_id);
+    return (u32)(counts_.size() - 1);
+  }
+
+  Status plan()
+  {
+    segs_.resize(counts_.size());
+    const int st = tkv_amq_plan((int)kind_, counts_.data(), page_ids_.data(), (u32)counts_.size(),
+                                (u32)bpk_, cap_, stride_, segs_.data(), &total_out_, &ws_bytes_,
+                                &max_blocks_);
+    if (st != TKV_AMQ_OK) return Status::from(st, "tkv_amq_plan");
+    if (!d_segs_.resize(segs_.size() * sizeof(tkv_amq_segment)) || !d_ws_.resize(ws_bytes_))
+      return Status::from(TKV_AMQ_RESOURCE_EXHAUSTED, "hipMalloc");
+    if (hipMemcpy(d_segs_.get(), segs_.data(), segs_.size() * sizeof(tkv_amq_segment),
+                  hipMemcpyHostToDevice) != hipSuccess)
+      return Status::from(TKV_AMQ_INTERNAL, "hipMemcpy plan");
+    planned_ = true;
+    return OkStatus();
+  }
+
+  // Device keys: fixed length (d_key_offsets == nullptr, key_stride bytes each) or
+  // variable length (d_key_offsets[n+1]).  Asynchronous on `stream`; call check().
+  Status build_all(const u8* d_keys, u32 key_stride, const u64* d_key_offsets, u8* d_out,
+                   hipStream_t stream = nullptr)
+  {
+    if (!planned_) TKV_AMQ_REQUIRE_OK(plan());
+    u64 n = 0;
+    for (u64 c : counts_) n += c;
+    return Status::from(tkv_amq_build((int)kind_, d_keys, d_key_offsets, key_stride, n,
+                                      d_segs_.get<tkv_amq_segment>(), (u32)segs_.size(),
+                                      max_blocks_, d_out, d_ws_.get(), ws_bytes_, stream),
+                        "tkv_amq_build");
+  }
+
+  Status check(hipStream_t stream = nullptr) const
+  {
+    return Status::from(tkv_amq_build_check((int)kind_, d_ws_.get(), ws_bytes_, stream),
+                        "vqf_insert (filter_builder.hpp:211)");
+  }
+
+  Status probe(const u8* d_filters, const u8* d_queries, u32 query_stride,
+               const u64* d_query_offsets, u64 n_queries, const u32* d_query_leaf, u8* d_result,
+               hipStream_t stream = nullptr) const
+  {
+    return Status::from(tkv_amq_probe((int)kind_, d_filters, d_segs_.get<tkv_amq_segment>(),
+                                      (u32)segs_.size(), d_queries, d_query_offsets, query_stride,
+                                      n_queries, d_query_leaf, d_result, stream),
+                        "tkv_amq_probe");
+  }
+
+  const std::vector<tkv_amq_segment>& segments() const { return segs_; }
+  u64 total_out_bytes() const { return total_out_; }
+  const tkv_amq_segment* device_segments() const { return d_segs_.get<tkv_amq_segment>(); }
+
+ private:
+  FilterKind kind_;
+  usize bpk_;
+  u64 cap_, stride_;
+  std::vector<u64> counts_, page_ids_;
+  std::vector<tkv_amq_segment> segs_;
+  u64 total_out_ = 0, ws_bytes_ = 0;
+  u32 max_blocks_ = 0;
+  bool planned_ = false;
+  DeviceBuffer d_segs_, d_ws_;
+};
+
+// ---------------------------------------------------------------------------------------
+// single-leaf entry points (host keys -> host page payload)
+// ---------------------------------------------------------------------------------------
+namespace detail {
+
+inline Status stage_keys(const std::vector<std::string_view>& items, DeviceBuffer& d_keys,
+                         DeviceBuffer& d_offs, bool& fixed, u32& stride)
+{
+  const usize n = items.size();
+  fixed = n > 0;
+  stride = n ? (u32)items[0].size() : 16;
+  std::vector<u64> offs(n + 1, 0);
+  for (usize i = 0; i < n; ++i) {
+    offs[i + 1] = offs[i] + items[i].size();
+    fixed = fixed && items[i].size() == stride;
+  }
+  if (fixed && stride == 0) fixed = false;
+  std::vector<u8> blob(offs[n] ? offs[n] : 1);
+  for (usize i = 0; i < n; ++i)
+    if (!items[i].empty()) std::memcpy(blob.data() + offs[i], items[i].data(), items[i].size());
+  if (!d_keys.resize(blob.size()) || !d_offs.resize(offs.size() * 8))
+    return Status::from(TKV_AMQ_RESOURCE_EXHAUSTED, "hipMalloc");
+  if (hipMemcpy(d_keys.get(), blob.data(), blob.size(), hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(d_offs.get(), offs.data(), offs.size() * 8, hipMemcpyHostToDevice) != hipSuccess)
+    return Status::from(TKV_AMQ_INTERNAL, "hipMemcpy keys");
+  return OkStatus();
+}
+
+inline Status build_one(FilterKind kind, usize bpk, u64 leaf_page_id,
+                        const std::vector<std::string_view>& items,
+                        std::vector<u8>& page_payload, u64 page_payload_bytes)
+{
+  if (bpk == 0) return OkStatus();  // filter_builder.hpp:115-117, :227-229
+  if (tkv_amq_device_count() == 0) return Status::from(TKV_AMQ_UNAVAILABLE, "no HIP device");
+  FilterBatchBuilder b{kind, bpk, page_payload_bytes};
+  b.add_leaf(leaf_page_id, items.size());
+  TKV_AMQ_REQUIRE_OK(b.plan());
+  DeviceBuffer d_keys, d_offs;
+  bool fixed = false;
+  u32 stride = 16;
+  TKV_AMQ_REQUIRE_OK(stage_keys(items, d_keys, d_offs, fixed, stride));
+  DeviceBuffer d_out(b.total_out_bytes());
+  TKV_AMQ_REQUIRE_OK(b.build_all(d_keys.get(), fixed ? stride : 0,
+                                 fixed ? nullptr : d_offs.get<u64>(), d_out.get()));
+  TKV_AMQ_REQUIRE_OK(b.check());
+  const u32 used = b.segments()[0].payload_bytes;
+  page_payload.assign(page_payload_bytes ? page_payload_bytes : used, 0);
+  if (hipMemcpy(page_payload.data(), d_out.get(), used, hipMemcpyDeviceToHost) != hipSuccess)
+    return Status::from(TKV_AMQ_INTERNAL, "hipMemcpy payload");
+  return OkStatus();
+}
+
+}  // namespace detail
+
+inline Status build_bloom_filter_for_leaf(usize filter_bits_per_key, u64 leaf_page_id,
+                                          const std::vector<std::string_view>& items,
+                                          std::vector<u8>& page_payload,
+                                          u64 page_payload_bytes = 0)
+{
+  return detail::build_one(FilterKind::kBloom, filter_bits_per_key, leaf_page_id, items,
+                           page_payload, page_payload_bytes);
+}
+
+inline Status build_quotient_filter_for_leaf(usize filter_bits_per_key, u64 leaf_page_id,
+                                             const std::vector<std::string_view>& items,
+                                             std::vector<u8>& page_payload,
+                                             u64 page_payload_bytes)
+{
+  return detail::build_one(FilterKind::kQuotient, filter_bits_per_key, leaf_page_id, items,
+                           page_payload, page_payload_bytes);
+}
+
+// Like the reference: a failed build is logged by the caller and the leaf gets no filter
+// (filter_builder.hpp:323-325); the returned Status carries the reason.
+inline Status build_filter_for_leaf_in_job(usize filter_bits_per_key, u64 leaf_page_id,
+                                           const std::vector<std::string_view>& items,
+                                           std::vector<u8>& page_payload,
+                                           u64 page_payload_bytes = 32768 - kPackedPageHeaderSize,
+                                           FilterKind kind = kDefaultFilterKind)
+{
+  page_payload.clear();
+  Status s = kind == FilterKind::kBloom
+                 ? build_bloom_filter_for_leaf(filter_bits_per_key, leaf_page_id, items,
+                                               page_payload, page_payload_bytes)
+                 : build_quotient_filter_for_leaf(filter_bits_per_key, leaf_page_id, items,
+                                                  page_payload, page_payload_bytes);
+  if (!s.ok()) page_payload.clear();
+  return s;
+}
+
+// ---------------------------------------------------------------------------------------
+// KeyQuery::reject_page for a batch of point queries against one filter page payload
+// ---------------------------------------------------------------------------------------
+enum class BoolStatus : int { kFalse = 0, kTrue = 1, kUnknown = 2 };
+
+class KeyQuery
+{
+ public:
+  explicit KeyQuery(std::vector<std::string_view> keys) : keys_{std::move(keys)} {}
+
+  // per key: kTrue = definitely absent; kFalse = maybe present; kUnknown = no filter or the
+  // filter belongs to another page (key_query.hpp:156-159, 207-212, 227-232)
+  Status reject_page(u64 page_id_to_reject, const std::vector<u8>* filter_payload,
+                     FilterKind kind, std::vector<BoolStatus>& out)
+  {
+    out.assign(keys_.size(), BoolStatus::kUnknown);
+    if (!filter_payload || filter_payload->size() < 64) return OkStatus();
+    u64 magic, src;
+    std::memcpy(&magic, filter_payload->data(), 8);
+    std::memcpy(&src, filter_payload->data() + (kind == FilterKind::kBloom ? 16 : 8), 8);
+    const u64 want = kind == FilterKind::kBloom ? PackedBloomFilterPage::kMagic : PackedVqfFilter::kMagic;
+    if (magic != want) return Status::from(TKV_AMQ_INTERNAL, "filter page magic");
+    if (src != page_id_to_reject) return OkStatus();
+    if (keys_.empty()) return OkStatus();
+    if (tkv_amq_device_count() == 0) return Status::from(TKV_AMQ_UNAVAILABLE, "no HIP device");
+
+    // single-segment plan whose payload sits at offset 0 of the staged page
+    tkv_amq_segment seg{};
+    if (kind == FilterKind::kBloom) {
+      PackedBloomFilterPage h;
+      std::memcpy(&h, filter_payload->data(), sizeof(h));
+      seg.n_blocks = h.block_count;
+      seg.hash_count = h.hash_count;
+    } else {
+      PackedVqfFilter h;
+      std::memcpy(&h, filter_payload->data(), sizeof(h));
+      const u64 buckets = h.metadata.key_remainder_bits == 8 ? 80 : 36;
+      seg.n_blocks = (u32)h.metadata.nblocks;
+      seg.tag_bits = (u8)h.metadata.key_remainder_bits;
+      seg.mod_magic = ~0ull / (h.metadata.nblocks * buckets);
+    }
+    seg.out_offset = 0;
+    DeviceBuffer d_keys, d_offs, d_page(filter_payload->size()), d_seg(sizeof(seg)),
+        d_leaf(4 * keys_.size()), d_res(keys_.size());
+    bool fixed = false;
+    u32 stride = 16;
+    TKV_AMQ_REQUIRE_OK(detail::stage_keys(keys_, d_keys, d_offs, fixed, stride));
+    (void)hipMemcpy(d_page.get(), filter_payload->data(), filter_payload->size(), hipMemcpyHostToDevice);
+    (void)hipMemcpy(d_seg.get(), &seg, sizeof(seg), hipMemcpyHostToDevice);
+    (void)hipMemset(d_leaf.get(), 0, 4 * keys_.size());
+    const int st = tkv_amq_probe((int)kind, d_page.get(), d_seg.get<tkv_amq_segment>(), 1,
+                                 d_keys.get(), fixed ? nullptr : d_offs.get<u64>(),
+                                 fixed ? stride : 0, keys_.size(), d_leaf.get<u32>(),
+                                 d_res.get(), nullptr);
+    if (st != TKV_AMQ_OK) return Status::from(st, "tkv_amq_probe");
+    std::vector<u8> res(keys_.size());
+    if (hipMemcpy(res.data(), d_res.get(), res.size(), hipMemcpyDeviceToHost) != hipSuccess)
+      return Status::from(TKV_AMQ_INTERNAL, "hipMemcpy result");
+    for (usize i = 0; i < res.size(); ++i) out[i] = res[i] ? BoolStatus::kFalse : BoolStatus::kTrue;
+    return OkStatus();
+  }
+
+ private:
+  std::vector<std::string_view> keys_;
+};
+
+}  // namespace turtle_kv_amd

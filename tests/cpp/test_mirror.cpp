@@ -1,0 +1,110 @@
+// C++ parity test of the header-only host mirror (include/turtle_kv_amd/filter_builder.hpp)
+// over libtkv_amq.so.  Reads the golden fixtures; exits non-zero on any mismatch.
+// Usage: test_mirror <tests/golden dir>
+#include <turtle_kv_amd/filter_builder.hpp>
+
+#include <cstdio>
+#include <fstream>
+#include <iterator>
+#include <string>
+#include <vector>
+
+using namespace turtle_kv_amd;
+
+static int failures = 0;
+#define EXPECT(c)                                                   \
+  do {                                                              \
+    if (!(c)) {                                                     \
+      std::fprintf(stderr, "FAILED %s:%d: %s\n", __FILE__, __LINE__, #c); \
+      ++failures;                                                   \
+    }                                                               \
+  } while (0)
+
+static std::vector<u8> read_file(const std::string& p)
+{
+  std::ifstream f(p, std::ios::binary);
+  return std::vector<u8>(std::istreambuf_iterator<char>(f), {});
+}
+
+int main(int argc, char** argv)
+{
+  const std::string dir = argc > 1 ? argv[1] : "tests/golden";
+  std::vector<std::string> keys;
+  {
+    std::ifstream f(dir + "/workload_e_keys.txt");
+    for (std::string line; std::getline(f, line);)
+      if (!line.empty()) keys.push_back(line);
+  }
+  std::vector<std::string_view> items(keys.begin(), keys.end());
+  EXPECT(items.size() == 4096);
+  EXPECT(filter_bits_per_key(std::nullopt) == 12);
+  EXPECT(filter_bits_per_key(10) == 12);
+  EXPECT(filter_bits_per_key(10, FilterKind::kBloom) == 10);
+  EXPECT(vqf_filter_load_factor<8>(12) == 10.2 / 12.0);
+
+  // build_filter_for_leaf_in_job, default kind = VQF (config.hpp:24)
+  std::vector<u8> vqf_page;
+  Status s = build_filter_for_leaf_in_job(12, 7, items, vqf_page);
+  if (tkv_amq_device_count() == 0) {
+    // no GPU: the device path must fail loudly, never fall back to a CPU build
+    EXPECT(s.code == TKV_AMQ_UNAVAILABLE && vqf_page.empty());
+    std::printf("%s (no device; %d failures)\n", failures ? "FAIL" : "NODEVICE-OK", failures);
+    return failures ? 1 : 0;
+  }
+  EXPECT(s.ok());
+  const std::vector<u8> want_vqf = read_file(dir + "/workload_e_vqf12.bin");
+  EXPECT(vqf_page.size() == 32768 - 64);
+  EXPECT(std::equal(want_vqf.begin(), want_vqf.end(), vqf_page.begin()));
+  PackedVqfFilter hdr;
+  std::memcpy(&hdr, vqf_page.data(), sizeof(hdr));
+  EXPECT(hdr.magic == PackedVqfFilter::kMagic && hdr.src_page_id == 7 && hdr.hash_seed == kVqfHashSeed);
+  EXPECT(hdr.metadata.key_remainder_bits == 8 && hdr.metadata.nelts == 4096);
+
+  std::vector<u8> bloom_page;
+  s = build_bloom_filter_for_leaf(10, 7, items, bloom_page);
+  EXPECT(s.ok());
+  EXPECT(bloom_page == read_file(dir + "/workload_e_bloom10.bin"));
+
+  // bits_per_key == 0: no filter, OK
+  std::vector<u8> none;
+  EXPECT(build_filter_for_leaf_in_job(0, 7, items, none).ok() && none.empty());
+  // VQF below the 12-bit minimum: InvalidArgument (vqf_filter_page_view.hpp:46)
+  EXPECT(build_quotient_filter_for_leaf(10, 7, items, none, 32704).code == TKV_AMQ_INVALID_ARGUMENT);
+
+  // reject_page: present keys are never rejected; wrong page => kUnknown
+  KeyQuery q(items);
+  std::vector<BoolStatus> r;
+  EXPECT(q.reject_page(7, &vqf_page, FilterKind::kQuotient, r).ok());
+  size_t n_false = 0;
+  for (auto v : r) n_false += v == BoolStatus::kFalse;
+  EXPECT(n_false == items.size());
+  EXPECT(q.reject_page(8, &vqf_page, FilterKind::kQuotient, r).ok() && r[0] == BoolStatus::kUnknown);
+  EXPECT(q.reject_page(7, &bloom_page, FilterKind::kBloom, r).ok() && r[5] == BoolStatus::kFalse);
+
+  std::vector<std::string> miss;
+  for (int i = 0; i < 4096; ++i) miss.push_back("miss" + std::to_string(1000000 + i * 7919) + "zz");
+  KeyQuery qm(std::vector<std::string_view>(miss.begin(), miss.end()));
+  EXPECT(qm.reject_page(7, &vqf_page, FilterKind::kQuotient, r).ok());
+  size_t n_true = 0;
+  for (auto v : r) n_true += v == BoolStatus::kTrue;
+  EXPECT(n_true > 4000);
+
+  // batched builder over device keys == per-leaf results
+  {
+    FilterBatchBuilder b{FilterKind::kQuotient, 12, 32704};
+    b.add_leaf(7, 4096);
+    b.add_leaf(8, 0);
+    EXPECT(b.plan().ok());
+    DeviceBuffer d_keys(4096 * 24), d_out(b.total_out_bytes());
+    std::string blob;
+    for (auto& k : keys) blob += k;
+    (void)hipMemcpy(d_keys.get(), blob.data(), blob.size(), hipMemcpyHostToDevice);
+    EXPECT(b.build_all(d_keys.get(), 24, nullptr, d_out.get()).ok());
+    EXPECT(b.check().ok());
+    std::vector<u8> out(want_vqf.size());
+    (void)hipMemcpy(out.data(), d_out.get(), out.size(), hipMemcpyDeviceToHost);
+    EXPECT(out == want_vqf);
+  }
+  std::printf("%s (%d failures)\n", failures ? "FAIL" : "OK", failures);
+  return failures ? 1 : 0;
+}
