@@ -142,22 +142,29 @@ __device__ inline uint32_t davalanche_lo9(uint64_t h)
   return (p_lo9 ^ h3_hi) & 511u;
 }
 
-// 16-byte key, seed-independent part precomputed once per key.
+// 16-byte key, seed-independent part precomputed once per key.  Rotation distributes over
+// XOR, so rotl(hinit ^ k1, 27) = rotl(hinit, 27) ^ rotl(k1, 27): the per-seed part is the
+// constant `rhinit` = rotl(seed + P5 + 16, 27) and rotl(k1, 27) is computed once per key.
 struct Xxh16 {
-  uint64_t k1, k2;
-  __device__ inline Xxh16(uint64_t lo, uint64_t hi) : k1{dround(0, lo)}, k2{dround(0, hi)} {}
-  // state before the avalanche; `hinit` = seed + P5 + 16
-  __device__ inline uint64_t pre(uint64_t hinit) const
+  uint64_t rk1, k2;
+  __device__ inline Xxh16(uint64_t lo, uint64_t hi) : rk1{drotl<27>(dround(0, lo))}, k2{dround(0, hi)} {}
+  // state before the avalanche
+  __device__ inline uint64_t pre(uint64_t rhinit) const
   {
-    uint64_t h = hinit ^ k1;
-    h = drotl<27>(h) * kP1 + kP4;
+    uint64_t h = (rhinit ^ rk1) * kP1 + kP4;
     h ^= k2;
     return drotl<27>(h) * kP1 + kP4;
   }
-  __device__ inline uint64_t finish(uint64_t hinit) const { return davalanche(pre(hinit)); }
+  __device__ inline uint64_t finish(uint64_t rhinit) const { return davalanche(pre(rhinit)); }
   // low 9 bits only (Bloom bit index inside a 512-bit block)
-  __device__ inline uint32_t finish_lo9(uint64_t hinit) const { return davalanche_lo9(pre(hinit)); }
+  __device__ inline uint32_t finish_lo9(uint64_t rhinit) const { return davalanche_lo9(pre(rhinit)); }
 };
+
+// rotl(seed + P5 + 16, 27): the per-seed constant Xxh16 takes
+__host__ __device__ constexpr inline uint64_t xxh16_rhinit(uint64_t seed)
+{
+  return rotl64(seed + kP5 + 16, 27);
+}
 
 __device__ inline uint64_t ld64_unaligned(const uint8_t* p)
 {
@@ -217,12 +224,14 @@ __device__ inline uint64_t xxh64_bytes(const uint8_t* p, uint64_t len, uint64_t 
   return davalanche(h);
 }
 
-// floor(x / d) for x < 2^64, d < 2^32, given m = floor((2^64 - 1) / d): one umulhi + fix-up.
+// x mod d for x < 2^64, d < 2^32, given m = floor((2^64 - 1) / d): q = umulhi(x, m) is at
+// most 2 below floor(x / d), so two branchless conditional subtracts finish the job.
 __device__ inline uint64_t mod_by_magic(uint64_t x, uint64_t d, uint64_t m)
 {
-  uint64_t q = __umul64hi(x, m);
+  const uint64_t q = __umul64hi(x, m);
   uint64_t r = x - q * d;
-  while (r >= d) r -= d;
+  r = r >= d ? r - d : r;
+  r = r >= d ? r - d : r;
   return r;
 }
 

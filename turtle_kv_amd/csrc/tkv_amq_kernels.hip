@@ -7,9 +7,9 @@
 //                        16-byte coalesced stores.  No MFMA: this is hashing and bit-set.
 //   vqf_decide           one wave per segment replays the reference's insert order exactly
 //                        (power-of-two-choice decisions depend only on per-block counts);
-//                        per 64-key chunk the dependency is resolved with bit-sliced ballots,
-//                        only keys whose primary block may be near the CHECK_ALT threshold
-//                        run the serial scan.  Emits (block, rank) -> (bucket, tag) records.
+//                        per 64-key chunk: bit-sliced ballot matches give every lane its
+//                        all-primary counts, then one ballot round per key that takes its
+//                        alternate block.  Emits (block, rank) -> (bucket, tag) records.
 //   vqf_place            one wave per 64-byte VQF block: stable rank by bucket offset with
 //                        ballots, metadata zeros at rank+offset, block image in LDS, 16-byte
 //                        stores.
@@ -30,7 +30,7 @@ namespace tkv {
 // ---------------------------------------------------------------------------------------
 struct BloomSeeds {
   uint64_t seed[kMaxBloomHashes];
-  uint64_t hinit16[kMaxBloomHashes];  // seed + P5 + 16 : XXH64 state after the len add
+  uint64_t rhinit16[kMaxBloomHashes];  // rotl(seed + P5 + 16, 27), see Xxh16
 };
 
 constexpr BloomSeeds make_bloom_seeds()
@@ -38,7 +38,7 @@ constexpr BloomSeeds make_bloom_seeds()
   BloomSeeds t{};
   for (uint32_t i = 0; i < kMaxBloomHashes; ++i) {
     t.seed[i] = bloom_seed(i);
-    t.hinit16[i] = t.seed[i] + kP5 + 16;
+    t.rhinit16[i] = xxh16_rhinit(t.seed[i]);
   }
   return t;
 }
@@ -50,6 +50,16 @@ __constant__ BloomSeeds c_bloom = make_bloom_seeds();
 // key access
 // ---------------------------------------------------------------------------------------
 enum KeyMode : int { kKey16 = 0, kKeyFixed = 1, kKeyVar = 2 };
+
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+
+// streaming (non-temporal) loads/stores for data touched exactly once, so it does not
+// evict reused data (the probe's filter array) from L2 / the Infinity Cache
+__device__ inline uint4 load_nt16(const void* p)
+{
+  const u32x4_t v = __builtin_nontemporal_load(static_cast<const u32x4_t*>(p));
+  return uint4{v.x, v.y, v.z, v.w};
+}
 
 template <int MODE>
 __device__ inline uint64_t hash_key(const uint8_t* keys, const uint64_t* offs, uint32_t stride,
@@ -68,7 +78,8 @@ __device__ inline uint64_t hash_key(const uint8_t* keys, const uint64_t* offs, u
 // ---------------------------------------------------------------------------------------
 __device__ inline void lds_set_bit(uint32_t* blk, uint32_t bit)
 {
-  atomicOr(blk + (bit >> 5), 1u << (bit & 31));
+  // word = bits 5..8 of the 9-bit index (v_bfe_u32); the shift uses bits 0..4 only
+  atomicOr(blk + __builtin_amdgcn_ubfe(bit, 5, 4), 1u << (bit & 31));
 }
 
 __device__ inline void write_bloom_header(uint8_t* payload, const tkv_amq_segment& sg, int part)
@@ -92,14 +103,14 @@ template <int K>
 __device__ inline void bloom_insert16(uint32_t* s_bits, uint32_t nb, uint32_t k, const uint4& kv)
 {
   const Xxh16 x((uint64_t)kv.x | ((uint64_t)kv.y << 32), (uint64_t)kv.z | ((uint64_t)kv.w << 32));
-  const uint64_t h0 = x.finish(c_bloom.hinit16[0]);
+  const uint64_t h0 = x.finish(c_bloom.rhinit16[0]);
   uint32_t* blk = s_bits + 16 * (uint32_t)__umul64hi(h0, (uint64_t)nb);
   lds_set_bit(blk, (uint32_t)h0 & 511u);
   if constexpr (K != 0) {
 #pragma unroll
-    for (uint32_t j = 1; j < (uint32_t)K; ++j) lds_set_bit(blk, x.finish_lo9(c_bloom.hinit16[j]));
+    for (uint32_t j = 1; j < (uint32_t)K; ++j) lds_set_bit(blk, x.finish_lo9(c_bloom.rhinit16[j]));
   } else {
-    for (uint32_t j = 1; j < k; ++j) lds_set_bit(blk, x.finish_lo9(c_bloom.hinit16[j]));
+    for (uint32_t j = 1; j < k; ++j) lds_set_bit(blk, x.finish_lo9(c_bloom.rhinit16[j]));
   }
 }
 
@@ -213,12 +224,12 @@ __global__ __launch_bounds__(256) void bloom_global_set(const uint8_t* __restric
     if constexpr (MODE == kKey16) {
       const uint4 kv = reinterpret_cast<const uint4*>(keys)[i];
       const Xxh16 x((uint64_t)kv.x | ((uint64_t)kv.y << 32), (uint64_t)kv.z | ((uint64_t)kv.w << 32));
-      h0 = x.finish(c_bloom.hinit16[0]);
+      h0 = x.finish(c_bloom.rhinit16[0]);
       uint32_t* blk = words + 16 * (uint64_t)__umul64hi(h0, (uint64_t)sg.n_blocks);
       const uint32_t b0 = (uint32_t)h0 & 511u;
       atomicOr(blk + (b0 >> 5), 1u << (b0 & 31));
       for (uint32_t j = 1; j < sg.hash_count; ++j) {
-        const uint32_t b = x.finish_lo9(c_bloom.hinit16[j]);
+        const uint32_t b = x.finish_lo9(c_bloom.rhinit16[j]);
         atomicOr(blk + (b >> 5), 1u << (b & 31));
       }
     } else {
@@ -248,36 +259,35 @@ __global__ __launch_bounds__(256) void bloom_probe(const uint8_t* __restrict__ f
 {
   const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
-  const tkv_amq_segment& sg = segs[qseg[i]];
+  const tkv_amq_segment& sg = segs[__builtin_nontemporal_load(qseg + i)];
   const uint32_t k = sg.hash_count;
-  if (k == 0) {  // no filter page: reject_page returns kUnknown => cannot reject
-    result[i] = 1;
-    return;
-  }
-  const uint64_t* words = reinterpret_cast<const uint64_t*>(filters + sg.out_offset + kBloomHeader);
   uint32_t ok = 1;
-  if constexpr (MODE == kKey16) {
-    const uint4 kv = reinterpret_cast<const uint4*>(q)[i];
-    const Xxh16 x((uint64_t)kv.x | ((uint64_t)kv.y << 32), (uint64_t)kv.z | ((uint64_t)kv.w << 32));
-    const uint64_t h0 = x.finish(c_bloom.hinit16[0]);
-    const uint64_t* blk = words + 8 * __umul64hi(h0, (uint64_t)sg.n_blocks);
-    uint32_t b = (uint32_t)h0 & 511u;
-    ok &= (uint32_t)(blk[b >> 6] >> (b & 63));
-    for (uint32_t j = 1; j < k; ++j) {
-      b = x.finish_lo9(c_bloom.hinit16[j]);
+  if (k != 0) {  // k == 0: no filter page => reject_page returns kUnknown => cannot reject
+    const uint64_t* words =
+        reinterpret_cast<const uint64_t*>(filters + sg.out_offset + kBloomHeader);
+    if constexpr (MODE == kKey16) {
+      const uint4 kv = load_nt16(q + 16 * i);
+      const Xxh16 x((uint64_t)kv.x | ((uint64_t)kv.y << 32), (uint64_t)kv.z | ((uint64_t)kv.w << 32));
+      const uint64_t h0 = x.finish(c_bloom.rhinit16[0]);
+      const uint64_t* blk = words + 8 * __umul64hi(h0, (uint64_t)sg.n_blocks);
+      uint32_t b = (uint32_t)h0 & 511u;
       ok &= (uint32_t)(blk[b >> 6] >> (b & 63));
-    }
-  } else {
-    const uint64_t h0 = hash_key<MODE>(q, qoffs, stride, i, c_bloom.seed[0]);
-    const uint64_t* blk = words + 8 * __umul64hi(h0, (uint64_t)sg.n_blocks);
-    uint32_t b = (uint32_t)h0 & 511u;
-    ok &= (uint32_t)(blk[b >> 6] >> (b & 63));
-    for (uint32_t j = 1; j < k; ++j) {
-      b = (uint32_t)hash_key<MODE>(q, qoffs, stride, i, c_bloom.seed[j]) & 511u;
+      for (uint32_t j = 1; j < k; ++j) {
+        b = x.finish_lo9(c_bloom.rhinit16[j]);
+        ok &= (uint32_t)(blk[b >> 6] >> (b & 63));
+      }
+    } else {
+      const uint64_t h0 = hash_key<MODE>(q, qoffs, stride, i, c_bloom.seed[0]);
+      const uint64_t* blk = words + 8 * __umul64hi(h0, (uint64_t)sg.n_blocks);
+      uint32_t b = (uint32_t)h0 & 511u;
       ok &= (uint32_t)(blk[b >> 6] >> (b & 63));
+      for (uint32_t j = 1; j < k; ++j) {
+        b = (uint32_t)hash_key<MODE>(q, qoffs, stride, i, c_bloom.seed[j]) & 511u;
+        ok &= (uint32_t)(blk[b >> 6] >> (b & 63));
+      }
     }
   }
-  result[i] = (uint8_t)(ok & 1u);
+  __builtin_nontemporal_store((uint8_t)(ok & 1u), result + i);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -332,19 +342,27 @@ __device__ inline uint32_t& vqf_count(VqfWorkspace ws, uint64_t block)
   return *reinterpret_cast<uint32_t*>(ws.temp + block * kVqfTempStride + kVqfCountByte);
 }
 
-// bit-sliced "which lanes hold the same value": returns the lanes j (within `valid`) with
-// value_j == mine, using one ballot per bit of the value.
-__device__ inline uint64_t match_lanes(uint32_t mine, uint32_t value, bool active, uint64_t valid,
-                                       int nbits)
+template <int MODE>
+__device__ inline uint64_t vqf_key_hash(const uint8_t* __restrict__ keys,
+                                        const uint64_t* __restrict__ offs, uint32_t stride,
+                                        uint64_t gi, const uint4& kv)
 {
-  uint64_t m = valid;
-  for (int j = 0; j < nbits; ++j) {
-    const uint64_t b = __ballot(active && ((value >> j) & 1u));
-    m &= ((mine >> j) & 1u) ? b : ~b;
+  if constexpr (MODE == kKey16) {
+    const Xxh16 x((uint64_t)kv.x | ((uint64_t)kv.y << 32), (uint64_t)kv.z | ((uint64_t)kv.w << 32));
+    return x.finish(xxh16_rhinit(kVqfHashSeed));
+  } else {
+    return hash_key<MODE>(keys, offs, stride, gi, kVqfHashSeed);
   }
-  return m;
 }
 
+// Exact replay of the reference insert order (build_vqf_filter<T>, filter_builder.hpp:204-214)
+// for one leaf, 64 keys per step.  The power-of-two-choice decision of key i depends only on
+// the element counts of its two candidate blocks at the time of its insertion, so a chunk is
+// resolved as follows: every lane starts from the counts it would see if all earlier lanes of
+// the chunk took their primary block (two bit-sliced ballot matches); the first lane whose
+// exact decision is "alternate" is found with one ballot, its move is applied to the later
+// lanes, and the scan repeats -- one round per alternate choice, not per key.  The count of
+// the chosen block at decision time is the key's insertion rank inside that block.
 template <int T, int MODE>
 __device__ void vqf_decide_body(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs,
                                 uint32_t stride, const tkv_amq_segment& sg, uint32_t seg_index,
@@ -361,26 +379,25 @@ __device__ void vqf_decide_body(const uint8_t* __restrict__ keys, const uint64_t
   const uint64_t lt = lanemask_lt();
   typename C::Entry* temp =
       reinterpret_cast<typename C::Entry*>(ws.temp + sg.block_base * kVqfTempStride);
+  const uint4* kp = reinterpret_cast<const uint4*>(keys) + sg.key_begin;
 
   for (uint32_t b = lane; b < nb; b += 64) cnt[b] = 0;
   __syncthreads();
 
   uint32_t nelts = 0;
   uint32_t fail = 0;
+  uint4 kv_next = {0, 0, 0, 0};
+  if constexpr (MODE == kKey16) {
+    if (lane < n) kv_next = kp[lane];
+  }
   for (uint32_t base = 0; base < n; base += 64) {
     const uint32_t i = base + lane;
     const bool valid = i < n;
-    uint64_t h = 0;
-    if (valid) {
-      const uint64_t gi = sg.key_begin + i;
-      if constexpr (MODE == kKey16) {
-        const uint4 kv = reinterpret_cast<const uint4*>(keys)[gi];
-        const Xxh16 x((uint64_t)kv.x | ((uint64_t)kv.y << 32), (uint64_t)kv.z | ((uint64_t)kv.w << 32));
-        h = x.finish(kVqfHashSeed + kP5 + 16);
-      } else {
-        h = hash_key<MODE>(keys, offs, stride, gi, kVqfHashSeed);
-      }
+    uint4 kv = kv_next;
+    if constexpr (MODE == kKey16) {  // prefetch the next chunk's keys
+      if (i + 64 < n) kv_next = kp[i + 64];
     }
+    const uint64_t h = valid ? vqf_key_hash<MODE>(keys, offs, stride, sg.key_begin + i, kv) : 0;
     const bool kept = valid && ((h & mask) == h);  // filter_builder.hpp:210
     const uint64_t keptmask = __ballot(kept);
     nelts += __popcll(keptmask);
@@ -391,42 +408,48 @@ __device__ void vqf_decide_body(const uint8_t* __restrict__ keys, const uint64_t
     const uint32_t pb = pi / C::kBuckets, po = pi - pb * C::kBuckets;
     const uint32_t ab = ai / C::kBuckets, ao = ai - ab * C::kBuckets;
 
-    const uint64_t Mpp = match_lanes(pb, pb, kept, keptmask, nbits);
-    const uint64_t Map = match_lanes(pb, ab, kept, keptmask, nbits);
-    const uint64_t Mpa = match_lanes(ab, pb, kept, keptmask, nbits);
-
-    const uint32_t cbp = kept ? cnt[pb] : 0;
-    const uint32_t cba = kept ? cnt[ab] : 0;
-    // upper bound of the primary block's count when this key is inserted
-    const uint32_t U = cbp + __popcll((Mpp | Map) & lt);
-    const uint64_t NT = __ballot(kept && U >= C::kThreshold);
-
+    // lanes with pb_j == my pb / with pb_j == my ab: one ballot per block-id bit; each
+    // 32-bit half of a match mask is updated with one v_bitop3 (m & ~(ballot ^ sext(bit)))
+    uint32_t mpp_lo = (uint32_t)keptmask, mpp_hi = (uint32_t)(keptmask >> 32);
+    uint32_t mpa_lo = mpp_lo, mpa_hi = mpp_hi;
+    for (int j = 0; j < nbits; ++j) {
+      const uint32_t xp = (uint32_t)((int32_t)(pb << (31 - j)) >> 31);  // 0 or ~0
+      const uint32_t xa = (uint32_t)((int32_t)(ab << (31 - j)) >> 31);
+      const uint64_t bp = __ballot(xp != 0);
+      const uint32_t bl = (uint32_t)bp, bh = (uint32_t)(bp >> 32);
+      mpp_lo &= ~(bl ^ xp);
+      mpp_hi &= ~(bh ^ xp);
+      mpa_lo &= ~(bl ^ xa);
+      mpa_hi &= ~(bh ^ xa);
+    }
+    const uint64_t Mpp = ((uint64_t)mpp_hi << 32) | mpp_lo;
+    const uint64_t Mpa = ((uint64_t)mpa_hi << 32) | mpa_lo;
+    uint32_t cp = 0, ca = 0;
+    if (kept) {
+      cp = cnt[pb] + __popcll(Mpp & lt);
+      ca = cnt[ab] + __popcll(Mpa & lt);
+    }
+    // rounds: the first lane (in insertion order) whose exact decision is "alternate"
     bool alt = false;
-    if (NT != 0) {
-      uint32_t cp = cbp + __popcll(Mpp & lt & ~NT);
-      uint32_t ca = cba + __popcll(Mpa & lt & ~NT);
-      uint64_t rem = NT;
-      while (rem != 0) {
-        const uint32_t k = (uint32_t)__ffsll((long long)rem) - 1;
-        rem &= rem - 1;
-        // decision of lane k (vqf_insert): consult the alternate block only when the
-        // primary is past CHECK_ALT; move iff the alternate is strictly emptier.
-        const bool my_alt = (cp >= C::kThreshold) && (pb != ab) && (ca < cp);
-        const bool my_full = my_alt ? (ca >= C::kSlots) : (cp >= C::kSlots);
-        const uint32_t my_ch = my_alt ? ab : pb;
-        const uint32_t ch_k = __builtin_amdgcn_readlane(my_ch, k);
-        fail |= (uint32_t)__builtin_amdgcn_readlane((int)my_full, k);
-        if (lane == k) alt = my_alt;
-        if (lane > k) {
-          cp += (pb == ch_k);
-          ca += (ab == ch_k);
-        }
-      }
+    uint64_t live = keptmask;
+    for (;;) {
+      const uint64_t A = __ballot(kept && !alt && (cp >= C::kThreshold) && (pb != ab) && (ca < cp)) & live;
+      if (A == 0) break;
+      const uint32_t k = (uint32_t)__ffsll((long long)A) - 1;
+      const uint32_t pk = __builtin_amdgcn_readlane(pb, k);
+      const uint32_t ak = __builtin_amdgcn_readlane(ab, k);
+      if (lane == k) alt = true;
+      const bool later = lane > k;
+      cp += (later && pb == ak) ? 1u : 0u;
+      cp -= (later && pb == pk) ? 1u : 0u;
+      ca += (later && ab == ak) ? 1u : 0u;
+      ca -= (later && ab == pk) ? 1u : 0u;
+      live &= ~((2ull << k) - 1);  // lanes after k
     }
     const uint32_t chosen = alt ? ab : pb;
     const uint32_t cho = alt ? ao : po;
-    const uint64_t Mcc = match_lanes(chosen, chosen, kept, keptmask, nbits);
-    const uint32_t r = (alt ? cba : cbp) + __popcll(Mcc & lt);
+    const uint32_t r = alt ? ca : cp;  // count of the chosen block when this key is inserted
+    fail |= (uint32_t)(__ballot(kept && r >= C::kSlots) != 0);
     if (kept) {
       if (r < C::kSlots)
         temp[(uint64_t)chosen * (kVqfTempStride / sizeof(typename C::Entry)) + r] =
@@ -611,13 +634,14 @@ __global__ __launch_bounds__(256) void vqf_probe(const uint8_t* __restrict__ fil
   if (i >= n) return;
   uint64_t h;
   if constexpr (MODE == kKey16) {
-    const uint4 kv = reinterpret_cast<const uint4*>(q)[i];
+    const uint4 kv = load_nt16(q + 16 * i);
     const Xxh16 x((uint64_t)kv.x | ((uint64_t)kv.y << 32), (uint64_t)kv.z | ((uint64_t)kv.w << 32));
-    h = x.finish(kVqfHashSeed + kP5 + 16);
+    h = x.finish(xxh16_rhinit(kVqfHashSeed));
   } else {
     h = hash_key<MODE>(q, qoffs, stride, i, kVqfHashSeed);
   }
-  result[i] = vqf_probe_one(filters, segs[qseg[i]], h);
+  __builtin_nontemporal_store(vqf_probe_one(filters, segs[__builtin_nontemporal_load(qseg + i)], h),
+                              result + i);
 }
 
 __global__ __launch_bounds__(256) void vqf_probe_hashed(const uint8_t* __restrict__ filters,
@@ -642,7 +666,7 @@ __global__ __launch_bounds__(256) void vqf_hash_kernel(const uint8_t* __restrict
   if constexpr (MODE == kKey16) {
     const uint4 kv = reinterpret_cast<const uint4*>(q)[i];
     const Xxh16 x((uint64_t)kv.x | ((uint64_t)kv.y << 32), (uint64_t)kv.z | ((uint64_t)kv.w << 32));
-    out[i] = x.finish(kVqfHashSeed + kP5 + 16);
+    out[i] = x.finish(xxh16_rhinit(kVqfHashSeed));
   } else {
     out[i] = hash_key<MODE>(q, qoffs, stride, i, kVqfHashSeed);
   }
