@@ -59,19 +59,20 @@ extern "C" {
 #define TKV_AMQ_VQF 1
 
 /* One leaf's filter ("segment"), produced on the host by tkv_amq_plan and read by the
- * device kernels.  64 bytes, little-endian, no padding. */
+ * device kernels.  64 bytes, little-endian, no padding.  The first 32 bytes are what a
+ * probe needs (two 16-byte loads). */
 typedef struct tkv_amq_segment {
-  uint64_t key_begin;     /* first key index of this leaf's (sorted) item range */
   uint64_t out_offset;    /* byte offset of the filter page payload in the output array */
-  uint64_t src_page_id;   /* leaf PageId stored in the filter header (reject_page check) */
-  uint64_t mod_magic;     /* VQF: floor((2^64-1) / (n_blocks * buckets_per_block)); Bloom: 0 */
-  uint64_t block_base;    /* prefix sum of n_blocks (VQF workspace addressing) */
-  uint32_t n_keys;        /* items in the leaf (tombstones included) */
   uint32_t n_blocks;      /* Bloom: 512-bit blocks; VQF: 64-byte vqf blocks */
-  uint32_t payload_bytes; /* bytes of payload the build writes (header + filter) */
   uint16_t hash_count;    /* Bloom k; VQF 0 */
   uint8_t tag_bits;       /* VQF 8 | 16; Bloom 0 */
   uint8_t hash_val_shift; /* VQF hash truncation (filter_builder.hpp:280-283) */
+  uint64_t mod_magic;     /* VQF: floor((2^64-1) / (n_blocks * buckets_per_block)); Bloom: 0 */
+  uint64_t key_begin;     /* first key index of this leaf's (sorted) item range */
+  uint64_t src_page_id;   /* leaf PageId stored in the filter header (reject_page check) */
+  uint64_t block_base;    /* prefix sum of n_blocks (VQF workspace addressing) */
+  uint32_t n_keys;        /* items in the leaf (tombstones included) */
+  uint32_t payload_bytes; /* bytes of payload the build writes (header + filter) */
   uint32_t bits_per_key;  /* effective bits/key after the TreeOptions clamp */
   uint32_t reserved;
 } tkv_amq_segment;

@@ -37,17 +37,17 @@ class TkvAmqError(RuntimeError):
 class Segment(ctypes.Structure):
     """tkv_amq_segment (64 bytes)."""
     _fields_ = [
-        ("key_begin", ctypes.c_uint64),
         ("out_offset", ctypes.c_uint64),
-        ("src_page_id", ctypes.c_uint64),
-        ("mod_magic", ctypes.c_uint64),
-        ("block_base", ctypes.c_uint64),
-        ("n_keys", ctypes.c_uint32),
         ("n_blocks", ctypes.c_uint32),
-        ("payload_bytes", ctypes.c_uint32),
         ("hash_count", ctypes.c_uint16),
         ("tag_bits", ctypes.c_uint8),
         ("hash_val_shift", ctypes.c_uint8),
+        ("mod_magic", ctypes.c_uint64),
+        ("key_begin", ctypes.c_uint64),
+        ("src_page_id", ctypes.c_uint64),
+        ("block_base", ctypes.c_uint64),
+        ("n_keys", ctypes.c_uint32),
+        ("payload_bytes", ctypes.c_uint32),
         ("bits_per_key", ctypes.c_uint32),
         ("reserved", ctypes.c_uint32),
     ]
@@ -56,10 +56,10 @@ class Segment(ctypes.Structure):
 assert ctypes.sizeof(Segment) == 64
 
 SEGMENT_DTYPE = np.dtype([
-    ("key_begin", "<u8"), ("out_offset", "<u8"), ("src_page_id", "<u8"),
-    ("mod_magic", "<u8"), ("block_base", "<u8"), ("n_keys", "<u4"), ("n_blocks", "<u4"),
-    ("payload_bytes", "<u4"), ("hash_count", "<u2"), ("tag_bits", "u1"),
-    ("hash_val_shift", "u1"), ("bits_per_key", "<u4"), ("reserved", "<u4")])
+    ("out_offset", "<u8"), ("n_blocks", "<u4"), ("hash_count", "<u2"), ("tag_bits", "u1"),
+    ("hash_val_shift", "u1"), ("mod_magic", "<u8"), ("key_begin", "<u8"), ("src_page_id", "<u8"),
+    ("block_base", "<u8"), ("n_keys", "<u4"), ("payload_bytes", "<u4"), ("bits_per_key", "<u4"),
+    ("reserved", "<u4")])
 assert SEGMENT_DTYPE.itemsize == 64
 
 # every symbol include/tkv_amq.h declares

@@ -248,6 +248,30 @@ __global__ __launch_bounds__(256) void bloom_global_set(const uint8_t* __restric
 // ---------------------------------------------------------------------------------------
 // Bloom probe
 // ---------------------------------------------------------------------------------------
+// Probe-side view of a segment: the first 16 bytes of tkv_amq_segment in one load.
+struct ProbeDesc {
+  uint64_t out_offset;
+  uint32_t n_blocks;
+  uint32_t hash_count, tag_bits, hash_val_shift;
+};
+
+__device__ inline ProbeDesc load_probe_desc(const tkv_amq_segment* segs, uint32_t s)
+{
+  const uint4 v = reinterpret_cast<const uint4*>(segs + s)[0];
+  ProbeDesc d;
+  d.out_offset = (uint64_t)v.x | ((uint64_t)v.y << 32);
+  d.n_blocks = v.z;
+  d.hash_count = v.w & 0xffffu;
+  d.tag_bits = (v.w >> 16) & 0xffu;
+  d.hash_val_shift = v.w >> 24;
+  return d;
+}
+
+// One lane per (query, leaf).  The 64-byte filter block is fetched with four 16-byte loads
+// (instead of k divergent 8-byte loads) and staged in a per-lane LDS slot; the k bit tests
+// are then LDS reads.  Stride 20 dwords keeps the slots 16-byte aligned and spreads banks.
+constexpr uint32_t kProbeSlotWords = 20;
+
 template <int MODE>
 __global__ __launch_bounds__(256) void bloom_probe(const uint8_t* __restrict__ filters,
                                                    const tkv_amq_segment* __restrict__ segs,
@@ -257,31 +281,45 @@ __global__ __launch_bounds__(256) void bloom_probe(const uint8_t* __restrict__ f
                                                    const uint32_t* __restrict__ qseg,
                                                    uint8_t* __restrict__ result)
 {
+  __shared__ uint4 s_blk[256 * kProbeSlotWords / 4];
   const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
-  const tkv_amq_segment& sg = segs[__builtin_nontemporal_load(qseg + i)];
-  const uint32_t k = sg.hash_count;
+  const ProbeDesc d = load_probe_desc(segs, __builtin_nontemporal_load(qseg + i));
   uint32_t ok = 1;
-  if (k != 0) {  // k == 0: no filter page => reject_page returns kUnknown => cannot reject
-    const uint64_t* words =
-        reinterpret_cast<const uint64_t*>(filters + sg.out_offset + kBloomHeader);
+  if (d.hash_count != 0) {  // 0: no filter page => reject_page returns kUnknown => cannot reject
+    const uint8_t* words = filters + d.out_offset + kBloomHeader;
+    uint4* slot = s_blk + threadIdx.x * (kProbeSlotWords / 4);
+    const uint32_t* slot32 = reinterpret_cast<const uint32_t*>(slot);
     if constexpr (MODE == kKey16) {
       const uint4 kv = load_nt16(q + 16 * i);
       const Xxh16 x((uint64_t)kv.x | ((uint64_t)kv.y << 32), (uint64_t)kv.z | ((uint64_t)kv.w << 32));
       const uint64_t h0 = x.finish(c_bloom.rhinit16[0]);
-      const uint64_t* blk = words + 8 * __umul64hi(h0, (uint64_t)sg.n_blocks);
-      uint32_t b = (uint32_t)h0 & 511u;
-      ok &= (uint32_t)(blk[b >> 6] >> (b & 63));
-      for (uint32_t j = 1; j < k; ++j) {
-        b = x.finish_lo9(c_bloom.rhinit16[j]);
-        ok &= (uint32_t)(blk[b >> 6] >> (b & 63));
+      const uint4* blk = reinterpret_cast<const uint4*>(words + 64 * __umul64hi(h0, (uint64_t)d.n_blocks));
+      const uint4 b0 = blk[0], b1 = blk[1], b2 = blk[2], b3 = blk[3];
+      slot[0] = b0;
+      slot[1] = b1;
+      slot[2] = b2;
+      slot[3] = b3;
+      uint32_t bit = (uint32_t)h0 & 511u;
+      ok &= slot32[bit >> 5] >> (bit & 31);
+      if (d.hash_count == 7) {
+#pragma unroll
+        for (uint32_t j = 1; j < 7; ++j) {
+          bit = x.finish_lo9(c_bloom.rhinit16[j]);
+          ok &= slot32[bit >> 5] >> (bit & 31);
+        }
+      } else {
+        for (uint32_t j = 1; j < d.hash_count; ++j) {
+          bit = x.finish_lo9(c_bloom.rhinit16[j]);
+          ok &= slot32[bit >> 5] >> (bit & 31);
+        }
       }
     } else {
       const uint64_t h0 = hash_key<MODE>(q, qoffs, stride, i, c_bloom.seed[0]);
-      const uint64_t* blk = words + 8 * __umul64hi(h0, (uint64_t)sg.n_blocks);
+      const uint64_t* blk = reinterpret_cast<const uint64_t*>(words + 64 * __umul64hi(h0, (uint64_t)d.n_blocks));
       uint32_t b = (uint32_t)h0 & 511u;
       ok &= (uint32_t)(blk[b >> 6] >> (b & 63));
-      for (uint32_t j = 1; j < k; ++j) {
+      for (uint32_t j = 1; j < d.hash_count; ++j) {
         b = (uint32_t)hash_key<MODE>(q, qoffs, stride, i, c_bloom.seed[j]) & 511u;
         ok &= (uint32_t)(blk[b >> 6] >> (b & 63));
       }
@@ -355,6 +393,29 @@ __device__ inline uint64_t vqf_key_hash(const uint8_t* __restrict__ keys,
   }
 }
 
+// Per-lane location of one key: primary / alternate block, bucket offsets, tag.
+struct VqfLoc {
+  uint32_t pb, po, ab, ao, tag;
+  bool kept;
+};
+
+template <int T>
+__device__ inline VqfLoc vqf_locate(uint64_t h, bool valid, uint64_t mask, uint64_t R,
+                                    uint64_t magic)
+{
+  using C = Vqf<T>;
+  VqfLoc l;
+  l.kept = valid && ((h & mask) == h);  // filter_builder.hpp:210
+  l.tag = (uint32_t)(h & ((1ull << T) - 1));
+  const uint32_t pi = (uint32_t)mod_by_magic(h >> T, R, magic);
+  const uint32_t ai = (uint32_t)mod_by_magic((h ^ ((uint64_t)l.tag * kVqfAltMul)) >> T, R, magic);
+  l.pb = pi / C::kBuckets;
+  l.po = pi - l.pb * C::kBuckets;
+  l.ab = ai / C::kBuckets;
+  l.ao = ai - l.ab * C::kBuckets;
+  return l;
+}
+
 // Exact replay of the reference insert order (build_vqf_filter<T>, filter_builder.hpp:204-214)
 // for one leaf, 64 keys per step.  The power-of-two-choice decision of key i depends only on
 // the element counts of its two candidate blocks at the time of its insertion, so a chunk is
@@ -363,7 +424,10 @@ __device__ inline uint64_t vqf_key_hash(const uint8_t* __restrict__ keys,
 // exact decision is "alternate" is found with one ballot, its move is applied to the later
 // lanes, and the scan repeats -- one round per alternate choice, not per key.  The count of
 // the chosen block at decision time is the key's insertion rank inside that block.
-template <int T, int MODE>
+// NBITS >= ceil(log2(n_blocks)) is a compile-time bound (extra high bits are zero in every
+// lane and leave the matches unchanged), so the match loop unrolls into the same basic
+// block as the next chunk's hashing and the two interleave.
+template <int T, int MODE, int NBITS>
 __device__ void vqf_decide_body(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs,
                                 uint32_t stride, const tkv_amq_segment& sg, uint32_t seg_index,
                                 VqfWorkspace ws, uint32_t* cnt)
@@ -374,8 +438,6 @@ __device__ void vqf_decide_body(const uint8_t* __restrict__ keys, const uint64_t
   const uint64_t R = (uint64_t)nb * C::kBuckets;
   const uint64_t magic = sg.mod_magic;
   const uint64_t mask = ~0ull << sg.hash_val_shift;  // filter_builder.hpp:187
-  const uint64_t tmask = (1ull << T) - 1;
-  const int nbits = nb <= 1 ? 0 : 32 - __clz(nb - 1);
   const uint64_t lt = lanemask_lt();
   typename C::Entry* temp =
       reinterpret_cast<typename C::Entry*>(ws.temp + sg.block_base * kVqfTempStride);
@@ -386,35 +448,48 @@ __device__ void vqf_decide_body(const uint8_t* __restrict__ keys, const uint64_t
 
   uint32_t nelts = 0;
   uint32_t fail = 0;
-  uint4 kv_next = {0, 0, 0, 0};
-  if constexpr (MODE == kKey16) {
-    if (lane < n) kv_next = kp[lane];
-  }
-  for (uint32_t base = 0; base < n; base += 64) {
-    const uint32_t i = base + lane;
-    const bool valid = i < n;
-    uint4 kv = kv_next;
-    if constexpr (MODE == kKey16) {  // prefetch the next chunk's keys
-      if (i + 64 < n) kv_next = kp[i + 64];
+
+  // One 64-key step.  `cur` = located keys of this chunk; `kv_hash` = raw keys of the next
+  // chunk (loaded one step earlier); `kv_load` receives the chunk after that.  The loop
+  // below is unrolled by two with the key buffers swapping roles, so no register copy of an
+  // in-flight load exists and the compiler waits only for that load, never for the scatter
+  // store issued after it.
+  // the record store of a chunk is issued at the start of the next step (after that step's
+  // loads), so a wait for the key prefetch never waits for a scatter store issued just
+  // before it
+  using Entry = typename C::Entry;
+  Entry* pend_ptr = temp;
+  Entry pend_val = 0;
+  bool pend = false;
+  auto step = [&](uint32_t base, VqfLoc& cur, const uint4& kv_hash, uint4& kv_load) {
+    const VqfLoc L = cur;
+    // block counts before this chunk (every lane reads: an invalid lane's blocks are 0)
+    const uint32_t cnt_p = cnt[L.pb], cnt_a = cnt[L.ab];
+    const uint32_t inext = base + 64 + lane;
+    const bool vnext = inext < n;
+    uint64_t hn;
+    if constexpr (MODE == kKey16) {
+      // branch-free (clamped index, select on the result): straight-line code lets the
+      // compiler count vmcnt exactly instead of draining every outstanding access
+      kv_load = kp[min(inext + 64, n - 1)];
+      if (pend) *pend_ptr = pend_val;
+      const uint64_t hh = vqf_key_hash<MODE>(keys, offs, stride, 0, kv_hash);
+      hn = vnext ? hh : 0;
+    } else {
+      if (pend) *pend_ptr = pend_val;
+      hn = vnext ? vqf_key_hash<MODE>(keys, offs, stride, sg.key_begin + inext, kv_hash) : 0;
     }
-    const uint64_t h = valid ? vqf_key_hash<MODE>(keys, offs, stride, sg.key_begin + i, kv) : 0;
-    const bool kept = valid && ((h & mask) == h);  // filter_builder.hpp:210
-    const uint64_t keptmask = __ballot(kept);
+
+    const uint64_t keptmask = __ballot(L.kept);
     nelts += __popcll(keptmask);
-
-    const uint32_t tag = (uint32_t)(h & tmask);
-    const uint32_t pi = (uint32_t)mod_by_magic(h >> T, R, magic);
-    const uint32_t ai = (uint32_t)mod_by_magic((h ^ ((uint64_t)tag * kVqfAltMul)) >> T, R, magic);
-    const uint32_t pb = pi / C::kBuckets, po = pi - pb * C::kBuckets;
-    const uint32_t ab = ai / C::kBuckets, ao = ai - ab * C::kBuckets;
-
     // lanes with pb_j == my pb / with pb_j == my ab: one ballot per block-id bit; each
     // 32-bit half of a match mask is updated with one v_bitop3 (m & ~(ballot ^ sext(bit)))
     uint32_t mpp_lo = (uint32_t)keptmask, mpp_hi = (uint32_t)(keptmask >> 32);
     uint32_t mpa_lo = mpp_lo, mpa_hi = mpp_hi;
-    for (int j = 0; j < nbits; ++j) {
-      const uint32_t xp = (uint32_t)((int32_t)(pb << (31 - j)) >> 31);  // 0 or ~0
-      const uint32_t xa = (uint32_t)((int32_t)(ab << (31 - j)) >> 31);
+#pragma unroll
+    for (int j = 0; j < NBITS; ++j) {
+      const uint32_t xp = (uint32_t)__builtin_amdgcn_sbfe((int32_t)L.pb, j, 1);  // 0 or ~0
+      const uint32_t xa = (uint32_t)__builtin_amdgcn_sbfe((int32_t)L.ab, j, 1);
       const uint64_t bp = __ballot(xp != 0);
       const uint32_t bl = (uint32_t)bp, bh = (uint32_t)(bp >> 32);
       mpp_lo &= ~(bl ^ xp);
@@ -422,41 +497,57 @@ __device__ void vqf_decide_body(const uint8_t* __restrict__ keys, const uint64_t
       mpa_lo &= ~(bl ^ xa);
       mpa_hi &= ~(bh ^ xa);
     }
+    cur = vqf_locate<T>(hn, vnext, mask, R, magic);
     const uint64_t Mpp = ((uint64_t)mpp_hi << 32) | mpp_lo;
     const uint64_t Mpa = ((uint64_t)mpa_hi << 32) | mpa_lo;
-    uint32_t cp = 0, ca = 0;
-    if (kept) {
-      cp = cnt[pb] + __popcll(Mpp & lt);
-      ca = cnt[ab] + __popcll(Mpa & lt);
-    }
+    uint32_t cp = L.kept ? cnt_p + __popcll(Mpp & lt) : 0u;
+    uint32_t ca = L.kept ? cnt_a + __popcll(Mpa & lt) : 0u;
+    const uint32_t pb = L.pb, ab = L.ab;
     // rounds: the first lane (in insertion order) whose exact decision is "alternate"
-    bool alt = false;
-    uint64_t live = keptmask;
+    const uint64_t cand = __ballot(L.kept && pb != ab);  // blocks differ (vqf_insert alt test)
+    uint64_t live = cand, altmask = 0;
     for (;;) {
-      const uint64_t A = __ballot(kept && !alt && (cp >= C::kThreshold) && (pb != ab) && (ca < cp)) & live;
+      const uint64_t A = __ballot((cp >= C::kThreshold) & (ca < cp)) & live;
       if (A == 0) break;
       const uint32_t k = (uint32_t)__ffsll((long long)A) - 1;
+      altmask |= 1ull << k;
       const uint32_t pk = __builtin_amdgcn_readlane(pb, k);
       const uint32_t ak = __builtin_amdgcn_readlane(ab, k);
-      if (lane == k) alt = true;
+      // the move only affects lanes after k; written as lane-predicates so that each update
+      // is one v_addc / v_subbrev with an SGPR carry mask
       const bool later = lane > k;
       cp += (later && pb == ak) ? 1u : 0u;
       cp -= (later && pb == pk) ? 1u : 0u;
       ca += (later && ab == ak) ? 1u : 0u;
       ca -= (later && ab == pk) ? 1u : 0u;
-      live &= ~((2ull << k) - 1);  // lanes after k
+      live &= ~((2ull << k) - 1);
     }
+    const bool alt = (altmask >> lane) & 1;
     const uint32_t chosen = alt ? ab : pb;
-    const uint32_t cho = alt ? ao : po;
+    const uint32_t cho = alt ? L.ao : L.po;
     const uint32_t r = alt ? ca : cp;  // count of the chosen block when this key is inserted
-    fail |= (uint32_t)(__ballot(kept && r >= C::kSlots) != 0);
-    if (kept) {
-      if (r < C::kSlots)
-        temp[(uint64_t)chosen * (kVqfTempStride / sizeof(typename C::Entry)) + r] =
-            (typename C::Entry)((cho << T) | tag);
-      atomicAdd(cnt + chosen, 1u);
+    fail |= (uint32_t)(__ballot(L.kept && r >= C::kSlots) != 0);
+    pend = L.kept && r < C::kSlots;
+    pend_ptr = temp + (uint64_t)chosen * (kVqfTempStride / sizeof(Entry)) + (r < C::kSlots ? r : 0);
+    pend_val = (Entry)((cho << T) | L.tag);
+    if (L.kept) atomicAdd(cnt + chosen, 1u);
+  };
+
+  uint4 kv0 = {0, 0, 0, 0}, kvA = {0, 0, 0, 0}, kvB = {0, 0, 0, 0};
+  if constexpr (MODE == kKey16) {
+    if (n > 0) {
+      kv0 = kp[min(lane, n - 1)];
+      kvA = kp[min(lane + 64, n - 1)];
     }
   }
+  VqfLoc cur = vqf_locate<T>(lane < n ? vqf_key_hash<MODE>(keys, offs, stride, sg.key_begin + lane, kv0) : 0,
+                             lane < n, mask, R, magic);
+  for (uint32_t base = 0; base < n; base += 128) {
+    step(base, cur, kvA, kvB);
+    if (base + 64 >= n) break;
+    step(base + 64, cur, kvB, kvA);
+  }
+  if (pend) *pend_ptr = pend_val;
   __syncthreads();
   for (uint32_t b = lane; b < nb; b += 64) {
     const uint32_t c = cnt[b];
@@ -468,6 +559,16 @@ __device__ void vqf_decide_body(const uint8_t* __restrict__ keys, const uint64_t
   }
 }
 
+template <int T, int MODE>
+__device__ inline void vqf_decide_dispatch(const uint8_t* keys, const uint64_t* offs,
+                                           uint32_t stride, const tkv_amq_segment& sg,
+                                           uint32_t seg_index, VqfWorkspace ws, uint32_t* cnt)
+{
+  // kVqfMaxLdsBlocks = 16384 -> at most 14 block-id bits
+  if (sg.n_blocks <= 512) vqf_decide_body<T, MODE, 9>(keys, offs, stride, sg, seg_index, ws, cnt);
+  else vqf_decide_body<T, MODE, 14>(keys, offs, stride, sg, seg_index, ws, cnt);
+}
+
 template <int MODE>
 __global__ __launch_bounds__(64) void vqf_decide(const uint8_t* __restrict__ keys,
                                                  const uint64_t* __restrict__ offs, uint32_t stride,
@@ -477,16 +578,28 @@ __global__ __launch_bounds__(64) void vqf_decide(const uint8_t* __restrict__ key
   extern __shared__ uint32_t s_cnt[];
   const tkv_amq_segment sg = segs[blockIdx.x];
   const VqfWorkspace ws = vqf_workspace(ws_base, n_segs);
-  if (sg.tag_bits == 8) vqf_decide_body<8, MODE>(keys, offs, stride, sg, blockIdx.x, ws, s_cnt);
-  else if (sg.tag_bits == 16) vqf_decide_body<16, MODE>(keys, offs, stride, sg, blockIdx.x, ws, s_cnt);
+  if (sg.tag_bits == 8) vqf_decide_dispatch<8, MODE>(keys, offs, stride, sg, blockIdx.x, ws, s_cnt);
+  else if (sg.tag_bits == 16) vqf_decide_dispatch<16, MODE>(keys, offs, stride, sg, blockIdx.x, ws, s_cnt);
 }
+
+// One thread per 64-byte VQF block: the block's records (bucket offset, tag) arrive in
+// insertion order; vqf_insert appends each tag at the end of its bucket, so the final block
+// is a stable counting sort by bucket offset.  Per-thread bucket counters are packed 4 per
+// LDS dword (counts <= 48 never carry into the next byte), the exclusive prefix is a SWAR
+// multiply, and the second pass takes each entry's slot with ds_add_rtn in insertion order.
+constexpr uint32_t kPlaceThreads = 128;
 
 template <int T>
 __device__ void vqf_place_body(const tkv_amq_segment& sg, uint32_t seg_index, VqfWorkspace ws,
-                               uint8_t* __restrict__ out, uint32_t* img)
+                               uint8_t* __restrict__ out, uint32_t* s_cnt, uint32_t* s_img)
 {
   using C = Vqf<T>;
-  const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  using E = typename C::Entry;
+  constexpr uint32_t kCntWords = (C::kBuckets + 3) / 4;  // 20 / 9
+  constexpr uint32_t kCntStride = kCntWords | 1;         // odd stride: no bank conflicts
+  constexpr uint32_t kImgStride = 17;
+  constexpr uint32_t kRecWords = C::kSlots * sizeof(E) / 16;  // 16-byte loads per record: 6 / 7
+  const uint32_t tid = threadIdx.x;
   const uint32_t nb = sg.n_blocks;
   uint8_t* payload = out + sg.out_offset;
 
@@ -506,70 +619,93 @@ __device__ void vqf_place_body(const tkv_amq_segment& sg, uint32_t seg_index, Vq
     reinterpret_cast<ulonglong2*>(payload)[tid] = v;
   }
 
-  const typename C::Entry* temp =
-      reinterpret_cast<const typename C::Entry*>(ws.temp + sg.block_base * kVqfTempStride);
-  uint32_t* my_img = img + 16 * wave;
+  uint32_t* cnt = s_cnt + tid * kCntStride;
+  uint32_t* img = s_img + tid * kImgStride;
   uint4* dst_blocks = reinterpret_cast<uint4*>(payload + kVqfHeader + kVqfMetadata);
-  const uint64_t lt = lanemask_lt();
 
-  for (uint32_t b = wave; b < nb; b += 4) {
-    const uint32_t c = vqf_count(ws, sg.block_base + b);
-    const bool has = lane < c;
-    uint32_t e = 0;
-    if (has) e = temp[(uint64_t)b * (kVqfTempStride / sizeof(typename C::Entry)) + lane];
-    const uint32_t o = e >> T, tag = e & ((1u << T) - 1);
-    // stable rank by bucket offset (insertion order breaks ties): tags of bucket o are
-    // appended at its end by vqf_insert, so the final layout is a stable sort by offset.
-    const uint64_t V = __ballot(has);
-    uint64_t less = 0, eq = V;
-    for (int bit = (int)C::kOffsetBits - 1; bit >= 0; --bit) {
-      const uint64_t bb = __ballot(has && ((o >> bit) & 1u));
-      if ((o >> bit) & 1u) {
-        less |= eq & ~bb;
-        eq &= bb;
-      } else {
-        eq &= ~bb;
+  for (uint32_t b = tid; b < nb; b += kPlaceThreads) {
+    const uint8_t* rec = ws.temp + (sg.block_base + b) * kVqfTempStride;
+    const uint32_t c = *reinterpret_cast<const uint32_t*>(rec + kVqfCountByte);
+    uint4 rv[kRecWords];
+#pragma unroll
+    for (uint32_t q = 0; q < kRecWords; ++q) rv[q] = reinterpret_cast<const uint4*>(rec)[q];
+    const E* ent = reinterpret_cast<const E*>(rv);
+
+#pragma unroll
+    for (uint32_t w = 0; w < kCntWords; ++w) cnt[w] = 0;
+#pragma unroll
+    for (uint32_t w = C::kMdBytes / 4; w < 16; ++w) img[w] = 0;
+    // pass 1: bucket histogram
+#pragma unroll
+    for (uint32_t i = 0; i < C::kSlots; ++i) {
+      if (i < c) {
+        const uint32_t o = ent[i] >> T;
+        atomicAdd(cnt + (o >> 2), 1u << (8 * (o & 3)));
       }
     }
-    const uint32_t rank = __popcll(less) + __popcll(eq & lt);
-
-    // block image: metadata all ones (top bit clear while empty), tags zero
-    if (lane < 16) {
-      uint32_t v = 0;
-      if (lane * 4 < C::kMdBytes) {
-        v = 0xffffffffu;
-        if (c == 0 && lane * 4 + 4 == C::kMdBytes) v = 0x7fffffffu;
+    // exclusive prefix over buckets (bytes): inclusive-in-dword = v * 0x01010101
+    uint32_t run = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < kCntWords; ++w) {
+      const uint32_t v = cnt[w];
+      const uint32_t incl = v * 0x01010101u;
+      cnt[w] = (incl - v) + run * 0x01010101u;
+      run += incl >> 24;
+    }
+    // pass 2: slot of each entry in insertion order; metadata zero at slot + offset
+    uint64_t md_lo = ~0ull, md_hi = T == 8 ? ~0ull : 0ull;
+#pragma unroll
+    for (uint32_t i = 0; i < C::kSlots; ++i) {
+      if (i < c) {
+        const uint32_t e = ent[i];
+        const uint32_t o = e >> T, tag = e & ((1u << T) - 1);
+        const uint32_t old = atomicAdd(cnt + (o >> 2), 1u << (8 * (o & 3)));
+        const uint32_t slot = (old >> (8 * (o & 3))) & 0xffu;
+        const uint32_t z = slot + o;
+        if (z < 64) md_lo &= ~(1ull << z);
+        else md_hi &= ~(1ull << (z - 64));
+        const uint32_t byte = C::kMdBytes + slot * (T / 8);
+        atomicOr(img + (byte >> 2), tag << (8 * (byte & 3)));
       }
-      my_img[lane] = v;
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    if (has) {
-      const uint32_t z = rank + o;  // the metadata zero for this tag
-      atomicAnd(my_img + (z >> 5), ~(1u << (z & 31)));
-      const uint32_t byte = C::kMdBytes + rank * (T / 8);
-      atomicOr(my_img + (byte >> 2), tag << (8 * (byte & 3)));
+    if (c == 0) {  // an empty block keeps the init metadata: top bit clear
+      if constexpr (T == 8) md_hi &= ~(1ull << 63);
+      else md_lo &= ~(1ull << 63);
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    if (lane < 4) {
-      const uint4 v = reinterpret_cast<const uint4*>(my_img)[lane];
-      dst_blocks[(uint64_t)b * 4 + lane] = v;
+    uint4 v0;
+    v0.x = (uint32_t)md_lo;
+    v0.y = (uint32_t)(md_lo >> 32);
+    if constexpr (T == 8) {
+      v0.z = (uint32_t)md_hi;
+      v0.w = (uint32_t)(md_hi >> 32);
+    } else {
+      v0.z = img[2];
+      v0.w = img[3];
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    __builtin_amdgcn_wave_barrier();
+    uint4* dst = dst_blocks + (uint64_t)b * 4;
+    dst[0] = v0;
+#pragma unroll
+    for (uint32_t q = 1; q < 4; ++q) {
+      uint4 v;
+      v.x = img[4 * q];
+      v.y = img[4 * q + 1];
+      v.z = img[4 * q + 2];
+      v.w = img[4 * q + 3];
+      dst[q] = v;
+    }
   }
 }
 
-__global__ __launch_bounds__(256) void vqf_place(const tkv_amq_segment* __restrict__ segs,
-                                                 void* ws_base, uint32_t n_segs,
-                                                 uint8_t* __restrict__ out)
+__global__ __launch_bounds__(kPlaceThreads) void vqf_place(const tkv_amq_segment* __restrict__ segs,
+                                                           void* ws_base, uint32_t n_segs,
+                                                           uint8_t* __restrict__ out)
 {
-  __shared__ uint32_t s_img[4 * 16];
+  __shared__ uint32_t s_cnt[kPlaceThreads * 21];
+  __shared__ uint32_t s_img[kPlaceThreads * 17];
   const tkv_amq_segment sg = segs[blockIdx.x];
   const VqfWorkspace ws = vqf_workspace(ws_base, n_segs);
-  if (sg.tag_bits == 8) vqf_place_body<8>(sg, blockIdx.x, ws, out, s_img);
-  else if (sg.tag_bits == 16) vqf_place_body<16>(sg, blockIdx.x, ws, out, s_img);
+  if (sg.tag_bits == 8) vqf_place_body<8>(sg, blockIdx.x, ws, out, s_cnt, s_img);
+  else if (sg.tag_bits == 16) vqf_place_body<16>(sg, blockIdx.x, ws, out, s_cnt, s_img);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -601,25 +737,29 @@ __device__ inline bool vqf_bucket_has(const uint8_t* blocks, uint32_t idx, uint3
 }
 
 template <int T>
-__device__ inline bool vqf_present(const uint8_t* payload, const tkv_amq_segment& sg, uint64_t h)
+__device__ inline bool vqf_present(const uint8_t* payload, uint32_t n_blocks, uint64_t magic,
+                                   uint64_t h)
 {
   using C = Vqf<T>;
-  const uint64_t R = (uint64_t)sg.n_blocks * C::kBuckets;
+  const uint64_t R = (uint64_t)n_blocks * C::kBuckets;
   const uint32_t tag = (uint32_t)(h & ((1ull << T) - 1));
-  const uint32_t pi = (uint32_t)mod_by_magic(h >> T, R, sg.mod_magic);
-  const uint32_t ai = (uint32_t)mod_by_magic((h ^ ((uint64_t)tag * kVqfAltMul)) >> T, R, sg.mod_magic);
+  const uint32_t pi = (uint32_t)mod_by_magic(h >> T, R, magic);
+  const uint32_t ai = (uint32_t)mod_by_magic((h ^ ((uint64_t)tag * kVqfAltMul)) >> T, R, magic);
   const uint8_t* blocks = payload + kVqfHeader + kVqfMetadata;
   return vqf_bucket_has<T>(blocks, pi, tag) || vqf_bucket_has<T>(blocks, ai, tag);
 }
 
-__device__ inline uint8_t vqf_probe_one(const uint8_t* filters, const tkv_amq_segment& sg, uint64_t h)
+__device__ inline uint8_t vqf_probe_one(const uint8_t* filters, const tkv_amq_segment* segs,
+                                        uint32_t s, uint64_t h)
 {
-  if (sg.tag_bits == 0) return 1;  // no filter: cannot reject
-  const uint8_t* payload = filters + sg.out_offset;
-  const uint64_t mask = *reinterpret_cast<const uint64_t*>(payload + 24);
-  if ((h & mask) != h) return 1;  // dropped hash values are always "maybe"
-  return sg.tag_bits == 8 ? (uint8_t)vqf_present<8>(payload, sg, h)
-                          : (uint8_t)vqf_present<16>(payload, sg, h);
+  const ProbeDesc d = load_probe_desc(segs, s);
+  if (d.tag_bits == 0) return 1;  // no filter: cannot reject
+  const uint8_t* payload = filters + d.out_offset;
+  const uint64_t mask = ~0ull << d.hash_val_shift;  // == PackedVqfFilter::hash_mask
+  if ((h & mask) != h) return 1;  // dropped hash values are always "maybe" (:115-117)
+  const uint64_t magic = segs[s].mod_magic;
+  return d.tag_bits == 8 ? (uint8_t)vqf_present<8>(payload, d.n_blocks, magic, h)
+                         : (uint8_t)vqf_present<16>(payload, d.n_blocks, magic, h);
 }
 
 template <int MODE>
@@ -640,7 +780,7 @@ __global__ __launch_bounds__(256) void vqf_probe(const uint8_t* __restrict__ fil
   } else {
     h = hash_key<MODE>(q, qoffs, stride, i, kVqfHashSeed);
   }
-  __builtin_nontemporal_store(vqf_probe_one(filters, segs[__builtin_nontemporal_load(qseg + i)], h),
+  __builtin_nontemporal_store(vqf_probe_one(filters, segs, __builtin_nontemporal_load(qseg + i), h),
                               result + i);
 }
 
@@ -652,7 +792,7 @@ __global__ __launch_bounds__(256) void vqf_probe_hashed(const uint8_t* __restric
 {
   const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
-  result[i] = vqf_probe_one(filters, segs[qseg[i]], hashes[i]);
+  result[i] = vqf_probe_one(filters, segs, qseg[i], hashes[i]);
 }
 
 template <int MODE>
@@ -918,7 +1058,7 @@ int tkv_amq_build(int kind, const uint8_t* keys, const uint64_t* offs, uint32_t 
   else
     hipLaunchKernelGGL(vqf_decide<kKeyVar>, dim3(n_segs), dim3(64), lds, s, keys, offs, stride,
                        d_segs, d_ws, n_segs);
-  hipLaunchKernelGGL(vqf_place, dim3(n_segs), dim3(256), 0, s, d_segs, d_ws, n_segs, d_out);
+  hipLaunchKernelGGL(vqf_place, dim3(n_segs), dim3(kPlaceThreads), 0, s, d_segs, d_ws, n_segs, d_out);
   return hipGetLastError() == hipSuccess ? TKV_AMQ_OK : TKV_AMQ_INTERNAL;
 }
 
