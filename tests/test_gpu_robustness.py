@@ -1,0 +1,138 @@
+"""GPU: failure reporting, concurrency and edge cases of the C ABI (all against the oracle)."""
+import threading
+
+import numpy as np
+import pytest
+import xxhash
+
+pytestmark = pytest.mark.gpu
+
+VQF_SEED = 0x9D0924DC03E79A75
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch as t
+    assert t.cuda.is_available()
+    return t
+
+
+def overflow_keys(oracle, n=50):
+    """Keys whose primary AND alternate bucket fall in block 0 of a 2-block, 8-bit VQF
+    (R = 2 * 80 buckets): the 49th insert finds both candidate blocks full."""
+    out = []
+    i = 0
+    while len(out) < n:
+        k = oracle.gen_keys16(1234, i, 1)[0]
+        i += 1
+        h = xxhash.xxh64_intdigest(k.tobytes(), VQF_SEED)
+        tag = h & 0xFF
+        pi = (h >> 8) % 160
+        ai = ((h ^ ((tag * 0x5BD1E995) & ((1 << 64) - 1))) >> 8) % 160
+        if pi < 80 and ai < 80:
+            out.append(k)
+    return np.stack(out)
+
+
+def test_vqf_block_overflow_is_reported(oracle, amq, torch):
+    keys = overflow_keys(oracle)
+    st, _, pl = oracle.vqf_build(keys, len(keys), 12, 32704)
+    assert pl.nblocks == 2 and st == 13, "oracle: vqf_insert failure (filter_builder.hpp:211)"
+    plan = amq.plan_filters(amq.VQF, [len(keys)], 12, payload_capacity=32704)
+    with pytest.raises(amq.TkvAmqError) as e:
+        amq.build_all_filters(plan, amq.KeyBatch.fixed(torch.from_numpy(keys).cuda()))
+    assert e.value.status == amq.abi.INTERNAL
+    # the per-leaf entry point logs and leaves the leaf without a filter (:323-325)
+    assert amq.build_filter_for_leaf_in_job(12, 1, amq.KeyBatch.fixed(torch.from_numpy(keys).cuda())) is None
+    # 48 of them fit exactly: no failure, bytes equal the oracle
+    st, ref, pl = oracle.vqf_build(keys[:48], 48, 12, 32704)
+    assert st == 0
+    plan = amq.plan_filters(amq.VQF, [48], 12, payload_capacity=32704)
+    out = amq.build_all_filters(plan, amq.KeyBatch.fixed(torch.from_numpy(keys[:48].copy()).cuda()))
+    assert out.cpu().numpy()[:pl.payload_used].tobytes() == ref[:pl.payload_used].tobytes()
+
+
+@pytest.mark.parametrize("kind", [0, 1])
+def test_concurrent_streams_two_threads(oracle, amq, torch, kind):
+    """The ABI is called concurrently from worker threads (build_all_pages); each call on its
+    own stream must produce exactly its own filters."""
+    results = {}
+
+    def work(seed):
+        counts = [16384] * 4 + [777]
+        keys = oracle.gen_keys16(seed, 0, sum(counts))
+        oracle.sort_segments(keys, np.concatenate([[0], np.cumsum(counts)]).astype(np.uint64))
+        s = torch.cuda.Stream()
+        with torch.cuda.stream(s):
+            plan = amq.plan_filters(kind, counts, 12, payload_capacity=32704)
+            d = torch.from_numpy(keys).cuda()
+            outs = [amq.build_all_filters(plan, amq.KeyBatch.fixed(d), stream=s) for _ in range(3)]
+            s.synchronize()
+        results[seed] = (plan, [o.cpu().numpy() for o in outs], keys, counts)
+
+    ts = [threading.Thread(target=work, args=(sd,)) for sd in (5, 6)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    for sd, (plan, outs, keys, counts) in results.items():
+        # payload regions only: the 64-byte alignment padding between VQF payloads is never
+        # written (like the unused tail of a reference page buffer)
+        regions = [(int(g["out_offset"]), int(g["payload_bytes"])) for g in plan.segs]
+        for o in outs[1:]:
+            assert all(np.array_equal(outs[0][a:a + b], o[a:a + b]) for a, b in regions)
+        sb = np.concatenate([[0], np.cumsum(counts)])
+        for s_, c in enumerate(counts):
+            if kind == 0:
+                st, ref = oracle.bloom_build(keys[sb[s_]:], c, 12, src_page_id=s_)
+                ref = ref.tobytes()
+            else:
+                st, ref, pl = oracle.vqf_build(keys[sb[s_]:], c, 12, 32704, src_page_id=s_)
+                ref = ref[:pl.payload_used].tobytes()
+            seg = plan.segs[s_]
+            o = int(seg["out_offset"])
+            assert outs[0][o:o + int(seg["payload_bytes"])].tobytes() == ref
+
+
+def test_empty_and_no_filter_batches(oracle, amq, torch):
+    keys = torch.zeros((0, 16), dtype=torch.uint8, device="cuda")
+    for kind in (0, 1):
+        plan = amq.plan_filters(kind, [], 12, payload_capacity=32704)
+        amq.build_all_filters(plan, amq.KeyBatch.fixed(keys))
+        plan = amq.plan_filters(kind, [0, 0], 12, payload_capacity=32704)
+        out = amq.build_all_filters(plan, amq.KeyBatch.fixed(keys)).cpu().numpy()
+        for s_ in range(2):   # empty leaves still get a valid (empty) filter page
+            seg = plan.segs[s_]
+            if kind == 0:
+                st, ref = oracle.bloom_build(np.zeros((1, 16), np.uint8), 0, 12, src_page_id=s_)
+                ref = ref.tobytes()
+            else:
+                st, ref, pl = oracle.vqf_build(np.zeros((1, 16), np.uint8), 0, 12, 32704, src_page_id=s_)
+                ref = ref[:pl.payload_used].tobytes()
+            o = int(seg["out_offset"])
+            assert out[o:o + int(seg["payload_bytes"])].tobytes() == ref
+    # bits_per_key == 0: no filters; every probe answers "maybe" (reject_page kUnknown)
+    k = amq.gen_keys16(3, 0, 1000)
+    for kind in (0, 1):
+        plan = amq.plan_filters(kind, [1000], 0, payload_capacity=32704)
+        out = amq.build_all_filters(plan, amq.KeyBatch.fixed(k))
+        miss = amq.gen_keys16(4, 0, 1000)
+        res = amq.probe_filters(plan, out, amq.KeyBatch.fixed(miss),
+                                torch.zeros(1000, dtype=torch.int32, device="cuda"))
+        assert bool(res.all())
+
+
+def test_invalid_arguments(amq, torch):
+    with pytest.raises(amq.TkvAmqError) as e:
+        amq.plan_filters(amq.VQF, [100], 11, payload_capacity=32704)
+    assert e.value.status == amq.abi.INVALID_ARGUMENT
+    with pytest.raises(amq.TkvAmqError) as e:
+        amq.plan_filters(amq.VQF, [100], 12, payload_capacity=100)
+    assert e.value.status == amq.abi.RESOURCE_EXHAUSTED
+    L = amq.abi.lib()
+    # misaligned 16-byte keys are rejected, not read out of bounds
+    buf = torch.zeros(33, dtype=torch.uint8, device="cuda")
+    plan = amq.plan_filters(amq.BLOOM, [1], 10)
+    st = L.tkv_amq_build(0, buf.data_ptr() + 1, None, 16, 1, plan.device_segs().data_ptr(), 1,
+                         plan.max_seg_blocks, buf.data_ptr(), None, 0, None)
+    assert st == amq.abi.INVALID_ARGUMENT

@@ -70,6 +70,11 @@ def allgather_filters(local, gathered=None, group=None):
     world = dist.get_world_size(group)
     if gathered is None:
         gathered = torch.empty(local.numel() * world, dtype=local.dtype, device=local.device)
+    if local.is_cuda and dist.get_backend(group) != "nccl":
+        # gloo (tests, CPU-only rehearsals): stage through host memory
+        g = allgather_filters(local.cpu(), None, group)
+        gathered.copy_(g)
+        return gathered
     try:
         dist.all_gather_into_tensor(gathered, local, group=group)
     except (RuntimeError, NotImplementedError, AttributeError):
