@@ -136,3 +136,22 @@ def test_invalid_arguments(amq, torch):
     st = L.tkv_amq_build(0, buf.data_ptr() + 1, None, 16, 1, plan.device_segs().data_ptr(), 1,
                          plan.max_seg_blocks, buf.data_ptr(), None, 0, None)
     assert st == amq.abi.INVALID_ARGUMENT
+
+
+@pytest.mark.parametrize("kind,bpk,cap", [(0, 10, 0), (1, 12, 32704)])
+def test_host_pipeline_matches_device_build(oracle, amq, torch, kind, bpk, cap):
+    """build_filters_from_host (chunked H2D -> build -> D2H on three streams) writes the same
+    filter pages as one device-resident build."""
+    counts = [16384] * 37 + [999, 0, 16384]
+    keys = oracle.gen_keys16(77, 0, sum(counts))
+    if kind == 1:
+        oracle.sort_segments(keys, np.concatenate([[0], np.cumsum(counts)]).astype(np.uint64))
+    host = torch.from_numpy(keys).pin_memory()
+    out, plan = amq.filters.build_filters_from_host(kind, counts, bpk, host, payload_capacity=cap,
+                                                    chunk_keys=100_000)
+    ref_plan = amq.plan_filters(kind, counts, bpk, payload_capacity=cap, out_stride=plan.segs[0]["out_offset"] * 0 + int(plan.segs[1]["out_offset"]))
+    ref = amq.build_all_filters(ref_plan, amq.KeyBatch.fixed(torch.from_numpy(keys).cuda())).cpu().numpy()
+    o = out.numpy()
+    for g in plan.segs:
+        a, b = int(g["out_offset"]), int(g["payload_bytes"])
+        assert np.array_equal(o[a:a + b], ref[a:a + b])

@@ -376,3 +376,120 @@ class KeyQuery:
         else:
             present = probe_filters(filter_page.plan, filter_page.payload, self.keys, qs)
         return [BoolStatus.kFalse if p else BoolStatus.kTrue for p in present.cpu().tolist()]
+
+
+# ---------------------------------------------------------------------------------------
+# host-resident keys -> host filter pages (keys come from host
+# checkpoint buffers and the filters return to host page memory)
+# ---------------------------------------------------------------------------------------
+class HostFilterPipeline:
+    """Host-resident keys -> host filter pages for one batch shape (a checkpoint's leaves).
+
+    Chunks of whole leaves flow H2D -> build -> D2H on three streams (copy-in, build,
+    copy-out), double-buffered, so PCIe transfers in both directions overlap the kernels.
+    Plans, device buffers and per-chunk plan uploads are prepared once in the constructor;
+    run() only enqueues copies and builds.  Output: the batch's filter pages at a fixed
+    per-leaf stride (leaf s at byte s * out_stride)."""
+
+    def __init__(self, kind: int, leaf_key_counts, bits_per_key: int, payload_capacity: int = 0,
+                 out_stride: int = 0, chunk_keys: int = 8 << 20, src_page_ids=None,
+                 key_bytes: int = 16, device=None):
+        torch = _torch()
+        _require_device()
+        self.kind, self.dev = kind, torch.device(device or "cuda")
+        counts = np.asarray(leaf_key_counts, dtype=np.int64)
+        if out_stride == 0:
+            biggest = int(counts.max()) if len(counts) else 0
+            p1 = plan_filters(kind, [biggest], bits_per_key, payload_capacity=payload_capacity)
+            out_stride = (int(p1.segs[0]["payload_bytes"]) + 63) // 64 * 64 or 64
+        self.out_stride = out_stride
+        self.plan = plan_filters(kind, counts, bits_per_key, payload_capacity=payload_capacity,
+                                 out_stride=out_stride, src_page_ids=src_page_ids)
+        bounds, acc = [0], 0
+        for i, c in enumerate(counts):
+            acc += int(c)
+            if acc >= chunk_keys:
+                bounds.append(i + 1)
+                acc = 0
+        if bounds[-1] != len(counts):
+            bounds.append(len(counts))
+        self.key_begin = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
+        self.chunks = list(zip(bounds, bounds[1:]))
+        self.plans = [plan_filters(kind, counts[b0:b1], bits_per_key,
+                                   payload_capacity=payload_capacity, out_stride=out_stride,
+                                   src_page_ids=self.plan.segs["src_page_id"][b0:b1])
+                      for b0, b1 in self.chunks]
+        max_keys = max((int(self.key_begin[b1] - self.key_begin[b0]) for b0, b1 in self.chunks), default=1)
+        max_leaves = max((b1 - b0 for b0, b1 in self.chunks), default=1)
+        ws_bytes = max((p.workspace_bytes for p in self.plans), default=0)
+        self.d_keys = [torch.empty((max(max_keys, 1), key_bytes), dtype=torch.uint8, device=self.dev)
+                       for _ in range(2)]
+        self.d_out = [torch.empty(max(max_leaves * out_stride, 1), dtype=torch.uint8, device=self.dev)
+                      for _ in range(2)]
+        self.d_ws = [torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=self.dev) for _ in range(2)]
+        for p in self.plans:
+            p.device_segs(self.dev)
+        self.s_in, self.s_run, self.s_out = (torch.cuda.Stream(self.dev) for _ in range(3))
+        self.fail = torch.zeros(1, dtype=torch.int32, device=self.dev)
+        torch.cuda.synchronize(self.dev)
+
+    def new_host_output(self):
+        return _torch().empty(self.plan.total_out_bytes, dtype=_torch().uint8, pin_memory=True)
+
+    def run(self, host_keys, host_out=None, check: bool = True):
+        torch = _torch()
+        if host_out is None:
+            host_out = self.new_host_output()
+        n = len(self.chunks)
+        ev_in = [torch.cuda.Event() for _ in range(n)]
+        ev_run = [torch.cuda.Event() for _ in range(n)]
+        ev_out = [torch.cuda.Event() for _ in range(n)]
+        st = self.out_stride
+        self.s_run.wait_stream(torch.cuda.current_stream(self.dev))
+        with torch.cuda.stream(self.s_run):
+            self.fail.zero_()
+        for c, (b0, b1) in enumerate(self.chunks):
+            slot = c & 1
+            k0, k1 = int(self.key_begin[b0]), int(self.key_begin[b1])
+            with torch.cuda.stream(self.s_in):
+                if c >= 2:
+                    self.s_in.wait_event(ev_run[c - 2])       # slot's keys no longer read
+                self.d_keys[slot][:k1 - k0].copy_(host_keys[k0:k1], non_blocking=True)
+                ev_in[c].record(self.s_in)
+            with torch.cuda.stream(self.s_run):
+                self.s_run.wait_event(ev_in[c])
+                if c >= 2:
+                    self.s_run.wait_event(ev_out[c - 2])      # slot's output copied out
+                    if self.kind == VQF:                      # fold chunk c-2's failure word
+                        self.fail.add_(self.d_ws[slot][:4].view(torch.int32))
+                build_all_filters(self.plans[c], KeyBatch.fixed(self.d_keys[slot][:k1 - k0]),
+                                  out=self.d_out[slot], workspace=self.d_ws[slot],
+                                  stream=self.s_run, check=False)
+                ev_run[c].record(self.s_run)
+            with torch.cuda.stream(self.s_out):
+                self.s_out.wait_event(ev_run[c])
+                nbytes = (b1 - b0) * st
+                host_out[b0 * st:b0 * st + nbytes].copy_(self.d_out[slot][:nbytes], non_blocking=True)
+                ev_out[c].record(self.s_out)
+        if self.kind == VQF:
+            with torch.cuda.stream(self.s_run):
+                for c in range(max(0, n - 2), n):
+                    self.fail.add_(self.d_ws[c & 1][:4].view(torch.int32))
+        self.s_out.synchronize()
+        if check and self.kind == VQF:
+            self.s_run.synchronize()
+            if int(self.fail.item()) != 0:
+                raise TkvAmqError(abi.INTERNAL, "vqf_insert (filter_builder.hpp:211)")
+        return host_out
+
+
+def build_filters_from_host(kind: int, leaf_key_counts, bits_per_key: int, host_keys,
+                            payload_capacity: int = 0, out_stride: int = 0, host_out=None,
+                            chunk_keys: int = 8 << 20, src_page_ids=None, device=None):
+    """One-shot HostFilterPipeline: returns (host_out, plan of the whole batch)."""
+    torch = _torch()
+    if not isinstance(host_keys, torch.Tensor):
+        host_keys = torch.from_numpy(np.ascontiguousarray(host_keys))
+    pipe = HostFilterPipeline(kind, leaf_key_counts, bits_per_key, payload_capacity, out_stride,
+                              chunk_keys, src_page_ids, host_keys.shape[1], device)
+    return pipe.run(host_keys, host_out), pipe.plan
