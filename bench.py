@@ -185,7 +185,18 @@ def main():
     else:
         alg_bytes = n * 16 + int(plan.segs["payload_bytes"].astype(np.int64).sum())
     achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
-    traffic = load_traffic(args.workload)
+    prof = load_profile(args.workload)
+    traffic = prof.get("hbm_bytes_per_launch")
+    valu_roof = None
+    if prof.get("valu_instr_per_key") and not probe:
+        # the bound this kernel actually sits on: integer VALU issue
+        wave_instr = prof["valu_instr_per_key"] * n / 64
+        ach = wave_instr / (kernel_ms * 1e-3) / 1e9
+        peak = prof.get("valu_peak_ginstr_s_at_2.4GHz", 614.4)
+        valu_roof = {"achieved": round(ach, 1), "peak": peak, "unit": "G wave64-VALU-instr/s",
+                     "frac": round(ach / peak, 4), "instr_per_key": prof["valu_instr_per_key"],
+                     "note": "PMC SQ_INSTS_VALU per key (profiles/traffic_*.json); peak = "
+                             "1024 SIMDs x 2.4 GHz / 4 cycles (tools/ubench_valu.hip)"}
 
     allgather_ms = None
     if world > 1 and not args.allgather:
@@ -239,6 +250,8 @@ def main():
                      "alg_bytes_per_launch": alg_bytes},
         "cpu_baseline": base,
     }
+    if valu_roof is not None:
+        line["valu_roofline"] = valu_roof
     if allgather_ms is not None:
         line["allgather_ms"] = round(allgather_ms, 3)
         line["build_plus_allgather_mkeys_s"] = round(units / ((ms_per_step + allgather_ms) * 1e-3) / 1e6, 2)
@@ -300,12 +313,14 @@ def end_to_end(torch, amq, kind, bpk, cap, counts, keys, iters=3):
                     "pipelined on three streams (HostFilterPipeline)"}
 
 
-def load_traffic(workload):
+def load_profile(workload):
+    """profiles/traffic_<workload>.json, written by tools/pmc_summary.py from rocprofv3 --pmc
+    passes of this bench (HBM bytes per launch, VALU instructions per key)."""
     p = os.path.join(ROOT, "profiles", f"traffic_{workload}.json")
     if os.path.exists(p):
         with open(p) as f:
-            return json.load(f).get("hbm_bytes_per_launch")
-    return None
+            return json.load(f)
+    return {}
 
 
 if __name__ == "__main__":

@@ -1,0 +1,71 @@
+"""Summarise rocprofv3 --pmc passes for one kernel into profiles/traffic_<workload>.json
+(read by bench.py for roofline.traffic and valu_roofline).
+
+  python tools/pmc_summary.py --workload bloom10 --kernel bloom_build \
+      --fetch gpurun_out/pmc_fetch --write gpurun_out/pmc_write --sq gpurun_out/pmc_sq \
+      --keys 100000000 --alg-bytes 1725390848
+
+HBM bytes follow MI355X_MICROARCH.md (HBM section): FETCH_SIZE counts half of a 16 B/lane
+streaming read on gfx950, so hbm = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024.
+"""
+from __future__ import annotations
+
+import argparse
+import collections
+import csv
+import json
+import os
+
+# gfx950 integer VALU issue: one wave64 instruction per ~4 cycles per SIMD, measured by
+# tools/ubench_valu.hip (profiles/r01/ubench_valu.log)
+SIMDS = 1024
+CYCLES_PER_VALU = 4.0
+CLOCK_GHZ = 2.4
+
+
+def agg(d, kernel):
+    rows = list(csv.DictReader(open(os.path.join(d, "run_counter_collection.csv"))))
+    out = collections.defaultdict(list)
+    for r in rows:
+        if kernel in r["Kernel_Name"]:
+            out[r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in out.items()}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workload", required=True)
+    ap.add_argument("--kernel", required=True)
+    ap.add_argument("--fetch", required=True)
+    ap.add_argument("--write", required=True)
+    ap.add_argument("--sq", required=True)
+    ap.add_argument("--keys", type=int, required=True)
+    ap.add_argument("--alg-bytes", type=int, required=True)
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+    f, w, sq = agg(a.fetch, a.kernel), agg(a.write, a.kernel), agg(a.sq, a.kernel)
+    hbm = int(2 * f["FETCH_SIZE"] * 1024 + w["WRITE_SIZE"] * 1024)
+    clk_cycles = sq["GRBM_GUI_ACTIVE"] / 8
+    valu = sq["SQ_INSTS_VALU"]
+    res = {
+        "kernel": a.kernel, "workload": a.workload,
+        "FETCH_SIZE_KiB": f["FETCH_SIZE"], "WRITE_SIZE_KiB": w["WRITE_SIZE"],
+        "correction": "hbm_bytes = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 FETCH_SIZE "
+                      "counts half of 16B/lane streaming reads)",
+        "hbm_bytes_per_launch": hbm, "algorithmic_bytes_per_launch": a.alg_bytes,
+        "traffic_over_algorithmic": round(hbm / a.alg_bytes, 4),
+        "SQ_INSTS_VALU_per_launch": valu, "SQ_WAVES": sq.get("SQ_WAVES"),
+        "valu_instr_per_key": round(valu * 64 / a.keys, 1),
+        "GRBM_GUI_ACTIVE_per_xcd": clk_cycles,
+        "valu_cycles_per_wave_instr_per_simd": round(clk_cycles / (valu / SIMDS), 3),
+        "valu_peak_ginstr_s_at_2.4GHz": SIMDS * CLOCK_GHZ / CYCLES_PER_VALU,
+        "source": f"rocprofv3 --pmc passes: {a.fetch}, {a.write}, {a.sq}",
+    }
+    out = a.out or os.path.join("profiles", f"traffic_{a.workload}.json")
+    with open(out, "w") as fh:
+        json.dump(res, fh, indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()

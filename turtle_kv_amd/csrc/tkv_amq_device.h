@@ -126,9 +126,17 @@ __device__ inline uint32_t mul_u24(uint32_t konst, uint32_t x)
   return r;
 }
 
-// low 9 bits of davalanche(h) with the last multiply narrowed: bits 0..8 and 32..40 of
-// y * P3 only need hi32(y_lo * P3_lo) and the low 9 bits of the two cross products, which
-// 24-bit multiplies (full rate) give exactly.
+__device__ inline uint32_t mad_u24(uint32_t konst, uint32_t x, uint32_t addend)
+{
+  uint32_t r;
+  asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(r) : "s"(konst), "v"(x), "v"(addend));
+  return r;
+}
+
+// davalanche(h) with the last multiply narrowed; only bits 0..8 of the result are valid
+// (callers take `& 511` or a bitfield of them).  Bits 0..8 and 32..40 of y * P3 only need
+// hi32(y_lo * P3_lo) and the low 9 bits of the two cross products, which 24-bit
+// multiply-adds (full rate) give exactly.
 __device__ inline uint32_t davalanche_lo9(uint64_t h)
 {
   h ^= dshr<33>(h);
@@ -136,10 +144,8 @@ __device__ inline uint32_t davalanche_lo9(uint64_t h)
   h ^= dshr<29>(h);
   const uint32_t yl = lo32(h), yh = hi32(h);
   constexpr uint32_t cl = (uint32_t)kP3, ch = (uint32_t)(kP3 >> 32);
-  const uint32_t p_hi = __umulhi(yl, cl);
-  const uint32_t p_lo9 = mul_u24(cl, yl);
-  const uint32_t h3_hi = p_hi + mul_u24(ch, yl) + mul_u24(cl, yh);
-  return (p_lo9 ^ h3_hi) & 511u;
+  const uint32_t h3_hi = mad_u24(cl, yh, mad_u24(ch, yl, __umulhi(yl, cl)));
+  return mul_u24(cl, yl) ^ h3_hi;
 }
 
 // 16-byte key, seed-independent part precomputed once per key.  Rotation distributes over
@@ -156,7 +162,7 @@ struct Xxh16 {
     return drotl<27>(h) * kP1 + kP4;
   }
   __device__ inline uint64_t finish(uint64_t rhinit) const { return davalanche(pre(rhinit)); }
-  // low 9 bits only (Bloom bit index inside a 512-bit block)
+  // bits 0..8 only are valid (Bloom bit index inside a 512-bit block)
   __device__ inline uint32_t finish_lo9(uint64_t rhinit) const { return davalanche_lo9(pre(rhinit)); }
 };
 

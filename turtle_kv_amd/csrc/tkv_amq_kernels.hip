@@ -78,8 +78,12 @@ __device__ inline uint64_t hash_key(const uint8_t* keys, const uint64_t* offs, u
 // ---------------------------------------------------------------------------------------
 __device__ inline void lds_set_bit(uint32_t* blk, uint32_t bit)
 {
-  // word = bits 5..8 of the 9-bit index (v_bfe_u32); the shift uses bits 0..4 only
-  atomicOr(blk + __builtin_amdgcn_ubfe(bit, 5, 4), 1u << (bit & 31));
+  // `bit`: bits 0..8 are the index, higher bits are ignored.  word = bits 5..8 (v_bfe_u32
+  // in asm: LLVM would re-canonicalize the extract-then-scale into lshr + and + add); the
+  // shift amount uses bits 0..4 only.
+  uint32_t word;
+  asm("v_bfe_u32 %0, %1, 5, 4" : "=v"(word) : "v"(bit));
+  atomicOr(blk + word, 1u << (bit & 31));
 }
 
 __device__ inline void write_bloom_header(uint8_t* payload, const tkv_amq_segment& sg, int part)
@@ -229,7 +233,7 @@ __global__ __launch_bounds__(256) void bloom_global_set(const uint8_t* __restric
       const uint32_t b0 = (uint32_t)h0 & 511u;
       atomicOr(blk + (b0 >> 5), 1u << (b0 & 31));
       for (uint32_t j = 1; j < sg.hash_count; ++j) {
-        const uint32_t b = x.finish_lo9(c_bloom.rhinit16[j]);
+        const uint32_t b = x.finish_lo9(c_bloom.rhinit16[j]) & 511u;
         atomicOr(blk + (b >> 5), 1u << (b & 31));
       }
     } else {
@@ -305,12 +309,12 @@ __global__ __launch_bounds__(256) void bloom_probe(const uint8_t* __restrict__ f
       if (d.hash_count == 7) {
 #pragma unroll
         for (uint32_t j = 1; j < 7; ++j) {
-          bit = x.finish_lo9(c_bloom.rhinit16[j]);
+          bit = x.finish_lo9(c_bloom.rhinit16[j]) & 511u;
           ok &= slot32[bit >> 5] >> (bit & 31);
         }
       } else {
         for (uint32_t j = 1; j < d.hash_count; ++j) {
-          bit = x.finish_lo9(c_bloom.rhinit16[j]);
+          bit = x.finish_lo9(c_bloom.rhinit16[j]) & 511u;
           ok &= slot32[bit >> 5] >> (bit & 31);
         }
       }
