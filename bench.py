@@ -104,10 +104,11 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        dist.init_process_group("nccl")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    if world > 1:
+        # one process per GPU; the communicator is bound to this rank's device (RCCL/xGMI)
+        dist.init_process_group("nccl", device_id=dev)
     kind, bpk, cap, label = WORKLOADS[args.workload]
     n = args.keys_per_gpu
     counts = segment_counts(n)

@@ -19,6 +19,8 @@
  *   tkv_amq_vqf_hash        vqf_hash_val (vqf_filter_page_view.hpp:32-35), hash-once per query
  *                           (tree/key_query.hpp:82)
  *   tkv_amq_vqf_probe_hashed PackedVqfFilter::is_present(hash_val) for pre-hashed queries
+ *   tkv_amq_bloom_hash /    BloomFilterQuery<KeyView> hash cache (tree/key_query.hpp:78,97)
+ *   tkv_amq_bloom_probe_hashed   and PackedBloomFilter::query on it (:219)
  *   tkv_amq_vqf_*sizing     vqf_filter_load_factor<T> (vqf_filter_page_view.hpp:39-59),
  *                           vqf_required_size<T> / vqf_nslots_for_size (vqf 0.2.4, used at
  *                           tree/filter_builder.hpp:243-244,270,274)
@@ -136,10 +138,26 @@ int tkv_amq_probe(int kind, const uint8_t* d_filters, const tkv_amq_segment* d_s
 int tkv_amq_vqf_hash(const uint8_t* keys, const uint64_t* key_offsets, uint32_t key_stride,
                      uint64_t n_keys, uint64_t* d_hash, void* stream);
 
-/* PackedVqfFilter::is_present(hash_val) for pre-hashed queries (hash once, probe many) */
+/* PackedVqfFilter::is_present(hash_val) for pre-hashed queries (hash once, probe many).
+ * Pair i probes leaf d_pair_leaf[i] with hash d_hash[d_pair_query ? d_pair_query[i] : i]:
+ * one query's hash serves every filter on its root-to-leaf path (tree/algo/nodes.hpp:165-178). */
 int tkv_amq_vqf_probe_hashed(const uint8_t* d_filters, const tkv_amq_segment* d_segs,
-                             uint32_t n_segs, const uint64_t* d_hash, uint64_t n_queries,
-                             const uint32_t* d_query_seg, uint8_t* d_result, void* stream);
+                             uint32_t n_segs, const uint64_t* d_hash,
+                             const uint32_t* d_pair_query, uint64_t n_pairs,
+                             const uint32_t* d_pair_leaf, uint8_t* d_result, void* stream);
+
+/* BloomFilterQuery<KeyView> (tree/key_query.hpp:78,97,219): the hashes one query needs,
+ * computed once and reused for every Bloom filter it is tested against.  Record i lives at
+ * d_query + i * tkv_amq_bloom_query_stride(k_max): u64 h0 (block selector and bit 0), then
+ * u16 bit index of hash j for j = 1 .. k_max-1.  k_max <= 32; a filter whose hash_count
+ * exceeds k_max cannot reject (result 1). */
+uint32_t tkv_amq_bloom_query_stride(uint32_t k_max);
+int tkv_amq_bloom_hash(const uint8_t* keys, const uint64_t* key_offsets, uint32_t key_stride,
+                       uint64_t n_keys, uint32_t k_max, uint8_t* d_query, void* stream);
+int tkv_amq_bloom_probe_hashed(const uint8_t* d_filters, const tkv_amq_segment* d_segs,
+                               uint32_t n_segs, const uint8_t* d_query, uint32_t k_max,
+                               const uint32_t* d_pair_query, uint64_t n_pairs,
+                               const uint32_t* d_pair_leaf, uint8_t* d_result, void* stream);
 
 /* Synthetic 16-byte keys on the device: key i = (splitmix64_at(seed, 2(first+i)+1),
  * splitmix64_at(seed, 2(first+i)+2)), little-endian (the bench input). */

@@ -250,3 +250,34 @@ def test_reference_api_mirror(oracle, amq, torch):
     assert amq.build_filter_for_leaf_in_job(0, 1, kb) is None        # bpk 0: no filter
     bp = amq.build_bloom_filter_for_leaf(10, 9, kb)
     assert all(r == amq.BoolStatus.kFalse for r in q.reject_page(9, bp))
+
+
+@pytest.mark.parametrize("kind,bpk", [(0, 10), (0, 12), (0, 20), (1, 12)])
+def test_hash_once_probe_many(oracle, amq, torch, kind, bpk):
+    """Multi-get fan-out: each query is hashed once (vqf_hash_val / BloomFilterQuery) and
+    tested against several leaves' filters (one per level on its path).  Must equal probing
+    every (query, leaf) pair from the raw key."""
+    counts = [S] * 6 + [1234]
+    keys = sorted_keys(oracle, 42, counts) if kind else oracle.gen_keys16(42, 0, sum(counts))
+    plan = amq.plan_filters(kind, counts, bpk, payload_capacity=65472 if kind else 0)
+    filt = amq.build_all_filters(plan, amq.KeyBatch.fixed(torch.from_numpy(keys).cuda()))
+    nq, fan = 50000, 4
+    q = np.concatenate([keys[:nq // 2], oracle.gen_keys16(43, 0, nq - nq // 2)])
+    rng = np.random.default_rng(5)
+    pair_query = np.repeat(np.arange(nq), fan).astype(np.int32)
+    pair_leaf = rng.integers(0, len(counts), nq * fan).astype(np.int32)
+    dq = amq.KeyBatch.fixed(torch.from_numpy(q).cuda())
+    if kind == 0:
+        qh = amq.bloom_query_hashes(dq, 32)
+        got = amq.bloom_probe_hashed(plan, filt, qh, 32, torch.from_numpy(pair_leaf).cuda(),
+                                     pair_query=torch.from_numpy(pair_query).cuda())
+    else:
+        hv = amq.vqf_hash_val(dq)
+        got = amq.vqf_probe_hashed(plan, filt, hv, torch.from_numpy(pair_leaf).cuda(),
+                                   pair_query=torch.from_numpy(pair_query).cuda())
+    expand = amq.KeyBatch.fixed(torch.from_numpy(q[pair_query]).cuda())
+    want = amq.probe_filters(plan, filt, expand, torch.from_numpy(pair_leaf).cuda())
+    assert torch.equal(got, want)
+    st, ref = oracle.probe_segments(kind, filt.cpu().numpy(), plan.segs["out_offset"],
+                                    q[pair_query], pair_leaf.astype(np.uint32))
+    assert np.array_equal(got.cpu().numpy(), ref)

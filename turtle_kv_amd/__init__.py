@@ -6,6 +6,7 @@ from .abi import BLOOM, VQF, TkvAmqError
 from .filters import (BoolStatus, FilterPage, FilterPlan, KeyBatch, KeyQuery, PackedVqfFilter,
                       build_all_filters, build_bloom_filter_for_leaf, build_filter_for_leaf_in_job,
                       build_quotient_filter_for_leaf, filter_bits_per_key, gen_keys16,
+                      bloom_query_hashes, bloom_probe_hashed, HostFilterPipeline,
                       plan_filters, probe_filters, vqf_filter_load_factor, vqf_hash_val,
                       vqf_nslots_for_size, vqf_probe_hashed, vqf_required_size)
 
@@ -14,5 +15,6 @@ __all__ = [
     "KeyQuery", "PackedVqfFilter", "build_all_filters", "build_bloom_filter_for_leaf",
     "build_filter_for_leaf_in_job", "build_quotient_filter_for_leaf", "filter_bits_per_key",
     "gen_keys16", "plan_filters", "probe_filters", "vqf_filter_load_factor", "vqf_hash_val",
-    "vqf_nslots_for_size", "vqf_probe_hashed", "vqf_required_size",
+    "vqf_nslots_for_size", "vqf_probe_hashed", "vqf_required_size", "bloom_query_hashes",
+    "bloom_probe_hashed", "HostFilterPipeline",
 ]

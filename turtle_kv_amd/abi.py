@@ -68,6 +68,7 @@ EXPORTS = [
     "tkv_amq_filter_bits_per_key", "tkv_amq_vqf_load_factor", "tkv_amq_vqf_required_size",
     "tkv_amq_vqf_nslots_for_size", "tkv_amq_plan", "tkv_amq_build", "tkv_amq_build_check",
     "tkv_amq_probe", "tkv_amq_vqf_hash", "tkv_amq_vqf_probe_hashed", "tkv_amq_gen_keys16",
+    "tkv_amq_bloom_query_stride", "tkv_amq_bloom_hash", "tkv_amq_bloom_probe_hashed",
 ]
 
 _lib = None
@@ -112,7 +113,13 @@ def lib(build_if_missing: bool = True):
     L.tkv_amq_vqf_hash.restype = i32
     L.tkv_amq_vqf_hash.argtypes = [vp, vp, u32, u64, vp, vp]
     L.tkv_amq_vqf_probe_hashed.restype = i32
-    L.tkv_amq_vqf_probe_hashed.argtypes = [vp, vp, u32, vp, u64, vp, vp, vp]
+    L.tkv_amq_vqf_probe_hashed.argtypes = [vp, vp, u32, vp, vp, u64, vp, vp, vp]
+    L.tkv_amq_bloom_query_stride.restype = u32
+    L.tkv_amq_bloom_query_stride.argtypes = [u32]
+    L.tkv_amq_bloom_hash.restype = i32
+    L.tkv_amq_bloom_hash.argtypes = [vp, vp, u32, u64, u32, vp, vp]
+    L.tkv_amq_bloom_probe_hashed.restype = i32
+    L.tkv_amq_bloom_probe_hashed.argtypes = [vp, vp, u32, vp, u32, vp, u64, vp, vp, vp]
     L.tkv_amq_gen_keys16.restype = i32
     L.tkv_amq_gen_keys16.argtypes = [u64, u64, u64, vp, vp]
     _lib = L

@@ -791,12 +791,79 @@ __global__ __launch_bounds__(256) void vqf_probe(const uint8_t* __restrict__ fil
 __global__ __launch_bounds__(256) void vqf_probe_hashed(const uint8_t* __restrict__ filters,
                                                         const tkv_amq_segment* __restrict__ segs,
                                                         const uint64_t* __restrict__ hashes,
+                                                        const uint32_t* __restrict__ pair_query,
                                                         uint64_t n, const uint32_t* __restrict__ qseg,
                                                         uint8_t* __restrict__ result)
 {
   const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
-  result[i] = vqf_probe_one(filters, segs, qseg[i], hashes[i]);
+  const uint64_t qi = pair_query ? pair_query[i] : i;
+  result[i] = vqf_probe_one(filters, segs, qseg[i], hashes[qi]);
+}
+
+// ---- Bloom query hash cache (BloomFilterQuery<KeyView>) ----
+__host__ __device__ inline uint32_t bloom_query_stride(uint32_t k_max)
+{
+  return (8 + 2 * (k_max > 1 ? k_max - 1 : 0) + 15) & ~15u;
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256) void bloom_hash_kernel(const uint8_t* __restrict__ q,
+                                                         const uint64_t* __restrict__ qoffs,
+                                                         uint32_t stride, uint64_t n, uint32_t k_max,
+                                                         uint8_t* __restrict__ out)
+{
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  uint8_t* rec = out + i * bloom_query_stride(k_max);
+  uint16_t* bits = reinterpret_cast<uint16_t*>(rec + 8);
+  if constexpr (MODE == kKey16) {
+    const uint4 kv = load_nt16(q + 16 * i);
+    const Xxh16 x((uint64_t)kv.x | ((uint64_t)kv.y << 32), (uint64_t)kv.z | ((uint64_t)kv.w << 32));
+    *reinterpret_cast<uint64_t*>(rec) = x.finish(c_bloom.rhinit16[0]);
+    for (uint32_t j = 1; j < k_max; ++j) bits[j - 1] = (uint16_t)(x.finish_lo9(c_bloom.rhinit16[j]) & 511u);
+  } else {
+    *reinterpret_cast<uint64_t*>(rec) = hash_key<MODE>(q, qoffs, stride, i, c_bloom.seed[0]);
+    for (uint32_t j = 1; j < k_max; ++j)
+      bits[j - 1] = (uint16_t)(hash_key<MODE>(q, qoffs, stride, i, c_bloom.seed[j]) & 511u);
+  }
+}
+
+__global__ __launch_bounds__(256) void bloom_probe_hashed(const uint8_t* __restrict__ filters,
+                                                          const tkv_amq_segment* __restrict__ segs,
+                                                          const uint8_t* __restrict__ qrec,
+                                                          uint32_t k_max,
+                                                          const uint32_t* __restrict__ pair_query,
+                                                          uint64_t n, const uint32_t* __restrict__ qseg,
+                                                          uint8_t* __restrict__ result)
+{
+  __shared__ uint4 s_blk[256 * kProbeSlotWords / 4];
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const ProbeDesc d = load_probe_desc(segs, qseg[i]);
+  uint32_t ok = 1;
+  if (d.hash_count != 0 && d.hash_count <= k_max) {
+    const uint64_t qi = pair_query ? pair_query[i] : i;
+    const uint8_t* rec = qrec + qi * bloom_query_stride(k_max);
+    const uint64_t h0 = *reinterpret_cast<const uint64_t*>(rec);
+    const uint16_t* bits = reinterpret_cast<const uint16_t*>(rec + 8);
+    const uint4* blk = reinterpret_cast<const uint4*>(filters + d.out_offset + kBloomHeader +
+                                                      64 * __umul64hi(h0, (uint64_t)d.n_blocks));
+    uint4* slot = s_blk + threadIdx.x * (kProbeSlotWords / 4);
+    const uint32_t* slot32 = reinterpret_cast<const uint32_t*>(slot);
+    const uint4 b0 = blk[0], b1 = blk[1], b2 = blk[2], b3 = blk[3];
+    slot[0] = b0;
+    slot[1] = b1;
+    slot[2] = b2;
+    slot[3] = b3;
+    uint32_t bit = (uint32_t)h0 & 511u;
+    ok &= slot32[bit >> 5] >> (bit & 31);
+    for (uint32_t j = 1; j < d.hash_count; ++j) {
+      bit = bits[j - 1];
+      ok &= slot32[bit >> 5] >> (bit & 31);
+    }
+  }
+  result[i] = (uint8_t)(ok & 1u);
 }
 
 template <int MODE>
@@ -1135,15 +1202,53 @@ int tkv_amq_vqf_hash(const uint8_t* q, const uint64_t* qoffs, uint32_t stride, u
 }
 
 int tkv_amq_vqf_probe_hashed(const uint8_t* d_filters, const tkv_amq_segment* d_segs,
-                             uint32_t n_segs, const uint64_t* d_hash, uint64_t n,
-                             const uint32_t* d_qseg, uint8_t* d_result, void* stream)
+                             uint32_t n_segs, const uint64_t* d_hash, const uint32_t* d_pair_query,
+                             uint64_t n, const uint32_t* d_qseg, uint8_t* d_result, void* stream)
 {
   if (tkv_amq_device_count() == 0) return TKV_AMQ_UNAVAILABLE;
   if (n == 0) return TKV_AMQ_OK;
   if (!d_filters || !d_segs || !d_hash || !d_qseg || !d_result || n_segs == 0)
     return TKV_AMQ_INVALID_ARGUMENT;
   hipLaunchKernelGGL(vqf_probe_hashed, dim3((uint32_t)div_up(n, 256)), dim3(256), 0,
-                     as_stream(stream), d_filters, d_segs, d_hash, n, d_qseg, d_result);
+                     as_stream(stream), d_filters, d_segs, d_hash, d_pair_query, n, d_qseg, d_result);
+  return hipGetLastError() == hipSuccess ? TKV_AMQ_OK : TKV_AMQ_INTERNAL;
+}
+
+uint32_t tkv_amq_bloom_query_stride(uint32_t k_max) { return bloom_query_stride(k_max); }
+
+int tkv_amq_bloom_hash(const uint8_t* q, const uint64_t* qoffs, uint32_t stride, uint64_t n,
+                       uint32_t k_max, uint8_t* d_query, void* stream)
+{
+  if (tkv_amq_device_count() == 0) return TKV_AMQ_UNAVAILABLE;
+  if (n == 0) return TKV_AMQ_OK;
+  if (!q || !d_query || (!qoffs && !stride) || k_max == 0 || k_max > kMaxBloomHashes)
+    return TKV_AMQ_INVALID_ARGUMENT;
+  const hipStream_t s = as_stream(stream);
+  const int mode = key_mode(qoffs, stride);
+  if (mode == kKey16 && (reinterpret_cast<uintptr_t>(q) & 15)) return TKV_AMQ_INVALID_ARGUMENT;
+  const dim3 grid((uint32_t)div_up(n, 256)), block(256);
+  if (mode == kKey16)
+    hipLaunchKernelGGL(bloom_hash_kernel<kKey16>, grid, block, 0, s, q, qoffs, stride, n, k_max, d_query);
+  else if (mode == kKeyFixed)
+    hipLaunchKernelGGL(bloom_hash_kernel<kKeyFixed>, grid, block, 0, s, q, qoffs, stride, n, k_max, d_query);
+  else
+    hipLaunchKernelGGL(bloom_hash_kernel<kKeyVar>, grid, block, 0, s, q, qoffs, stride, n, k_max, d_query);
+  return hipGetLastError() == hipSuccess ? TKV_AMQ_OK : TKV_AMQ_INTERNAL;
+}
+
+int tkv_amq_bloom_probe_hashed(const uint8_t* d_filters, const tkv_amq_segment* d_segs,
+                               uint32_t n_segs, const uint8_t* d_query, uint32_t k_max,
+                               const uint32_t* d_pair_query, uint64_t n, const uint32_t* d_qseg,
+                               uint8_t* d_result, void* stream)
+{
+  if (tkv_amq_device_count() == 0) return TKV_AMQ_UNAVAILABLE;
+  if (n == 0) return TKV_AMQ_OK;
+  if (!d_filters || !d_segs || !d_query || !d_qseg || !d_result || n_segs == 0 || k_max == 0 ||
+      k_max > kMaxBloomHashes)
+    return TKV_AMQ_INVALID_ARGUMENT;
+  hipLaunchKernelGGL(bloom_probe_hashed, dim3((uint32_t)div_up(n, 256)), dim3(256), 0,
+                     as_stream(stream), d_filters, d_segs, d_query, k_max, d_pair_query, n, d_qseg,
+                     d_result);
   return hipGetLastError() == hipSuccess ? TKV_AMQ_OK : TKV_AMQ_INTERNAL;
 }
 

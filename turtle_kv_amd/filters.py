@@ -253,17 +253,53 @@ def vqf_hash_val(keys: KeyBatch, stream=None):
     return out
 
 
-def vqf_probe_hashed(plan: FilterPlan, filters, hash_vals, query_seg, out=None, stream=None):
+def vqf_probe_hashed(plan: FilterPlan, filters, hash_vals, query_seg, out=None, stream=None,
+                     pair_query=None):
+    """PackedVqfFilter::is_present for pre-hashed queries; pair i tests leaf query_seg[i]
+    with hash_vals[pair_query[i]] (identity when pair_query is None)."""
     torch = _torch()
     _require_device()
     dev = filters.device
+    n = query_seg.numel()
     if out is None:
-        out = torch.empty(hash_vals.numel(), dtype=torch.uint8, device=dev)
+        out = torch.empty(n, dtype=torch.uint8, device=dev)
     qs = query_seg.to(dtype=torch.int32)
+    pq = None if pair_query is None else pair_query.to(dtype=torch.int32)
     abi.check(abi.lib().tkv_amq_vqf_probe_hashed(_ptr(filters), _ptr(plan.device_segs(dev)),
-                                                 plan.n_segs, _ptr(hash_vals), hash_vals.numel(),
+                                                 plan.n_segs, _ptr(hash_vals), _ptr(pq), n,
                                                  _ptr(qs), _ptr(out), _stream_handle(stream)),
               "tkv_amq_vqf_probe_hashed")
+    return out
+
+
+def bloom_query_hashes(keys: KeyBatch, k_max: int, stream=None):
+    """BloomFilterQuery<KeyView> cache for a batch of queries (tree/key_query.hpp:78,97):
+    one record per query (h0 + k_max-1 bit indices), computed once."""
+    torch = _torch()
+    _require_device()
+    stride = int(abi.lib().tkv_amq_bloom_query_stride(k_max))
+    out = torch.empty(max(keys.n, 1) * stride, dtype=torch.uint8, device=keys.data.device)
+    abi.check(abi.lib().tkv_amq_bloom_hash(_ptr(keys.data), _ptr(keys.offsets), keys.stride, keys.n,
+                                           k_max, _ptr(out), _stream_handle(stream)),
+              "tkv_amq_bloom_hash")
+    return out
+
+
+def bloom_probe_hashed(plan: FilterPlan, filters, query_hashes, k_max: int, query_seg, out=None,
+                       stream=None, pair_query=None):
+    """PackedBloomFilter::query(BloomFilterQuery) for (query, leaf) pairs."""
+    torch = _torch()
+    _require_device()
+    dev = filters.device
+    n = query_seg.numel()
+    if out is None:
+        out = torch.empty(n, dtype=torch.uint8, device=dev)
+    qs = query_seg.to(dtype=torch.int32)
+    pq = None if pair_query is None else pair_query.to(dtype=torch.int32)
+    abi.check(abi.lib().tkv_amq_bloom_probe_hashed(_ptr(filters), _ptr(plan.device_segs(dev)),
+                                                   plan.n_segs, _ptr(query_hashes), k_max, _ptr(pq),
+                                                   n, _ptr(qs), _ptr(out), _stream_handle(stream)),
+              "tkv_amq_bloom_probe_hashed")
     return out
 
 
@@ -350,12 +386,16 @@ class PackedVqfFilter:
 
 
 class KeyQuery:
-    """KeyQuery (tree/key_query.hpp:33-253) for a batch of point-query keys: the VQF hash is
-    computed once (key_query.hpp:82) and reused for every filter probed."""
+    """KeyQuery (tree/key_query.hpp:33-253) for a batch of point-query keys.  The hashes are
+    computed once per query and reused for every filter probed: the VQF hash_val
+    (key_query.hpp:82) and the Bloom BloomFilterQuery cache (:78,97)."""
+
+    BLOOM_K_MAX = 32
 
     def __init__(self, keys: KeyBatch):
         self.keys = keys
         self.hash_val = vqf_hash_val(keys)
+        self.bloom_query = bloom_query_hashes(keys, self.BLOOM_K_MAX)
 
     def reject_page(self, page_id_to_reject: int, filter_page: FilterPage | None) -> list:
         """Per key: kTrue = filter says definitely absent; kFalse = maybe present;
@@ -374,7 +414,8 @@ class KeyQuery:
         if filter_page.kind == VQF:
             present = vqf_probe_hashed(filter_page.plan, filter_page.payload, self.hash_val, qs)
         else:
-            present = probe_filters(filter_page.plan, filter_page.payload, self.keys, qs)
+            present = bloom_probe_hashed(filter_page.plan, filter_page.payload, self.bloom_query,
+                                         self.BLOOM_K_MAX, qs)
         return [BoolStatus.kFalse if p else BoolStatus.kTrue for p in present.cpu().tolist()]
 
 
