@@ -230,14 +230,15 @@ __device__ inline uint64_t xxh64_bytes(const uint8_t* p, uint64_t len, uint64_t 
   return davalanche(h);
 }
 
-// x mod d for x < 2^64, d < 2^32, given m = floor((2^64 - 1) / d): q = umulhi(x, m) is at
-// most 2 below floor(x / d), so two branchless conditional subtracts finish the job.
-__device__ inline uint64_t mod_by_magic(uint64_t x, uint64_t d, uint64_t m)
+// x mod d for x < 2^64, d < 2^31, given m = floor((2^64 - 1) / d): q = umulhi(x, m) is at
+// most 2 below floor(x / d), so x - q*d < 3d < 2^32 and the whole fix-up runs in 32 bits
+// (min(r, r - d) subtracts d exactly when r >= d: otherwise r - d wraps above r).
+__device__ inline uint32_t mod_by_magic(uint64_t x, uint32_t d, uint64_t m)
 {
   const uint64_t q = __umul64hi(x, m);
-  uint64_t r = x - q * d;
-  r = r >= d ? r - d : r;
-  r = r >= d ? r - d : r;
+  uint32_t r = (uint32_t)x - (uint32_t)q * d;
+  r = min(r, r - d);
+  r = min(r, r - d);
   return r;
 }
 
