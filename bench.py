@@ -37,7 +37,9 @@ WORKLOADS = {
     "bloom12": (0, 12, 0, "Bloom @12 bits/key"),
     "vqf12": (1, 12, 32704, "VQF @12 bits/key (reference clamp of 10 -> 12)"),
     "probe10": (0, 10, 0, "Bloom @10 probe, 50% hits"),
+    "bloom10k24": (0, 10, 0, "Bloom @10 bits/key, 24-byte keys (TurtleKV default key size)"),
 }
+KEY_BYTES = {"bloom10k24": 24}
 
 
 def parse():
@@ -120,7 +122,13 @@ def main():
     stride = tdist.leaf_stride(kind, bpk, SEG_KEYS, cap)
     plan = tdist.plan_shard(kind, counts * world, bpk, shard, stride, payload_capacity=cap)
     assert shard.key_end - shard.key_begin == n
-    keys = amq.gen_keys16(42, shard.key_begin, n, device=dev)
+    key_bytes = KEY_BYTES.get(args.workload, 16)
+    if key_bytes == 16:
+        keys = amq.gen_keys16(42, shard.key_begin, n, device=dev)
+    else:
+        g = torch.Generator(device=dev)
+        g.manual_seed(42 + rank)
+        keys = torch.randint(0, 256, (n, key_bytes), dtype=torch.uint8, device=dev, generator=g)
     if kind == 1:
         # VQF inserts in leaf key order: sort each leaf's keys (memcmp order) on the device
         keys = sort_segments_device(torch, keys, counts)
@@ -184,7 +192,7 @@ def main():
     if probe:
         alg_bytes = q.shape[0] * (16 + 4 + 1)
     else:
-        alg_bytes = n * 16 + int(plan.segs["payload_bytes"].astype(np.int64).sum())
+        alg_bytes = n * key_bytes + int(plan.segs["payload_bytes"].astype(np.int64).sum())
     achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
     prof = load_profile(args.workload)
     traffic = prof.get("hbm_bytes_per_launch")
@@ -210,7 +218,7 @@ def main():
         allgather_ms = (time.perf_counter() - g0) / 3 * 1e3
 
     e2e = None
-    if rank == 0 and world == 1 and not args.no_e2e and not probe:
+    if rank == 0 and world == 1 and not args.no_e2e and not probe and key_bytes == 16:
         e2e = end_to_end(torch, amq, kind, bpk, cap, counts, keys)
 
     if world > 1:
@@ -221,7 +229,7 @@ def main():
 
     base = None
     if world == 1 and not args.no_cpu_baseline:
-        if probe:
+        if probe or key_bytes != 16:
             base = None
         else:
             base = cpu_baseline(kind, bpk, cap, keys.cpu().numpy(), counts, args.cpu_threads)

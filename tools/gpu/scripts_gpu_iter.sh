@@ -3,7 +3,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-R=$GRAFT_REPO_ROOT
+R=$GRAFT_REPO_ROOT; cd $R
 timeout -k 10 400 python -m pytest tests -x -q -m gpu > gpurun_out/gpu_tests.log 2>&1 || exit 2
 for w in ${WORKLOADS:-bloom10 vqf12 probe10}; do
   timeout -k 10 300 python bench.py --steps 10 --warmup 2 --workload $w --no-e2e --no-cpu-baseline > gpurun_out/bench_$w.log 2>&1 || exit 3

@@ -3,7 +3,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-R=$GRAFT_REPO_ROOT
+R=$GRAFT_REPO_ROOT; cd $R
 timeout -k 10 400 python -m pytest tests -x -q -m gpu > gpurun_out/gpu_tests.log 2>&1 || exit 2
 timeout -k 10 300 python bench.py --steps 20 --warmup 3 > gpurun_out/bench_bloom10.log 2>&1 || exit 3
 timeout -k 10 300 python bench.py --steps 10 --warmup 2 --workload vqf12 --no-e2e > gpurun_out/bench_vqf12.log 2>&1 || exit 4

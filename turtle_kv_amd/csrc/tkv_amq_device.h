@@ -166,6 +166,41 @@ struct Xxh16 {
   __device__ inline uint32_t finish_lo9(uint64_t rhinit) const { return davalanche_lo9(pre(rhinit)); }
 };
 
+// Fixed key length L (multiple of 8, 8 <= L < 32): the same split for any short key.  All L/8
+// lane rounds are seed-independent; the per-seed constant is rotl(seed + P5 + L, 27).
+// (TurtleKV's default key size hint is 24 bytes, tree/tree_options.hpp:58.)
+template <int L>
+struct XxhFixed {
+  static_assert(L % 8 == 0 && L >= 8 && L < 32, "short fixed-length keys only");
+  static constexpr int N = L / 8;
+  uint64_t rk0;
+  uint64_t k[N > 1 ? N - 1 : 1];
+  __device__ inline explicit XxhFixed(const uint64_t (&lanes)[N])
+  {
+    rk0 = drotl<27>(dround(0, lanes[0]));
+#pragma unroll
+    for (int i = 1; i < N; ++i) k[i - 1] = dround(0, lanes[i]);
+  }
+  __device__ inline uint64_t pre(uint64_t rc) const
+  {
+    uint64_t h = (rc ^ rk0) * kP1 + kP4;
+#pragma unroll
+    for (int i = 1; i < N; ++i) {
+      h ^= k[i - 1];
+      h = drotl<27>(h) * kP1 + kP4;
+    }
+    return h;
+  }
+  __device__ inline uint64_t finish(uint64_t rc) const { return davalanche(pre(rc)); }
+  __device__ inline uint32_t finish_lo9(uint64_t rc) const { return davalanche_lo9(pre(rc)); }
+};
+
+template <int L>
+__host__ __device__ constexpr inline uint64_t xxh_fixed_rc(uint64_t seed)
+{
+  return rotl64(seed + kP5 + L, 27);
+}
+
 // rotl(seed + P5 + 16, 27): the per-seed constant Xxh16 takes
 __host__ __device__ constexpr inline uint64_t xxh16_rhinit(uint64_t seed)
 {
@@ -174,6 +209,7 @@ __host__ __device__ constexpr inline uint64_t xxh16_rhinit(uint64_t seed)
 
 __device__ inline uint64_t ld64_unaligned(const uint8_t* p)
 {
+  if ((reinterpret_cast<uintptr_t>(p) & 7) == 0) return *reinterpret_cast<const uint64_t*>(p);
   uint64_t v = 0;
 #pragma unroll
   for (int i = 0; i < 8; ++i) v |= (uint64_t)p[i] << (8 * i);

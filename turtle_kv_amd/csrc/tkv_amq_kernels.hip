@@ -49,7 +49,9 @@ __constant__ BloomSeeds c_bloom = make_bloom_seeds();
 // ---------------------------------------------------------------------------------------
 // key access
 // ---------------------------------------------------------------------------------------
-enum KeyMode : int { kKey16 = 0, kKeyFixed = 1, kKeyVar = 2 };
+// kKey24: fixed 24-byte keys, 8-byte aligned (Bloom build fast path; other kernels hash them
+// through the generic fixed-stride path)
+enum KeyMode : int { kKey16 = 0, kKeyFixed = 1, kKeyVar = 2, kKey24 = 3 };
 
 typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
 
@@ -65,7 +67,7 @@ template <int MODE>
 __device__ inline uint64_t hash_key(const uint8_t* keys, const uint64_t* offs, uint32_t stride,
                                     uint64_t i, uint64_t seed)
 {
-  if constexpr (MODE == kKeyFixed) {
+  if constexpr (MODE == kKeyFixed || MODE == kKey24) {
     return xxh64_bytes(keys + i * stride, stride, seed);
   } else {
     const uint64_t b = offs[i];
@@ -139,6 +141,41 @@ __device__ inline void bloom_keys16_lds(const uint4* __restrict__ kp, uint32_t n
   }
 }
 
+template <int K, int L>
+__device__ inline void bloom_keysL_lds(const uint64_t* __restrict__ kp, uint32_t n, uint32_t nb,
+                                       uint32_t k, uint32_t* s_bits)
+{
+  constexpr int N = L / 8;
+  const uint32_t tid = threadIdx.x;
+  constexpr int U = 2;
+  for (uint32_t base = 0; base < n; base += 256 * U) {
+    uint64_t lanes[U][N];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t i = min(base + u * 256 + tid, n - 1);
+#pragma unroll
+      for (int w = 0; w < N; ++w) lanes[u][w] = kp[(uint64_t)i * N + w];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (base + u * 256 + tid < n) {
+        const XxhFixed<L> x(lanes[u]);
+        const uint64_t h0 = x.finish(xxh_fixed_rc<L>(c_bloom.seed[0]));
+        uint32_t* blk = s_bits + 16 * (uint32_t)__umul64hi(h0, (uint64_t)nb);
+        lds_set_bit(blk, (uint32_t)h0 & 511u);
+        if constexpr (K != 0) {
+#pragma unroll
+          for (uint32_t j = 1; j < (uint32_t)K; ++j)
+            lds_set_bit(blk, x.finish_lo9(xxh_fixed_rc<L>(c_bloom.seed[j])));
+        } else {
+          for (uint32_t j = 1; j < k; ++j)
+            lds_set_bit(blk, x.finish_lo9(xxh_fixed_rc<L>(c_bloom.seed[j])));
+        }
+      }
+    }
+  }
+}
+
 template <int MODE>
 __global__ __launch_bounds__(256) void bloom_build_lds(const uint8_t* __restrict__ keys,
                                                        const uint64_t* __restrict__ offs,
@@ -162,6 +199,13 @@ __global__ __launch_bounds__(256) void bloom_build_lds(const uint8_t* __restrict
     if (k == 7) bloom_keys16_lds<7>(kp, n, nb, k, s_bits);
     else if (k == 8) bloom_keys16_lds<8>(kp, n, nb, k, s_bits);
     else bloom_keys16_lds<0>(kp, n, nb, k, s_bits);
+  } else if constexpr (MODE == kKey24) {
+    const uint64_t* kp = reinterpret_cast<const uint64_t*>(keys) + 3 * sg.key_begin;
+    if (n != 0) {
+      if (k == 7) bloom_keysL_lds<7, 24>(kp, n, nb, k, s_bits);
+      else if (k == 8) bloom_keysL_lds<8, 24>(kp, n, nb, k, s_bits);
+      else bloom_keysL_lds<0, 24>(kp, n, nb, k, s_bits);
+    }
   } else {
     for (uint32_t i = tid; i < n; i += 256) {
       const uint64_t gi = sg.key_begin + i;
@@ -922,6 +966,13 @@ inline int key_mode(const uint64_t* offs, uint32_t stride)
   return stride == 16 ? kKey16 : kKeyFixed;
 }
 
+// the Bloom build additionally has a 24-byte fast path (needs 8-byte aligned keys)
+inline int build_key_mode(const uint8_t* keys, const uint64_t* offs, uint32_t stride)
+{
+  if (!offs && stride == 24 && (reinterpret_cast<uintptr_t>(keys) & 7) == 0) return kKey24;
+  return key_mode(offs, stride);
+}
+
 inline hipStream_t as_stream(void* s) { return static_cast<hipStream_t>(s); }
 
 inline uint64_t div_up(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
@@ -1085,7 +1136,11 @@ int tkv_amq_build(int kind, const uint8_t* keys, const uint64_t* offs, uint32_t 
     if (max_blocks == 0) return TKV_AMQ_OK;
     if (lds <= kBloomLdsBudget) {
       const dim3 grid(n_segs), block(256);
-      if (mode == kKey16)
+      const int bmode = build_key_mode(keys, offs, stride);
+      if (bmode == kKey24)
+        hipLaunchKernelGGL(bloom_build_lds<kKey24>, grid, block, lds, s, keys, offs, stride, d_segs,
+                           d_out);
+      else if (mode == kKey16)
         hipLaunchKernelGGL(bloom_build_lds<kKey16>, grid, block, lds, s, keys, offs, stride, d_segs,
                            d_out);
       else if (mode == kKeyFixed)
