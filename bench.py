@@ -1,7 +1,8 @@
 """Filter-build benchmark (BASELINE.json metric: filter-build Mkeys/s, device-resident,
 16-byte keys @ 10 bits/key, bit-exact).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload bloom10|bloom12|vqf12|probe10]
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+                  [--workload bloom10|bloom12|vqf12|probe10|probe_vqf12|bloom10k24] [--total-keys T]
 
 One step = one pass of the hot path over one batch: build every leaf filter of
 `--keys-per-gpu` (default 100M, BASELINE config 2) 16-byte keys held in HBM, S = 16,384 keys
@@ -37,6 +38,7 @@ WORKLOADS = {
     "bloom12": (0, 12, 0, "Bloom @12 bits/key"),
     "vqf12": (1, 12, 32704, "VQF @12 bits/key (reference clamp of 10 -> 12)"),
     "probe10": (0, 10, 0, "Bloom @10 probe, 50% hits"),
+    "probe_vqf12": (1, 12, 32704, "VQF @12 probe, 50% hits"),
     "bloom10k24": (0, 10, 0, "Bloom @10 bits/key, 24-byte keys (TurtleKV default key size)"),
 }
 KEY_BYTES = {"bloom10k24": 24}
@@ -49,7 +51,15 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="bloom10", choices=sorted(WORKLOADS))
     ap.add_argument("--keys-per-gpu", type=int, default=100_000_000)
+    ap.add_argument("--total-keys", type=int, default=None,
+                    help="strong scaling: one checkpoint of this many keys split over the "
+                         "ranks by leaf range (BASELINE config 5: --workload bloom12 "
+                         "--total-keys 1000000000)")
     ap.add_argument("--allgather", action="store_true", help="time the RCCL all-gather in-step")
+    ap.add_argument("--ramp-ms", type=float, default=500.0,
+                    help="untimed clock ramp before the warmup steps: repeat the step for at "
+                         "least this long (the GPU needs ~0.1-0.3 s of load to reach its "
+                         "steady clock; 0 disables)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
@@ -112,16 +122,22 @@ def main():
         # one process per GPU; the communicator is bound to this rank's device (RCCL/xGMI)
         dist.init_process_group("nccl", device_id=dev)
     kind, bpk, cap, label = WORKLOADS[args.workload]
-    n = args.keys_per_gpu
-    counts = segment_counts(n)
-    # weak scaling: the checkpoint has `world` x (this GPU's leaves); rank r builds the
-    # contiguous leaf range turtle_kv_amd.dist.shard_leaves gives it, at a fixed per-leaf
-    # stride so leaf s sits at s * stride in the all-gathered array
     from turtle_kv_amd import dist as tdist
-    shard = tdist.shard_leaves(counts * world, world, rank)
+    strong = args.total_keys is not None
+    if strong:
+        # strong scaling: one checkpoint of --total-keys keys; rank r builds its leaf range
+        all_counts = segment_counts(args.total_keys)
+    else:
+        # weak scaling: the checkpoint has `world` x (this GPU's leaves)
+        all_counts = segment_counts(args.keys_per_gpu) * world
+    # rank r builds the contiguous leaf range turtle_kv_amd.dist.shard_leaves gives it, at a
+    # fixed per-leaf stride so leaf s sits at s * stride in the all-gathered array
+    shard = tdist.shard_leaves(all_counts, world, rank)
     stride = tdist.leaf_stride(kind, bpk, SEG_KEYS, cap)
-    plan = tdist.plan_shard(kind, counts * world, bpk, shard, stride, payload_capacity=cap)
-    assert shard.key_end - shard.key_begin == n
+    plan = tdist.plan_shard(kind, all_counts, bpk, shard, stride, payload_capacity=cap)
+    counts = all_counts[shard.leaf_begin:shard.leaf_end]
+    n = shard.key_end - shard.key_begin
+    total_keys = sum(all_counts)
     key_bytes = KEY_BYTES.get(args.workload, 16)
     if key_bytes == 16:
         keys = amq.gen_keys16(42, shard.key_begin, n, device=dev)
@@ -141,7 +157,7 @@ def main():
     probe = args.workload.startswith("probe")
     if probe:
         amq.build_all_filters(plan, kb, out=out, workspace=ws)
-        q, qseg = make_probe_queries(torch, amq, n, counts, dev, rank)
+        q, qseg = make_probe_queries(torch, amq, n, counts, dev, shard.key_begin)
         qb = amq.KeyBatch.fixed(q)
         res = torch.empty(q.shape[0], dtype=torch.uint8, device=dev)
 
@@ -155,6 +171,14 @@ def main():
         if args.allgather and world > 1:
             tdist.allgather_filters(out, gathered)
 
+    # clock ramp (untimed): a 1 ms step from an idle GPU runs ~15% below the steady clock
+    ramp0 = time.perf_counter()
+    n_ramp = 0
+    while (time.perf_counter() - ramp0) * 1e3 < args.ramp_ms:
+        for _ in range(8):
+            step()
+        n_ramp += 8
+        torch.cuda.synchronize()
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -183,14 +207,21 @@ def main():
         wall = float(t.item())
     kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
 
-    units = (q.shape[0] if probe else n) * world
+    units = 2 * total_keys if probe else total_keys
     ms_per_step = wall / args.steps * 1e3
     value = units * args.steps / wall / 1e6
 
     # algorithmic bytes per launch: build = 16 B/key in + filter payload out;
     # probe = 16 B key + 4 B leaf id + 1 B result per lookup
+    fpr = None
     if probe:
         alg_bytes = q.shape[0] * (16 + 4 + 1)
+        r2 = res.view(-1, 2)
+        if not bool(r2[:, 0].all()):
+            bad = torch.nonzero(r2[:, 0] == 0).flatten()
+            raise SystemExit(f"false negatives in the probe: {bad.numel()} of {r2.shape[0]} hits, "
+                             f"first key indices {bad[:8].tolist()}")
+        fpr = float(r2[:, 1].float().mean())
     else:
         alg_bytes = n * key_bytes + int(plan.segs["payload_bytes"].astype(np.int64).sum())
     achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
@@ -218,7 +249,8 @@ def main():
         allgather_ms = (time.perf_counter() - g0) / 3 * 1e3
 
     e2e = None
-    if rank == 0 and world == 1 and not args.no_e2e and not probe and key_bytes == 16:
+    if (rank == 0 and world == 1 and not args.no_e2e and not probe and key_bytes == 16
+            and n <= 200_000_000):
         e2e = end_to_end(torch, amq, kind, bpk, cap, counts, keys)
 
     if world > 1:
@@ -232,7 +264,11 @@ def main():
         if probe or key_bytes != 16:
             base = None
         else:
-            base = cpu_baseline(kind, bpk, cap, keys.cpu().numpy(), counts, args.cpu_threads)
+            # the CPU sample is bounded (~10 s); copy at most the first 100M keys to the host
+            nk_host = sum(counts[:100_000_000 // SEG_KEYS]) if n > 100_000_000 else n
+            base = cpu_baseline(kind, bpk, cap, keys[:nk_host].cpu().numpy(),
+                                counts[:100_000_000 // SEG_KEYS] if n > 100_000_000 else counts,
+                                args.cpu_threads)
 
     line = {
         "metric": f"filter-build Mkeys/s (device-resident), 16B keys @10 bits/key; bit-exact"
@@ -242,15 +278,17 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
+        "ramp_steps": n_ramp,
         "ms_per_step": round(ms_per_step, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
         "dtype": "u64",
         "data": "synthetic (splitmix64 seed 42 keys generated on the device)",
-        "config": {"workload": f"{label}: {n} x 16B keys per GPU, {SEG_KEYS}-key leaves "
-                               f"({len(counts)} filters per GPU)",
-                   "keys_per_gpu": n, "leaf_keys": SEG_KEYS, "bits_per_key": bpk,
+        "config": {"workload": (f"{label}: {total_keys} x {key_bytes}B keys over {world} GPU(s)"
+                                if strong else f"{label}: {n} x {key_bytes}B keys per GPU")
+                               + f", {SEG_KEYS}-key leaves ({len(counts)} filters on rank 0)",
+                   "keys_per_gpu": n, "total_keys": total_keys, "key_bytes": key_bytes, "leaf_keys": SEG_KEYS, "bits_per_key": bpk,
                    "filter": "bloom-blocked512" if kind == 0 else "vqf",
                    "parallelism": f"leaf-sharded x{world}"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
@@ -266,16 +304,41 @@ def main():
         line["build_plus_allgather_mkeys_s"] = round(units / ((ms_per_step + allgather_ms) * 1e-3) / 1e6, 2)
     if e2e is not None:
         line["e2e_pcie_inclusive"] = e2e
+    if fpr is not None:
+        line["probe"] = {"lookups": int(q.shape[0]), "hits_all_true": True,
+                         "false_positive_rate": round(fpr, 6)}
     print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
 
-def sort_segments_device(torch, keys, counts):
+def sort_segments_device(torch, keys, counts, chunk_keys=1 << 23):
     """memcmp order within each leaf: lexicographic on the big-endian view of the two
-    8-byte words, via two stable sorts (low word, then high word) and a stable leaf sort."""
+    8-byte words, via two stable sorts (low word, then high word) and a stable leaf sort.
+    Runs over groups of whole leaves of at most `chunk_keys` keys: the same torch sequence
+    applied to all 100M keys at once returned rows that were not a permutation of the input
+    past leaf ~2007 on this ROCm build (argsort and repeat_interleave alone check out at
+    100M, tools/gpu/diag_torch_sort.py; the failing op was not isolated).  Chunked, the
+    result equals the oracle's sort at full size (tests/test_gpu_scale.py)."""
+    out = torch.empty_like(keys)
+    b = 0
+    i = 0
+    while i < len(counts):
+        j, nk = i, 0
+        while j < len(counts) and (nk == 0 or nk + counts[j] <= chunk_keys):
+            nk += counts[j]
+            j += 1
+        out[b:b + nk] = _sort_leaves(torch, keys[b:b + nk], counts[i:j])
+        b += nk
+        i = j
+    return out
+
+
+def _sort_leaves(torch, keys, counts):
     n = keys.shape[0]
-    w = keys.view(torch.int64).reshape(n, 2)
+    if n == 0:
+        return keys
+    w = keys.reshape(n, 16).view(torch.int64).reshape(n, 2)
     def be(x):  # byte-swap to big-endian order, map unsigned -> signed order
         b = x.view(torch.uint8).reshape(-1, 8).flip(1).contiguous().view(torch.int64).reshape(-1)
         return b ^ torch.iinfo(torch.int64).min
@@ -285,14 +348,14 @@ def sort_segments_device(torch, keys, counts):
     idx = torch.argsort(lo, stable=True)
     idx = idx[torch.argsort(hi[idx], stable=True)]
     idx = idx[torch.argsort(seg[idx], stable=True)]
-    return keys[idx].contiguous()
+    return keys[idx]
 
 
-def make_probe_queries(torch, amq, n, counts, dev, rank):
+def make_probe_queries(torch, amq, n, counts, dev, key_begin):
     """BASELINE config 4: n hits (the inserted keys, each probing its own leaf) + n misses
     (seed 43 keys, probing a seed-44 random leaf), interleaved."""
-    hits = amq.gen_keys16(42, rank * n, n, device=dev)
-    miss = amq.gen_keys16(43, rank * n, n, device=dev)
+    hits = amq.gen_keys16(42, key_begin, n, device=dev)
+    miss = amq.gen_keys16(43, key_begin, n, device=dev)
     q = torch.stack([hits, miss], dim=1).reshape(2 * n, 16).contiguous()
     seg_hit = torch.repeat_interleave(torch.arange(len(counts), device=dev, dtype=torch.int32),
                                       torch.tensor(counts, device=dev))

@@ -320,6 +320,41 @@ __device__ inline ProbeDesc load_probe_desc(const tkv_amq_segment* segs, uint32_
 // are then LDS reads.  Stride 20 dwords keeps the slots 16-byte aligned and spreads banks.
 constexpr uint32_t kProbeSlotWords = 20;
 
+// The block's four 16-byte loads are issued first and the remaining k-1 bit indices are
+// hashed while they are in flight; only then is the block staged in the lane's LDS slot.
+template <int K>
+__device__ inline uint32_t probe_block16(const Xxh16& x, uint64_t h0, const uint4* blk, uint4* slot,
+                                         uint32_t k_rt = K)
+{
+  const uint4 b0 = blk[0], b1 = blk[1], b2 = blk[2], b3 = blk[3];
+  const uint32_t* slot32 = reinterpret_cast<const uint32_t*>(slot);
+  uint32_t ok = 1;
+  if constexpr (K > 0) {
+    uint32_t bit[K];
+    bit[0] = (uint32_t)h0 & 511u;
+#pragma unroll
+    for (int j = 1; j < K; ++j) bit[j] = x.finish_lo9(c_bloom.rhinit16[j]) & 511u;
+    slot[0] = b0;
+    slot[1] = b1;
+    slot[2] = b2;
+    slot[3] = b3;
+#pragma unroll
+    for (int j = 0; j < K; ++j) ok &= slot32[bit[j] >> 5] >> (bit[j] & 31);
+  } else {
+    slot[0] = b0;
+    slot[1] = b1;
+    slot[2] = b2;
+    slot[3] = b3;
+    uint32_t b = (uint32_t)h0 & 511u;
+    ok &= slot32[b >> 5] >> (b & 31);
+    for (uint32_t j = 1; j < k_rt; ++j) {
+      b = x.finish_lo9(c_bloom.rhinit16[j]) & 511u;
+      ok &= slot32[b >> 5] >> (b & 31);
+    }
+  }
+  return ok;
+}
+
 template <int MODE>
 __global__ __launch_bounds__(256) void bloom_probe(const uint8_t* __restrict__ filters,
                                                    const tkv_amq_segment* __restrict__ segs,
@@ -332,37 +367,26 @@ __global__ __launch_bounds__(256) void bloom_probe(const uint8_t* __restrict__ f
   __shared__ uint4 s_blk[256 * kProbeSlotWords / 4];
   const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
-  const ProbeDesc d = load_probe_desc(segs, __builtin_nontemporal_load(qseg + i));
+  const uint32_t sidx = __builtin_nontemporal_load(qseg + i);
   uint32_t ok = 1;
-  if (d.hash_count != 0) {  // 0: no filter page => reject_page returns kUnknown => cannot reject
-    const uint8_t* words = filters + d.out_offset + kBloomHeader;
+  if constexpr (MODE == kKey16) {
+    // the key load, the descriptor and the first hash do not depend on the "has a filter"
+    // test, so they are issued before it: one dependent chain qseg -> descriptor -> block
+    const uint4 kv = load_nt16(q + 16 * i);
+    const ProbeDesc d = load_probe_desc(segs, sidx);
+    const Xxh16 x((uint64_t)kv.x | ((uint64_t)kv.y << 32), (uint64_t)kv.z | ((uint64_t)kv.w << 32));
+    const uint64_t h0 = x.finish(c_bloom.rhinit16[0]);
+    const uint4* blk = reinterpret_cast<const uint4*>(filters + d.out_offset + kBloomHeader +
+                                                      64 * __umul64hi(h0, (uint64_t)d.n_blocks));
     uint4* slot = s_blk + threadIdx.x * (kProbeSlotWords / 4);
-    const uint32_t* slot32 = reinterpret_cast<const uint32_t*>(slot);
-    if constexpr (MODE == kKey16) {
-      const uint4 kv = load_nt16(q + 16 * i);
-      const Xxh16 x((uint64_t)kv.x | ((uint64_t)kv.y << 32), (uint64_t)kv.z | ((uint64_t)kv.w << 32));
-      const uint64_t h0 = x.finish(c_bloom.rhinit16[0]);
-      const uint4* blk = reinterpret_cast<const uint4*>(words + 64 * __umul64hi(h0, (uint64_t)d.n_blocks));
-      const uint4 b0 = blk[0], b1 = blk[1], b2 = blk[2], b3 = blk[3];
-      slot[0] = b0;
-      slot[1] = b1;
-      slot[2] = b2;
-      slot[3] = b3;
-      uint32_t bit = (uint32_t)h0 & 511u;
-      ok &= slot32[bit >> 5] >> (bit & 31);
-      if (d.hash_count == 7) {
-#pragma unroll
-        for (uint32_t j = 1; j < 7; ++j) {
-          bit = x.finish_lo9(c_bloom.rhinit16[j]) & 511u;
-          ok &= slot32[bit >> 5] >> (bit & 31);
-        }
-      } else {
-        for (uint32_t j = 1; j < d.hash_count; ++j) {
-          bit = x.finish_lo9(c_bloom.rhinit16[j]) & 511u;
-          ok &= slot32[bit >> 5] >> (bit & 31);
-        }
-      }
-    } else {
+    // hash_count 0: no filter page => reject_page returns kUnknown => cannot reject
+    if (d.hash_count == 7) ok = probe_block16<7>(x, h0, blk, slot);
+    else if (d.hash_count == 8) ok = probe_block16<8>(x, h0, blk, slot);
+    else if (d.hash_count != 0) ok = probe_block16<0>(x, h0, blk, slot, d.hash_count);
+  } else {
+    const ProbeDesc d = load_probe_desc(segs, sidx);
+    if (d.hash_count != 0) {
+      const uint8_t* words = filters + d.out_offset + kBloomHeader;
       const uint64_t h0 = hash_key<MODE>(q, qoffs, stride, i, c_bloom.seed[0]);
       const uint64_t* blk = reinterpret_cast<const uint64_t*>(words + 64 * __umul64hi(h0, (uint64_t)d.n_blocks));
       uint32_t b = (uint32_t)h0 & 511u;
@@ -760,28 +784,46 @@ __global__ __launch_bounds__(kPlaceThreads) void vqf_place(const tkv_amq_segment
 // VQF probe (PackedVqfFilter::is_present, vqf_filter_page_view.hpp:113-125)
 // ---------------------------------------------------------------------------------------
 template <int T>
-__device__ inline bool vqf_bucket_has(const uint8_t* blocks, uint32_t idx, uint32_t tag)
+struct VqfBucketRef {
+  const uint8_t* bp;  // the 64-byte block
+  uint32_t o;         // bucket offset inside it
+  uint64_t lo, hi;    // block metadata
+};
+
+template <int T>
+__device__ inline VqfBucketRef<T> vqf_bucket_ref(const uint8_t* blocks, uint32_t idx)
 {
   using C = Vqf<T>;
-  const uint32_t blk = idx / C::kBuckets, o = idx - blk * C::kBuckets;
-  const uint8_t* bp = blocks + (uint64_t)blk * 64;
-  uint64_t lo, hi = 0;
+  VqfBucketRef<T> r;
+  const uint32_t blk = idx / C::kBuckets;
+  r.o = idx - blk * C::kBuckets;
+  r.bp = blocks + (uint64_t)blk * 64;
   if constexpr (T == 8) {
-    const ulonglong2 md = *reinterpret_cast<const ulonglong2*>(bp);
-    lo = md.x;
-    hi = md.y;
+    const ulonglong2 md = *reinterpret_cast<const ulonglong2*>(r.bp);
+    r.lo = md.x;
+    r.hi = md.y;
   } else {
-    lo = *reinterpret_cast<const uint64_t*>(bp);
+    r.lo = *reinterpret_cast<const uint64_t*>(r.bp);
+    r.hi = 0;
   }
-  const int start = o == 0 ? 0 : select128(lo, hi, (int)o - 1) - ((int)o - 1);
-  const int end = select128(lo, hi, (int)o) - (int)o;
+  return r;
+}
+
+template <int T>
+__device__ inline bool vqf_bucket_has(const VqfBucketRef<T>& r, uint32_t tag)
+{
+  using C = Vqf<T>;
+  const int o = (int)r.o;
+  const int start = o == 0 ? 0 : select128(r.lo, r.hi, o - 1) - (o - 1);
+  const int end = select128(r.lo, r.hi, o) - o;
+  bool hit = false;
   for (int p = start; p < end; ++p) {
     uint32_t tv;
-    if constexpr (T == 8) tv = bp[C::kMdBytes + p];
-    else tv = *reinterpret_cast<const uint16_t*>(bp + C::kMdBytes + 2 * p);
-    if (tv == tag) return true;
+    if constexpr (T == 8) tv = r.bp[C::kMdBytes + p];
+    else tv = *reinterpret_cast<const uint16_t*>(r.bp + C::kMdBytes + 2 * p);
+    hit |= tv == tag;
   }
-  return false;
+  return hit;
 }
 
 template <int T>
@@ -794,7 +836,11 @@ __device__ inline bool vqf_present(const uint8_t* payload, uint32_t n_blocks, ui
   const uint32_t pi = (uint32_t)mod_by_magic(h >> T, R, magic);
   const uint32_t ai = (uint32_t)mod_by_magic((h ^ ((uint64_t)tag * kVqfAltMul)) >> T, R, magic);
   const uint8_t* blocks = payload + kVqfHeader + kVqfMetadata;
-  return vqf_bucket_has<T>(blocks, pi, tag) || vqf_bucket_has<T>(blocks, ai, tag);
+  // both blocks' metadata loads are issued before either bucket is scanned (the reference's
+  // primary-then-alternate order only matters for the answer, which is an OR)
+  const VqfBucketRef<T> rp = vqf_bucket_ref<T>(blocks, pi);
+  const VqfBucketRef<T> ra = vqf_bucket_ref<T>(blocks, ai);
+  return vqf_bucket_has<T>(rp, tag) | vqf_bucket_has<T>(ra, tag);
 }
 
 __device__ inline uint8_t vqf_probe_one(const uint8_t* filters, const tkv_amq_segment* segs,
@@ -884,12 +930,15 @@ __global__ __launch_bounds__(256) void bloom_probe_hashed(const uint8_t* __restr
   __shared__ uint4 s_blk[256 * kProbeSlotWords / 4];
   const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
-  const ProbeDesc d = load_probe_desc(segs, qseg[i]);
+  // qseg[i] and pair_query[i], then the descriptor and the query record, are independent
+  // loads issued side by side; only the block load waits for both
+  const uint32_t sidx = qseg[i];
+  const uint64_t qi = pair_query ? pair_query[i] : i;
+  const uint8_t* rec = qrec + qi * bloom_query_stride(k_max);
+  const ProbeDesc d = load_probe_desc(segs, sidx);
+  const uint64_t h0 = *reinterpret_cast<const uint64_t*>(rec);
   uint32_t ok = 1;
   if (d.hash_count != 0 && d.hash_count <= k_max) {
-    const uint64_t qi = pair_query ? pair_query[i] : i;
-    const uint8_t* rec = qrec + qi * bloom_query_stride(k_max);
-    const uint64_t h0 = *reinterpret_cast<const uint64_t*>(rec);
     const uint16_t* bits = reinterpret_cast<const uint16_t*>(rec + 8);
     const uint4* blk = reinterpret_cast<const uint4*>(filters + d.out_offset + kBloomHeader +
                                                       64 * __umul64hi(h0, (uint64_t)d.n_blocks));
