@@ -575,24 +575,46 @@ __device__ void vqf_decide_body(const uint8_t* __restrict__ keys, const uint64_t
     uint32_t cp = L.kept ? cnt_p + __popcll(Mpp & lt) : 0u;
     uint32_t ca = L.kept ? cnt_a + __popcll(Mpa & lt) : 0u;
     const uint32_t pb = L.pb, ab = L.ab;
-    // rounds: the first lane (in insertion order) whose exact decision is "alternate"
-    const uint64_t cand = __ballot(L.kept && pb != ab);  // blocks differ (vqf_insert alt test)
-    uint64_t live = cand, altmask = 0;
-    for (;;) {
-      const uint64_t A = __ballot((cp >= C::kThreshold) & (ca < cp)) & live;
-      if (A == 0) break;
-      const uint32_t k = (uint32_t)__ffsll((long long)A) - 1;
-      altmask |= 1ull << k;
-      const uint32_t pk = __builtin_amdgcn_readlane(pb, k);
-      const uint32_t ak = __builtin_amdgcn_readlane(ab, k);
-      // the move only affects lanes after k; written as lane-predicates so that each update
-      // is one v_addc / v_subbrev with an SGPR carry mask
-      const bool later = lane > k;
-      cp += (later && pb == ak) ? 1u : 0u;
-      cp -= (later && pb == pk) ? 1u : 0u;
-      ca += (later && ab == ak) ? 1u : 0u;
-      ca -= (later && ab == pk) ? 1u : 0u;
-      live &= ~((2ull << k) - 1);
+    // Decisions in insertion order, resolved in rounds.  Lane k's choice depends only on the
+    // counts of its two blocks, which an earlier lane j changes only by moving (pb_j -> ab_j)
+    // and only if {pb_j, ab_j} meets {pb_k, ab_k}.  So every undecided lane with no undecided
+    // earlier lane sharing a block is final now: all of them decide in one round and the
+    // movers' effects are applied to later lanes with four masked popcounts.
+    uint64_t U = __ballot(L.kept && pb != ab);  // blocks differ (vqf_insert alt test)
+    uint64_t altmask = 0;
+    uint64_t F = __ballot((cp >= C::kThreshold) & (ca < cp)) & U;
+    if (F != 0) {
+      // lanes whose alternate block is my primary / my alternate
+      uint32_t map_lo = (uint32_t)keptmask, map_hi = (uint32_t)(keptmask >> 32);
+      uint32_t maa_lo = map_lo, maa_hi = map_hi;
+#pragma unroll
+      for (int j = 0; j < NBITS; ++j) {
+        const uint32_t xp = (uint32_t)__builtin_amdgcn_sbfe((int32_t)pb, j, 1);
+        const uint32_t xa = (uint32_t)__builtin_amdgcn_sbfe((int32_t)ab, j, 1);
+        const uint64_t ba = __ballot(xa != 0);
+        const uint32_t bl = (uint32_t)ba, bh = (uint32_t)(ba >> 32);
+        map_lo &= ~(bl ^ xp);
+        map_hi &= ~(bh ^ xp);
+        maa_lo &= ~(bl ^ xa);
+        maa_hi &= ~(bh ^ xa);
+      }
+      const uint64_t Map = ((uint64_t)map_hi << 32) | map_lo;
+      const uint64_t Maa = ((uint64_t)maa_hi << 32) | maa_lo;
+      const uint64_t conf = (Mpp | Mpa | Map | Maa) & lt;  // earlier lanes sharing a block
+      // a lane whose primary cannot reach the threshold even if every earlier lane with its
+      // alternate there moved in stays primary: it is decided already
+      U &= __ballot(cp + (uint32_t)__popcll(Map & lt) >= C::kThreshold);
+      F &= U;
+      while (F != 0) {
+        const uint64_t res = __ballot((conf & U) == 0) & U;
+        const uint64_t A = res & F;
+        altmask |= A;
+        U &= ~res;
+        const uint64_t Al = A & lt;
+        cp = cp + (uint32_t)__popcll(Map & Al) - (uint32_t)__popcll(Mpp & Al);
+        ca = ca + (uint32_t)__popcll(Maa & Al) - (uint32_t)__popcll(Mpa & Al);
+        F = __ballot((cp >= C::kThreshold) & (ca < cp)) & U;
+      }
     }
     const bool alt = (altmask >> lane) & 1;
     const uint32_t chosen = alt ? ab : pb;
