@@ -79,7 +79,7 @@ def lib(build_if_missing: bool = True):
     global _lib
     if _lib is not None:
         return _lib
-    path = _build.LIB
+    path = os.environ.get("TKV_AMQ_LIB") or _build.LIB  # override: kernel experiments
     if not os.path.exists(path):
         if not build_if_missing:
             raise RuntimeError(f"libtkv_amq.so not built ({path}); run __graft_entry__.build()")

@@ -16,6 +16,8 @@
 //   *_probe              one lane per (query, segment) test.
 #include <hip/hip_runtime.h>
 
+#include <mutex>
+
 #include <math.h>
 #include <stdint.h>
 #include <string.h>
@@ -320,6 +322,10 @@ __device__ inline ProbeDesc load_probe_desc(const tkv_amq_segment* segs, uint32_
 // are then LDS reads.  Stride 20 dwords keeps the slots 16-byte aligned and spreads banks.
 constexpr uint32_t kProbeSlotWords = 20;
 
+#ifndef TKV_EXP
+#define TKV_EXP 0  // kernel experiments only (tools/exp_variants.sh); 0 = the product build
+#endif
+
 // The block's four 16-byte loads are issued first and the remaining k-1 bit indices are
 // hashed while they are in flight; only then is the block staged in the lane's LDS slot.
 template <int K>
@@ -424,7 +430,11 @@ constexpr uint32_t kVqfTempStride = 128;  // workspace bytes per block (>= slots
 constexpr uint32_t kVqfMaxLdsBlocks = 16384;
 
 // workspace: [status u32 x16][nelts u32 x n_segs][pad to 256][128-byte record per block]
-// record = slots x Entry (insertion order) ... u32 final count at byte 124
+//            [u64 placement record per key]
+// block record = slots x Entry (insertion order) ... u32 final count at byte 124
+// key record (written by vqf_decide in key order, coalesced; scattered by vqf_scatter):
+//   hi 32 = global block * 64 + rank in the block, or ~0 for a key that is not inserted
+//   lo 32 = Entry ((bucket offset << T) | tag), bit 31 set for 32-bit entries (T = 16)
 struct VqfWorkspace {
   uint32_t* status;
   uint32_t* nelts;
@@ -445,6 +455,13 @@ __host__ __device__ inline VqfWorkspace vqf_workspace(void* base, uint32_t n_seg
   w.nelts = reinterpret_cast<uint32_t*>(p + 64);
   w.temp = p + vqf_temp_offset(n_segs);
   return w;
+}
+
+// the key records follow the last segment's blocks
+__device__ inline uint64_t* vqf_records(VqfWorkspace ws, const tkv_amq_segment* segs, uint32_t n_segs)
+{
+  const tkv_amq_segment& last = segs[n_segs - 1];
+  return reinterpret_cast<uint64_t*>(ws.temp + kVqfTempStride * (last.block_base + last.n_blocks));
 }
 
 __device__ inline uint32_t& vqf_count(VqfWorkspace ws, uint64_t block)
@@ -502,7 +519,7 @@ __device__ inline VqfLoc vqf_locate(uint64_t h, bool valid, uint64_t mask, uint6
 template <int T, int MODE, int NBITS>
 __device__ void vqf_decide_body(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs,
                                 uint32_t stride, const tkv_amq_segment& sg, uint32_t seg_index,
-                                VqfWorkspace ws, uint32_t* cnt)
+                                VqfWorkspace ws, uint64_t* __restrict__ recs, uint32_t* cnt)
 {
   using C = Vqf<T>;
   const uint32_t lane = threadIdx.x;
@@ -511,8 +528,7 @@ __device__ void vqf_decide_body(const uint8_t* __restrict__ keys, const uint64_t
   const uint64_t magic = sg.mod_magic;
   const uint64_t mask = ~0ull << sg.hash_val_shift;  // filter_builder.hpp:187
   const uint64_t lt = lanemask_lt();
-  typename C::Entry* temp =
-      reinterpret_cast<typename C::Entry*>(ws.temp + sg.block_base * kVqfTempStride);
+  uint64_t* rec = recs + sg.key_begin;
   const uint4* kp = reinterpret_cast<const uint4*>(keys) + sg.key_begin;
 
   for (uint32_t b = lane; b < nb; b += 64) cnt[b] = 0;
@@ -526,12 +542,12 @@ __device__ void vqf_decide_body(const uint8_t* __restrict__ keys, const uint64_t
   // below is unrolled by two with the key buffers swapping roles, so no register copy of an
   // in-flight load exists and the compiler waits only for that load, never for the scatter
   // store issued after it.
-  // the record store of a chunk is issued at the start of the next step (after that step's
-  // loads), so a wait for the key prefetch never waits for a scatter store issued just
-  // before it
-  using Entry = typename C::Entry;
-  Entry* pend_ptr = temp;
-  Entry pend_val = 0;
+  // The chunk's placement records are one coalesced 512-byte store, issued at the start of
+  // the next step (after that step's loads), so a wait for the key prefetch never waits
+  // for a store issued just before it.  (Scattering each tag straight into its block's
+  // record from here made every step wait on partial-line writes: 2.1x slower.)
+  uint64_t* pend_ptr = rec;
+  uint64_t pend_val = 0;
   bool pend = false;
   auto step = [&](uint32_t base, VqfLoc& cur, const uint4& kv_hash, uint4& kv_load) {
     const VqfLoc L = cur;
@@ -543,9 +559,19 @@ __device__ void vqf_decide_body(const uint8_t* __restrict__ keys, const uint64_t
     if constexpr (MODE == kKey16) {
       // branch-free (clamped index, select on the result): straight-line code lets the
       // compiler count vmcnt exactly instead of draining every outstanding access
+#if TKV_EXP == 2
+      kv_load = make_uint4(inext * 0x9e3779b9u, inext ^ sg.key_begin, inext + 77u, (uint32_t)sg.key_begin);
+#else
       kv_load = kp[min(inext + 64, n - 1)];
+#endif
+#if TKV_EXP != 1
       if (pend) *pend_ptr = pend_val;
+#endif
+#if TKV_EXP == 5
+      const uint64_t hh = ((uint64_t)kv_hash.x << 32 | kv_hash.y) * 0x9e3779b97f4a7c15ull ^ kv_hash.z;
+#else
       const uint64_t hh = vqf_key_hash<MODE>(keys, offs, stride, 0, kv_hash);
+#endif
       hn = vnext ? hh : 0;
     } else {
       if (pend) *pend_ptr = pend_val;
@@ -559,7 +585,7 @@ __device__ void vqf_decide_body(const uint8_t* __restrict__ keys, const uint64_t
     uint32_t mpp_lo = (uint32_t)keptmask, mpp_hi = (uint32_t)(keptmask >> 32);
     uint32_t mpa_lo = mpp_lo, mpa_hi = mpp_hi;
 #pragma unroll
-    for (int j = 0; j < NBITS; ++j) {
+    for (int j = 0; j < (TKV_EXP == 3 ? 0 : NBITS); ++j) {
       const uint32_t xp = (uint32_t)__builtin_amdgcn_sbfe((int32_t)L.pb, j, 1);  // 0 or ~0
       const uint32_t xa = (uint32_t)__builtin_amdgcn_sbfe((int32_t)L.ab, j, 1);
       const uint64_t bp = __ballot(xp != 0);
@@ -583,7 +609,7 @@ __device__ void vqf_decide_body(const uint8_t* __restrict__ keys, const uint64_t
     uint64_t U = __ballot(L.kept && pb != ab);  // blocks differ (vqf_insert alt test)
     uint64_t altmask = 0;
     uint64_t F = __ballot((cp >= C::kThreshold) & (ca < cp)) & U;
-    if (F != 0) {
+    if (TKV_EXP != 4 && F != 0) {
       // lanes whose alternate block is my primary / my alternate
       uint32_t map_lo = (uint32_t)keptmask, map_hi = (uint32_t)(keptmask >> 32);
       uint32_t maa_lo = map_lo, maa_hi = map_hi;
@@ -621,9 +647,11 @@ __device__ void vqf_decide_body(const uint8_t* __restrict__ keys, const uint64_t
     const uint32_t cho = alt ? L.ao : L.po;
     const uint32_t r = alt ? ca : cp;  // count of the chosen block when this key is inserted
     fail |= (uint32_t)(__ballot(L.kept && r >= C::kSlots) != 0);
-    pend = L.kept && r < C::kSlots;
-    pend_ptr = temp + (uint64_t)chosen * (kVqfTempStride / sizeof(Entry)) + (r < C::kSlots ? r : 0);
-    pend_val = (Entry)((cho << T) | L.tag);
+    pend = base + lane < n;
+    pend_ptr = rec + base + lane;
+    const uint32_t slot_hi = (L.kept && r < C::kSlots)
+                                 ? (uint32_t)((sg.block_base + chosen) * 64 + r) : 0xffffffffu;
+    pend_val = ((uint64_t)slot_hi << 32) | ((cho << T) | L.tag) | (T == 16 ? 0x80000000u : 0u);
     if (L.kept) atomicAdd(cnt + chosen, 1u);
   };
 
@@ -656,11 +684,12 @@ __device__ void vqf_decide_body(const uint8_t* __restrict__ keys, const uint64_t
 template <int T, int MODE>
 __device__ inline void vqf_decide_dispatch(const uint8_t* keys, const uint64_t* offs,
                                            uint32_t stride, const tkv_amq_segment& sg,
-                                           uint32_t seg_index, VqfWorkspace ws, uint32_t* cnt)
+                                           uint32_t seg_index, VqfWorkspace ws, uint64_t* recs,
+                                           uint32_t* cnt)
 {
   // kVqfMaxLdsBlocks = 16384 -> at most 14 block-id bits
-  if (sg.n_blocks <= 512) vqf_decide_body<T, MODE, 9>(keys, offs, stride, sg, seg_index, ws, cnt);
-  else vqf_decide_body<T, MODE, 14>(keys, offs, stride, sg, seg_index, ws, cnt);
+  if (sg.n_blocks <= 512) vqf_decide_body<T, MODE, 9>(keys, offs, stride, sg, seg_index, ws, recs, cnt);
+  else vqf_decide_body<T, MODE, 14>(keys, offs, stride, sg, seg_index, ws, recs, cnt);
 }
 
 template <int MODE>
@@ -672,8 +701,27 @@ __global__ __launch_bounds__(64) void vqf_decide(const uint8_t* __restrict__ key
   extern __shared__ uint32_t s_cnt[];
   const tkv_amq_segment sg = segs[blockIdx.x];
   const VqfWorkspace ws = vqf_workspace(ws_base, n_segs);
-  if (sg.tag_bits == 8) vqf_decide_dispatch<8, MODE>(keys, offs, stride, sg, blockIdx.x, ws, s_cnt);
-  else if (sg.tag_bits == 16) vqf_decide_dispatch<16, MODE>(keys, offs, stride, sg, blockIdx.x, ws, s_cnt);
+  uint64_t* recs = vqf_records(ws, segs, n_segs);
+  if (sg.tag_bits == 8) vqf_decide_dispatch<8, MODE>(keys, offs, stride, sg, blockIdx.x, ws, recs, s_cnt);
+  else if (sg.tag_bits == 16) vqf_decide_dispatch<16, MODE>(keys, offs, stride, sg, blockIdx.x, ws, recs, s_cnt);
+}
+
+// One thread per key: moves the key's entry from its coalesced placement record into the
+// block record (insertion rank = slot).  Fully parallel, so the partial-line writes overlap.
+__global__ __launch_bounds__(256) void vqf_scatter(const tkv_amq_segment* __restrict__ segs,
+                                                   void* ws_base, uint32_t n_segs, uint64_t n_keys)
+{
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  const tkv_amq_segment& last = segs[n_segs - 1];
+  if (i >= n_keys || i >= last.key_begin + last.n_keys) return;
+  const VqfWorkspace ws = vqf_workspace(ws_base, n_segs);
+  const uint64_t r = __builtin_nontemporal_load(vqf_records(ws, segs, n_segs) + i);
+  const uint32_t hi = (uint32_t)(r >> 32), lo = (uint32_t)r;
+  if (hi == 0xffffffffu) return;
+  uint8_t* p = ws.temp + (uint64_t)(hi >> 6) * kVqfTempStride;
+  const uint32_t rank = hi & 63u;
+  if (lo >> 31) *reinterpret_cast<uint32_t*>(p + 4 * rank) = lo & 0x7fffffffu;
+  else *reinterpret_cast<uint16_t*>(p + 2 * rank) = (uint16_t)lo;
 }
 
 // One thread per 64-byte VQF block: the block's records (bucket offset, tag) arrive in
@@ -683,9 +731,12 @@ __global__ __launch_bounds__(64) void vqf_decide(const uint8_t* __restrict__ key
 // multiply, and the second pass takes each entry's slot with ds_add_rtn in insertion order.
 constexpr uint32_t kPlaceThreads = 128;
 
-template <int T>
+// kLds: the block records come from the leaf's LDS image (kSlots entries per block, counts in
+// lds_cnt) built by vqf_place_fused; otherwise from the workspace's 128-byte block records.
+template <int T, bool kLds = false>
 __device__ void vqf_place_body(const tkv_amq_segment& sg, uint32_t seg_index, VqfWorkspace ws,
-                               uint8_t* __restrict__ out, uint32_t* s_cnt, uint32_t* s_img)
+                               uint8_t* __restrict__ out, uint32_t* s_cnt, uint32_t* s_img,
+                               const uint8_t* lds_img = nullptr, const uint32_t* lds_cnt = nullptr)
 {
   using C = Vqf<T>;
   using E = typename C::Entry;
@@ -718,8 +769,15 @@ __device__ void vqf_place_body(const tkv_amq_segment& sg, uint32_t seg_index, Vq
   uint4* dst_blocks = reinterpret_cast<uint4*>(payload + kVqfHeader + kVqfMetadata);
 
   for (uint32_t b = tid; b < nb; b += kPlaceThreads) {
-    const uint8_t* rec = ws.temp + (sg.block_base + b) * kVqfTempStride;
-    const uint32_t c = *reinterpret_cast<const uint32_t*>(rec + kVqfCountByte);
+    const uint8_t* rec;
+    uint32_t c;
+    if constexpr (kLds) {
+      rec = lds_img + b * (C::kSlots * sizeof(E));
+      c = lds_cnt[b];
+    } else {
+      rec = ws.temp + (sg.block_base + b) * kVqfTempStride;
+      c = *reinterpret_cast<const uint32_t*>(rec + kVqfCountByte);
+    }
     uint4 rv[kRecWords];
 #pragma unroll
     for (uint32_t q = 0; q < kRecWords; ++q) rv[q] = reinterpret_cast<const uint4*>(rec)[q];
@@ -729,13 +787,13 @@ __device__ void vqf_place_body(const tkv_amq_segment& sg, uint32_t seg_index, Vq
     for (uint32_t w = 0; w < kCntWords; ++w) cnt[w] = 0;
 #pragma unroll
     for (uint32_t w = C::kMdBytes / 4; w < 16; ++w) img[w] = 0;
-    // pass 1: bucket histogram
+    // pass 1: bucket histogram.  Branch-free (slots >= c add 0 to bucket 0) so the LDS
+    // atomics issue back to back instead of one waitcnt per predicated slot.
 #pragma unroll
     for (uint32_t i = 0; i < C::kSlots; ++i) {
-      if (i < c) {
-        const uint32_t o = ent[i] >> T;
-        atomicAdd(cnt + (o >> 2), 1u << (8 * (o & 3)));
-      }
+      const bool live = i < c;
+      const uint32_t o = live ? (uint32_t)(ent[i] >> T) : 0u;
+      atomicAdd(cnt + (o >> 2), live ? 1u << (8 * (o & 3)) : 0u);
     }
     // exclusive prefix over buckets (bytes): inclusive-in-dword = v * 0x01010101
     uint32_t run = 0;
@@ -748,18 +806,26 @@ __device__ void vqf_place_body(const tkv_amq_segment& sg, uint32_t seg_index, Vq
     }
     // pass 2: slot of each entry in insertion order; metadata zero at slot + offset
     uint64_t md_lo = ~0ull, md_hi = T == 8 ? ~0ull : 0ull;
+    // (branch-free as in pass 1; slots are distinct, so each tag is a plain byte/short store,
+    // dead slots store into the image's pad dword)
+    uint8_t* img8 = reinterpret_cast<uint8_t*>(img);
 #pragma unroll
     for (uint32_t i = 0; i < C::kSlots; ++i) {
-      if (i < c) {
-        const uint32_t e = ent[i];
-        const uint32_t o = e >> T, tag = e & ((1u << T) - 1);
-        const uint32_t old = atomicAdd(cnt + (o >> 2), 1u << (8 * (o & 3)));
-        const uint32_t slot = (old >> (8 * (o & 3))) & 0xffu;
-        const uint32_t z = slot + o;
-        if (z < 64) md_lo &= ~(1ull << z);
-        else md_hi &= ~(1ull << (z - 64));
-        const uint32_t byte = C::kMdBytes + slot * (T / 8);
-        atomicOr(img + (byte >> 2), tag << (8 * (byte & 3)));
+      const bool live = i < c;
+      const uint32_t e = ent[i];
+      const uint32_t o = live ? e >> T : 0u, tag = e & ((1u << T) - 1);
+      const uint32_t old = atomicAdd(cnt + (o >> 2), live ? 1u << (8 * (o & 3)) : 0u);
+      const uint32_t slot = (old >> (8 * (o & 3))) & 0xffu;
+      const uint32_t z = slot + o;
+      const uint64_t clr = live ? 1ull << (z & 63) : 0ull;
+      if (z < 64) md_lo &= ~clr;
+      else md_hi &= ~clr;
+      const uint32_t byte = live ? C::kMdBytes + slot * (T / 8) : 64u;
+      if constexpr (T == 8) {
+        img8[byte] = (uint8_t)tag;
+      } else {
+        const uint16_t t16 = (uint16_t)tag;
+        __builtin_memcpy(img8 + byte, &t16, 2);  // (memcpy: the image is read back as u32)
       }
     }
     if (c == 0) {  // an empty block keeps the init metadata: top bit clear
@@ -800,6 +866,84 @@ __global__ __launch_bounds__(kPlaceThreads) void vqf_place(const tkv_amq_segment
   const VqfWorkspace ws = vqf_workspace(ws_base, n_segs);
   if (sg.tag_bits == 8) vqf_place_body<8>(sg, blockIdx.x, ws, out, s_cnt, s_img);
   else if (sg.tag_bits == 16) vqf_place_body<16>(sg, blockIdx.x, ws, out, s_cnt, s_img);
+}
+
+// Fused scatter + place for leaves whose block records fit in LDS (one workgroup per leaf):
+// the leaf's placement records stream in coalesced, each entry lands at [block][rank] of an
+// LDS image (no partial-line global writes), then the per-block counting sort runs on it.
+constexpr uint32_t kFusedThreads = 256;
+constexpr uint32_t kFusedLdsBudget = 80 * 1024;
+
+__host__ __device__ inline uint32_t vqf_fused_img_bytes(uint32_t nb)
+{
+  return nb * 112u;  // max over T of kSlots * sizeof(Entry): 48 x 2 / 28 x 4
+}
+
+__host__ __device__ inline uint32_t vqf_fused_lds_bytes(uint32_t max_nb)
+{
+  return vqf_fused_img_bytes(max_nb) + 4 * ((max_nb + 3) & ~3u) +
+         kPlaceThreads * (21 + 17) * 4;
+}
+
+template <int T>
+__device__ void vqf_place_fused_body(const tkv_amq_segment& sg, uint32_t seg_index,
+                                     VqfWorkspace ws, const uint64_t* __restrict__ recs,
+                                     uint8_t* __restrict__ out, uint8_t* lds)
+{
+  using C = Vqf<T>;
+  using E = typename C::Entry;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t nb = sg.n_blocks, n = sg.n_keys;
+  E* img = reinterpret_cast<E*>(lds);
+  uint32_t* cnt = reinterpret_cast<uint32_t*>(lds + vqf_fused_img_bytes(nb));
+  uint32_t* s_cnt = cnt + ((nb + 3) & ~3u);
+  uint32_t* s_img = s_cnt + kPlaceThreads * 21;
+  for (uint32_t b = tid; b < nb; b += kFusedThreads) cnt[b] = 0;
+  __syncthreads();
+  // 16-byte loads (two records each), 8 in flight per thread: 32 KB per workgroup
+  const uint64_t a0 = sg.key_begin & ~1ull;  // records start 128-byte aligned in the workspace
+  const uint4* r2 = reinterpret_cast<const uint4*>(recs + a0);
+  const uint32_t lo_skip = (uint32_t)(sg.key_begin - a0);  // 0 or 1
+  const uint32_t n_pairs = (lo_skip + n + 1) / 2;
+  const uint32_t gb0 = (uint32_t)sg.block_base;
+  constexpr uint32_t kU = 8;
+  auto put = [&](uint64_t v, uint32_t k) {
+    const uint32_t hi = (uint32_t)(v >> 32);
+    if (k >= lo_skip && k < lo_skip + n && hi != 0xffffffffu) {
+      const uint32_t blk = (hi >> 6) - gb0;
+      img[blk * C::kSlots + (hi & 63u)] = (E)((uint32_t)v & 0x7fffffffu);
+      atomicAdd(cnt + blk, 1u);
+    }
+  };
+  for (uint32_t p0 = 0; p0 < n_pairs; p0 += kFusedThreads * kU) {
+    uint4 v[kU];
+#pragma unroll
+    for (uint32_t u = 0; u < kU; ++u) {
+      const uint32_t p = p0 + u * kFusedThreads + tid;
+      v[u] = p < n_pairs ? load_nt16(r2 + p) : make_uint4(0, ~0u, 0, ~0u);
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < kU; ++u) {
+      const uint32_t k = 2 * (p0 + u * kFusedThreads + tid);
+      put((uint64_t)v[u].x | ((uint64_t)v[u].y << 32), k);
+      put((uint64_t)v[u].z | ((uint64_t)v[u].w << 32), k + 1);
+    }
+  }
+  __syncthreads();
+  if (TKV_EXP != 6 && tid < kPlaceThreads)
+    vqf_place_body<T, true>(sg, seg_index, ws, out, s_cnt, s_img, lds, cnt);
+}
+
+__global__ __launch_bounds__(kFusedThreads) void vqf_place_fused(const tkv_amq_segment* __restrict__ segs,
+                                                                 void* ws_base, uint32_t n_segs,
+                                                                 uint8_t* __restrict__ out)
+{
+  extern __shared__ __attribute__((aligned(16))) uint8_t s_lds[];
+  const tkv_amq_segment sg = segs[blockIdx.x];
+  const VqfWorkspace ws = vqf_workspace(ws_base, n_segs);
+  const uint64_t* recs = vqf_records(ws, segs, n_segs);
+  if (sg.tag_bits == 8) vqf_place_fused_body<8>(sg, blockIdx.x, ws, recs, out, s_lds);
+  else if (sg.tag_bits == 16) vqf_place_fused_body<16>(sg, blockIdx.x, ws, recs, out, s_lds);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1184,7 +1328,7 @@ int tkv_amq_plan(int kind, const uint64_t* counts, const uint64_t* src_ids, uint
   if (ws_bytes) {
     *ws_bytes = 0;
     if (kind == TKV_AMQ_VQF && bpk != 0)
-      *ws_bytes = vqf_temp_offset(n_segs) + kVqfTempStride * block_base;
+      *ws_bytes = vqf_temp_offset(n_segs) + kVqfTempStride * block_base + 8 * key_begin + 64;
   }
   if (max_blocks_out) *max_blocks_out = max_blocks;
   return TKV_AMQ_OK;
@@ -1255,7 +1399,22 @@ int tkv_amq_build(int kind, const uint8_t* keys, const uint64_t* offs, uint32_t 
   else
     hipLaunchKernelGGL(vqf_decide<kKeyVar>, dim3(n_segs), dim3(64), lds, s, keys, offs, stride,
                        d_segs, d_ws, n_segs);
-  hipLaunchKernelGGL(vqf_place, dim3(n_segs), dim3(kPlaceThreads), 0, s, d_segs, d_ws, n_segs, d_out);
+  const uint32_t fused_lds = vqf_fused_lds_bytes(max_blocks);
+  if (fused_lds <= kFusedLdsBudget) {
+    static std::once_flag lds_attr;
+    std::call_once(lds_attr, [] {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&vqf_place_fused),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kFusedLdsBudget);
+    });
+    hipLaunchKernelGGL(vqf_place_fused, dim3(n_segs), dim3(kFusedThreads), fused_lds, s, d_segs,
+                       d_ws, n_segs, d_out);
+  } else {
+    if (n_keys)
+      hipLaunchKernelGGL(vqf_scatter, dim3((uint32_t)div_up(n_keys, 256)), dim3(256), 0, s,
+                         d_segs, d_ws, n_segs, n_keys);
+    hipLaunchKernelGGL(vqf_place, dim3(n_segs), dim3(kPlaceThreads), 0, s, d_segs, d_ws, n_segs,
+                       d_out);
+  }
   return hipGetLastError() == hipSuccess ? TKV_AMQ_OK : TKV_AMQ_INTERNAL;
 }
 
