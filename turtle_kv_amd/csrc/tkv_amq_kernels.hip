@@ -733,10 +733,12 @@ constexpr uint32_t kPlaceThreads = 128;
 
 // kLds: the block records come from the leaf's LDS image (kSlots entries per block, counts in
 // lds_cnt) built by vqf_place_fused; otherwise from the workspace's 128-byte block records.
-template <int T, bool kLds = false>
+// kLds: the bucket counters live in the block's own LDS record once it is in registers, so
+// the only per-thread scratch is the 68-byte output image.
+template <int T, bool kLds = false, uint32_t kThreads = kPlaceThreads>
 __device__ void vqf_place_body(const tkv_amq_segment& sg, uint32_t seg_index, VqfWorkspace ws,
                                uint8_t* __restrict__ out, uint32_t* s_cnt, uint32_t* s_img,
-                               const uint8_t* lds_img = nullptr, const uint32_t* lds_cnt = nullptr)
+                               uint8_t* lds_img = nullptr, const uint32_t* lds_cnt = nullptr)
 {
   using C = Vqf<T>;
   using E = typename C::Entry;
@@ -764,11 +766,11 @@ __device__ void vqf_place_body(const tkv_amq_segment& sg, uint32_t seg_index, Vq
     reinterpret_cast<ulonglong2*>(payload)[tid] = v;
   }
 
-  uint32_t* cnt = s_cnt + tid * kCntStride;
+  uint32_t* cnt = kLds ? nullptr : s_cnt + tid * kCntStride;
   uint32_t* img = s_img + tid * kImgStride;
   uint4* dst_blocks = reinterpret_cast<uint4*>(payload + kVqfHeader + kVqfMetadata);
 
-  for (uint32_t b = tid; b < nb; b += kPlaceThreads) {
+  for (uint32_t b = tid; b < nb; b += kThreads) {
     const uint8_t* rec;
     uint32_t c;
     if constexpr (kLds) {
@@ -782,6 +784,10 @@ __device__ void vqf_place_body(const tkv_amq_segment& sg, uint32_t seg_index, Vq
 #pragma unroll
     for (uint32_t q = 0; q < kRecWords; ++q) rv[q] = reinterpret_cast<const uint4*>(rec)[q];
     const E* ent = reinterpret_cast<const E*>(rv);
+    if constexpr (kLds) {
+      asm volatile("" ::: "memory");  // the record is in registers before its bytes are reused
+      cnt = reinterpret_cast<uint32_t*>(lds_img + b * (C::kSlots * sizeof(E)));
+    }
 
 #pragma unroll
     for (uint32_t w = 0; w < kCntWords; ++w) cnt[w] = 0;
@@ -881,8 +887,7 @@ __host__ __device__ inline uint32_t vqf_fused_img_bytes(uint32_t nb)
 
 __host__ __device__ inline uint32_t vqf_fused_lds_bytes(uint32_t max_nb)
 {
-  return vqf_fused_img_bytes(max_nb) + 4 * ((max_nb + 3) & ~3u) +
-         kPlaceThreads * (21 + 17) * 4;
+  return vqf_fused_img_bytes(max_nb) + 4 * ((max_nb + 3) & ~3u) + kFusedThreads * 17 * 4;
 }
 
 template <int T>
@@ -896,8 +901,7 @@ __device__ void vqf_place_fused_body(const tkv_amq_segment& sg, uint32_t seg_ind
   const uint32_t nb = sg.n_blocks, n = sg.n_keys;
   E* img = reinterpret_cast<E*>(lds);
   uint32_t* cnt = reinterpret_cast<uint32_t*>(lds + vqf_fused_img_bytes(nb));
-  uint32_t* s_cnt = cnt + ((nb + 3) & ~3u);
-  uint32_t* s_img = s_cnt + kPlaceThreads * 21;
+  uint32_t* s_img = cnt + ((nb + 3) & ~3u);
   for (uint32_t b = tid; b < nb; b += kFusedThreads) cnt[b] = 0;
   __syncthreads();
   // 16-byte loads (two records each), 8 in flight per thread: 32 KB per workgroup
@@ -930,8 +934,8 @@ __device__ void vqf_place_fused_body(const tkv_amq_segment& sg, uint32_t seg_ind
     }
   }
   __syncthreads();
-  if (TKV_EXP != 6 && tid < kPlaceThreads)
-    vqf_place_body<T, true>(sg, seg_index, ws, out, s_cnt, s_img, lds, cnt);
+  if (TKV_EXP != 6)
+    vqf_place_body<T, true, kFusedThreads>(sg, seg_index, ws, out, nullptr, s_img, lds, cnt);
 }
 
 __global__ __launch_bounds__(kFusedThreads) void vqf_place_fused(const tkv_amq_segment* __restrict__ segs,
