@@ -428,6 +428,7 @@ struct Vqf<16> {
 
 constexpr uint32_t kVqfTempStride = 128;  // workspace bytes per block (>= slots * entry)
 constexpr uint32_t kVqfMaxLdsBlocks = 16384;
+constexpr uint32_t kVqfMatchLdsBlocks = 512;  // vqf_decide's LDS lane-mask table (8 B/block)
 
 // workspace: [status u32 x16][nelts u32 x n_segs][pad to 256][128-byte record per block]
 //            [u64 placement record per key]
@@ -516,7 +517,11 @@ __device__ inline VqfLoc vqf_locate(uint64_t h, bool valid, uint64_t mask, uint6
 // NBITS >= ceil(log2(n_blocks)) is a compile-time bound (extra high bits are zero in every
 // lane and leave the matches unchanged), so the match loop unrolls into the same basic
 // block as the next chunk's hashing and the two interleave.
-template <int T, int MODE, int NBITS>
+// kLdsMatch: the four lane-match masks come from an LDS table of 64-bit lane masks, one per
+// block (each lane ORs its bit into its block's entry, then reads the entries it needs,
+// then clears): a handful of LDS operations instead of ~7 VALU per block-id bit.  Needs
+// 8 B of LDS per block, so it is used for leaves of <= kVqfMatchLdsBlocks blocks.
+template <int T, int MODE, int NBITS, bool kLdsMatch>
 __device__ void vqf_decide_body(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs,
                                 uint32_t stride, const tkv_amq_segment& sg, uint32_t seg_index,
                                 VqfWorkspace ws, uint64_t* __restrict__ recs, uint32_t* cnt)
@@ -531,8 +536,13 @@ __device__ void vqf_decide_body(const uint8_t* __restrict__ keys, const uint64_t
   uint64_t* rec = recs + sg.key_begin;
   const uint4* kp = reinterpret_cast<const uint4*>(keys) + sg.key_begin;
 
-  for (uint32_t b = lane; b < nb; b += 64) cnt[b] = 0;
+  unsigned long long* mt = reinterpret_cast<unsigned long long*>(cnt + ((nb + 1) & ~1u));
+  for (uint32_t b = lane; b < nb; b += 64) {
+    cnt[b] = 0;
+    if constexpr (kLdsMatch) mt[b] = 0;
+  }
   __syncthreads();
+  const unsigned long long mybit = 1ull << lane;
 
   uint32_t nelts = 0;
   uint32_t fail = 0;
@@ -584,8 +594,19 @@ __device__ void vqf_decide_body(const uint8_t* __restrict__ keys, const uint64_t
     // 32-bit half of a match mask is updated with one v_bitop3 (m & ~(ballot ^ sext(bit)))
     uint32_t mpp_lo = (uint32_t)keptmask, mpp_hi = (uint32_t)(keptmask >> 32);
     uint32_t mpa_lo = mpp_lo, mpa_hi = mpp_hi;
+    if constexpr (kLdsMatch) {
+      if (L.kept) atomicOr(mt + L.pb, mybit);
+      asm volatile("" ::: "memory");
+      const uint64_t a = mt[L.pb], b = mt[L.ab];
+      asm volatile("" ::: "memory");
+      if (L.kept) mt[L.pb] = 0;
+      mpp_lo &= (uint32_t)a;
+      mpp_hi &= (uint32_t)(a >> 32);
+      mpa_lo &= (uint32_t)b;
+      mpa_hi &= (uint32_t)(b >> 32);
+    }
 #pragma unroll
-    for (int j = 0; j < (TKV_EXP == 3 ? 0 : NBITS); ++j) {
+    for (int j = 0; j < (kLdsMatch ? 0 : NBITS); ++j) {
       const uint32_t xp = (uint32_t)__builtin_amdgcn_sbfe((int32_t)L.pb, j, 1);  // 0 or ~0
       const uint32_t xa = (uint32_t)__builtin_amdgcn_sbfe((int32_t)L.ab, j, 1);
       const uint64_t bp = __ballot(xp != 0);
@@ -613,8 +634,19 @@ __device__ void vqf_decide_body(const uint8_t* __restrict__ keys, const uint64_t
       // lanes whose alternate block is my primary / my alternate
       uint32_t map_lo = (uint32_t)keptmask, map_hi = (uint32_t)(keptmask >> 32);
       uint32_t maa_lo = map_lo, maa_hi = map_hi;
+      if constexpr (kLdsMatch) {
+        if (L.kept) atomicOr(mt + ab, mybit);
+        asm volatile("" ::: "memory");
+        const uint64_t a = mt[pb], b = mt[ab];
+        asm volatile("" ::: "memory");
+        if (L.kept) mt[ab] = 0;
+        map_lo &= (uint32_t)a;
+        map_hi &= (uint32_t)(a >> 32);
+        maa_lo &= (uint32_t)b;
+        maa_hi &= (uint32_t)(b >> 32);
+      }
 #pragma unroll
-      for (int j = 0; j < NBITS; ++j) {
+      for (int j = 0; j < (kLdsMatch ? 0 : NBITS); ++j) {
         const uint32_t xp = (uint32_t)__builtin_amdgcn_sbfe((int32_t)pb, j, 1);
         const uint32_t xa = (uint32_t)__builtin_amdgcn_sbfe((int32_t)ab, j, 1);
         const uint64_t ba = __ballot(xa != 0);
@@ -685,25 +717,31 @@ template <int T, int MODE>
 __device__ inline void vqf_decide_dispatch(const uint8_t* keys, const uint64_t* offs,
                                            uint32_t stride, const tkv_amq_segment& sg,
                                            uint32_t seg_index, VqfWorkspace ws, uint64_t* recs,
-                                           uint32_t* cnt)
+                                           uint32_t* cnt, bool match_lds)
 {
   // kVqfMaxLdsBlocks = 16384 -> at most 14 block-id bits
-  if (sg.n_blocks <= 512) vqf_decide_body<T, MODE, 9>(keys, offs, stride, sg, seg_index, ws, recs, cnt);
-  else vqf_decide_body<T, MODE, 14>(keys, offs, stride, sg, seg_index, ws, recs, cnt);
+  if (sg.n_blocks <= kVqfMatchLdsBlocks && match_lds)
+    vqf_decide_body<T, MODE, 9, true>(keys, offs, stride, sg, seg_index, ws, recs, cnt);
+  else if (sg.n_blocks <= 512)
+    vqf_decide_body<T, MODE, 9, false>(keys, offs, stride, sg, seg_index, ws, recs, cnt);
+  else
+    vqf_decide_body<T, MODE, 14, false>(keys, offs, stride, sg, seg_index, ws, recs, cnt);
 }
 
 template <int MODE>
 __global__ __launch_bounds__(64) void vqf_decide(const uint8_t* __restrict__ keys,
                                                  const uint64_t* __restrict__ offs, uint32_t stride,
                                                  const tkv_amq_segment* __restrict__ segs,
-                                                 void* ws_base, uint32_t n_segs)
+                                                 void* ws_base, uint32_t n_segs, int match_lds)
 {
-  extern __shared__ uint32_t s_cnt[];
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_cnt[];
   const tkv_amq_segment sg = segs[blockIdx.x];
   const VqfWorkspace ws = vqf_workspace(ws_base, n_segs);
   uint64_t* recs = vqf_records(ws, segs, n_segs);
-  if (sg.tag_bits == 8) vqf_decide_dispatch<8, MODE>(keys, offs, stride, sg, blockIdx.x, ws, recs, s_cnt);
-  else if (sg.tag_bits == 16) vqf_decide_dispatch<16, MODE>(keys, offs, stride, sg, blockIdx.x, ws, recs, s_cnt);
+  if (sg.tag_bits == 8)
+    vqf_decide_dispatch<8, MODE>(keys, offs, stride, sg, blockIdx.x, ws, recs, s_cnt, match_lds != 0);
+  else if (sg.tag_bits == 16)
+    vqf_decide_dispatch<16, MODE>(keys, offs, stride, sg, blockIdx.x, ws, recs, s_cnt, match_lds != 0);
 }
 
 // One thread per key: moves the key's entry from its coalesced placement record into the
@@ -1393,16 +1431,18 @@ int tkv_amq_build(int kind, const uint8_t* keys, const uint64_t* offs, uint32_t 
   if (!d_ws) return TKV_AMQ_INVALID_ARGUMENT;
   if (ws_bytes < vqf_temp_offset(n_segs)) return TKV_AMQ_INVALID_ARGUMENT;
   if (hipMemsetAsync(d_ws, 0, 64, s) != hipSuccess) return TKV_AMQ_INTERNAL;
-  const size_t lds = 4ull * max_blocks;
+  // LDS: u32 block counts (+ the u64 lane-mask table when every leaf is small enough)
+  const int match_lds = max_blocks <= kVqfMatchLdsBlocks;
+  const size_t lds = 4ull * ((max_blocks + 1) & ~1u) + (match_lds ? 8ull * max_blocks : 0);
   if (mode == kKey16)
     hipLaunchKernelGGL(vqf_decide<kKey16>, dim3(n_segs), dim3(64), lds, s, keys, offs, stride,
-                       d_segs, d_ws, n_segs);
+                       d_segs, d_ws, n_segs, match_lds);
   else if (mode == kKeyFixed)
     hipLaunchKernelGGL(vqf_decide<kKeyFixed>, dim3(n_segs), dim3(64), lds, s, keys, offs, stride,
-                       d_segs, d_ws, n_segs);
+                       d_segs, d_ws, n_segs, match_lds);
   else
     hipLaunchKernelGGL(vqf_decide<kKeyVar>, dim3(n_segs), dim3(64), lds, s, keys, offs, stride,
-                       d_segs, d_ws, n_segs);
+                       d_segs, d_ws, n_segs, match_lds);
   const uint32_t fused_lds = vqf_fused_lds_bytes(max_blocks);
   if (fused_lds <= kFusedLdsBudget) {
     static std::once_flag lds_attr;
