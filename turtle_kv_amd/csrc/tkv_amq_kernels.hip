@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include <mutex>
+#include <type_traits>
 
 #include <math.h>
 #include <stdint.h>
@@ -521,7 +522,9 @@ __device__ inline VqfLoc vqf_locate(uint64_t h, bool valid, uint64_t mask, uint6
 // block (each lane ORs its bit into its block's entry, then reads the entries it needs,
 // then clears): a handful of LDS operations instead of ~7 VALU per block-id bit.  Needs
 // 8 B of LDS per block, so it is used for leaves of <= kVqfMatchLdsBlocks blocks.
-template <int T, int MODE, int NBITS, bool kLdsMatch>
+// kCompact (T = 8, <= 512 blocks, fused place): 4-byte key records
+//   block << 21 | rank << 15 | (bucket offset << 8 | tag), or ~0 for a key not inserted
+template <int T, int MODE, int NBITS, bool kLdsMatch, bool kCompact>
 __device__ void vqf_decide_body(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs,
                                 uint32_t stride, const tkv_amq_segment& sg, uint32_t seg_index,
                                 VqfWorkspace ws, uint64_t* __restrict__ recs, uint32_t* cnt)
@@ -533,7 +536,8 @@ __device__ void vqf_decide_body(const uint8_t* __restrict__ keys, const uint64_t
   const uint64_t magic = sg.mod_magic;
   const uint64_t mask = ~0ull << sg.hash_val_shift;  // filter_builder.hpp:187
   const uint64_t lt = lanemask_lt();
-  uint64_t* rec = recs + sg.key_begin;
+  using Rec = typename std::conditional<kCompact, uint32_t, uint64_t>::type;
+  Rec* rec = reinterpret_cast<Rec*>(recs + sg.key_begin);
   const uint4* kp = reinterpret_cast<const uint4*>(keys) + sg.key_begin;
 
   unsigned long long* mt = reinterpret_cast<unsigned long long*>(cnt + ((nb + 1) & ~1u));
@@ -556,8 +560,8 @@ __device__ void vqf_decide_body(const uint8_t* __restrict__ keys, const uint64_t
   // the next step (after that step's loads), so a wait for the key prefetch never waits
   // for a store issued just before it.  (Scattering each tag straight into its block's
   // record from here made every step wait on partial-line writes: 2.1x slower.)
-  uint64_t* pend_ptr = rec;
-  uint64_t pend_val = 0;
+  Rec* pend_ptr = rec;
+  Rec pend_val = 0;
   bool pend = false;
   auto step = [&](uint32_t base, VqfLoc& cur, const uint4& kv_hash, uint4& kv_load) {
     const VqfLoc L = cur;
@@ -681,9 +685,14 @@ __device__ void vqf_decide_body(const uint8_t* __restrict__ keys, const uint64_t
     fail |= (uint32_t)(__ballot(L.kept && r >= C::kSlots) != 0);
     pend = base + lane < n;
     pend_ptr = rec + base + lane;
-    const uint32_t slot_hi = (L.kept && r < C::kSlots)
-                                 ? (uint32_t)((sg.block_base + chosen) * 64 + r) : 0xffffffffu;
-    pend_val = ((uint64_t)slot_hi << 32) | ((cho << T) | L.tag) | (T == 16 ? 0x80000000u : 0u);
+    if constexpr (kCompact) {
+      pend_val = (L.kept && r < C::kSlots) ? (chosen << 21) | (r << 15) | (cho << T) | L.tag
+                                           : 0xffffffffu;
+    } else {
+      const uint32_t slot_hi = (L.kept && r < C::kSlots)
+                                   ? (uint32_t)((sg.block_base + chosen) * 64 + r) : 0xffffffffu;
+      pend_val = ((uint64_t)slot_hi << 32) | ((cho << T) | L.tag) | (T == 16 ? 0x80000000u : 0u);
+    }
     if (L.kept) atomicAdd(cnt + chosen, 1u);
   };
 
@@ -717,31 +726,38 @@ template <int T, int MODE>
 __device__ inline void vqf_decide_dispatch(const uint8_t* keys, const uint64_t* offs,
                                            uint32_t stride, const tkv_amq_segment& sg,
                                            uint32_t seg_index, VqfWorkspace ws, uint64_t* recs,
-                                           uint32_t* cnt, bool match_lds)
+                                           uint32_t* cnt, bool match_lds, bool compact_ok)
 {
   // kVqfMaxLdsBlocks = 16384 -> at most 14 block-id bits
-  if (sg.n_blocks <= kVqfMatchLdsBlocks && match_lds)
-    vqf_decide_body<T, MODE, 9, true>(keys, offs, stride, sg, seg_index, ws, recs, cnt);
-  else if (sg.n_blocks <= 512)
-    vqf_decide_body<T, MODE, 9, false>(keys, offs, stride, sg, seg_index, ws, recs, cnt);
-  else
-    vqf_decide_body<T, MODE, 14, false>(keys, offs, stride, sg, seg_index, ws, recs, cnt);
+  if (sg.n_blocks <= 512) {
+    static_assert(kVqfMatchLdsBlocks == 512, "");
+    if (T == 8 && compact_ok) {
+      if (match_lds) vqf_decide_body<T, MODE, 9, true, T == 8>(keys, offs, stride, sg, seg_index, ws, recs, cnt);
+      else vqf_decide_body<T, MODE, 9, false, T == 8>(keys, offs, stride, sg, seg_index, ws, recs, cnt);
+    } else {
+      if (match_lds) vqf_decide_body<T, MODE, 9, true, false>(keys, offs, stride, sg, seg_index, ws, recs, cnt);
+      else vqf_decide_body<T, MODE, 9, false, false>(keys, offs, stride, sg, seg_index, ws, recs, cnt);
+    }
+  } else {
+    vqf_decide_body<T, MODE, 14, false, false>(keys, offs, stride, sg, seg_index, ws, recs, cnt);
+  }
 }
 
 template <int MODE>
 __global__ __launch_bounds__(64) void vqf_decide(const uint8_t* __restrict__ keys,
                                                  const uint64_t* __restrict__ offs, uint32_t stride,
                                                  const tkv_amq_segment* __restrict__ segs,
-                                                 void* ws_base, uint32_t n_segs, int match_lds)
+                                                 void* ws_base, uint32_t n_segs, int flags)
 {
+  const bool match_lds = flags & 1, compact_ok = flags & 2;
   extern __shared__ __attribute__((aligned(16))) uint32_t s_cnt[];
   const tkv_amq_segment sg = segs[blockIdx.x];
   const VqfWorkspace ws = vqf_workspace(ws_base, n_segs);
   uint64_t* recs = vqf_records(ws, segs, n_segs);
   if (sg.tag_bits == 8)
-    vqf_decide_dispatch<8, MODE>(keys, offs, stride, sg, blockIdx.x, ws, recs, s_cnt, match_lds != 0);
+    vqf_decide_dispatch<8, MODE>(keys, offs, stride, sg, blockIdx.x, ws, recs, s_cnt, match_lds, compact_ok);
   else if (sg.tag_bits == 16)
-    vqf_decide_dispatch<16, MODE>(keys, offs, stride, sg, blockIdx.x, ws, recs, s_cnt, match_lds != 0);
+    vqf_decide_dispatch<16, MODE>(keys, offs, stride, sg, blockIdx.x, ws, recs, s_cnt, match_lds, compact_ok);
 }
 
 // One thread per key: moves the key's entry from its coalesced placement record into the
@@ -942,33 +958,64 @@ __device__ void vqf_place_fused_body(const tkv_amq_segment& sg, uint32_t seg_ind
   uint32_t* s_img = cnt + ((nb + 3) & ~3u);
   for (uint32_t b = tid; b < nb; b += kFusedThreads) cnt[b] = 0;
   __syncthreads();
-  // 16-byte loads (two records each), 8 in flight per thread: 32 KB per workgroup
-  const uint64_t a0 = sg.key_begin & ~1ull;  // records start 128-byte aligned in the workspace
-  const uint4* r2 = reinterpret_cast<const uint4*>(recs + a0);
-  const uint32_t lo_skip = (uint32_t)(sg.key_begin - a0);  // 0 or 1
-  const uint32_t n_pairs = (lo_skip + n + 1) / 2;
   const uint32_t gb0 = (uint32_t)sg.block_base;
-  constexpr uint32_t kU = 8;
-  auto put = [&](uint64_t v, uint32_t k) {
-    const uint32_t hi = (uint32_t)(v >> 32);
-    if (k >= lo_skip && k < lo_skip + n && hi != 0xffffffffu) {
-      const uint32_t blk = (hi >> 6) - gb0;
-      img[blk * C::kSlots + (hi & 63u)] = (E)((uint32_t)v & 0x7fffffffu);
-      atomicAdd(cnt + blk, 1u);
-    }
-  };
-  for (uint32_t p0 = 0; p0 < n_pairs; p0 += kFusedThreads * kU) {
-    uint4 v[kU];
+  constexpr uint32_t kU = 8;  // 16-byte loads in flight per thread: 32 KB per workgroup
+  if (T == 8 && nb <= 512) {
+    // compact 4-byte records (vqf_decide kCompact), four per load
+    const uint32_t* r32 = reinterpret_cast<const uint32_t*>(recs + sg.key_begin);
+    const uint32_t skip = (uint32_t)((reinterpret_cast<uintptr_t>(r32) & 15) >> 2);  // 0 or 2
+    const uint4* r4 = reinterpret_cast<const uint4*>(r32 - skip);
+    const uint32_t n_quads = (skip + n + 3) / 4;
+    auto put = [&](uint32_t v, uint32_t k) {
+      if (k >= skip && k < skip + n && v != 0xffffffffu) {
+        const uint32_t blk = v >> 21;
+        img[blk * C::kSlots + ((v >> 15) & 63u)] = (E)(v & 0x7fffu);
+        atomicAdd(cnt + blk, 1u);
+      }
+    };
+    for (uint32_t q0 = 0; q0 < n_quads; q0 += kFusedThreads * kU) {
+      uint4 v[kU];
 #pragma unroll
-    for (uint32_t u = 0; u < kU; ++u) {
-      const uint32_t p = p0 + u * kFusedThreads + tid;
-      v[u] = p < n_pairs ? load_nt16(r2 + p) : make_uint4(0, ~0u, 0, ~0u);
-    }
+      for (uint32_t u = 0; u < kU; ++u) {
+        const uint32_t q = q0 + u * kFusedThreads + tid;
+        v[u] = q < n_quads ? load_nt16(r4 + q) : make_uint4(~0u, ~0u, ~0u, ~0u);
+      }
 #pragma unroll
-    for (uint32_t u = 0; u < kU; ++u) {
-      const uint32_t k = 2 * (p0 + u * kFusedThreads + tid);
-      put((uint64_t)v[u].x | ((uint64_t)v[u].y << 32), k);
-      put((uint64_t)v[u].z | ((uint64_t)v[u].w << 32), k + 1);
+      for (uint32_t u = 0; u < kU; ++u) {
+        const uint32_t k = 4 * (q0 + u * kFusedThreads + tid);
+        put(v[u].x, k);
+        put(v[u].y, k + 1);
+        put(v[u].z, k + 2);
+        put(v[u].w, k + 3);
+      }
+    }
+  } else {
+    // 8-byte records, two per load; records start 128-byte aligned in the workspace
+    const uint64_t a0 = sg.key_begin & ~1ull;
+    const uint4* r2 = reinterpret_cast<const uint4*>(recs + a0);
+    const uint32_t lo_skip = (uint32_t)(sg.key_begin - a0);  // 0 or 1
+    const uint32_t n_pairs = (lo_skip + n + 1) / 2;
+    auto put = [&](uint64_t v, uint32_t k) {
+      const uint32_t hi = (uint32_t)(v >> 32);
+      if (k >= lo_skip && k < lo_skip + n && hi != 0xffffffffu) {
+        const uint32_t blk = (hi >> 6) - gb0;
+        img[blk * C::kSlots + (hi & 63u)] = (E)((uint32_t)v & 0x7fffffffu);
+        atomicAdd(cnt + blk, 1u);
+      }
+    };
+    for (uint32_t p0 = 0; p0 < n_pairs; p0 += kFusedThreads * kU) {
+      uint4 v[kU];
+#pragma unroll
+      for (uint32_t u = 0; u < kU; ++u) {
+        const uint32_t p = p0 + u * kFusedThreads + tid;
+        v[u] = p < n_pairs ? load_nt16(r2 + p) : make_uint4(0, ~0u, 0, ~0u);
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < kU; ++u) {
+        const uint32_t k = 2 * (p0 + u * kFusedThreads + tid);
+        put((uint64_t)v[u].x | ((uint64_t)v[u].y << 32), k);
+        put((uint64_t)v[u].z | ((uint64_t)v[u].w << 32), k + 1);
+      }
     }
   }
   __syncthreads();
@@ -1433,18 +1480,20 @@ int tkv_amq_build(int kind, const uint8_t* keys, const uint64_t* offs, uint32_t 
   if (hipMemsetAsync(d_ws, 0, 64, s) != hipSuccess) return TKV_AMQ_INTERNAL;
   // LDS: u32 block counts (+ the u64 lane-mask table when every leaf is small enough)
   const int match_lds = max_blocks <= kVqfMatchLdsBlocks;
+  const uint32_t fused_lds = vqf_fused_lds_bytes(max_blocks);
+  const bool fused = fused_lds <= kFusedLdsBudget;  // compact records are read only there
+  const int flags = match_lds | (fused ? 2 : 0);
   const size_t lds = 4ull * ((max_blocks + 1) & ~1u) + (match_lds ? 8ull * max_blocks : 0);
   if (mode == kKey16)
     hipLaunchKernelGGL(vqf_decide<kKey16>, dim3(n_segs), dim3(64), lds, s, keys, offs, stride,
-                       d_segs, d_ws, n_segs, match_lds);
+                       d_segs, d_ws, n_segs, flags);
   else if (mode == kKeyFixed)
     hipLaunchKernelGGL(vqf_decide<kKeyFixed>, dim3(n_segs), dim3(64), lds, s, keys, offs, stride,
-                       d_segs, d_ws, n_segs, match_lds);
+                       d_segs, d_ws, n_segs, flags);
   else
     hipLaunchKernelGGL(vqf_decide<kKeyVar>, dim3(n_segs), dim3(64), lds, s, keys, offs, stride,
-                       d_segs, d_ws, n_segs, match_lds);
-  const uint32_t fused_lds = vqf_fused_lds_bytes(max_blocks);
-  if (fused_lds <= kFusedLdsBudget) {
+                       d_segs, d_ws, n_segs, flags);
+  if (fused) {
     static std::once_flag lds_attr;
     std::call_once(lds_attr, [] {
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&vqf_place_fused),
