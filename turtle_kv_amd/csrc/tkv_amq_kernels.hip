@@ -785,6 +785,14 @@ __global__ __launch_bounds__(256) void vqf_scatter(const tkv_amq_segment* __rest
 // multiply, and the second pass takes each entry's slot with ds_add_rtn in insertion order.
 constexpr uint32_t kPlaceThreads = 128;
 
+// Per-block record stride in vqf_place_fused's LDS image: slots x entry bytes padded to an
+// 8-byte multiple whose dword count is 2 mod 4 (26 / 30 dwords), so the per-thread bucket
+// counters that later reuse the record spread over the banks.
+__host__ __device__ constexpr inline uint32_t vqf_lds_rec_stride(int t)
+{
+  return t == 8 ? 104u : 120u;
+}
+
 // kLds: the block records come from the leaf's LDS image (kSlots entries per block, counts in
 // lds_cnt) built by vqf_place_fused; otherwise from the workspace's 128-byte block records.
 // kLds: the bucket counters live in the block's own LDS record once it is in registers, so
@@ -828,7 +836,7 @@ __device__ void vqf_place_body(const tkv_amq_segment& sg, uint32_t seg_index, Vq
     const uint8_t* rec;
     uint32_t c;
     if constexpr (kLds) {
-      rec = lds_img + b * (C::kSlots * sizeof(E));
+      rec = lds_img + b * vqf_lds_rec_stride(T);
       c = lds_cnt[b];
     } else {
       rec = ws.temp + (sg.block_base + b) * kVqfTempStride;
@@ -836,11 +844,19 @@ __device__ void vqf_place_body(const tkv_amq_segment& sg, uint32_t seg_index, Vq
     }
     uint4 rv[kRecWords];
 #pragma unroll
-    for (uint32_t q = 0; q < kRecWords; ++q) rv[q] = reinterpret_cast<const uint4*>(rec)[q];
+    for (uint32_t q = 0; q < kRecWords; ++q) {
+      if constexpr (kLds) {  // 8-byte aligned records (padded stride)
+        const uint2 lo = reinterpret_cast<const uint2*>(rec)[2 * q];
+        const uint2 hi = reinterpret_cast<const uint2*>(rec)[2 * q + 1];
+        rv[q] = make_uint4(lo.x, lo.y, hi.x, hi.y);
+      } else {
+        rv[q] = reinterpret_cast<const uint4*>(rec)[q];
+      }
+    }
     const E* ent = reinterpret_cast<const E*>(rv);
     if constexpr (kLds) {
       asm volatile("" ::: "memory");  // the record is in registers before its bytes are reused
-      cnt = reinterpret_cast<uint32_t*>(lds_img + b * (C::kSlots * sizeof(E)));
+      cnt = reinterpret_cast<uint32_t*>(lds_img + b * vqf_lds_rec_stride(T));
     }
 
 #pragma unroll
@@ -936,7 +952,7 @@ constexpr uint32_t kFusedLdsBudget = 80 * 1024;
 
 __host__ __device__ inline uint32_t vqf_fused_img_bytes(uint32_t nb)
 {
-  return nb * 112u;  // max over T of kSlots * sizeof(Entry): 48 x 2 / 28 x 4
+  return nb * 120u;  // max over T of vqf_lds_rec_stride
 }
 
 __host__ __device__ inline uint32_t vqf_fused_lds_bytes(uint32_t max_nb)
@@ -969,7 +985,7 @@ __device__ void vqf_place_fused_body(const tkv_amq_segment& sg, uint32_t seg_ind
     auto put = [&](uint32_t v, uint32_t k) {
       if (k >= skip && k < skip + n && v != 0xffffffffu) {
         const uint32_t blk = v >> 21;
-        img[blk * C::kSlots + ((v >> 15) & 63u)] = (E)(v & 0x7fffu);
+        img[blk * (vqf_lds_rec_stride(T) / sizeof(E)) + ((v >> 15) & 63u)] = (E)(v & 0x7fffu);
         atomicAdd(cnt + blk, 1u);
       }
     };
@@ -999,7 +1015,7 @@ __device__ void vqf_place_fused_body(const tkv_amq_segment& sg, uint32_t seg_ind
       const uint32_t hi = (uint32_t)(v >> 32);
       if (k >= lo_skip && k < lo_skip + n && hi != 0xffffffffu) {
         const uint32_t blk = (hi >> 6) - gb0;
-        img[blk * C::kSlots + (hi & 63u)] = (E)((uint32_t)v & 0x7fffffffu);
+        img[blk * (vqf_lds_rec_stride(T) / sizeof(E)) + (hi & 63u)] = (E)((uint32_t)v & 0x7fffffffu);
         atomicAdd(cnt + blk, 1u);
       }
     };
