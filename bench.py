@@ -157,7 +157,7 @@ def main():
     probe = args.workload.startswith("probe")
     if probe:
         amq.build_all_filters(plan, kb, out=out, workspace=ws)
-        q, qseg = make_probe_queries(torch, amq, n, counts, dev, shard.key_begin)
+        q, qseg, is_hit = make_probe_queries(torch, amq, n, counts, dev, shard.key_begin)
         qb = amq.KeyBatch.fixed(q)
         res = torch.empty(q.shape[0], dtype=torch.uint8, device=dev)
 
@@ -216,12 +216,12 @@ def main():
     fpr = None
     if probe:
         alg_bytes = q.shape[0] * (16 + 4 + 1)
-        r2 = res.view(-1, 2)
-        if not bool(r2[:, 0].all()):
-            bad = torch.nonzero(r2[:, 0] == 0).flatten()
-            raise SystemExit(f"false negatives in the probe: {bad.numel()} of {r2.shape[0]} hits, "
-                             f"first key indices {bad[:8].tolist()}")
-        fpr = float(r2[:, 1].float().mean())
+        hit_res = res[is_hit]
+        if not bool(hit_res.all()):
+            bad = torch.nonzero(hit_res == 0).flatten()
+            raise SystemExit(f"false negatives in the probe: {bad.numel()} of {hit_res.numel()} "
+                             f"hits, first indices {bad[:8].tolist()}")
+        fpr = float(res[~is_hit].float().mean())
     else:
         alg_bytes = n * key_bytes + int(plan.segs["payload_bytes"].astype(np.int64).sum())
     achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
@@ -351,19 +351,46 @@ def _sort_leaves(torch, keys, counts):
     return keys[idx]
 
 
+def _lsr(x, s):
+    """logical right shift of an int64 tensor"""
+    return (x >> s) & ((1 << (64 - s)) - 1)
+
+
+def _s64(c):
+    return c - (1 << 64) if c >= 1 << 63 else c
+
+
+def splitmix_keys16(torch, seed, idx):
+    """Key idx[i] of oracle/tkv_amq_oracle.c tkvo_gen_keys16 (== turtle_kv_amd.gen_keys16),
+    computed elementwise: (splitmix64_at(seed, 2g+1), splitmix64_at(seed, 2g+2)), little
+    endian.  `seed` is an int or an int64 tensor like idx."""
+    def at(n):
+        z = seed + n * _s64(0x9E3779B97F4A7C15)
+        z = (z ^ _lsr(z, 30)) * _s64(0xBF58476D1CE4E5B9)
+        z = (z ^ _lsr(z, 27)) * _s64(0x94D049BB133111EB)
+        return z ^ _lsr(z, 31)
+    w = torch.stack([at(2 * idx + 1), at(2 * idx + 2)], dim=1)
+    return w.view(torch.uint8).reshape(idx.shape[0], 16)
+
+
 def make_probe_queries(torch, amq, n, counts, dev, key_begin):
-    """BASELINE config 4: n hits (the inserted keys, each probing its own leaf) + n misses
-    (seed 43 keys, probing a seed-44 random leaf), interleaved."""
-    hits = amq.gen_keys16(42, key_begin, n, device=dev)
-    miss = amq.gen_keys16(43, key_begin, n, device=dev)
-    q = torch.stack([hits, miss], dim=1).reshape(2 * n, 16).contiguous()
+    """BASELINE config 4: n hits (the inserted keys, each probing its own
+    leaf) + n misses (seed 43 keys, each probing a random leaf), shuffled with seed 44.
+    The shuffled keys are generated in place (no 3.2 GB row gather: torch's index kernels
+    returned wrong rows on multi-GB uint8 tensors on this ROCm build, see
+    sort_segments_device)."""
     seg_hit = torch.repeat_interleave(torch.arange(len(counts), device=dev, dtype=torch.int32),
                                       torch.tensor(counts, device=dev))
     g = torch.Generator(device=dev)
     g.manual_seed(44)
     seg_miss = torch.randint(0, len(counts), (n,), device=dev, dtype=torch.int32, generator=g)
-    qs = torch.stack([seg_hit, seg_miss], dim=1).reshape(-1).contiguous()
-    return q, qs
+    perm = torch.randperm(2 * n, device=dev, generator=g)
+    is_hit = perm < n
+    gi = torch.where(is_hit, perm, perm - n) + key_begin
+    seed = torch.where(is_hit, 42, 43).to(torch.int64)
+    q = splitmix_keys16(torch, seed, gi).contiguous()
+    qs = torch.cat([seg_hit, seg_miss])[perm].contiguous()
+    return q, qs, is_hit
 
 
 def end_to_end(torch, amq, kind, bpk, cap, counts, keys, iters=3):

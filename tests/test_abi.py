@@ -112,3 +112,17 @@ def test_device_calls_fail_loudly_without_gpu(amq):
     assert amq.abi.lib().tkv_amq_probe(0, None, None, 0, None, None, 16, 0, None, None, None) == 14
     with pytest.raises(amq.TkvAmqError):
         amq.gen_keys16(42, 0, 16)
+
+
+def test_bench_splitmix_keys_match_oracle(oracle):
+    """bench.py's elementwise key generator (shuffled probe queries) == the oracle's keys."""
+    import numpy as np
+    import torch
+    import bench
+    idx = torch.tensor([0, 1, 2, 77, 123456, 99_999_999], dtype=torch.int64)
+    got = bench.splitmix_keys16(torch, 42, idx).numpy()
+    for r, i in enumerate(idx.tolist()):
+        assert np.array_equal(got[r], oracle.gen_keys16(42, i, 1)[0])
+    seed = torch.tensor([43] * len(idx), dtype=torch.int64)
+    got = bench.splitmix_keys16(torch, seed, idx).numpy()
+    assert np.array_equal(got[3], oracle.gen_keys16(43, 77, 1)[0])

@@ -1080,6 +1080,19 @@ __device__ inline VqfBucketRef<T> vqf_bucket_ref(const uint8_t* blocks, uint32_t
   return r;
 }
 
+// exact per-byte / per-halfword equality mask (high bit of each lane set where x's lane is 0)
+__device__ inline uint32_t zero_bytes(uint32_t x)
+{
+  return ~(((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x | 0x7f7f7f7fu);
+}
+__device__ inline uint32_t zero_halves(uint32_t x)
+{
+  return ~(((x & 0x7fff7fffu) + 0x7fff7fffu) | x | 0x7fff7fffu);
+}
+
+// Tags of bucket o are slots [start, end).  One 16-byte load of the tag area starting at the
+// dword that holds slot `start` covers the bucket in almost every case (a bucket holds ~0.6
+// tags on average); longer buckets finish with a per-slot loop.
 template <int T>
 __device__ inline bool vqf_bucket_has(const VqfBucketRef<T>& r, uint32_t tag)
 {
@@ -1087,8 +1100,35 @@ __device__ inline bool vqf_bucket_has(const VqfBucketRef<T>& r, uint32_t tag)
   const int o = (int)r.o;
   const int start = o == 0 ? 0 : select128(r.lo, r.hi, o - 1) - (o - 1);
   const int end = select128(r.lo, r.hi, o) - o;
-  bool hit = false;
-  for (int p = start; p < end; ++p) {
+  if (end <= start) return false;
+  constexpr int kPer = 4 / (T / 8);                     // slots per dword: 4 / 2
+  const int d0 = start / kPer;                          // first dword of the window
+  const int last_dword = (C::kSlots * (T / 8)) / 4 - 1; // 11 / 13
+  const int d = d0 + 3 <= last_dword ? d0 : last_dword - 3;
+  const uint4 w = *reinterpret_cast<const uint4*>(r.bp + C::kMdBytes + 4 * d);
+  const int s0 = start - d * kPer, s1 = end - d * kPer;  // window-relative slot range
+  const uint32_t rep = T == 8 ? tag * 0x01010101u : tag * 0x00010001u;
+  uint32_t m[4];
+  const uint32_t wv[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) m[i] = T == 8 ? zero_bytes(wv[i] ^ rep) : zero_halves(wv[i] ^ rep);
+  // pack one bit per slot: slot j of the window <-> bit j
+  uint32_t bits = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if constexpr (T == 8) {
+      const uint32_t b4 = ((m[i] >> 7) & 1u) | ((m[i] >> 14) & 2u) | ((m[i] >> 21) & 4u) | ((m[i] >> 28) & 8u);
+      bits |= b4 << (4 * i);
+    } else {
+      const uint32_t b2 = ((m[i] >> 15) & 1u) | ((m[i] >> 30) & 2u);
+      bits |= b2 << (2 * i);
+    }
+  }
+  constexpr int kWin = 4 * kPer;  // 16 / 8 slots
+  const int hi_in = s1 < kWin ? s1 : kWin;
+  const uint32_t range = (hi_in > s0 ? ((1u << (hi_in - s0)) - 1u) : 0u) << s0;
+  bool hit = (bits & range) != 0;
+  for (int p = d * kPer + kWin; p < end; ++p) {  // rare: bucket runs past the window
     uint32_t tv;
     if constexpr (T == 8) tv = r.bp[C::kMdBytes + p];
     else tv = *reinterpret_cast<const uint16_t*>(r.bp + C::kMdBytes + 2 * p);
