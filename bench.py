@@ -40,7 +40,11 @@ WORKLOADS = {
     "probe10": (0, 10, 0, "Bloom @10 probe, 50% hits"),
     "probe_vqf12": (1, 12, 32704, "VQF @12 probe, 50% hits"),
     "bloom10k24": (0, 10, 0, "Bloom @10 bits/key, 24-byte keys (TurtleKV default key size)"),
+    "bloom10mono": (0, 10, 0, "Bloom @10 bits/key, one monolithic filter per GPU"),
 }
+# workloads whose one filter spans every key of the GPU (the monolithic
+# single-filter Bloom variant)
+MONOLITHIC = {"bloom10mono"}
 KEY_BYTES = {"bloom10k24": 24}
 
 
@@ -51,6 +55,9 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="bloom10", choices=sorted(WORKLOADS))
     ap.add_argument("--keys-per-gpu", type=int, default=100_000_000)
+    ap.add_argument("--leaf-keys", type=int, default=None,
+                    help=f"keys per leaf filter (default {SEG_KEYS}; monolithic workloads: all "
+                         "keys of the GPU)")
     ap.add_argument("--total-keys", type=int, default=None,
                     help="strong scaling: one checkpoint of this many keys split over the "
                          "ranks by leaf range (BASELINE config 5: --workload bloom12 "
@@ -66,12 +73,12 @@ def parse():
     return ap.parse_args()
 
 
-def segment_counts(n_keys):
-    full, rem = divmod(n_keys, SEG_KEYS)
-    return [SEG_KEYS] * full + ([rem] if rem else [])
+def segment_counts(n_keys, leaf_keys=SEG_KEYS):
+    full, rem = divmod(n_keys, leaf_keys)
+    return [leaf_keys] * full + ([rem] if rem else [])
 
 
-def cpu_baseline(kind, bpk, cap, keys_host, counts, threads):
+def cpu_baseline(kind, bpk, cap, keys_host, counts, threads, leaf_keys=SEG_KEYS):
     """Oracle (C, -O3, one filter per thread at a time, leaves spread over `threads` workers
     like TreeSerializeContext::build_all_pages) over the same keys; bounded to <= ~20 s."""
     from oracle import oracle as O
@@ -97,12 +104,16 @@ def cpu_baseline(kind, bpk, cap, keys_host, counts, threads):
     n0, t0 = run(probe_segs)
     rate = n0 / max(t0, 1e-9)
     target_keys = min(int(sum(counts)), int(rate * 10.0))
-    ns = n_segs if target_keys >= sum(counts) else max(probe_segs, target_keys // SEG_KEYS)
-    nk, dt = run(ns)
-    return {"value": round(nk / dt / 1e6, 2), "unit": "Mkeys/s", "cores": threads,
+    ns = n_segs if target_keys >= sum(counts) else max(probe_segs, target_keys // leaf_keys)
+    if ns == probe_segs:
+        nk, dt = n0, t0
+    else:
+        nk, dt = run(ns)
+    used = min(threads, ns)  # one filter per thread at a time
+    return {"value": round(nk / dt / 1e6, 2), "unit": "Mkeys/s", "cores": used,
             "kind": "port",
-            "sample": f"{ns} leaves x {SEG_KEYS} keys ({nk} keys) of the same workload, C oracle "
-                      f"(oracle/tkv_amq_oracle.c, -O3 -march=x86-64-v3), {threads} threads, "
+            "sample": f"{ns} leaves x {leaf_keys} keys ({nk} keys) of the same workload, C oracle "
+                      f"(oracle/tkv_amq_oracle.c, -O3 -march=x86-64-v3), {used} threads, "
                       f"{dt:.2f} s wall"}
 
 
@@ -124,16 +135,19 @@ def main():
     kind, bpk, cap, label = WORKLOADS[args.workload]
     from turtle_kv_amd import dist as tdist
     strong = args.total_keys is not None
+    leaf_keys = args.leaf_keys or SEG_KEYS
+    if args.workload in MONOLITHIC and args.leaf_keys is None:
+        leaf_keys = args.total_keys // world if strong else args.keys_per_gpu
     if strong:
         # strong scaling: one checkpoint of --total-keys keys; rank r builds its leaf range
-        all_counts = segment_counts(args.total_keys)
+        all_counts = segment_counts(args.total_keys, leaf_keys)
     else:
         # weak scaling: the checkpoint has `world` x (this GPU's leaves)
-        all_counts = segment_counts(args.keys_per_gpu) * world
+        all_counts = segment_counts(args.keys_per_gpu, leaf_keys) * world
     # rank r builds the contiguous leaf range turtle_kv_amd.dist.shard_leaves gives it, at a
     # fixed per-leaf stride so leaf s sits at s * stride in the all-gathered array
     shard = tdist.shard_leaves(all_counts, world, rank)
-    stride = tdist.leaf_stride(kind, bpk, SEG_KEYS, cap)
+    stride = tdist.leaf_stride(kind, bpk, max(all_counts), cap)
     plan = tdist.plan_shard(kind, all_counts, bpk, shard, stride, payload_capacity=cap)
     counts = all_counts[shard.leaf_begin:shard.leaf_end]
     n = shard.key_end - shard.key_begin
@@ -250,7 +264,7 @@ def main():
 
     e2e = None
     if (rank == 0 and world == 1 and not args.no_e2e and not probe and key_bytes == 16
-            and n <= 200_000_000):
+            and n <= 200_000_000 and args.workload not in MONOLITHIC):
         e2e = end_to_end(torch, amq, kind, bpk, cap, counts, keys)
 
     if world > 1:
@@ -265,10 +279,11 @@ def main():
             base = None
         else:
             # the CPU sample is bounded (~10 s); copy at most the first 100M keys to the host
-            nk_host = sum(counts[:100_000_000 // SEG_KEYS]) if n > 100_000_000 else n
+            lim = max(1, 100_000_000 // leaf_keys)
+            nk_host = sum(counts[:lim]) if n > 100_000_000 else n
             base = cpu_baseline(kind, bpk, cap, keys[:nk_host].cpu().numpy(),
-                                counts[:100_000_000 // SEG_KEYS] if n > 100_000_000 else counts,
-                                args.cpu_threads)
+                                counts[:lim] if n > 100_000_000 else counts,
+                                args.cpu_threads, leaf_keys)
 
     line = {
         "metric": f"filter-build Mkeys/s (device-resident), 16B keys @10 bits/key; bit-exact"
@@ -287,8 +302,8 @@ def main():
         "data": "synthetic (splitmix64 seed 42 keys generated on the device)",
         "config": {"workload": (f"{label}: {total_keys} x {key_bytes}B keys over {world} GPU(s)"
                                 if strong else f"{label}: {n} x {key_bytes}B keys per GPU")
-                               + f", {SEG_KEYS}-key leaves ({len(counts)} filters on rank 0)",
-                   "keys_per_gpu": n, "total_keys": total_keys, "key_bytes": key_bytes, "leaf_keys": SEG_KEYS, "bits_per_key": bpk,
+                               + f", {leaf_keys}-key leaves ({len(counts)} filters on rank 0)",
+                   "keys_per_gpu": n, "total_keys": total_keys, "key_bytes": key_bytes, "leaf_keys": leaf_keys, "bits_per_key": bpk,
                    "filter": "bloom-blocked512" if kind == 0 else "vqf",
                    "parallelism": f"leaf-sharded x{world}"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,

@@ -222,13 +222,37 @@ def test_vqf_hash_matches_xxhash(amq, torch):
     assert [int(x) for x in h16] == [xxhash.xxh64_intdigest(k.tobytes(), VQF_SEED) for k in k16]
 
 
-def test_bloom_monolithic_global_path(oracle, amq, torch):
-    # one filter larger than the LDS image budget (64 KiB) -> global-atomic build kernel
-    n = 120000
-    keys = oracle.gen_keys16(8, 0, n)
+@pytest.mark.parametrize("n,bpk,seed", [(120000, 10, 8), (3000000, 10, 9), (1500000, 12, 10),
+                                         (400000, 5, 11), (10000, 64, 12)])
+def test_bloom_monolithic_partitioned(oracle, amq, torch, n, bpk, seed):
+    """One filter larger than the LDS image budget (64 KiB): tiled build over keys partitioned
+    by tile (bloom_part_keys / bloom_tile_build), byte-identical to the oracle.  Covers a
+    ragged last tile, k = 7 / 8 / generic, and 58 tiles over 733 partition workgroups."""
+    keys = oracle.gen_keys16(seed, 0, n)
+    ref = oracle_per_segment(oracle, 0, keys, [n], bpk)
+    plan, out = gpu_build(amq, torch, 0, torch.from_numpy(keys).cuda(), [n], bpk)
+    assert plan.max_seg_blocks * 64 > 64 * 1024
+    assert plan.workspace_bytes >= 16 * n  # the partitioned path's workspace
+    assert_same(plan, out, ref)
+
+
+def test_bloom_monolithic_duplicate_keys(oracle, amq, torch):
+    """Every key identical (one tile receives the whole batch) and a few distinct ones."""
+    n = 200000
+    keys = np.repeat(oracle.gen_keys16(13, 0, 1), n, axis=0)
+    keys[::50000] = oracle.gen_keys16(14, 0, len(keys[::50000]))
     ref = oracle_per_segment(oracle, 0, keys, [n], 10)
     plan, out = gpu_build(amq, torch, 0, torch.from_numpy(keys).cuda(), [n], 10)
-    assert plan.max_seg_blocks * 64 > 64 * 1024
+    assert_same(plan, out, ref)
+
+
+def test_bloom_oversize_leaf_in_batch_global_path(oracle, amq, torch):
+    """A multi-leaf batch holding a leaf beyond the LDS budget takes the device-atomic path."""
+    counts = [120000, 500, 16384]
+    keys = oracle.gen_keys16(15, 0, sum(counts))
+    ref = oracle_per_segment(oracle, 0, keys, counts, 10)
+    plan, out = gpu_build(amq, torch, 0, torch.from_numpy(keys).cuda(), counts, 10)
+    assert plan.workspace_bytes == 0
     assert_same(plan, out, ref)
 
 

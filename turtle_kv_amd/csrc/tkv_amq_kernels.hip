@@ -22,6 +22,7 @@
 #include <math.h>
 #include <stdint.h>
 #include <string.h>
+#include <stdlib.h>
 
 #include "tkv_amq.h"
 #include "tkv_amq_device.h"
@@ -108,12 +109,15 @@ __device__ inline void write_bloom_header(uint8_t* payload, const tkv_amq_segmen
   reinterpret_cast<ulonglong2*>(payload)[part] = v;
 }
 
+// `first`: block index of s_bits[0] (0 for a whole leaf image; a tile's first block for the
+// monolithic build's tile images)
 template <int K>
-__device__ inline void bloom_insert16(uint32_t* s_bits, uint32_t nb, uint32_t k, const uint4& kv)
+__device__ inline void bloom_insert16(uint32_t* s_bits, uint32_t nb, uint32_t k, const uint4& kv,
+                                      uint32_t first)
 {
   const Xxh16 x((uint64_t)kv.x | ((uint64_t)kv.y << 32), (uint64_t)kv.z | ((uint64_t)kv.w << 32));
   const uint64_t h0 = x.finish(c_bloom.rhinit16[0]);
-  uint32_t* blk = s_bits + 16 * (uint32_t)__umul64hi(h0, (uint64_t)nb);
+  uint32_t* blk = s_bits + 16 * ((uint32_t)__umul64hi(h0, (uint64_t)nb) - first);
   lds_set_bit(blk, (uint32_t)h0 & 511u);
   if constexpr (K != 0) {
 #pragma unroll
@@ -123,23 +127,23 @@ __device__ inline void bloom_insert16(uint32_t* s_bits, uint32_t nb, uint32_t k,
   }
 }
 
-template <int K>
+template <int K, uint32_t NT = 256>
 __device__ inline void bloom_keys16_lds(const uint4* __restrict__ kp, uint32_t n, uint32_t nb,
-                                        uint32_t k, uint32_t* s_bits)
+                                        uint32_t k, uint32_t* s_bits, uint32_t first = 0)
 {
   const uint32_t tid = threadIdx.x;
   constexpr int U = 4;  // 4 x 16-byte loads in flight per lane
-  for (uint32_t base = 0; base < n; base += 256 * U) {
+  for (uint32_t base = 0; base < n; base += NT * U) {
     uint4 kv[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const uint32_t i = base + u * 256 + tid;
+      const uint32_t i = base + u * NT + tid;
       if (i < n) kv[u] = kp[i];
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const uint32_t i = base + u * 256 + tid;
-      if (i < n) bloom_insert16<K>(s_bits, nb, k, kv[u]);
+      const uint32_t i = base + u * NT + tid;
+      if (i < n) bloom_insert16<K>(s_bits, nb, k, kv[u], first);
     }
   }
 }
@@ -294,6 +298,200 @@ __global__ __launch_bounds__(256) void bloom_global_set(const uint8_t* __restric
       }
     }
   }
+}
+
+// ---------------------------------------------------------------------------------------
+// Bloom build, monolithic filter (one filter larger than the LDS budget, 16-byte keys:
+// SURVEY.md 8(d)'s single-filter variant; the reference's build_bloom_filter_page over one
+// item range, tree/filter_builder.hpp:126-135).  The filter is cut into tiles of
+// kBloomTileBlocks 512-bit blocks (64 KiB, one LDS image each) and the keys are partitioned
+// by tile before each tile is built in LDS exactly like a leaf:
+//   bloom_part_count      P workgroups over contiguous key ranges: h0 -> tile, LDS
+//                         histogram, one row of H[P][n_tiles]
+//   bloom_part_scan_cols  per tile: exclusive scan of its column of H (each workgroup's
+//                         offset inside the tile's bucket) and the tile total
+//   bloom_part_scan_tiles exclusive scan of the tile totals (bucket bases)
+//   bloom_part_scatter    the same key ranges again: h0 -> tile, an LDS cursor gives the
+//                         key's slot in its tile's bucket; the 16-byte key is copied there
+//   bloom_tile_build      one 512-thread workgroup per tile: the bucket's keys through the
+//                         leaf kernel's k-hash LDS insert, then 16-byte stores of the image
+// The bits set do not depend on the order of keys inside a bucket, so the filter is
+// byte-identical to the leaf kernel's and the oracle's.  Device atomics (bloom_global_set,
+// one 4-byte memory-side atomic per bit) ran at 3.6 Gkeys/s on 100M keys.
+// ---------------------------------------------------------------------------------------
+constexpr uint32_t kBloomTileBlocks = 1024;     // 64 KiB LDS image per tile
+constexpr uint32_t kBloomPartMaxTiles = 32768;  // LDS histogram / cursors <= 128 KiB
+constexpr uint32_t kBloomPartMaxWgs = 1024;    // (256 / 512 / 128 measured slower)
+constexpr uint32_t kBloomTileThreads = 1024;    // 2 workgroups per CU (512: 6% slower)
+
+struct BloomPartGeom {
+  uint32_t P;         // partition workgroups
+  uint32_t n_tiles;
+  uint32_t per;       // keys per partition workgroup
+  uint64_t h_words;   // P * n_tiles
+  uint64_t part_off;  // byte offset of the partitioned keys in the workspace
+  uint64_t bytes;     // workspace bytes
+};
+
+__host__ __device__ inline BloomPartGeom bloom_part_geom(uint64_t n_keys, uint64_t nb)
+{
+  BloomPartGeom g;
+  g.n_tiles = (uint32_t)((nb + kBloomTileBlocks - 1) / kBloomTileBlocks);
+  uint64_t p = (n_keys + 4095) / 4096;
+  g.P = (uint32_t)(p < 1 ? 1 : (p > kBloomPartMaxWgs ? kBloomPartMaxWgs : p));
+  g.per = (uint32_t)((n_keys + g.P - 1) / g.P);
+  g.h_words = (uint64_t)g.P * g.n_tiles;
+  // [H: P x n_tiles u32][tile totals: n_tiles u32][bucket bases: n_tiles + 1 u32][keys]
+  g.part_off = (4 * (g.h_words + 2ull * g.n_tiles + 1) + 255) & ~255ull;
+  g.bytes = g.part_off + 16 * n_keys;
+  return g;
+}
+
+__device__ inline uint32_t bloom_tile_of(const uint4& kv, uint32_t nb)
+{
+  const Xxh16 x((uint64_t)kv.x | ((uint64_t)kv.y << 32), (uint64_t)kv.z | ((uint64_t)kv.w << 32));
+  const uint64_t h0 = x.finish(c_bloom.rhinit16[0]);
+  return (uint32_t)__umul64hi(h0, (uint64_t)nb) / kBloomTileBlocks;
+}
+
+// PASS 0: histogram; PASS 1: scatter.  Both walk the same key range in the same way.
+template <int PASS>
+__global__ __launch_bounds__(256) void bloom_part_keys(const uint4* __restrict__ keys,
+                                                       const tkv_amq_segment* __restrict__ segs,
+                                                       uint32_t* __restrict__ ws, uint32_t n_tiles,
+                                                       uint32_t per, uint64_t part_off)
+{
+  extern __shared__ uint32_t s_tile[];
+  const tkv_amq_segment sg = segs[0];
+  const uint32_t tid = threadIdx.x, w = blockIdx.x;
+  uint32_t* H = ws + (uint64_t)w * n_tiles;
+  const uint32_t* base = ws + (uint64_t)gridDim.x * n_tiles + n_tiles;
+  for (uint32_t t = tid; t < n_tiles; t += 256) s_tile[t] = PASS == 0 ? 0u : base[t] + H[t];
+  __syncthreads();
+  const uint32_t n = sg.n_keys, nb = sg.n_blocks;
+  const uint32_t b = min(n, w * per), e = min(n, b + per);
+  const uint4* kp = keys + sg.key_begin;
+  uint4* part = reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(ws) + part_off);
+  constexpr int U = 4;
+  for (uint32_t i0 = b; i0 < e; i0 += 256 * U) {
+    uint4 kv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t i = i0 + u * 256 + tid;
+      if (i < e) kv[u] = load_nt16(kp + i);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t i = i0 + u * 256 + tid;
+      if (i < e) {
+        const uint32_t t = bloom_tile_of(kv[u], nb);
+        if constexpr (PASS == 0) {
+          atomicAdd(s_tile + t, 1u);
+        } else {
+          const uint32_t slot = atomicAdd(s_tile + t, 1u);
+          part[slot] = kv[u];
+        }
+      }
+    }
+  }
+  if constexpr (PASS == 0) {
+    __syncthreads();
+    for (uint32_t t = tid; t < n_tiles; t += 256) H[t] = s_tile[t];
+  }
+}
+
+// exclusive scan of 256 per-thread values in a 256-thread block; returns this thread's prefix
+// and sets *total
+__device__ inline uint32_t block_exclusive_scan256(uint32_t v, uint32_t* s, uint32_t* total)
+{
+  const uint32_t tid = threadIdx.x;
+  s[tid] = v;
+  __syncthreads();
+  for (uint32_t d = 1; d < 256; d <<= 1) {
+    const uint32_t a = tid >= d ? s[tid - d] : 0u;
+    __syncthreads();
+    s[tid] += a;
+    __syncthreads();
+  }
+  *total = s[255];
+  const uint32_t r = s[tid] - v;
+  __syncthreads();
+  return r;
+}
+
+// One workgroup per tile: H[w][t] <- sum of H[w'][t] over w' < w; totals[t] <- column sum.
+__global__ __launch_bounds__(256) void bloom_part_scan_cols(uint32_t* __restrict__ ws, uint32_t P,
+                                                            uint32_t n_tiles)
+{
+  __shared__ uint32_t s[256];
+  const uint32_t t = blockIdx.x, tid = threadIdx.x;
+  constexpr uint32_t R = kBloomPartMaxWgs / 256;  // rows per thread
+  uint32_t v[R];
+  uint32_t sum = 0;
+#pragma unroll
+  for (uint32_t r = 0; r < R; ++r) {
+    const uint32_t w = tid * R + r;
+    v[r] = w < P ? ws[(uint64_t)w * n_tiles + t] : 0u;
+    sum += v[r];
+  }
+  uint32_t total;
+  uint32_t run = block_exclusive_scan256(sum, s, &total);
+#pragma unroll
+  for (uint32_t r = 0; r < R; ++r) {
+    const uint32_t w = tid * R + r;
+    if (w < P) ws[(uint64_t)w * n_tiles + t] = run;
+    run += v[r];
+  }
+  if (tid == 0) ws[(uint64_t)P * n_tiles + t] = total;
+}
+
+// One workgroup: bases[t] = sum of totals[t'] over t' < t, bases[n_tiles] = key count.
+__global__ __launch_bounds__(256) void bloom_part_scan_tiles(uint32_t* __restrict__ ws, uint32_t P,
+                                                             uint32_t n_tiles)
+{
+  __shared__ uint32_t s[256];
+  const uint32_t* tot = ws + (uint64_t)P * n_tiles;
+  uint32_t* base = ws + (uint64_t)P * n_tiles + n_tiles;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t per = (n_tiles + 255) / 256;  // consecutive tiles per thread
+  const uint32_t t0 = min(n_tiles, tid * per), t1 = min(n_tiles, t0 + per);
+  uint32_t sum = 0;
+  for (uint32_t t = t0; t < t1; ++t) sum += tot[t];
+  uint32_t total;
+  uint32_t run = block_exclusive_scan256(sum, s, &total);
+  for (uint32_t t = t0; t < t1; ++t) {
+    base[t] = run;
+    run += tot[t];
+  }
+  if (tid == 0) base[n_tiles] = total;
+}
+
+// One workgroup per tile of the monolithic filter (segment 0).
+template <uint32_t NT>
+__global__ __launch_bounds__(NT) void bloom_tile_build(
+    const tkv_amq_segment* __restrict__ segs, const uint32_t* __restrict__ ws, uint32_t P,
+    uint32_t n_tiles, uint64_t part_off, uint8_t* __restrict__ out)
+{
+  extern __shared__ uint32_t s_bits[];
+  const tkv_amq_segment sg = segs[0];
+  const uint32_t t = blockIdx.x, tid = threadIdx.x;
+  const uint32_t nb = sg.n_blocks, k = sg.hash_count;
+  const uint32_t first = t * kBloomTileBlocks;
+  const uint32_t tb = min(kBloomTileBlocks, nb - first);
+  for (uint32_t w = tid; w < tb * 16; w += NT) s_bits[w] = 0;
+  __syncthreads();
+  const uint32_t* base = ws + (uint64_t)P * n_tiles + n_tiles;
+  const uint32_t kb = base[t], ke = base[t + 1];
+  const uint4* kp = reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(ws) + part_off) + kb;
+  if (k == 7) bloom_keys16_lds<7, NT>(kp, ke - kb, nb, k, s_bits, first);
+  else if (k == 8) bloom_keys16_lds<8, NT>(kp, ke - kb, nb, k, s_bits, first);
+  else bloom_keys16_lds<0, NT>(kp, ke - kb, nb, k, s_bits, first);
+  __syncthreads();
+  uint8_t* payload = out + sg.out_offset;
+  if (t == 0 && tid < 4) write_bloom_header(payload, sg, tid);
+  uint4* dst = reinterpret_cast<uint4*>(payload + kBloomHeader + 64ull * first);
+  const uint4* src = reinterpret_cast<const uint4*>(s_bits);
+  for (uint32_t q = tid; q < tb * 4; q += NT) dst[q] = src[q];
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1337,6 +1535,14 @@ inline hipStream_t as_stream(void* s) { return static_cast<hipStream_t>(s); }
 
 inline uint64_t div_up(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
 
+// a one-filter Bloom batch too large for one LDS image takes the tiled, partitioned build
+// (it needs a workspace of bloom_part_geom(n_keys, n_blocks).bytes and 16-byte keys)
+inline bool bloom_partitioned(uint32_t n_segs, uint64_t max_blocks, uint64_t n_keys)
+{
+  return n_segs == 1 && 64 * max_blocks > kBloomLdsBudget && n_keys <= 0xffffffffull &&
+         div_up(max_blocks, kBloomTileBlocks) <= kBloomPartMaxTiles;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1474,6 +1680,8 @@ int tkv_amq_plan(int kind, const uint64_t* counts, const uint64_t* src_ids, uint
     *ws_bytes = 0;
     if (kind == TKV_AMQ_VQF && bpk != 0)
       *ws_bytes = vqf_temp_offset(n_segs) + kVqfTempStride * block_base + 8 * key_begin + 64;
+    if (kind == TKV_AMQ_BLOOM && bloom_partitioned(n_segs, max_blocks, key_begin))
+      *ws_bytes = bloom_part_geom(key_begin, max_blocks).bytes;  // 16-byte keys
   }
   if (max_blocks_out) *max_blocks_out = max_blocks;
   return TKV_AMQ_OK;
@@ -1509,7 +1717,36 @@ int tkv_amq_build(int kind, const uint8_t* keys, const uint64_t* offs, uint32_t 
       else
         hipLaunchKernelGGL(bloom_build_lds<kKeyVar>, grid, block, lds, s, keys, offs, stride, d_segs,
                            d_out);
+      return hipGetLastError() == hipSuccess ? TKV_AMQ_OK : TKV_AMQ_INTERNAL;
+    }
+    const BloomPartGeom pg = bloom_part_geom(n_keys, max_blocks);
+    if (bloom_partitioned(n_segs, max_blocks, n_keys) && mode == kKey16 && d_ws &&
+        ws_bytes >= pg.bytes) {
+      // one monolithic filter: partition the keys by tile, build every tile in LDS
+      static std::once_flag lds_attr;
+      std::call_once(lds_attr, [] {
+        const int cap = (int)(4 * kBloomPartMaxTiles);
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&bloom_part_keys<0>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, cap);
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&bloom_part_keys<1>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, cap);
+      });
+      uint32_t* w = static_cast<uint32_t*>(d_ws);
+      const uint4* k4 = reinterpret_cast<const uint4*>(keys);
+      const size_t hl = 4ull * pg.n_tiles;
+      hipLaunchKernelGGL(bloom_part_keys<0>, dim3(pg.P), dim3(256), hl, s, k4, d_segs, w,
+                         pg.n_tiles, pg.per, pg.part_off);
+      hipLaunchKernelGGL(bloom_part_scan_cols, dim3(pg.n_tiles), dim3(256), 0, s, w, pg.P,
+                         pg.n_tiles);
+      hipLaunchKernelGGL(bloom_part_scan_tiles, dim3(1), dim3(256), 0, s, w, pg.P, pg.n_tiles);
+      hipLaunchKernelGGL(bloom_part_keys<1>, dim3(pg.P), dim3(256), hl, s, k4, d_segs, w,
+                         pg.n_tiles, pg.per, pg.part_off);
+      hipLaunchKernelGGL(bloom_tile_build<kBloomTileThreads>, dim3(pg.n_tiles),
+                         dim3(kBloomTileThreads), 64ull * kBloomTileBlocks, s, d_segs, w, pg.P,
+                         pg.n_tiles, pg.part_off, d_out);
     } else {
+      // leaves beyond the LDS budget in a multi-leaf batch, or keys that are not 16 bytes:
+      // device atomics
       const dim3 g1(n_segs), b(256);
       hipLaunchKernelGGL(bloom_global_init, g1, b, 0, s, d_segs, d_out);
       const uint32_t g2 = (uint32_t)(div_up(n_keys, 256) < 8192 ? div_up(n_keys, 256) : 8192);
