@@ -63,6 +63,9 @@ def parse():
                          "ranks by leaf range (BASELINE config 5: --workload bloom12 "
                          "--total-keys 1000000000)")
     ap.add_argument("--allgather", action="store_true", help="time the RCCL all-gather in-step")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="process-group backend for N > 1 (nccl = RCCL; gloo only to rehearse "
+                         "the multi-rank logic on one GPU)")
     ap.add_argument("--ramp-ms", type=float, default=500.0,
                     help="untimed clock ramp before the warmup steps: repeat the step for at "
                          "least this long (the GPU needs ~0.1-0.3 s of load to reach its "
@@ -127,11 +130,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one process per GPU (rehearsals with more ranks than GPUs share devices round-robin)
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        # one process per GPU; the communicator is bound to this rank's device (RCCL/xGMI)
-        dist.init_process_group("nccl", device_id=dev)
+        if args.backend == "nccl":
+            # the communicator is bound to this rank's device (RCCL over xGMI)
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.backend)
     kind, bpk, cap, label = WORKLOADS[args.workload]
     from turtle_kv_amd import dist as tdist
     strong = args.total_keys is not None
@@ -216,7 +224,8 @@ def main():
         dist.barrier()
     wall = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([wall], dtype=torch.float64, device=dev)
+        t = torch.tensor([wall], dtype=torch.float64,
+                         device=dev if args.backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         wall = float(t.item())
     kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))

@@ -24,18 +24,26 @@ CLOCK_GHZ = 2.4
 
 
 def agg(d, kernel):
+    """Per-launch counter values of the step: for each comma-separated kernel-name substring,
+    the mean over its dispatches; summed over the kernels (one step = one launch of each;
+    GRBM_GUI_ACTIVE sums to the step's busy clock)."""
     rows = list(csv.DictReader(open(os.path.join(d, "run_counter_collection.csv"))))
-    out = collections.defaultdict(list)
-    for r in rows:
-        if kernel in r["Kernel_Name"]:
-            out[r["Counter_Name"]].append(float(r["Counter_Value"]))
-    return {k: sum(v) / len(v) for k, v in out.items()}
+    total = collections.defaultdict(float)
+    for name in kernel.split(","):
+        out = collections.defaultdict(list)
+        for r in rows:
+            if name in r["Kernel_Name"]:
+                out[r["Counter_Name"]].append(float(r["Counter_Value"]))
+        for k, v in out.items():
+            total[k] += sum(v) / len(v)
+    return dict(total)
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--workload", required=True)
-    ap.add_argument("--kernel", required=True)
+    ap.add_argument("--kernel", required=True,
+                    help="kernel-name substring; several, comma-separated, for a multi-kernel step")
     ap.add_argument("--fetch", required=True)
     ap.add_argument("--write", required=True)
     ap.add_argument("--sq", required=True)
