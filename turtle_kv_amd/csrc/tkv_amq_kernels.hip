@@ -359,7 +359,8 @@ template <int PASS>
 __global__ __launch_bounds__(256) void bloom_part_keys(const uint4* __restrict__ keys,
                                                        const tkv_amq_segment* __restrict__ segs,
                                                        uint32_t* __restrict__ ws, uint32_t n_tiles,
-                                                       uint32_t per, uint64_t part_off)
+                                                       uint32_t per, uint64_t part_off,
+                                                       uint32_t n_cap)
 {
   extern __shared__ uint32_t s_tile[];
   const tkv_amq_segment sg = segs[0];
@@ -368,7 +369,8 @@ __global__ __launch_bounds__(256) void bloom_part_keys(const uint4* __restrict__
   const uint32_t* base = ws + (uint64_t)gridDim.x * n_tiles + n_tiles;
   for (uint32_t t = tid; t < n_tiles; t += 256) s_tile[t] = PASS == 0 ? 0u : base[t] + H[t];
   __syncthreads();
-  const uint32_t n = sg.n_keys, nb = sg.n_blocks;
+  // n_cap: keys the caller passed (the partition buffer holds that many)
+  const uint32_t n = min(sg.n_keys, n_cap), nb = sg.n_blocks;
   const uint32_t b = min(n, w * per), e = min(n, b + per);
   const uint4* kp = keys + sg.key_begin;
   uint4* part = reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(ws) + part_off);
@@ -682,9 +684,11 @@ __device__ inline uint64_t vqf_key_hash(const uint8_t* __restrict__ keys,
   }
 }
 
-// Per-lane location of one key: primary / alternate block, bucket offsets, tag.
+// Per-lane location of one key: primary block and bucket offset, tag, and the hash (the
+// alternate block is derived from it only when a step needs it: vqf_locate_alt).
 struct VqfLoc {
-  uint32_t pb, po, ab, ao, tag;
+  uint64_t h;
+  uint32_t pb, po, tag;
   bool kept;
 };
 
@@ -694,15 +698,24 @@ __device__ inline VqfLoc vqf_locate(uint64_t h, bool valid, uint64_t mask, uint6
 {
   using C = Vqf<T>;
   VqfLoc l;
+  l.h = h;
   l.kept = valid && ((h & mask) == h);  // filter_builder.hpp:210
   l.tag = (uint32_t)(h & ((1ull << T) - 1));
   const uint32_t pi = (uint32_t)mod_by_magic(h >> T, R, magic);
-  const uint32_t ai = (uint32_t)mod_by_magic((h ^ ((uint64_t)l.tag * kVqfAltMul)) >> T, R, magic);
   l.pb = pi / C::kBuckets;
   l.po = pi - l.pb * C::kBuckets;
-  l.ab = ai / C::kBuckets;
-  l.ao = ai - l.ab * C::kBuckets;
   return l;
+}
+
+// alternate bucket ((h ^ tag * 0x5bd1e995) >> T) mod R -> (block, offset)
+template <int T>
+__device__ inline void vqf_locate_alt(const VqfLoc& l, uint64_t R, uint64_t magic, uint32_t& ab,
+                                      uint32_t& ao)
+{
+  using C = Vqf<T>;
+  const uint32_t ai = (uint32_t)mod_by_magic((l.h ^ ((uint64_t)l.tag * kVqfAltMul)) >> T, R, magic);
+  ab = ai / C::kBuckets;
+  ao = ai - ab * C::kBuckets;
 }
 
 // Exact replay of the reference insert order (build_vqf_filter<T>, filter_builder.hpp:204-214)
@@ -763,8 +776,8 @@ __device__ void vqf_decide_body(const uint8_t* __restrict__ keys, const uint64_t
   bool pend = false;
   auto step = [&](uint32_t base, VqfLoc& cur, const uint4& kv_hash, uint4& kv_load) {
     const VqfLoc L = cur;
-    // block counts before this chunk (every lane reads: an invalid lane's blocks are 0)
-    const uint32_t cnt_p = cnt[L.pb], cnt_a = cnt[L.ab];
+    // primary block counts before this chunk (every lane reads: an invalid lane's block is 0)
+    const uint32_t cnt_p = cnt[L.pb];
     const uint32_t inext = base + 64 + lane;
     const bool vnext = inext < n;
     uint64_t hn;
@@ -792,93 +805,117 @@ __device__ void vqf_decide_body(const uint8_t* __restrict__ keys, const uint64_t
 
     const uint64_t keptmask = __ballot(L.kept);
     nelts += __popcll(keptmask);
-    // lanes with pb_j == my pb / with pb_j == my ab: one ballot per block-id bit; each
-    // 32-bit half of a match mask is updated with one v_bitop3 (m & ~(ballot ^ sext(bit)))
+    // lanes with pb_j == my pb: one LDS lane-mask table round trip, or one ballot per
+    // block-id bit, each 32-bit half of the match mask updated with one v_bitop3
+    // (m & ~(ballot ^ sext(bit)))
     uint32_t mpp_lo = (uint32_t)keptmask, mpp_hi = (uint32_t)(keptmask >> 32);
-    uint32_t mpa_lo = mpp_lo, mpa_hi = mpp_hi;
     if constexpr (kLdsMatch) {
       if (L.kept) atomicOr(mt + L.pb, mybit);
       asm volatile("" ::: "memory");
-      const uint64_t a = mt[L.pb], b = mt[L.ab];
+      const uint64_t a = mt[L.pb];
       asm volatile("" ::: "memory");
       if (L.kept) mt[L.pb] = 0;
       mpp_lo &= (uint32_t)a;
       mpp_hi &= (uint32_t)(a >> 32);
-      mpa_lo &= (uint32_t)b;
-      mpa_hi &= (uint32_t)(b >> 32);
     }
 #pragma unroll
     for (int j = 0; j < (kLdsMatch ? 0 : NBITS); ++j) {
       const uint32_t xp = (uint32_t)__builtin_amdgcn_sbfe((int32_t)L.pb, j, 1);  // 0 or ~0
-      const uint32_t xa = (uint32_t)__builtin_amdgcn_sbfe((int32_t)L.ab, j, 1);
       const uint64_t bp = __ballot(xp != 0);
-      const uint32_t bl = (uint32_t)bp, bh = (uint32_t)(bp >> 32);
-      mpp_lo &= ~(bl ^ xp);
-      mpp_hi &= ~(bh ^ xp);
-      mpa_lo &= ~(bl ^ xa);
-      mpa_hi &= ~(bh ^ xa);
+      mpp_lo &= ~((uint32_t)bp ^ xp);
+      mpp_hi &= ~((uint32_t)(bp >> 32) ^ xp);
     }
     cur = vqf_locate<T>(hn, vnext, mask, R, magic);
     const uint64_t Mpp = ((uint64_t)mpp_hi << 32) | mpp_lo;
-    const uint64_t Mpa = ((uint64_t)mpa_hi << 32) | mpa_lo;
+    // count of my primary block if every earlier lane of the chunk took its primary
     uint32_t cp = L.kept ? cnt_p + __popcll(Mpp & lt) : 0u;
-    uint32_t ca = L.kept ? cnt_a + __popcll(Mpa & lt) : 0u;
-    const uint32_t pb = L.pb, ab = L.ab;
-    // Decisions in insertion order, resolved in rounds.  Lane k's choice depends only on the
-    // counts of its two blocks, which an earlier lane j changes only by moving (pb_j -> ab_j)
-    // and only if {pb_j, ab_j} meets {pb_k, ab_k}.  So every undecided lane with no undecided
-    // earlier lane sharing a block is final now: all of them decide in one round and the
-    // movers' effects are applied to later lanes with four masked popcounts.
-    uint64_t U = __ballot(L.kept && pb != ab);  // blocks differ (vqf_insert alt test)
+    const uint32_t pb = L.pb;
+    uint32_t ab = pb, ao = L.po, ca = 0;
     uint64_t altmask = 0;
-    uint64_t F = __ballot((cp >= C::kThreshold) & (ca < cp)) & U;
-    if (TKV_EXP != 4 && F != 0) {
-      // lanes whose alternate block is my primary / my alternate
-      uint32_t map_lo = (uint32_t)keptmask, map_hi = (uint32_t)(keptmask >> 32);
-      uint32_t maa_lo = map_lo, maa_hi = map_hi;
+    // No lane at the threshold: every key of the chunk stays primary (a lane moves only when
+    // its primary holds >= kThreshold elements, and with all earlier lanes primary it holds
+    // cp).  This is most steps of a leaf (blocks fill towards ~0.85 x slots), and they skip
+    // the alternate block entirely.
+    if (__ballot(L.kept && cp >= C::kThreshold) != 0) {
+      vqf_locate_alt<T>(L, R, magic, ab, ao);
+      const uint32_t cnt_a = cnt[ab];
+      // lanes with pb_j == my ab
+      uint32_t mpa_lo = (uint32_t)keptmask, mpa_hi = (uint32_t)(keptmask >> 32);
       if constexpr (kLdsMatch) {
-        if (L.kept) atomicOr(mt + ab, mybit);
+        if (L.kept) atomicOr(mt + pb, mybit);
         asm volatile("" ::: "memory");
-        const uint64_t a = mt[pb], b = mt[ab];
+        const uint64_t b = mt[ab];
         asm volatile("" ::: "memory");
-        if (L.kept) mt[ab] = 0;
-        map_lo &= (uint32_t)a;
-        map_hi &= (uint32_t)(a >> 32);
-        maa_lo &= (uint32_t)b;
-        maa_hi &= (uint32_t)(b >> 32);
+        if (L.kept) mt[pb] = 0;
+        mpa_lo &= (uint32_t)b;
+        mpa_hi &= (uint32_t)(b >> 32);
       }
 #pragma unroll
       for (int j = 0; j < (kLdsMatch ? 0 : NBITS); ++j) {
         const uint32_t xp = (uint32_t)__builtin_amdgcn_sbfe((int32_t)pb, j, 1);
         const uint32_t xa = (uint32_t)__builtin_amdgcn_sbfe((int32_t)ab, j, 1);
-        const uint64_t ba = __ballot(xa != 0);
-        const uint32_t bl = (uint32_t)ba, bh = (uint32_t)(ba >> 32);
-        map_lo &= ~(bl ^ xp);
-        map_hi &= ~(bh ^ xp);
-        maa_lo &= ~(bl ^ xa);
-        maa_hi &= ~(bh ^ xa);
+        const uint64_t bp = __ballot(xp != 0);
+        mpa_lo &= ~((uint32_t)bp ^ xa);
+        mpa_hi &= ~((uint32_t)(bp >> 32) ^ xa);
       }
-      const uint64_t Map = ((uint64_t)map_hi << 32) | map_lo;
-      const uint64_t Maa = ((uint64_t)maa_hi << 32) | maa_lo;
-      const uint64_t conf = (Mpp | Mpa | Map | Maa) & lt;  // earlier lanes sharing a block
-      // a lane whose primary cannot reach the threshold even if every earlier lane with its
-      // alternate there moved in stays primary: it is decided already
-      U &= __ballot(cp + (uint32_t)__popcll(Map & lt) >= C::kThreshold);
-      F &= U;
-      while (F != 0) {
-        const uint64_t res = __ballot((conf & U) == 0) & U;
-        const uint64_t A = res & F;
-        altmask |= A;
-        U &= ~res;
-        const uint64_t Al = A & lt;
-        cp = cp + (uint32_t)__popcll(Map & Al) - (uint32_t)__popcll(Mpp & Al);
-        ca = ca + (uint32_t)__popcll(Maa & Al) - (uint32_t)__popcll(Mpa & Al);
-        F = __ballot((cp >= C::kThreshold) & (ca < cp)) & U;
+      const uint64_t Mpa = ((uint64_t)mpa_hi << 32) | mpa_lo;
+      ca = L.kept ? cnt_a + __popcll(Mpa & lt) : 0u;
+      // Decisions in insertion order, resolved in rounds.  Lane k's choice depends only on
+      // the counts of its two blocks, which an earlier lane j changes only by moving
+      // (pb_j -> ab_j) and only if {pb_j, ab_j} meets {pb_k, ab_k}.  So every undecided lane
+      // with no undecided earlier lane sharing a block is final now: all of them decide in
+      // one round and the movers' effects are applied to later lanes with four masked
+      // popcounts.
+      uint64_t U = __ballot(L.kept && pb != ab);  // blocks differ (vqf_insert alt test)
+      uint64_t F = __ballot((cp >= C::kThreshold) & (ca < cp)) & U;
+      if (TKV_EXP != 4 && F != 0) {
+        // lanes whose alternate block is my primary / my alternate
+        uint32_t map_lo = (uint32_t)keptmask, map_hi = (uint32_t)(keptmask >> 32);
+        uint32_t maa_lo = map_lo, maa_hi = map_hi;
+        if constexpr (kLdsMatch) {
+          if (L.kept) atomicOr(mt + ab, mybit);
+          asm volatile("" ::: "memory");
+          const uint64_t a = mt[pb], b = mt[ab];
+          asm volatile("" ::: "memory");
+          if (L.kept) mt[ab] = 0;
+          map_lo &= (uint32_t)a;
+          map_hi &= (uint32_t)(a >> 32);
+          maa_lo &= (uint32_t)b;
+          maa_hi &= (uint32_t)(b >> 32);
+        }
+#pragma unroll
+        for (int j = 0; j < (kLdsMatch ? 0 : NBITS); ++j) {
+          const uint32_t xp = (uint32_t)__builtin_amdgcn_sbfe((int32_t)pb, j, 1);
+          const uint32_t xa = (uint32_t)__builtin_amdgcn_sbfe((int32_t)ab, j, 1);
+          const uint64_t ba = __ballot(xa != 0);
+          const uint32_t bl = (uint32_t)ba, bh = (uint32_t)(ba >> 32);
+          map_lo &= ~(bl ^ xp);
+          map_hi &= ~(bh ^ xp);
+          maa_lo &= ~(bl ^ xa);
+          maa_hi &= ~(bh ^ xa);
+        }
+        const uint64_t Map = ((uint64_t)map_hi << 32) | map_lo;
+        const uint64_t Maa = ((uint64_t)maa_hi << 32) | maa_lo;
+        const uint64_t conf = (Mpp | Mpa | Map | Maa) & lt;  // earlier lanes sharing a block
+        // a lane whose primary cannot reach the threshold even if every earlier lane with
+        // its alternate there moved in stays primary: it is decided already
+        U &= __ballot(cp + (uint32_t)__popcll(Map & lt) >= C::kThreshold);
+        F &= U;
+        while (F != 0) {
+          const uint64_t res = __ballot((conf & U) == 0) & U;
+          const uint64_t A = res & F;
+          altmask |= A;
+          U &= ~res;
+          const uint64_t Al = A & lt;
+          cp = cp + (uint32_t)__popcll(Map & Al) - (uint32_t)__popcll(Mpp & Al);
+          ca = ca + (uint32_t)__popcll(Maa & Al) - (uint32_t)__popcll(Mpa & Al);
+          F = __ballot((cp >= C::kThreshold) & (ca < cp)) & U;
+        }
       }
     }
     const bool alt = (altmask >> lane) & 1;
     const uint32_t chosen = alt ? ab : pb;
-    const uint32_t cho = alt ? L.ao : L.po;
+    const uint32_t cho = alt ? ao : L.po;
     const uint32_t r = alt ? ca : cp;  // count of the chosen block when this key is inserted
     fail |= (uint32_t)(__ballot(L.kept && r >= C::kSlots) != 0);
     pend = base + lane < n;
@@ -1735,12 +1772,12 @@ int tkv_amq_build(int kind, const uint8_t* keys, const uint64_t* offs, uint32_t 
       const uint4* k4 = reinterpret_cast<const uint4*>(keys);
       const size_t hl = 4ull * pg.n_tiles;
       hipLaunchKernelGGL(bloom_part_keys<0>, dim3(pg.P), dim3(256), hl, s, k4, d_segs, w,
-                         pg.n_tiles, pg.per, pg.part_off);
+                         pg.n_tiles, pg.per, pg.part_off, (uint32_t)n_keys);
       hipLaunchKernelGGL(bloom_part_scan_cols, dim3(pg.n_tiles), dim3(256), 0, s, w, pg.P,
                          pg.n_tiles);
       hipLaunchKernelGGL(bloom_part_scan_tiles, dim3(1), dim3(256), 0, s, w, pg.P, pg.n_tiles);
       hipLaunchKernelGGL(bloom_part_keys<1>, dim3(pg.P), dim3(256), hl, s, k4, d_segs, w,
-                         pg.n_tiles, pg.per, pg.part_off);
+                         pg.n_tiles, pg.per, pg.part_off, (uint32_t)n_keys);
       hipLaunchKernelGGL(bloom_tile_build<kBloomTileThreads>, dim3(pg.n_tiles),
                          dim3(kBloomTileThreads), 64ull * kBloomTileBlocks, s, d_segs, w, pg.P,
                          pg.n_tiles, pg.part_off, d_out);
