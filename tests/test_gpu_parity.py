@@ -246,6 +246,24 @@ def test_bloom_monolithic_duplicate_keys(oracle, amq, torch):
     assert_same(plan, out, ref)
 
 
+def test_bloom_monolithic_unstaged_matches_atomic_path(amq, torch):
+    """A filter of more tiles than the LDS staging holds (2060 > 2048) takes the unstaged
+    scatter; its bytes must equal the device-atomic path's for the same keys (planned as a
+    two-leaf batch, which routes the big leaf through bloom_global_set)."""
+    n = 108_000_000
+    keys = amq.KeyBatch.fixed(amq.gen_keys16(16, 0, n + 1))
+    mono = amq.plan_filters(0, [n], 10)
+    assert -(-mono.max_seg_blocks // 1024) > 2048
+    kb = amq.KeyBatch.fixed(keys.data[:n])
+    a = amq.build_all_filters(mono, kb)
+    two = amq.plan_filters(0, [n, 1], 10)
+    assert two.workspace_bytes == 0
+    b = amq.build_all_filters(two, keys)
+    pa = int(mono.segs[0]["payload_bytes"])
+    assert int(two.segs[0]["payload_bytes"]) == pa
+    assert torch.equal(a[:pa], b[:pa])
+
+
 def test_bloom_oversize_leaf_in_batch_global_path(oracle, amq, torch):
     """A multi-leaf batch holding a leaf beyond the LDS budget takes the device-atomic path."""
     counts = [120000, 500, 16384]

@@ -321,13 +321,31 @@ __global__ __launch_bounds__(256) void bloom_global_set(const uint8_t* __restric
 // ---------------------------------------------------------------------------------------
 constexpr uint32_t kBloomTileBlocks = 1024;     // 64 KiB LDS image per tile
 constexpr uint32_t kBloomPartMaxTiles = 32768;  // LDS histogram / cursors <= 128 KiB
-constexpr uint32_t kBloomPartMaxWgs = 1024;    // (256 / 512 / 128 measured slower)
+constexpr uint32_t kBloomPartMaxWgs = 1024;     // unstaged scatter (256 / 512 / 128 slower)
 constexpr uint32_t kBloomTileThreads = 1024;    // 2 workgroups per CU (512: 6% slower)
+// Staged scatter (filters of <= kStageMaxTiles tiles): one 1024-thread workgroup per CU
+// stages kStageKeys keys per tile in LDS and writes each full bucket as one aligned 64-byte
+// piece.  Every (workgroup, tile) run is padded to a multiple of kStageKeys with copies of
+// one of its keys, which set the same bits again.
+constexpr uint32_t kStageKeys = 4;
+constexpr uint32_t kStageThreads = 1024;
+constexpr uint32_t kStageMaxWgs = 256;
+constexpr uint32_t kStageMaxTiles = 2048;  // 2048 x (64 + 8) B = 144 KiB of LDS
+#ifndef TKV_STAGE_R
+#define TKV_STAGE_R 2  // keys staged per thread per round
+#endif
+
+__host__ __device__ constexpr inline uint32_t bloom_stage_lds_bytes(uint32_t n_tiles)
+{
+  return n_tiles * (16 * kStageKeys + 8);
+}
 
 struct BloomPartGeom {
   uint32_t P;         // partition workgroups
   uint32_t n_tiles;
   uint32_t per;       // keys per partition workgroup
+  uint32_t threads;   // threads per partition workgroup
+  bool staged;
   uint64_t h_words;   // P * n_tiles
   uint64_t part_off;  // byte offset of the partitioned keys in the workspace
   uint64_t bytes;     // workspace bytes
@@ -337,13 +355,17 @@ __host__ __device__ inline BloomPartGeom bloom_part_geom(uint64_t n_keys, uint64
 {
   BloomPartGeom g;
   g.n_tiles = (uint32_t)((nb + kBloomTileBlocks - 1) / kBloomTileBlocks);
-  uint64_t p = (n_keys + 4095) / 4096;
-  g.P = (uint32_t)(p < 1 ? 1 : (p > kBloomPartMaxWgs ? kBloomPartMaxWgs : p));
+  g.staged = g.n_tiles <= kStageMaxTiles;
+  const uint64_t chunk = g.staged ? 16384 : 4096, cap = g.staged ? kStageMaxWgs : kBloomPartMaxWgs;
+  const uint64_t p = (n_keys + chunk - 1) / chunk;
+  g.P = (uint32_t)(p < 1 ? 1 : (p > cap ? cap : p));
+  g.threads = g.staged ? kStageThreads : 256;
   g.per = (uint32_t)((n_keys + g.P - 1) / g.P);
   g.h_words = (uint64_t)g.P * g.n_tiles;
   // [H: P x n_tiles u32][tile totals: n_tiles u32][bucket bases: n_tiles + 1 u32][keys]
   g.part_off = (4 * (g.h_words + 2ull * g.n_tiles + 1) + 255) & ~255ull;
-  g.bytes = g.part_off + 16 * n_keys;
+  const uint64_t pad = g.staged ? (uint64_t)(kStageKeys - 1) * g.h_words : 0;
+  g.bytes = g.part_off + 16 * (n_keys + pad);
   return g;
 }
 
@@ -355,8 +377,8 @@ __device__ inline uint32_t bloom_tile_of(const uint4& kv, uint32_t nb)
 }
 
 // PASS 0: histogram; PASS 1: scatter.  Both walk the same key range in the same way.
-template <int PASS>
-__global__ __launch_bounds__(256) void bloom_part_keys(const uint4* __restrict__ keys,
+template <int PASS, uint32_t NT>
+__global__ __launch_bounds__(NT) void bloom_part_keys(const uint4* __restrict__ keys,
                                                        const tkv_amq_segment* __restrict__ segs,
                                                        uint32_t* __restrict__ ws, uint32_t n_tiles,
                                                        uint32_t per, uint64_t part_off,
@@ -367,7 +389,7 @@ __global__ __launch_bounds__(256) void bloom_part_keys(const uint4* __restrict__
   const uint32_t tid = threadIdx.x, w = blockIdx.x;
   uint32_t* H = ws + (uint64_t)w * n_tiles;
   const uint32_t* base = ws + (uint64_t)gridDim.x * n_tiles + n_tiles;
-  for (uint32_t t = tid; t < n_tiles; t += 256) s_tile[t] = PASS == 0 ? 0u : base[t] + H[t];
+  for (uint32_t t = tid; t < n_tiles; t += NT) s_tile[t] = PASS == 0 ? 0u : base[t] + H[t];
   __syncthreads();
   // n_cap: keys the caller passed (the partition buffer holds that many)
   const uint32_t n = min(sg.n_keys, n_cap), nb = sg.n_blocks;
@@ -375,16 +397,16 @@ __global__ __launch_bounds__(256) void bloom_part_keys(const uint4* __restrict__
   const uint4* kp = keys + sg.key_begin;
   uint4* part = reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(ws) + part_off);
   constexpr int U = 4;
-  for (uint32_t i0 = b; i0 < e; i0 += 256 * U) {
+  for (uint32_t i0 = b; i0 < e; i0 += NT * U) {
     uint4 kv[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const uint32_t i = i0 + u * 256 + tid;
+      const uint32_t i = i0 + u * NT + tid;
       if (i < e) kv[u] = load_nt16(kp + i);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const uint32_t i = i0 + u * 256 + tid;
+      const uint32_t i = i0 + u * NT + tid;
       if (i < e) {
         const uint32_t t = bloom_tile_of(kv[u], nb);
         if constexpr (PASS == 0) {
@@ -398,7 +420,100 @@ __global__ __launch_bounds__(256) void bloom_part_keys(const uint4* __restrict__
   }
   if constexpr (PASS == 0) {
     __syncthreads();
-    for (uint32_t t = tid; t < n_tiles; t += 256) H[t] = s_tile[t];
+    for (uint32_t t = tid; t < n_tiles; t += NT) H[t] = s_tile[t];
+  }
+}
+
+// The staged scatter pass.  Keys arrive one per thread per round (prefetched kU rounds
+// ahead); each takes a slot of its tile's LDS bucket, and the thread that takes the last slot
+// writes the full bucket to the tile's next aligned 64-byte piece of this workgroup's run.
+// Keys that find their bucket full retry after the flush (a uniform loop: every thread
+// reaches every barrier).  The runs start at the padded offsets of bloom_part_scan_cols.
+__global__ __launch_bounds__(kStageThreads) void bloom_part_scatter_staged(
+    const uint4* __restrict__ keys, const tkv_amq_segment* __restrict__ segs,
+    uint32_t* __restrict__ ws, uint32_t n_tiles, uint32_t per, uint64_t part_off, uint32_t n_cap)
+{
+  extern __shared__ __attribute__((aligned(16))) uint8_t s_stage[];
+  uint4* stage = reinterpret_cast<uint4*>(s_stage);                       // [tile][kStageKeys]
+  uint32_t* fill = reinterpret_cast<uint32_t*>(s_stage + 16 * kStageKeys * n_tiles);
+  uint32_t* cur = fill + n_tiles;  // next 64-byte piece of the tile's run (key index)
+  const tkv_amq_segment sg = segs[0];
+  const uint32_t tid = threadIdx.x, w = blockIdx.x;
+  const uint32_t* H = ws + (uint64_t)w * n_tiles;
+  const uint32_t* base = ws + (uint64_t)gridDim.x * n_tiles + n_tiles;
+  for (uint32_t t = tid; t < n_tiles; t += kStageThreads) {
+    fill[t] = 0;
+    cur[t] = base[t] + H[t];
+  }
+  __syncthreads();
+  const uint32_t n = min(sg.n_keys, n_cap), nb = sg.n_blocks;
+  const uint32_t b = min(n, w * per), e = min(n, b + per);
+  const uint4* kp = keys + sg.key_begin;
+  uint4* part = reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(ws) + part_off);
+  // each round, every thread stages kR keys (prefetched one round ahead)
+  constexpr uint32_t kR = TKV_STAGE_R;
+  constexpr uint32_t kRound = kR * kStageThreads;
+  uint4 ring[kR];
+#pragma unroll
+  for (uint32_t u = 0; u < kR; ++u) {
+    const uint32_t i = b + u * kStageThreads + tid;
+    ring[u] = i < e ? load_nt16(kp + i) : make_uint4(0, 0, 0, 0);
+  }
+  for (uint32_t c0 = b; c0 < e; c0 += kRound) {
+    uint4 kv[kR];
+    uint32_t t[kR];
+    bool pend[kR];
+#pragma unroll
+    for (uint32_t u = 0; u < kR; ++u) {
+      const uint32_t i = c0 + u * kStageThreads + tid;
+      kv[u] = ring[u];
+      if (i + kRound < e) ring[u] = load_nt16(kp + i + kRound);
+      pend[u] = i < e;
+      t[u] = pend[u] ? bloom_tile_of(kv[u], nb) : 0u;
+    }
+    for (;;) {
+      uint32_t slot[kR];
+#pragma unroll
+      for (uint32_t u = 0; u < kR; ++u) {
+        slot[u] = ~0u;
+        if (pend[u]) {
+          slot[u] = atomicAdd(fill + t[u], 1u);
+          if (slot[u] < kStageKeys) {
+            stage[t[u] * kStageKeys + slot[u]] = kv[u];
+            pend[u] = false;
+          }
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (uint32_t u = 0; u < kR; ++u) {
+        if (slot[u] == kStageKeys - 1) {
+          // this key filled the bucket: write it out, reopen it (keys that found it full
+          // incremented fill past kStageKeys before the barrier and retry below)
+          const uint32_t pos = cur[t[u]];
+          cur[t[u]] = pos + kStageKeys;
+#pragma unroll
+          for (uint32_t q = 0; q < kStageKeys; ++q)
+            part[pos + q] = stage[t[u] * kStageKeys + q];
+          fill[t[u]] = 0;
+        }
+      }
+      bool any = false;
+#pragma unroll
+      for (uint32_t u = 0; u < kR; ++u) any |= pend[u];
+      if (!__syncthreads_or(any)) break;
+    }
+  }
+  __syncthreads();
+  // partly filled buckets: pad with the bucket's first key
+  for (uint32_t t = tid; t < n_tiles; t += kStageThreads) {
+    const uint32_t c = fill[t];
+    if (c != 0) {
+      const uint32_t pos = cur[t];
+      const uint4 k0 = stage[t * kStageKeys];
+#pragma unroll
+      for (uint32_t q = 0; q < kStageKeys; ++q) part[pos + q] = q < c ? stage[t * kStageKeys + q] : k0;
+    }
   }
 }
 
@@ -422,8 +537,9 @@ __device__ inline uint32_t block_exclusive_scan256(uint32_t v, uint32_t* s, uint
 }
 
 // One workgroup per tile: H[w][t] <- sum of H[w'][t] over w' < w; totals[t] <- column sum.
+// pad4: the staged scatter's runs, rounded up to whole staging buckets
 __global__ __launch_bounds__(256) void bloom_part_scan_cols(uint32_t* __restrict__ ws, uint32_t P,
-                                                            uint32_t n_tiles)
+                                                            uint32_t n_tiles, uint32_t pad4)
 {
   __shared__ uint32_t s[256];
   const uint32_t t = blockIdx.x, tid = threadIdx.x;
@@ -434,6 +550,7 @@ __global__ __launch_bounds__(256) void bloom_part_scan_cols(uint32_t* __restrict
   for (uint32_t r = 0; r < R; ++r) {
     const uint32_t w = tid * R + r;
     v[r] = w < P ? ws[(uint64_t)w * n_tiles + t] : 0u;
+    if (pad4) v[r] = (v[r] + kStageKeys - 1) & ~(kStageKeys - 1);
     sum += v[r];
   }
   uint32_t total;
@@ -1763,21 +1880,34 @@ int tkv_amq_build(int kind, const uint8_t* keys, const uint64_t* offs, uint32_t 
       static std::once_flag lds_attr;
       std::call_once(lds_attr, [] {
         const int cap = (int)(4 * kBloomPartMaxTiles);
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&bloom_part_keys<0>),
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&bloom_part_keys<0, 256>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, cap);
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&bloom_part_keys<1>),
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&bloom_part_keys<1, 256>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, cap);
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&bloom_part_scatter_staged),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)bloom_stage_lds_bytes(kStageMaxTiles));
       });
       uint32_t* w = static_cast<uint32_t*>(d_ws);
       const uint4* k4 = reinterpret_cast<const uint4*>(keys);
       const size_t hl = 4ull * pg.n_tiles;
-      hipLaunchKernelGGL(bloom_part_keys<0>, dim3(pg.P), dim3(256), hl, s, k4, d_segs, w,
-                         pg.n_tiles, pg.per, pg.part_off, (uint32_t)n_keys);
+      const uint32_t nk = (uint32_t)n_keys;
+      if (pg.staged)
+        hipLaunchKernelGGL((bloom_part_keys<0, kStageThreads>), dim3(pg.P), dim3(kStageThreads), hl,
+                           s, k4, d_segs, w, pg.n_tiles, pg.per, pg.part_off, nk);
+      else
+        hipLaunchKernelGGL((bloom_part_keys<0, 256>), dim3(pg.P), dim3(256), hl, s, k4, d_segs, w,
+                           pg.n_tiles, pg.per, pg.part_off, nk);
       hipLaunchKernelGGL(bloom_part_scan_cols, dim3(pg.n_tiles), dim3(256), 0, s, w, pg.P,
-                         pg.n_tiles);
+                         pg.n_tiles, (uint32_t)pg.staged);
       hipLaunchKernelGGL(bloom_part_scan_tiles, dim3(1), dim3(256), 0, s, w, pg.P, pg.n_tiles);
-      hipLaunchKernelGGL(bloom_part_keys<1>, dim3(pg.P), dim3(256), hl, s, k4, d_segs, w,
-                         pg.n_tiles, pg.per, pg.part_off, (uint32_t)n_keys);
+      if (pg.staged)
+        hipLaunchKernelGGL(bloom_part_scatter_staged, dim3(pg.P), dim3(kStageThreads),
+                           bloom_stage_lds_bytes(pg.n_tiles), s, k4, d_segs, w, pg.n_tiles, pg.per,
+                           pg.part_off, nk);
+      else
+        hipLaunchKernelGGL((bloom_part_keys<1, 256>), dim3(pg.P), dim3(256), hl, s, k4, d_segs, w,
+                           pg.n_tiles, pg.per, pg.part_off, nk);
       hipLaunchKernelGGL(bloom_tile_build<kBloomTileThreads>, dim3(pg.n_tiles),
                          dim3(kBloomTileThreads), 64ull * kBloomTileBlocks, s, d_segs, w, pg.P,
                          pg.n_tiles, pg.part_off, d_out);
