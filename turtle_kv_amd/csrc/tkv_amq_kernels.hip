@@ -1689,6 +1689,20 @@ inline hipStream_t as_stream(void* s) { return static_cast<hipStream_t>(s); }
 
 inline uint64_t div_up(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
 
+// Kernel attributes (dynamic LDS above 64 KiB) are set once per device: a process may drive
+// several GPUs from different threads.
+constexpr int kMaxDevices = 64;
+template <typename Fn>
+inline void once_per_device(std::once_flag (&flags)[kMaxDevices], Fn&& fn)
+{
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) {
+    fn();
+    return;
+  }
+  std::call_once(flags[dev], fn);
+}
+
 // a one-filter Bloom batch too large for one LDS image takes the tiled, partitioned build
 // (it needs a workspace of bloom_part_geom(n_keys, n_blocks).bytes and 16-byte keys)
 inline bool bloom_partitioned(uint32_t n_segs, uint64_t max_blocks, uint64_t n_keys)
@@ -1877,8 +1891,8 @@ int tkv_amq_build(int kind, const uint8_t* keys, const uint64_t* offs, uint32_t 
     if (bloom_partitioned(n_segs, max_blocks, n_keys) && mode == kKey16 && d_ws &&
         ws_bytes >= pg.bytes) {
       // one monolithic filter: partition the keys by tile, build every tile in LDS
-      static std::once_flag lds_attr;
-      std::call_once(lds_attr, [] {
+      static std::once_flag lds_attr[kMaxDevices];
+      once_per_device(lds_attr, [] {
         const int cap = (int)(4 * kBloomPartMaxTiles);
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&bloom_part_keys<0, 256>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, cap);
@@ -1954,8 +1968,8 @@ int tkv_amq_build(int kind, const uint8_t* keys, const uint64_t* offs, uint32_t 
     hipLaunchKernelGGL(vqf_decide<kKeyVar>, dim3(n_segs), dim3(64), lds, s, keys, offs, stride,
                        d_segs, d_ws, n_segs, flags);
   if (fused) {
-    static std::once_flag lds_attr;
-    std::call_once(lds_attr, [] {
+    static std::once_flag lds_attr[kMaxDevices];
+    once_per_device(lds_attr, [] {
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&vqf_place_fused),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)kFusedLdsBudget);
     });
