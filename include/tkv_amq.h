@@ -24,6 +24,9 @@
  *   tkv_amq_vqf_*sizing     vqf_filter_load_factor<T> (vqf_filter_page_view.hpp:39-59),
  *                           vqf_required_size<T> / vqf_nslots_for_size (vqf 0.2.4, used at
  *                           tree/filter_builder.hpp:243-244,270,274)
+ *   tkv_amq_stage_keys      the EditView key range build_filter_for_leaf_in_job iterates
+ *                           (core/merge_compactor.hpp:107-139) gathered into one contiguous
+ *                           host key buffer for the H2D copy (host only)
  *
  * Conventions
  *  - Plain pointers and sizes only.  Pointers documented "device" are HIP device pointers
@@ -158,6 +161,25 @@ int tkv_amq_bloom_probe_hashed(const uint8_t* d_filters, const tkv_amq_segment* 
                                uint32_t n_segs, const uint8_t* d_query, uint32_t k_max,
                                const uint32_t* d_pair_query, uint64_t n_pairs,
                                const uint32_t* d_pair_leaf, uint8_t* d_result, void* stream);
+
+/* Key staging, host only (no device needed): the H2D front end.  The reference passes the
+ * build a flattened range of EditView whose keys are KeyView = std::string_view into leaf /
+ * edit memory (core/merge_compactor.hpp:107-139, tree/filter_builder.hpp:307-331).  This
+ * gathers the viewed key bytes into one contiguous, caller-owned (normally pinned) buffer
+ * with up to n_threads host threads (<= 0: min(hardware threads, 16)).
+ *  views, view_stride  view i is the tkv_amq_key_view at (const uint8_t*)views + i*view_stride;
+ *                      the struct has the libstdc++ std::string_view layout {size, data}, so
+ *                      &edits[0].key with stride sizeof(EditView) is read in place
+ *  fixed_len > 0       every key must be fixed_len bytes (else InvalidArgument); key i lands
+ *                      at dst + i*fixed_len (the fixed-stride key form of tkv_amq_build)
+ *  fixed_len == 0      variable length: dst_offsets[n+1] (out) byte offsets into dst
+ *  dst_capacity        bytes available at dst (ResourceExhausted if the keys do not fit) */
+typedef struct tkv_amq_key_view {
+  uint64_t size;
+  const uint8_t* data;
+} tkv_amq_key_view;
+int tkv_amq_stage_keys(const void* views, uint64_t view_stride, uint64_t n_keys, uint32_t fixed_len,
+                       uint8_t* dst, uint64_t dst_capacity, uint64_t* dst_offsets, int n_threads);
 
 /* Synthetic 16-byte keys on the device: key i = (splitmix64_at(seed, 2(first+i)+1),
  * splitmix64_at(seed, 2(first+i)+2)), little-endian (the bench input). */

@@ -243,21 +243,44 @@ class FilterBatchBuilder
 // ---------------------------------------------------------------------------------------
 namespace detail {
 
+// std::string_view is read in place as tkv_amq_key_view when the layouts agree (libstdc++:
+// {size, data}); otherwise the views are copied into tkv_amq_key_view records first.
+inline bool string_view_is_key_view()
+{
+  static_assert(sizeof(std::string_view) == sizeof(tkv_amq_key_view), "string_view size");
+  const char probe[2] = {'a', 0};
+  const std::string_view sv(probe, 1);
+  tkv_amq_key_view kv;
+  std::memcpy(&kv, &sv, sizeof(kv));
+  return kv.size == 1 && kv.data == reinterpret_cast<const u8*>(probe);
+}
+
 inline Status stage_keys(const std::vector<std::string_view>& items, DeviceBuffer& d_keys,
                          DeviceBuffer& d_offs, bool& fixed, u32& stride)
 {
   const usize n = items.size();
   fixed = n > 0;
   stride = n ? (u32)items[0].size() : 16;
-  std::vector<u64> offs(n + 1, 0);
+  u64 total = 0;
   for (usize i = 0; i < n; ++i) {
-    offs[i + 1] = offs[i] + items[i].size();
+    total += items[i].size();
     fixed = fixed && items[i].size() == stride;
   }
   if (fixed && stride == 0) fixed = false;
-  std::vector<u8> blob(offs[n] ? offs[n] : 1);
-  for (usize i = 0; i < n; ++i)
-    if (!items[i].empty()) std::memcpy(blob.data() + offs[i], items[i].data(), items[i].size());
+  std::vector<tkv_amq_key_view> copied;
+  const void* views = items.data();
+  if (!string_view_is_key_view()) {
+    copied.resize(n);
+    for (usize i = 0; i < n; ++i)
+      copied[i] = tkv_amq_key_view{items[i].size(), reinterpret_cast<const u8*>(items[i].data())};
+    views = copied.data();
+  }
+  // tkv_amq_stage_keys: the host gather (the EditView key range -> one contiguous buffer)
+  std::vector<u64> offs(n + 1, 0);
+  std::vector<u8> blob(total ? total : 1);
+  const int st = tkv_amq_stage_keys(views, sizeof(tkv_amq_key_view), n, fixed ? stride : 0,
+                                    blob.data(), blob.size(), fixed ? nullptr : offs.data(), 0);
+  if (st != TKV_AMQ_OK) return Status::from(st, "tkv_amq_stage_keys");
   if (!d_keys.resize(blob.size()) || !d_offs.resize(offs.size() * 8))
     return Status::from(TKV_AMQ_RESOURCE_EXHAUSTED, "hipMalloc");
   if (hipMemcpy(d_keys.get(), blob.data(), blob.size(), hipMemcpyHostToDevice) != hipSuccess ||

@@ -155,3 +155,21 @@ def test_host_pipeline_matches_device_build(oracle, amq, torch, kind, bpk, cap):
     for g in plan.segs:
         a, b = int(g["out_offset"]), int(g["payload_bytes"])
         assert np.array_equal(o[a:a + b], ref[a:a + b])
+
+
+@pytest.mark.parametrize("kind,bpk,cap", [(0, 10, 0), (1, 12, 32704)])
+def test_host_pipeline_from_key_views(oracle, amq, torch, kind, bpk, cap):
+    """run_views: keys gathered from EditView-like records (key at byte 8 of 40-byte records)
+    by tkv_amq_stage_keys, chunk by chunk, give the same pages as run() on contiguous keys."""
+    counts = [16384] * 9 + [123, 0, 5000]
+    keys = oracle.gen_keys16(78, 0, sum(counts))
+    if kind == 1:
+        oracle.sort_segments(keys, np.concatenate([[0], np.cumsum(counts)]).astype(np.uint64))
+    n, rec = len(keys), 40
+    buf = np.zeros((n, rec), np.uint8)
+    buf[:, 8:24] = keys
+    views = amq.key_views(buf, np.arange(n, dtype=np.uint64) * rec + 8, 16)
+    pipe = amq.HostFilterPipeline(kind, counts, bpk, payload_capacity=cap, chunk_keys=50_000)
+    a = pipe.run_views(views).clone()
+    b = pipe.run(torch.from_numpy(keys).pin_memory())
+    assert torch.equal(a, b)

@@ -8,7 +8,8 @@ from .filters import (BoolStatus, FilterPage, FilterPlan, KeyBatch, KeyQuery, Pa
                       build_quotient_filter_for_leaf, filter_bits_per_key, gen_keys16,
                       bloom_query_hashes, bloom_probe_hashed, HostFilterPipeline,
                       plan_filters, probe_filters, vqf_filter_load_factor, vqf_hash_val,
-                      vqf_nslots_for_size, vqf_probe_hashed, vqf_required_size)
+                      vqf_nslots_for_size, vqf_probe_hashed, vqf_required_size, key_views,
+                      stage_keys)
 
 __all__ = [
     "abi", "BLOOM", "VQF", "TkvAmqError", "BoolStatus", "FilterPage", "FilterPlan", "KeyBatch",
@@ -16,5 +17,5 @@ __all__ = [
     "build_filter_for_leaf_in_job", "build_quotient_filter_for_leaf", "filter_bits_per_key",
     "gen_keys16", "plan_filters", "probe_filters", "vqf_filter_load_factor", "vqf_hash_val",
     "vqf_nslots_for_size", "vqf_probe_hashed", "vqf_required_size", "bloom_query_hashes",
-    "bloom_probe_hashed", "HostFilterPipeline",
+    "bloom_probe_hashed", "HostFilterPipeline", "key_views", "stage_keys",
 ]

@@ -8,7 +8,8 @@ import subprocess
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 LIB = os.path.join(HERE, "libtkv_amq.so")
-SOURCES = [os.path.join(HERE, "csrc", "tkv_amq_kernels.hip")]
+SOURCES = [os.path.join(HERE, "csrc", "tkv_amq_kernels.hip"),
+           os.path.join(HERE, "csrc", "tkv_amq_stage.cpp")]
 DEPS = SOURCES + [os.path.join(HERE, "csrc", "tkv_amq_device.h"),
                   os.path.join(ROOT, "include", "tkv_amq.h")]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")

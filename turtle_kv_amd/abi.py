@@ -69,7 +69,11 @@ EXPORTS = [
     "tkv_amq_vqf_nslots_for_size", "tkv_amq_plan", "tkv_amq_build", "tkv_amq_build_check",
     "tkv_amq_probe", "tkv_amq_vqf_hash", "tkv_amq_vqf_probe_hashed", "tkv_amq_gen_keys16",
     "tkv_amq_bloom_query_stride", "tkv_amq_bloom_hash", "tkv_amq_bloom_probe_hashed",
+    "tkv_amq_stage_keys",
 ]
+
+# tkv_amq_key_view (libstdc++ std::string_view layout)
+KEY_VIEW_DTYPE = np.dtype([("size", "<u8"), ("data", "<u8")])
 
 _lib = None
 
@@ -122,6 +126,8 @@ def lib(build_if_missing: bool = True):
     L.tkv_amq_bloom_probe_hashed.argtypes = [vp, vp, u32, vp, u32, vp, u64, vp, vp, vp]
     L.tkv_amq_gen_keys16.restype = i32
     L.tkv_amq_gen_keys16.argtypes = [u64, u64, u64, vp, vp]
+    L.tkv_amq_stage_keys.restype = i32
+    L.tkv_amq_stage_keys.argtypes = [vp, u64, u64, u32, vp, u64, vp, i32]
     _lib = L
     return L
 

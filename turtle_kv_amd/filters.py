@@ -188,6 +188,51 @@ class KeyBatch:
         return KeyBatch.variable(data, torch.from_numpy(offs).to(dev))
 
 
+def key_views(buf: np.ndarray, offsets, lengths) -> np.ndarray:
+    """tkv_amq_key_view records (KeyView = std::string_view {size, data}) for keys stored at
+    byte `offsets[i]` (length `lengths[i]`) of host buffer `buf` -- the shape of the EditView
+    key range the reference iterates (core/merge_compactor.hpp:107-139)."""
+    offsets = np.asarray(offsets, dtype=np.uint64)
+    v = np.empty(len(offsets), dtype=abi.KEY_VIEW_DTYPE)
+    v["size"] = np.broadcast_to(np.asarray(lengths, dtype=np.uint64), offsets.shape)
+    v["data"] = np.uint64(buf.ctypes.data) + offsets
+    return v
+
+
+def stage_keys(views, n: int | None = None, fixed_len: int = 16, out=None, view_stride: int = 16,
+               n_threads: int = 0):
+    """Gather viewed keys into one contiguous host buffer (tkv_amq_stage_keys, host threads).
+    `views`: KEY_VIEW_DTYPE array or the address of the first view (then `n` and
+    `view_stride` say how many and how far apart).  fixed_len > 0: returns `out` ([n,
+    fixed_len] uint8, numpy or pinned torch); fixed_len == 0: returns (bytes, offsets[n+1])."""
+    if isinstance(views, np.ndarray):
+        assert views.dtype == abi.KEY_VIEW_DTYPE and views.flags.c_contiguous
+        addr, n, view_stride = views.ctypes.data, len(views), abi.KEY_VIEW_DTYPE.itemsize
+    else:
+        addr = int(views)
+    if fixed_len:
+        if out is None:
+            out = np.empty((n, fixed_len), dtype=np.uint8)
+        cap = out.nbytes if isinstance(out, np.ndarray) else out.numel()
+        st = abi.lib().tkv_amq_stage_keys(ctypes.c_void_p(addr), view_stride, n, fixed_len,
+                                          _ptr(out), cap, None, n_threads)
+        abi.check(st, "tkv_amq_stage_keys")
+        return out
+    sizes = np.ctypeslib.as_array((ctypes.c_uint64 * (2 * n)).from_address(addr)) if n and \
+        view_stride == 16 else None
+    total = int(sizes[0::2].sum()) if sizes is not None else (0 if n == 0 else None)
+    if out is None:
+        if total is None:
+            raise TkvAmqError(abi.INVALID_ARGUMENT, "pass `out` for strided variable-length views")
+        out = np.empty(max(total, 1), dtype=np.uint8)
+    offs = np.empty(n + 1, dtype=np.uint64)
+    cap = out.nbytes if isinstance(out, np.ndarray) else out.numel()
+    st = abi.lib().tkv_amq_stage_keys(ctypes.c_void_p(addr), view_stride, n, 0, _ptr(out), cap,
+                                      _ptr(offs), n_threads)
+    abi.check(st, "tkv_amq_stage_keys")
+    return out, offs
+
+
 def gen_keys16(seed: int, first: int, n: int, device=None, stream=None):
     """Synthetic bench keys on the device (splitmix64 stream)."""
     torch = _torch()
@@ -438,6 +483,7 @@ class HostFilterPipeline:
         torch = _torch()
         _require_device()
         self.kind, self.dev = kind, torch.device(device or "cuda")
+        self.key_bytes = key_bytes
         counts = np.asarray(leaf_key_counts, dtype=np.int64)
         if out_stride == 0:
             biggest = int(counts.max()) if len(counts) else 0
@@ -477,7 +523,34 @@ class HostFilterPipeline:
     def new_host_output(self):
         return _torch().empty(self.plan.total_out_bytes, dtype=_torch().uint8, pin_memory=True)
 
-    def run(self, host_keys, host_out=None, check: bool = True):
+    def run_views(self, views, host_out=None, view_stride: int = 16, n_threads: int = 0,
+                  check: bool = True):
+        """Keys given as tkv_amq_key_view records (the EditView key range; KEY_VIEW_DTYPE
+        array or the address of the first view).  Each chunk's keys are gathered into a
+        pinned staging buffer by host threads (tkv_amq_stage_keys) just before its H2D copy
+        is enqueued, so the gather of chunk c+1 overlaps the copies and build of chunk c."""
+        torch = _torch()
+        if isinstance(views, np.ndarray):
+            assert views.dtype == abi.KEY_VIEW_DTYPE and views.flags.c_contiguous
+            addr, view_stride = views.ctypes.data, abi.KEY_VIEW_DTYPE.itemsize
+        else:
+            addr = int(views)
+        n_keys = int(self.key_begin[-1])
+        if getattr(self, "_h_stage", None) is None or self._h_stage.shape[0] < n_keys:
+            self._h_stage = torch.empty((max(n_keys, 1), self.key_bytes), dtype=torch.uint8,
+                                        pin_memory=True)
+        h = self._h_stage
+
+        def stage(k0, k1):
+            if k1 > k0:
+                stage_keys(addr + k0 * view_stride, k1 - k0, self.key_bytes, out=h[k0:k1],
+                           view_stride=view_stride, n_threads=n_threads)
+
+        return self.run(h, host_out, check, stage=stage)
+
+    def run(self, host_keys, host_out=None, check: bool = True, stage=None):
+        """`stage(k0, k1)`, if given, fills host_keys[k0:k1] before that chunk's H2D copy is
+        enqueued (run_views)."""
         torch = _torch()
         if host_out is None:
             host_out = self.new_host_output()
@@ -492,6 +565,8 @@ class HostFilterPipeline:
         for c, (b0, b1) in enumerate(self.chunks):
             slot = c & 1
             k0, k1 = int(self.key_begin[b0]), int(self.key_begin[b1])
+            if stage is not None:
+                stage(k0, k1)
             with torch.cuda.stream(self.s_in):
                 if c >= 2:
                     self.s_in.wait_event(ev_run[c - 2])       # slot's keys no longer read
