@@ -7,7 +7,8 @@ EXPS=${EXPS:-0 1 2 3 4 5}
 if [ "$1" != "run" ]; then
   for e in $EXPS; do
     /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -std=c++17 -shared -fPIC -DTKV_EXP=$e \
-      -I$R/include -o $R/tools/exp/libtkv_amq_exp$e.so $R/turtle_kv_amd/csrc/tkv_amq_kernels.hip &
+      -I$R/include -o $R/tools/exp/libtkv_amq_exp$e.so $R/turtle_kv_amd/csrc/tkv_amq_kernels.hip \
+      $R/turtle_kv_amd/csrc/tkv_amq_stage.cpp &
   done
   wait
   exit 0
