@@ -31,6 +31,7 @@ sys.path.insert(0, ROOT)
 
 SEG_KEYS = 16384
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s peak (spec)
+FABRIC_LINES_G_PER_S = 61.7  # MI355X_MICROARCH.md: random rows of a 151 MB table, 7.9 TB/s / 128 B
 
 WORKLOADS = {
     # name: (kind, bits_per_key, payload_capacity, metric label)
@@ -261,6 +262,18 @@ def main():
                      "note": "PMC SQ_INSTS_VALU per key (profiles/traffic_*.json); peak = "
                              "1024 SIMDs x 2.4 GHz / 4 cycles (tools/ubench_valu.hip)"}
 
+    fabric_roof = None
+    if probe and prof.get("TCC_EA0_RDREQ_per_launch"):
+        # the bound a random-gather probe sits on: L2 -> fabric read requests (one 128-B line
+        # each) per second, against the random-row gather rate MI355X_MICROARCH.md measures
+        # for a 151 MB table (7.4-7.9 TB/s = 58-62 G lines/s)
+        req = prof["TCC_EA0_RDREQ_per_launch"] / (kernel_ms * 1e-3) / 1e9
+        fabric_roof = {"achieved": round(req, 2), "peak": FABRIC_LINES_G_PER_S,
+                       "unit": "G fabric read requests/s", "frac": round(req / FABRIC_LINES_G_PER_S, 4),
+                       "requests_per_lookup": prof.get("ea_read_requests_per_unit"),
+                       "note": "PMC TCC_EA0_RDREQ per launch (profiles/traffic_*.json); peak = "
+                               "7.9 TB/s / 128 B, the guide's random-row gather rate"}
+
     allgather_ms = None
     if world > 1 and not args.allgather:
         torch.cuda.synchronize()
@@ -323,6 +336,8 @@ def main():
     }
     if valu_roof is not None:
         line["valu_roofline"] = valu_roof
+    if fabric_roof is not None:
+        line["fabric_roofline"] = fabric_roof
     if allgather_ms is not None:
         line["allgather_ms"] = round(allgather_ms, 3)
         line["build_plus_allgather_mkeys_s"] = round(units / ((ms_per_step + allgather_ms) * 1e-3) / 1e6, 2)

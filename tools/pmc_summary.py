@@ -46,15 +46,17 @@ def main():
                     help="kernel-name substring; several, comma-separated, for a multi-kernel step")
     ap.add_argument("--fetch", required=True)
     ap.add_argument("--write", required=True)
-    ap.add_argument("--sq", required=True)
+    ap.add_argument("--sq", default=None)
+    ap.add_argument("--tcc", default=None,
+                    help="pass with TCC_EA0_RDREQ_sum / TCC_HIT_sum / TCC_MISS_sum (probes)")
+    ap.add_argument("--ms", type=float, default=None,
+                    help="kernel time per launch (ms), for the request rate of --tcc")
     ap.add_argument("--keys", type=int, required=True)
     ap.add_argument("--alg-bytes", type=int, required=True)
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
-    f, w, sq = agg(a.fetch, a.kernel), agg(a.write, a.kernel), agg(a.sq, a.kernel)
+    f, w = agg(a.fetch, a.kernel), agg(a.write, a.kernel)
     hbm = int(2 * f["FETCH_SIZE"] * 1024 + w["WRITE_SIZE"] * 1024)
-    clk_cycles = sq["GRBM_GUI_ACTIVE"] / 8
-    valu = sq["SQ_INSTS_VALU"]
     res = {
         "kernel": a.kernel, "workload": a.workload,
         "FETCH_SIZE_KiB": f["FETCH_SIZE"], "WRITE_SIZE_KiB": w["WRITE_SIZE"],
@@ -62,13 +64,29 @@ def main():
                       "counts half of 16B/lane streaming reads)",
         "hbm_bytes_per_launch": hbm, "algorithmic_bytes_per_launch": a.alg_bytes,
         "traffic_over_algorithmic": round(hbm / a.alg_bytes, 4),
-        "SQ_INSTS_VALU_per_launch": valu, "SQ_WAVES": sq.get("SQ_WAVES"),
-        "valu_instr_per_key": round(valu * 64 / a.keys, 1),
-        "GRBM_GUI_ACTIVE_per_xcd": clk_cycles,
-        "valu_cycles_per_wave_instr_per_simd": round(clk_cycles / (valu / SIMDS), 3),
-        "valu_peak_ginstr_s_at_2.4GHz": SIMDS * CLOCK_GHZ / CYCLES_PER_VALU,
-        "source": f"rocprofv3 --pmc passes: {a.fetch}, {a.write}, {a.sq}",
     }
+    if a.sq:
+        sq = agg(a.sq, a.kernel)
+        clk_cycles = sq["GRBM_GUI_ACTIVE"] / 8
+        valu = sq["SQ_INSTS_VALU"]
+        res.update({
+            "SQ_INSTS_VALU_per_launch": valu, "SQ_WAVES": sq.get("SQ_WAVES"),
+            "valu_instr_per_key": round(valu * 64 / a.keys, 1),
+            "GRBM_GUI_ACTIVE_per_xcd": clk_cycles,
+            "valu_cycles_per_wave_instr_per_simd": round(clk_cycles / (valu / SIMDS), 3),
+            "valu_peak_ginstr_s_at_2.4GHz": SIMDS * CLOCK_GHZ / CYCLES_PER_VALU,
+        })
+    if a.tcc:
+        t = agg(a.tcc, a.kernel)
+        req = t["TCC_EA0_RDREQ_sum"]
+        res.update({
+            "TCC_EA0_RDREQ_per_launch": req, "TCC_HIT_per_launch": t.get("TCC_HIT_sum"),
+            "TCC_MISS_per_launch": t.get("TCC_MISS_sum"),
+            "ea_read_requests_per_unit": round(req / a.keys, 4),
+        })
+        if a.ms:
+            res["ea_read_requests_g_per_s"] = round(req / (a.ms * 1e-3) / 1e9, 2)
+    res["source"] = f"rocprofv3 --pmc passes: {a.fetch}, {a.write}, {a.sq or '-'}, {a.tcc or '-'}"
     out = a.out or os.path.join("profiles", f"traffic_{a.workload}.json")
     with open(out, "w") as fh:
         json.dump(res, fh, indent=1)
