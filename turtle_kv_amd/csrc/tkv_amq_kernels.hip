@@ -1137,22 +1137,9 @@ __global__ __launch_bounds__(256) void vqf_scatter(const tkv_amq_segment* __rest
 // multiply, and the second pass takes each entry's slot with ds_add_rtn in insertion order.
 constexpr uint32_t kPlaceThreads = 128;
 
-// Per-block record stride in vqf_place_fused's LDS image: slots x entry bytes padded to an
-// 8-byte multiple whose dword count is 2 mod 4 (26 / 30 dwords), so the per-thread bucket
-// counters that later reuse the record spread over the banks.
-__host__ __device__ constexpr inline uint32_t vqf_lds_rec_stride(int t)
-{
-  return t == 8 ? 104u : 120u;
-}
-
-// kLds: the block records come from the leaf's LDS image (kSlots entries per block, counts in
-// lds_cnt) built by vqf_place_fused; otherwise from the workspace's 128-byte block records.
-// kLds: the bucket counters live in the block's own LDS record once it is in registers, so
-// the only per-thread scratch is the 68-byte output image.
-template <int T, bool kLds = false, uint32_t kThreads = kPlaceThreads>
+template <int T>
 __device__ void vqf_place_body(const tkv_amq_segment& sg, uint32_t seg_index, VqfWorkspace ws,
-                               uint8_t* __restrict__ out, uint32_t* s_cnt, uint32_t* s_img,
-                               uint8_t* lds_img = nullptr, const uint32_t* lds_cnt = nullptr)
+                               uint8_t* __restrict__ out, uint32_t* s_cnt, uint32_t* s_img)
 {
   using C = Vqf<T>;
   using E = typename C::Entry;
@@ -1180,36 +1167,17 @@ __device__ void vqf_place_body(const tkv_amq_segment& sg, uint32_t seg_index, Vq
     reinterpret_cast<ulonglong2*>(payload)[tid] = v;
   }
 
-  uint32_t* cnt = kLds ? nullptr : s_cnt + tid * kCntStride;
+  uint32_t* cnt = s_cnt + tid * kCntStride;
   uint32_t* img = s_img + tid * kImgStride;
   uint4* dst_blocks = reinterpret_cast<uint4*>(payload + kVqfHeader + kVqfMetadata);
 
-  for (uint32_t b = tid; b < nb; b += kThreads) {
-    const uint8_t* rec;
-    uint32_t c;
-    if constexpr (kLds) {
-      rec = lds_img + b * vqf_lds_rec_stride(T);
-      c = lds_cnt[b];
-    } else {
-      rec = ws.temp + (sg.block_base + b) * kVqfTempStride;
-      c = *reinterpret_cast<const uint32_t*>(rec + kVqfCountByte);
-    }
+  for (uint32_t b = tid; b < nb; b += kPlaceThreads) {
+    const uint8_t* rec = ws.temp + (sg.block_base + b) * kVqfTempStride;
+    const uint32_t c = *reinterpret_cast<const uint32_t*>(rec + kVqfCountByte);
     uint4 rv[kRecWords];
 #pragma unroll
-    for (uint32_t q = 0; q < kRecWords; ++q) {
-      if constexpr (kLds) {  // 8-byte aligned records (padded stride)
-        const uint2 lo = reinterpret_cast<const uint2*>(rec)[2 * q];
-        const uint2 hi = reinterpret_cast<const uint2*>(rec)[2 * q + 1];
-        rv[q] = make_uint4(lo.x, lo.y, hi.x, hi.y);
-      } else {
-        rv[q] = reinterpret_cast<const uint4*>(rec)[q];
-      }
-    }
+    for (uint32_t q = 0; q < kRecWords; ++q) rv[q] = reinterpret_cast<const uint4*>(rec)[q];
     const E* ent = reinterpret_cast<const E*>(rv);
-    if constexpr (kLds) {
-      asm volatile("" ::: "memory");  // the record is in registers before its bytes are reused
-      cnt = reinterpret_cast<uint32_t*>(lds_img + b * vqf_lds_rec_stride(T));
-    }
 
 #pragma unroll
     for (uint32_t w = 0; w < kCntWords; ++w) cnt[w] = 0;
@@ -1299,35 +1267,211 @@ __global__ __launch_bounds__(kPlaceThreads) void vqf_place(const tkv_amq_segment
 // Fused scatter + place for leaves whose block records fit in LDS (one workgroup per leaf):
 // the leaf's placement records stream in coalesced, each entry lands at [block][rank] of an
 // LDS image (no partial-line global writes), then the per-block counting sort runs on it.
+//
+// LDS image: one 33-dword (132-byte) region per block -- an odd dword stride, so threads
+// working on consecutive blocks at the same offset hit distinct banks.  Phase 1 writes the
+// block's entries at [0, slots * entry bytes); the block's count comes from the workspace,
+// where vqf_decide leaves it.  Phase 2 loads a block's entries into registers, then reuses
+// the region (dword 32 takes the dead slots' tag stores): packed bucket counters
+// in dwords [0, kCntWords), the tag image (bytes kMdBytes..63 of the output block) at
+// kTagDword; the metadata stays in registers.  No per-thread scratch: a 402-block leaf takes
+// 53 KB of LDS (registers, ~234 VGPRs, still hold the kernel to two workgroups per CU; forcing
+// three spilled and ran 29% slower).
 constexpr uint32_t kFusedThreads = 256;
 constexpr uint32_t kFusedLdsBudget = 80 * 1024;
+constexpr uint32_t kFusedRegionWords = 33;
+constexpr uint32_t kFusedCountWord = 32;
 
 __host__ __device__ inline uint32_t vqf_fused_img_bytes(uint32_t nb)
 {
-  return nb * 120u;  // max over T of vqf_lds_rec_stride
+  return nb * kFusedRegionWords * 4u;
 }
 
 __host__ __device__ inline uint32_t vqf_fused_lds_bytes(uint32_t max_nb)
 {
-  return vqf_fused_img_bytes(max_nb) + 4 * ((max_nb + 3) & ~3u) + kFusedThreads * 17 * 4;
+  return vqf_fused_img_bytes(max_nb);
+}
+
+// Phase 2: one thread per block (NB > 1: NB blocks per thread interleaved; NB = 2 doubled the
+// registers to 450 and ran slower).  Measured: phase 2 is bound by its LDS operations
+// (3 per slot, random bucket words, so bank conflicts), not by their latency.
+template <int T, int NB>
+__device__ void vqf_place_fused_sort(const tkv_amq_segment& sg, uint32_t seg_index,
+                                     VqfWorkspace ws, uint8_t* __restrict__ out, uint32_t* lds)
+{
+  using C = Vqf<T>;
+  using E = typename C::Entry;
+  constexpr uint32_t kCntWords = (C::kBuckets + 3) / 4;                // 20 / 9
+  constexpr uint32_t kEntWords = C::kSlots * sizeof(E) / 4;            // 24 / 28
+  constexpr uint32_t kTagDword = T == 8 ? 20 : 12;                     // tag image start
+  constexpr uint32_t kTagWords = (64 - C::kMdBytes) / 4;               // 12 / 14
+  static_assert(kTagDword + kTagWords <= kFusedCountWord && kEntWords <= kFusedCountWord, "");
+  static_assert(kCntWords <= kTagDword, "");
+  constexpr uint32_t kGroup = 12;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t nb = sg.n_blocks;
+  uint8_t* payload = out + sg.out_offset;
+
+  if (tid < 5) {
+    // PackedVqfFilter header (vqf_filter_page_view.hpp:79-94) + vqf_metadata
+    uint64_t w0, w1;
+    switch (tid) {
+      case 0: w0 = kVqfMagic; w1 = sg.src_page_id; break;
+      case 1: w0 = kVqfHashSeed; w1 = ~0ull << sg.hash_val_shift; break;
+      case 2: w0 = 64ull * nb; w1 = T; break;
+      case 3: w0 = (uint64_t)nb * C::kBuckets << T; w1 = nb; break;
+      default: w0 = ws.nelts[seg_index]; w1 = (uint64_t)nb * C::kSlots; break;
+    }
+    ulonglong2 v;
+    v.x = w0;
+    v.y = w1;
+    reinterpret_cast<ulonglong2*>(payload)[tid] = v;
+  }
+  uint4* dst_blocks = reinterpret_cast<uint4*>(payload + kVqfHeader + kVqfMetadata);
+
+  for (uint32_t b0 = tid; b0 < nb; b0 += NB * kFusedThreads) {
+    uint32_t* reg[NB];
+    uint32_t c[NB];
+    bool live[NB];
+    uint32_t ent[NB][kEntWords];
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const uint32_t b = b0 + j * kFusedThreads;
+      live[j] = b < nb;
+      reg[j] = lds + (live[j] ? b : b0) * kFusedRegionWords;
+      // the block's final count, as vqf_decide left it in the workspace
+      c[j] = live[j] ? vqf_count(ws, sg.block_base + b) : 0u;
+#pragma unroll
+      for (uint32_t w = 0; w < kEntWords; ++w) ent[j][w] = reg[j][w];
+    }
+    asm volatile("" ::: "memory");  // entries are in registers before their words are reused
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      if (!live[j]) continue;
+#pragma unroll
+      for (uint32_t w = 0; w < kCntWords; ++w) reg[j][w] = 0;
+#pragma unroll
+      for (uint32_t w = 0; w < kTagWords; ++w) reg[j][kTagDword + w] = 0;
+    }
+    // pass 1: bucket histogram (bytes, 4 buckets per dword).  Branch-free: dead slots add 0.
+#pragma unroll
+    for (uint32_t i = 0; i < C::kSlots; ++i) {
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        const E e = reinterpret_cast<const E*>(ent[j])[i];
+        const bool on = live[j] && i < c[j];
+        const uint32_t o = on ? (uint32_t)(e >> T) : 0u;
+        atomicAdd(reg[j] + (o >> 2), on ? 1u << (8 * (o & 3)) : 0u);
+      }
+    }
+    // exclusive prefix over buckets: inclusive-in-dword = v * 0x01010101
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      uint32_t run = 0;
+#pragma unroll
+      for (uint32_t w = 0; w < kCntWords; ++w) {
+        const uint32_t v = reg[j][w];
+        const uint32_t incl = v * 0x01010101u;
+        reg[j][w] = (incl - v) + run * 0x01010101u;
+        run += incl >> 24;
+      }
+    }
+    // pass 2a: each entry's slot in insertion order (ds_add_rtn on its bucket counter).  The
+    // atomics are issued back to back: no store whose address depends on a returned slot
+    // sits between them (that ordering made every atomic wait for the previous one).
+    uint32_t slots[NB][(C::kSlots + 3) / 4];  // 4 slot bytes per dword
+#pragma unroll
+    for (uint32_t i = 0; i < C::kSlots; ++i) {
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        const uint32_t e = reinterpret_cast<const E*>(ent[j])[i];
+        const bool on = live[j] && i < c[j];
+        const uint32_t o = on ? e >> T : 0u;
+        const uint32_t old = atomicAdd(reg[j] + (o >> 2), on ? 1u << (8 * (o & 3)) : 0u);
+        const uint32_t slot = (old >> (8 * (o & 3))) & 0xffu;
+        if (i % 4 == 0) slots[j][i / 4] = slot;
+        else slots[j][i / 4] |= slot << (8 * (i % 4));
+      }
+      // groups of kGroup: bounded live ranges (registers set the workgroups per CU)
+      if (i % kGroup == kGroup - 1) __builtin_amdgcn_sched_barrier(0);
+    }
+    // pass 2b: metadata zero at slot + offset; tag bytes into the image
+    uint64_t md_lo[NB], md_hi[NB];
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      md_lo[j] = ~0ull;
+      md_hi[j] = T == 8 ? ~0ull : 0ull;
+    }
+#pragma unroll
+    for (uint32_t i = 0; i < C::kSlots; ++i) {
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        const uint32_t e = reinterpret_cast<const E*>(ent[j])[i];
+        const bool on = live[j] && i < c[j];
+        const uint32_t o = on ? e >> T : 0u, tag = e & ((1u << T) - 1);
+        const uint32_t slot = (slots[j][i / 4] >> (8 * (i % 4))) & 0xffu;
+        const uint32_t z = slot + o;
+        const uint64_t clr = on ? 1ull << (z & 63) : 0ull;
+        if (z < 64) md_lo[j] &= ~clr;
+        else md_hi[j] &= ~clr;
+        // dead slots store into the region's count word (no longer read)
+        uint8_t* r8 = reinterpret_cast<uint8_t*>(reg[j]);
+        const uint32_t byte = on ? 4 * kTagDword + slot * (T / 8) : 4 * kFusedCountWord;
+        if constexpr (T == 8) {
+          r8[byte] = (uint8_t)tag;
+        } else {
+          const uint16_t t16 = (uint16_t)tag;
+          __builtin_memcpy(r8 + byte, &t16, 2);
+        }
+      }
+      if (i % kGroup == kGroup - 1) __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      if (!live[j]) continue;
+      if (c[j] == 0) {  // an empty block keeps the init metadata: top bit clear
+        if constexpr (T == 8) md_hi[j] &= ~(1ull << 63);
+        else md_lo[j] &= ~(1ull << 63);
+      }
+      const uint32_t* tg = reg[j] + kTagDword;
+      uint4* dst = dst_blocks + (uint64_t)(b0 + j * kFusedThreads) * 4;
+      uint4 v0;
+      v0.x = (uint32_t)md_lo[j];
+      v0.y = (uint32_t)(md_lo[j] >> 32);
+      if constexpr (T == 8) {
+        v0.z = (uint32_t)md_hi[j];
+        v0.w = (uint32_t)(md_hi[j] >> 32);
+        dst[0] = v0;
+#pragma unroll
+        for (uint32_t q = 0; q < 3; ++q) dst[1 + q] = make_uint4(tg[4 * q], tg[4 * q + 1], tg[4 * q + 2], tg[4 * q + 3]);
+      } else {
+        v0.z = tg[0];
+        v0.w = tg[1];
+        dst[0] = v0;
+#pragma unroll
+        for (uint32_t q = 0; q < 3; ++q)
+          dst[1 + q] = make_uint4(tg[2 + 4 * q], tg[3 + 4 * q], tg[4 + 4 * q], tg[5 + 4 * q]);
+      }
+    }
+  }
 }
 
 template <int T>
 __device__ void vqf_place_fused_body(const tkv_amq_segment& sg, uint32_t seg_index,
                                      VqfWorkspace ws, const uint64_t* __restrict__ recs,
-                                     uint8_t* __restrict__ out, uint8_t* lds)
+                                     uint8_t* __restrict__ out, uint32_t* lds)
 {
   using C = Vqf<T>;
   using E = typename C::Entry;
   const uint32_t tid = threadIdx.x;
   const uint32_t nb = sg.n_blocks, n = sg.n_keys;
-  E* img = reinterpret_cast<E*>(lds);
-  uint32_t* cnt = reinterpret_cast<uint32_t*>(lds + vqf_fused_img_bytes(nb));
-  uint32_t* s_img = cnt + ((nb + 3) & ~3u);
-  for (uint32_t b = tid; b < nb; b += kFusedThreads) cnt[b] = 0;
-  __syncthreads();
   const uint32_t gb0 = (uint32_t)sg.block_base;
   constexpr uint32_t kU = 8;  // 16-byte loads in flight per thread: 32 KB per workgroup
+  auto put_entry = [&](uint32_t blk, uint32_t rank, uint32_t e) {
+    uint32_t* r = lds + blk * kFusedRegionWords;
+    if constexpr (T == 8) reinterpret_cast<uint16_t*>(r)[rank] = (uint16_t)e;
+    else r[rank] = e;
+  };
   if (T == 8 && nb <= 512) {
     // compact 4-byte records (vqf_decide kCompact), four per load
     const uint32_t* r32 = reinterpret_cast<const uint32_t*>(recs + sg.key_begin);
@@ -1335,11 +1479,7 @@ __device__ void vqf_place_fused_body(const tkv_amq_segment& sg, uint32_t seg_ind
     const uint4* r4 = reinterpret_cast<const uint4*>(r32 - skip);
     const uint32_t n_quads = (skip + n + 3) / 4;
     auto put = [&](uint32_t v, uint32_t k) {
-      if (k >= skip && k < skip + n && v != 0xffffffffu) {
-        const uint32_t blk = v >> 21;
-        img[blk * (vqf_lds_rec_stride(T) / sizeof(E)) + ((v >> 15) & 63u)] = (E)(v & 0x7fffu);
-        atomicAdd(cnt + blk, 1u);
-      }
+      if (k >= skip && k < skip + n && v != 0xffffffffu) put_entry(v >> 21, (v >> 15) & 63u, v & 0x7fffu);
     };
     for (uint32_t q0 = 0; q0 < n_quads; q0 += kFusedThreads * kU) {
       uint4 v[kU];
@@ -1365,11 +1505,8 @@ __device__ void vqf_place_fused_body(const tkv_amq_segment& sg, uint32_t seg_ind
     const uint32_t n_pairs = (lo_skip + n + 1) / 2;
     auto put = [&](uint64_t v, uint32_t k) {
       const uint32_t hi = (uint32_t)(v >> 32);
-      if (k >= lo_skip && k < lo_skip + n && hi != 0xffffffffu) {
-        const uint32_t blk = (hi >> 6) - gb0;
-        img[blk * (vqf_lds_rec_stride(T) / sizeof(E)) + (hi & 63u)] = (E)((uint32_t)v & 0x7fffffffu);
-        atomicAdd(cnt + blk, 1u);
-      }
+      if (k >= lo_skip && k < lo_skip + n && hi != 0xffffffffu)
+        put_entry((hi >> 6) - gb0, hi & 63u, (uint32_t)v & 0x7fffffffu);
     };
     for (uint32_t p0 = 0; p0 < n_pairs; p0 += kFusedThreads * kU) {
       uint4 v[kU];
@@ -1387,15 +1524,14 @@ __device__ void vqf_place_fused_body(const tkv_amq_segment& sg, uint32_t seg_ind
     }
   }
   __syncthreads();
-  if (TKV_EXP != 6)
-    vqf_place_body<T, true, kFusedThreads>(sg, seg_index, ws, out, nullptr, s_img, lds, cnt);
+  if (TKV_EXP != 6) vqf_place_fused_sort<T, 1>(sg, seg_index, ws, out, lds);
 }
 
 __global__ __launch_bounds__(kFusedThreads) void vqf_place_fused(const tkv_amq_segment* __restrict__ segs,
                                                                  void* ws_base, uint32_t n_segs,
                                                                  uint8_t* __restrict__ out)
 {
-  extern __shared__ __attribute__((aligned(16))) uint8_t s_lds[];
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_lds[];
   const tkv_amq_segment sg = segs[blockIdx.x];
   const VqfWorkspace ws = vqf_workspace(ws_base, n_segs);
   const uint64_t* recs = vqf_records(ws, segs, n_segs);
