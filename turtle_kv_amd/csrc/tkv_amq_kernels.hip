@@ -855,7 +855,8 @@ __device__ inline void vqf_locate_alt(const VqfLoc& l, uint64_t R, uint64_t magi
 template <int T, int MODE, int NBITS, bool kLdsMatch, bool kCompact>
 __device__ void vqf_decide_body(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs,
                                 uint32_t stride, const tkv_amq_segment& sg, uint32_t seg_index,
-                                VqfWorkspace ws, uint64_t* __restrict__ recs, uint32_t* cnt)
+                                VqfWorkspace ws, uint64_t* __restrict__ recs, uint32_t* cnt,
+                                bool fused)
 {
   using C = Vqf<T>;
   const uint32_t lane = threadIdx.x;
@@ -1064,9 +1065,13 @@ __device__ void vqf_decide_body(const uint8_t* __restrict__ keys, const uint64_t
   }
   if (pend) *pend_ptr = pend_val;
   __syncthreads();
-  for (uint32_t b = lane; b < nb; b += 64) {
-    const uint32_t c = cnt[b];
-    vqf_count(ws, sg.block_base + b) = c < C::kSlots ? c : C::kSlots;
+  // the final per-block counts feed only the unfused place path (the fused one recounts in
+  // LDS): 4 bytes per 128-byte block record, so skip them when they are not read
+  if (!fused) {
+    for (uint32_t b = lane; b < nb; b += 64) {
+      const uint32_t c = cnt[b];
+      vqf_count(ws, sg.block_base + b) = c < C::kSlots ? c : C::kSlots;
+    }
   }
   if (lane == 0) {
     ws.nelts[seg_index] = nelts;
@@ -1084,14 +1089,14 @@ __device__ inline void vqf_decide_dispatch(const uint8_t* keys, const uint64_t* 
   if (sg.n_blocks <= 512) {
     static_assert(kVqfMatchLdsBlocks == 512, "");
     if (T == 8 && compact_ok) {
-      if (match_lds) vqf_decide_body<T, MODE, 9, true, T == 8>(keys, offs, stride, sg, seg_index, ws, recs, cnt);
-      else vqf_decide_body<T, MODE, 9, false, T == 8>(keys, offs, stride, sg, seg_index, ws, recs, cnt);
+      if (match_lds) vqf_decide_body<T, MODE, 9, true, T == 8>(keys, offs, stride, sg, seg_index, ws, recs, cnt, compact_ok);
+      else vqf_decide_body<T, MODE, 9, false, T == 8>(keys, offs, stride, sg, seg_index, ws, recs, cnt, compact_ok);
     } else {
-      if (match_lds) vqf_decide_body<T, MODE, 9, true, false>(keys, offs, stride, sg, seg_index, ws, recs, cnt);
-      else vqf_decide_body<T, MODE, 9, false, false>(keys, offs, stride, sg, seg_index, ws, recs, cnt);
+      if (match_lds) vqf_decide_body<T, MODE, 9, true, false>(keys, offs, stride, sg, seg_index, ws, recs, cnt, compact_ok);
+      else vqf_decide_body<T, MODE, 9, false, false>(keys, offs, stride, sg, seg_index, ws, recs, cnt, compact_ok);
     }
   } else {
-    vqf_decide_body<T, MODE, 14, false, false>(keys, offs, stride, sg, seg_index, ws, recs, cnt);
+    vqf_decide_body<T, MODE, 14, false, false>(keys, offs, stride, sg, seg_index, ws, recs, cnt, compact_ok);
   }
 }
 
@@ -1270,9 +1275,10 @@ __global__ __launch_bounds__(kPlaceThreads) void vqf_place(const tkv_amq_segment
 //
 // LDS image: one 33-dword (132-byte) region per block -- an odd dword stride, so threads
 // working on consecutive blocks at the same offset hit distinct banks.  Phase 1 writes the
-// block's entries at [0, slots * entry bytes); the block's count comes from the workspace,
-// where vqf_decide leaves it.  Phase 2 loads a block's entries into registers, then reuses
-// the region (dword 32 takes the dead slots' tag stores): packed bucket counters
+// block's entries at [0, slots * entry bytes) and counts them in dword 32 (reading the counts
+// vqf_decide could leave in the workspace instead cost 4-byte reads of 128-byte lines: +0.31 GB
+// per 100M keys; on this path vqf_decide does not write them).  Phase 2 loads a block's
+// entries and count into registers, then reuses the region: packed bucket counters
 // in dwords [0, kCntWords), the tag image (bytes kMdBytes..63 of the output block) at
 // kTagDword; the metadata stays in registers.  No per-thread scratch: a 402-block leaf takes
 // 53 KB of LDS (registers, ~234 VGPRs, still hold the kernel to two workgroups per CU; forcing
@@ -1339,8 +1345,7 @@ __device__ void vqf_place_fused_sort(const tkv_amq_segment& sg, uint32_t seg_ind
       const uint32_t b = b0 + j * kFusedThreads;
       live[j] = b < nb;
       reg[j] = lds + (live[j] ? b : b0) * kFusedRegionWords;
-      // the block's final count, as vqf_decide left it in the workspace
-      c[j] = live[j] ? vqf_count(ws, sg.block_base + b) : 0u;
+      c[j] = live[j] ? reg[j][kFusedCountWord] : 0u;
 #pragma unroll
       for (uint32_t w = 0; w < kEntWords; ++w) ent[j][w] = reg[j][w];
     }
@@ -1465,12 +1470,15 @@ __device__ void vqf_place_fused_body(const tkv_amq_segment& sg, uint32_t seg_ind
   using E = typename C::Entry;
   const uint32_t tid = threadIdx.x;
   const uint32_t nb = sg.n_blocks, n = sg.n_keys;
+  for (uint32_t b = tid; b < nb; b += kFusedThreads) lds[b * kFusedRegionWords + kFusedCountWord] = 0;
+  __syncthreads();
   const uint32_t gb0 = (uint32_t)sg.block_base;
   constexpr uint32_t kU = 8;  // 16-byte loads in flight per thread: 32 KB per workgroup
   auto put_entry = [&](uint32_t blk, uint32_t rank, uint32_t e) {
     uint32_t* r = lds + blk * kFusedRegionWords;
     if constexpr (T == 8) reinterpret_cast<uint16_t*>(r)[rank] = (uint16_t)e;
     else r[rank] = e;
+    atomicAdd(r + kFusedCountWord, 1u);
   };
   if (T == 8 && nb <= 512) {
     // compact 4-byte records (vqf_decide kCompact), four per load
