@@ -523,12 +523,15 @@ class HostFilterPipeline:
     def new_host_output(self):
         return _torch().empty(self.plan.total_out_bytes, dtype=_torch().uint8, pin_memory=True)
 
-    def run_views(self, views, host_out=None, view_stride: int = 16, n_threads: int = 0,
+    def run_views(self, views, host_out=None, view_stride: int = 16, n_threads: int = 16,
                   check: bool = True):
         """Keys given as tkv_amq_key_view records (the EditView key range; KEY_VIEW_DTYPE
         array or the address of the first view).  Each chunk's keys are gathered into a
-        pinned staging buffer by host threads (tkv_amq_stage_keys) just before its H2D copy
-        is enqueued, so the gather of chunk c+1 overlaps the copies and build of chunk c."""
+        pinned staging buffer by host threads just before its H2D copy is enqueued, so the
+        gather of chunk c+1 overlaps the copies and build of chunk c.  The threads are a
+        persistent pool, each running tkv_amq_stage_keys on a slice (ctypes releases the GIL),
+        so no threads are created per chunk."""
+        import concurrent.futures
         torch = _torch()
         if isinstance(views, np.ndarray):
             assert views.dtype == abi.KEY_VIEW_DTYPE and views.flags.c_contiguous
@@ -540,11 +543,21 @@ class HostFilterPipeline:
             self._h_stage = torch.empty((max(n_keys, 1), self.key_bytes), dtype=torch.uint8,
                                         pin_memory=True)
         h = self._h_stage
+        if getattr(self, "_pool", None) is None or self._pool_threads != n_threads:
+            self._pool = concurrent.futures.ThreadPoolExecutor(max(1, n_threads))
+            self._pool_threads = n_threads
+
+        def one(a, b):
+            stage_keys(addr + a * view_stride, b - a, self.key_bytes, out=h[a:b],
+                       view_stride=view_stride, n_threads=1)
 
         def stage(k0, k1):
-            if k1 > k0:
-                stage_keys(addr + k0 * view_stride, k1 - k0, self.key_bytes, out=h[k0:k1],
-                           view_stride=view_stride, n_threads=n_threads)
+            if k1 <= k0:
+                return
+            parts = max(1, min(n_threads, (k1 - k0) // 16384))
+            cuts = [k0 + (k1 - k0) * i // parts for i in range(parts + 1)]
+            for f in [self._pool.submit(one, a, b) for a, b in zip(cuts, cuts[1:])]:
+                f.result()
 
         return self.run(h, host_out, check, stage=stage)
 
