@@ -173,3 +173,21 @@ def test_host_pipeline_from_key_views(oracle, amq, torch, kind, bpk, cap):
     a = pipe.run_views(views).clone()
     b = pipe.run(torch.from_numpy(keys).pin_memory())
     assert torch.equal(a, b)
+
+
+def test_build_records_reference_metrics(oracle, amq, torch):
+    """A checked build folds its leaves into BloomFilterMetrics / QuotientFilterMetrics with a
+    build latency, as build_{bloom,vqf}_filter do per leaf (filter_builder.hpp:139-147,198-202)."""
+    counts = [16384, 777]
+    keys = oracle.gen_keys16(5, 0, sum(counts))
+    oracle.sort_segments(keys, np.concatenate([[0], np.cumsum(counts)]).astype(np.uint64))
+    kb = amq.KeyBatch.fixed(torch.from_numpy(keys).cuda())
+    for kind, m in ((amq.BLOOM, amq.BloomFilterMetrics.instance()),
+                    (amq.VQF, amq.QuotientFilterMetrics.instance())):
+        plan = amq.plan_filters(kind, counts, 12, payload_capacity=32704)
+        c0, t0, l0 = m.item_count_stats.count, m.item_count_stats.total, m.build_page_latency.count
+        amq.build_all_filters(plan, kb)
+        assert m.item_count_stats.count == c0 + 2 and m.item_count_stats.total == t0 + sum(counts)
+        assert m.build_page_latency.count == l0 + 2 and m.build_page_latency.total_usec > 0
+        amq.build_all_filters(plan, kb, check=False)   # unchecked launches record nothing
+        assert m.item_count_stats.count == c0 + 2

@@ -9,7 +9,8 @@ from .filters import (BoolStatus, FilterPage, FilterPlan, KeyBatch, KeyQuery, Pa
                       bloom_query_hashes, bloom_probe_hashed, HostFilterPipeline,
                       plan_filters, probe_filters, vqf_filter_load_factor, vqf_hash_val,
                       vqf_nslots_for_size, vqf_probe_hashed, vqf_required_size, key_views,
-                      stage_keys)
+                      stage_keys, BloomFilterMetrics, QuotientFilterMetrics,
+                      plan_filter_stats, record_filter_metrics)
 
 __all__ = [
     "abi", "BLOOM", "VQF", "TkvAmqError", "BoolStatus", "FilterPage", "FilterPlan", "KeyBatch",
@@ -18,4 +19,5 @@ __all__ = [
     "gen_keys16", "plan_filters", "probe_filters", "vqf_filter_load_factor", "vqf_hash_val",
     "vqf_nslots_for_size", "vqf_probe_hashed", "vqf_required_size", "bloom_query_hashes",
     "bloom_probe_hashed", "HostFilterPipeline", "key_views", "stage_keys",
+    "BloomFilterMetrics", "QuotientFilterMetrics", "plan_filter_stats", "record_filter_metrics",
 ]

@@ -23,6 +23,8 @@ from __future__ import annotations
 import ctypes
 import enum
 import logging
+import threading
+import time
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -113,6 +115,7 @@ class FilterPlan:
     max_seg_blocks: int
     n_keys: int
     _device: dict = field(default_factory=dict, repr=False)
+    _stats: dict | None = field(default=None, repr=False)
 
     @property
     def n_segs(self) -> int:
@@ -246,6 +249,131 @@ def gen_keys16(seed: int, first: int, n: int, device=None, stream=None):
 # ---------------------------------------------------------------------------------------
 # build
 # ---------------------------------------------------------------------------------------
+# ---------------------------------------------------------------------------------------
+# build metrics (BloomFilterMetrics, tree/filter_builder.hpp:39-56,136-147;
+# QuotientFilterMetrics, :156-172,198-202)
+# ---------------------------------------------------------------------------------------
+class StatsMetric:
+    """batt StatsMetric<u64>: count, total, min, max of the values it was updated with."""
+
+    def __init__(self):
+        self._lock = threading.Lock()
+        self.count, self.total, self.min, self.max = 0, 0, None, None
+
+    def merge(self, count: int, total: int, lo: int, hi: int) -> None:
+        if count == 0:
+            return
+        with self._lock:
+            self.count += count
+            self.total += total
+            self.min = lo if self.min is None else min(self.min, lo)
+            self.max = hi if self.max is None else max(self.max, hi)
+
+    def update(self, v: int) -> None:
+        self.merge(1, int(v), int(v), int(v))
+
+    @property
+    def mean(self) -> float:
+        return self.total / self.count if self.count else 0.0
+
+    def __repr__(self):
+        return f"StatsMetric(count={self.count}, total={self.total}, min={self.min}, max={self.max})"
+
+
+class LatencyMetric:
+    """LatencyMetric: count and total microseconds (per leaf filter, amortised over a batch)."""
+
+    def __init__(self):
+        self._lock = threading.Lock()
+        self.count, self.total_usec = 0, 0
+
+    def add(self, count: int, usec: float) -> None:
+        with self._lock:
+            self.count += count
+            self.total_usec += int(usec)
+
+
+class BloomFilterMetrics:
+    """tree/filter_builder.hpp:39-56 (one process-wide instance, like Self::instance())."""
+    _inst = None
+
+    def __init__(self):
+        self.word_count_stats = StatsMetric()
+        self.byte_size_stats = StatsMetric()
+        self.bit_size_stats = StatsMetric()
+        self.bit_count_stats = StatsMetric()
+        self.item_count_stats = StatsMetric()
+        self.build_page_latency = LatencyMetric()
+
+    @classmethod
+    def instance(cls) -> "BloomFilterMetrics":
+        if cls._inst is None:
+            cls._inst = cls()
+        return cls._inst
+
+
+class QuotientFilterMetrics:
+    """tree/filter_builder.hpp:156-172."""
+    _inst = None
+
+    def __init__(self):
+        self.byte_size_stats = StatsMetric()
+        self.bit_size_stats = StatsMetric()
+        self.item_count_stats = StatsMetric()
+        self.bits_per_key_stats = StatsMetric()
+        self.build_page_latency = LatencyMetric()
+
+    @classmethod
+    def instance(cls) -> "QuotientFilterMetrics":
+        if cls._inst is None:
+            cls._inst = cls()
+        return cls._inst
+
+
+def _agg(v: np.ndarray):
+    return (len(v), int(v.sum()), int(v.min()), int(v.max())) if len(v) else (0, 0, 0, 0)
+
+
+def plan_filter_stats(plan: FilterPlan) -> dict:
+    """The per-leaf values the reference records for every filter of a plan, aggregated
+    (count, total, min, max), keyed by metric name.  Leaves without a filter (bits_per_key 0)
+    record nothing; an empty VQF leaf skips bits_per_key (the reference would divide by
+    zero, :202)."""
+    if plan._stats is not None:
+        return plan._stats
+    segs = plan.segs
+    n = segs["n_keys"].astype(np.int64)
+    if plan.kind == BLOOM:
+        has = segs["hash_count"] != 0
+        words = 8 * segs["n_blocks"][has].astype(np.int64)        # PackedBloomFilter::word_count()
+        st = {"word_count_stats": _agg(words), "byte_size_stats": _agg(8 * words),
+              "bit_size_stats": _agg(64 * words),
+              "bit_count_stats": _agg(512 * segs["n_blocks"][has].astype(np.int64)),  # header bit_count
+              "item_count_stats": _agg(n[has])}
+    else:
+        has = segs["tag_bits"] != 0
+        size = segs["payload_bytes"][has].astype(np.int64) - 32   # vqf_filter_size (:194)
+        nz = n[has] > 0
+        st = {"byte_size_stats": _agg(size), "bit_size_stats": _agg(8 * size),
+              "item_count_stats": _agg(n[has]),
+              "bits_per_key_stats": _agg((size[nz] * 8 + 4) // n[has][nz])}
+    plan._stats = st
+    return st
+
+
+def record_filter_metrics(plan: FilterPlan, latency_usec: float | None = None) -> None:
+    """Fold one built batch into BloomFilterMetrics / QuotientFilterMetrics, as the reference
+    does per built leaf filter (filter_builder.hpp:139-147, :198-202)."""
+    m = BloomFilterMetrics.instance() if plan.kind == BLOOM else QuotientFilterMetrics.instance()
+    st = plan_filter_stats(plan)
+    for name, agg in st.items():
+        getattr(m, name).merge(*agg)
+    if latency_usec is not None:
+        leaves = st["item_count_stats"][0]
+        if leaves:
+            m.build_page_latency.add(leaves, latency_usec)
+
+
 def build_all_filters(plan: FilterPlan, keys: KeyBatch, out=None, workspace=None, stream=None,
                       check: bool = True):
     """Build every planned filter into one device array (the filter half of
@@ -260,14 +388,17 @@ def build_all_filters(plan: FilterPlan, keys: KeyBatch, out=None, workspace=None
     if plan.workspace_bytes and workspace is None:
         workspace = torch.empty(plan.workspace_bytes, dtype=torch.uint8, device=dev)
     sh = _stream_handle(stream)
+    t0 = time.perf_counter()
     st = abi.lib().tkv_amq_build(plan.kind, _ptr(keys.data), _ptr(keys.offsets), keys.stride,
                                  keys.n, _ptr(plan.device_segs(dev)), plan.n_segs,
                                  plan.max_seg_blocks, _ptr(out), _ptr(workspace),
                                  plan.workspace_bytes, sh)
     abi.check(st, "tkv_amq_build")
     if check:
+        # synchronous: the batch is known good, record its metrics with the build latency
         abi.check(abi.lib().tkv_amq_build_check(plan.kind, _ptr(workspace), plan.workspace_bytes,
                                                 sh), "vqf_insert (filter_builder.hpp:211)")
+        record_filter_metrics(plan, (time.perf_counter() - t0) * 1e6)
     return out
 
 
@@ -565,6 +696,7 @@ class HostFilterPipeline:
         """`stage(k0, k1)`, if given, fills host_keys[k0:k1] before that chunk's H2D copy is
         enqueued (run_views)."""
         torch = _torch()
+        t_run = time.perf_counter()
         if host_out is None:
             host_out = self.new_host_output()
         n = len(self.chunks)
@@ -609,6 +741,8 @@ class HostFilterPipeline:
             self.s_run.synchronize()
             if int(self.fail.item()) != 0:
                 raise TkvAmqError(abi.INTERNAL, "vqf_insert (filter_builder.hpp:211)")
+        if check or self.kind == BLOOM:
+            record_filter_metrics(self.plan, (time.perf_counter() - t_run) * 1e6)
         return host_out
 
 
