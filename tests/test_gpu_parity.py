@@ -151,6 +151,22 @@ def test_vqf_parity(oracle, amq, torch, bpk, cap):
     assert_same(plan, out, ref)
 
 
+@pytest.mark.parametrize("bpk,cap", [(22, 65472), (32, 16320)])
+def test_vqf_parity_fused_16bit_tags(oracle, amq, torch, bpk, cap):
+    """16-bit tags (and, at 32 bpk in 16 KB pages, 8-bit truncated and 16-bit leaves in one
+    batch) through the fused LDS place path: every leaf small enough that the batch's LDS
+    image fits."""
+    counts = [8000, 777, 5000, 1, 0, 64, 7000]
+    keys = sorted_keys(oracle, 43, counts)
+    src = [900 + i for i in range(len(counts))]
+    ref = oracle_per_segment(oracle, 1, keys, counts, bpk, cap=cap, src=src)
+    plan, out = gpu_build(amq, torch, 1, torch.from_numpy(keys).cuda(), counts, bpk, cap=cap,
+                          src=src)
+    assert plan.max_seg_blocks * 132 <= 80 * 1024, "batch should take the fused place"
+    assert 16 in set(plan.segs["tag_bits"].tolist())
+    assert_same(plan, out, ref)
+
+
 def test_vqf_config1_sha256(oracle, amq, torch):
     g = json.load(open(os.path.join(GOLDEN, "filters.json")))["config1_vqf12_1M"]
     n = g["n_keys"]
