@@ -42,11 +42,12 @@ WORKLOADS = {
     "probe_vqf12": (1, 12, 32704, "VQF @12 probe, 50% hits"),
     "bloom10k24": (0, 10, 0, "Bloom @10 bits/key, 24-byte keys (TurtleKV default key size)"),
     "bloom10mono": (0, 10, 0, "Bloom @10 bits/key, one monolithic filter per GPU"),
+    "bloom10var": (0, 10, 0, "Bloom @10 bits/key, variable-length keys (8-31 B)"),
 }
 # workloads whose one filter spans every key of the GPU (the monolithic
 # single-filter Bloom variant)
 MONOLITHIC = {"bloom10mono"}
-KEY_BYTES = {"bloom10k24": 24}
+KEY_BYTES = {"bloom10k24": 24, "bloom10var": 0}  # 0: variable length (offsets)
 
 
 def parse():
@@ -162,8 +163,18 @@ def main():
     n = shard.key_end - shard.key_begin
     total_keys = sum(all_counts)
     key_bytes = KEY_BYTES.get(args.workload, 16)
+    var_lens = None
     if key_bytes == 16:
         keys = amq.gen_keys16(42, shard.key_begin, n, device=dev)
+    elif key_bytes == 0:
+        # variable-length keys (the reference's KeyView ranges): lengths uniform in [8, 32)
+        g = torch.Generator(device=dev)
+        g.manual_seed(42 + rank)
+        var_lens = torch.randint(8, 32, (n,), dtype=torch.int64, device=dev, generator=g)
+        offsets = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+        torch.cumsum(var_lens, 0, out=offsets[1:])
+        keys = torch.randint(0, 256, (int(offsets[-1].item()),), dtype=torch.uint8, device=dev,
+                             generator=g)
     else:
         g = torch.Generator(device=dev)
         g.manual_seed(42 + rank)
@@ -171,7 +182,7 @@ def main():
     if kind == 1:
         # VQF inserts in leaf key order: sort each leaf's keys (memcmp order) on the device
         keys = sort_segments_device(torch, keys, counts)
-    kb = amq.KeyBatch.fixed(keys)
+    kb = amq.KeyBatch.variable(keys, offsets) if var_lens is not None else amq.KeyBatch.fixed(keys)
     out = torch.empty(plan.total_out_bytes, dtype=torch.uint8, device=dev)
     ws = torch.empty(max(plan.workspace_bytes, 1), dtype=torch.uint8, device=dev)
     gathered = (torch.empty(plan.total_out_bytes * world, dtype=torch.uint8, device=dev)
@@ -247,7 +258,8 @@ def main():
                              f"hits, first indices {bad[:8].tolist()}")
         fpr = float(res[~is_hit].float().mean())
     else:
-        alg_bytes = n * key_bytes + int(plan.segs["payload_bytes"].astype(np.int64).sum())
+        key_in = n * key_bytes if var_lens is None else keys.numel() + 8 * (n + 1)
+        alg_bytes = key_in + int(plan.segs["payload_bytes"].astype(np.int64).sum())
     achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
     prof = load_profile(args.workload)
     traffic = prof.get("hbm_bytes_per_launch")
@@ -307,6 +319,7 @@ def main():
                                 counts[:lim] if n > 100_000_000 else counts,
                                 args.cpu_threads, leaf_keys)
 
+    kdesc = f"{key_bytes}B" if key_bytes else "8-31B (mean %.1f B)" % (keys.numel() / max(n, 1))
     line = {
         "metric": f"filter-build Mkeys/s (device-resident), 16B keys @10 bits/key; bit-exact"
         if args.workload == "bloom10" else f"{label} Mkeys/s (device-resident)",
@@ -322,8 +335,8 @@ def main():
         "vs_baseline": None,
         "dtype": "u64",
         "data": "synthetic (splitmix64 seed 42 keys generated on the device)",
-        "config": {"workload": (f"{label}: {total_keys} x {key_bytes}B keys over {world} GPU(s)"
-                                if strong else f"{label}: {n} x {key_bytes}B keys per GPU")
+        "config": {"workload": (f"{label}: {total_keys} x {kdesc} keys over {world} GPU(s)"
+                                if strong else f"{label}: {n} x {kdesc} keys per GPU")
                                + f", {leaf_keys}-key leaves ({len(counts)} filters on rank 0)",
                    "keys_per_gpu": n, "total_keys": total_keys, "key_bytes": key_bytes, "leaf_keys": leaf_keys, "bits_per_key": bpk,
                    "filter": "bloom-blocked512" if kind == 0 else "vqf",

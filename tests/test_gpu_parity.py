@@ -339,3 +339,63 @@ def test_hash_once_probe_many(oracle, amq, torch, kind, bpk):
     st, ref = oracle.probe_segments(kind, filt.cpu().numpy(), plan.segs["out_offset"],
                                     q[pair_query], pair_leaf.astype(np.uint32))
     assert np.array_equal(got.cpu().numpy(), ref)
+
+
+def _bloom_seed(i):
+    m = (1 << 64) - 1
+    z = (0x243F6A8885A308D3 + i * 0x9E3779B97F4A7C15) & m
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & m
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & m
+    return z ^ (z >> 31)
+
+
+def test_variable_length_probe(oracle, amq, torch):
+    """Probes of variable-length keys (0-71 bytes: the shared-lane short-key hash below 32
+    bytes, the full XXH64 above): Bloom answers equal a python-xxhash evaluation of the
+    tkv-amq v1 bit test; VQF hashes equal python-xxhash; raw-key and hash-once probes agree;
+    no false negatives."""
+    import xxhash
+    rng = np.random.default_rng(21)
+    counts = [3000, 17, 4096, 1]
+    nq_miss = 3000
+    # inserted keys 4-71 bytes (unique, as a leaf's keys are); miss queries 0-71 bytes
+    lens = np.concatenate([rng.integers(4, 72, sum(counts)), rng.integers(0, 72, nq_miss)])
+    blob = rng.integers(0, 256, int(lens.sum()), dtype=np.uint8)
+    offs = np.zeros(len(lens) + 1, np.int64)
+    offs[1:] = np.cumsum(lens)
+    n = sum(counts)
+    kb = amq.KeyBatch.variable(torch.from_numpy(blob[:offs[n]].copy()).cuda(),
+                               torch.from_numpy(offs[:n + 1].copy()).cuda())
+    qb = amq.KeyBatch.variable(torch.from_numpy(blob).cuda(), torch.from_numpy(offs).cuda())
+    seg_of_key = np.repeat(np.arange(len(counts)), counts)
+    qseg = np.concatenate([seg_of_key, rng.integers(0, len(counts), nq_miss)]).astype(np.int32)
+    key = lambda i: blob[offs[i]:offs[i + 1]].tobytes()
+    for kind, bpk in ((0, 10), (1, 13)):
+        plan = amq.plan_filters(kind, counts, bpk, payload_capacity=32704 if kind else 0)
+        filt = amq.build_all_filters(plan, kb)
+        res = amq.probe_filters(plan, filt, qb, torch.from_numpy(qseg).cuda()).cpu().numpy()
+        assert res[:n].all(), "false negative"
+        if kind == 0:
+            f = filt.cpu().numpy()
+            want = np.zeros(len(qseg), np.uint8)
+            for i in range(len(qseg)):
+                sg = plan.segs[qseg[i]]
+                k = int(sg["hash_count"])
+                h0 = xxhash.xxh64_intdigest(key(i), _bloom_seed(0))
+                blk = (h0 * int(sg["n_blocks"])) >> 64
+                base = int(sg["out_offset"]) + 64 + 64 * blk
+                bits = [h0 & 511] + [xxhash.xxh64_intdigest(key(i), _bloom_seed(j)) & 511
+                                     for j in range(1, k)]
+                want[i] = all((f[base + (b >> 3)] >> (b & 7)) & 1 for b in bits)
+            assert np.array_equal(res, want)
+            qh = amq.bloom_query_hashes(qb, 32)
+            got = amq.bloom_probe_hashed(plan, filt, qh, 32, torch.from_numpy(qseg).cuda())
+            assert np.array_equal(got.cpu().numpy(), res)
+        else:
+            hv = amq.vqf_hash_val(qb).cpu().numpy().view(np.uint64)
+            want_h = np.array([xxhash.xxh64_intdigest(key(i), VQF_SEED) for i in range(len(qseg))],
+                              dtype=np.uint64)
+            assert np.array_equal(hv, want_h)
+            got = amq.vqf_probe_hashed(plan, filt, torch.from_numpy(hv.view(np.int64)).cuda(),
+                                       torch.from_numpy(qseg).cuda())
+            assert np.array_equal(got.cpu().numpy(), res)

@@ -207,22 +207,73 @@ __host__ __device__ constexpr inline uint64_t xxh16_rhinit(uint64_t seed)
   return rotl64(seed + kP5 + 16, 27);
 }
 
+// Unaligned global loads: gfx950 (HSA, unaligned access mode) serves a dwordx2 / dword load
+// at any byte address; memcpy from a byte pointer compiles to exactly that
+// (tools/probe/unaligned_load.hip checks every byte offset on the device).
 __device__ inline uint64_t ld64_unaligned(const uint8_t* p)
 {
-  if ((reinterpret_cast<uintptr_t>(p) & 7) == 0) return *reinterpret_cast<const uint64_t*>(p);
-  uint64_t v = 0;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) v |= (uint64_t)p[i] << (8 * i);
+  uint64_t v;
+  __builtin_memcpy(&v, p, 8);
   return v;
 }
 
 __device__ inline uint32_t ld32_unaligned(const uint8_t* p)
 {
-  uint32_t v = 0;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) v |= (uint32_t)p[i] << (8 * i);
+  uint32_t v;
+  __builtin_memcpy(&v, p, 4);
   return v;
 }
+
+// Any key shorter than 32 bytes (XXH64's short-input path), any alignment: the 8-byte lane
+// rounds and the 4-byte / 1-byte tail products do not depend on the seed, so they are
+// computed once per key; per seed only the chained rotate-multiply steps and the avalanche
+// remain.  Lanes of one wave may have different lengths: the steps a key does not have are
+// predicated off.
+struct XxhShort {
+  uint32_t len;
+  uint64_t r[3];   // round(0, lane j), j < len / 8
+  uint64_t t4;     // (4-byte tail) * P1, if len & 4
+  uint64_t tb[3];  // byte k of the 1..3-byte tail * P5
+  __device__ inline XxhShort(const uint8_t* p, uint32_t n) : len{n}
+  {
+    const uint32_t n8 = n >> 3;
+#pragma unroll
+    for (uint32_t j = 0; j < 3; ++j) r[j] = j < n8 ? dround(0, ld64_unaligned(p + 8 * j)) : 0ull;
+    const uint8_t* q = p + 8 * n8;
+    t4 = (n & 4) ? (uint64_t)ld32_unaligned(q) * kP1 : 0ull;
+    q += (n & 4);
+    const uint32_t nb = n & 3;
+#pragma unroll
+    for (uint32_t k = 0; k < 3; ++k) tb[k] = k < nb ? (uint64_t)q[k] * kP5 : 0ull;
+  }
+  // state before the avalanche; seed_p5 = seed + P5
+  __device__ inline uint64_t pre(uint64_t seed_p5) const
+  {
+    uint64_t h = seed_p5 + len;
+    const uint32_t n8 = len >> 3, nb = len & 3;
+#pragma unroll
+    for (uint32_t j = 0; j < 3; ++j) {
+      if (j < n8) {
+        h ^= r[j];
+        h = drotl<27>(h) * kP1 + kP4;
+      }
+    }
+    if (len & 4) {
+      h ^= t4;
+      h = drotl<23>(h) * kP2 + kP3;
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < 3; ++k) {
+      if (k < nb) {
+        h ^= tb[k];
+        h = drotl<11>(h) * kP1;
+      }
+    }
+    return h;
+  }
+  __device__ inline uint64_t finish(uint64_t seed_p5) const { return davalanche(pre(seed_p5)); }
+  __device__ inline uint32_t finish_lo9(uint64_t seed_p5) const { return davalanche_lo9(pre(seed_p5)); }
+};
 
 // XXH64 of an arbitrary byte string in device memory.
 __device__ inline uint64_t xxh64_bytes(const uint8_t* p, uint64_t len, uint64_t seed)

@@ -35,6 +35,7 @@ namespace tkv {
 struct BloomSeeds {
   uint64_t seed[kMaxBloomHashes];
   uint64_t rhinit16[kMaxBloomHashes];  // rotl(seed + P5 + 16, 27), see Xxh16
+  uint64_t seed_p5[kMaxBloomHashes];   // seed + P5, see XxhShort
 };
 
 constexpr BloomSeeds make_bloom_seeds()
@@ -43,6 +44,7 @@ constexpr BloomSeeds make_bloom_seeds()
   for (uint32_t i = 0; i < kMaxBloomHashes; ++i) {
     t.seed[i] = bloom_seed(i);
     t.rhinit16[i] = xxh16_rhinit(t.seed[i]);
+    t.seed_p5[i] = t.seed[i] + kP5;
   }
   return t;
 }
@@ -67,16 +69,29 @@ __device__ inline uint4 load_nt16(const void* p)
   return uint4{v.x, v.y, v.z, v.w};
 }
 
+// key i of a fixed-stride or offset-indexed key array: its bytes and length
+template <int MODE>
+__device__ inline const uint8_t* key_at(const uint8_t* keys, const uint64_t* offs, uint32_t stride,
+                                        uint64_t i, uint32_t& len)
+{
+  if constexpr (MODE == kKeyFixed || MODE == kKey24) {
+    len = stride;
+    return keys + i * stride;
+  } else {
+    const uint64_t b = offs[i];
+    len = (uint32_t)(offs[i + 1] - b);
+    return keys + b;
+  }
+}
+
 template <int MODE>
 __device__ inline uint64_t hash_key(const uint8_t* keys, const uint64_t* offs, uint32_t stride,
                                     uint64_t i, uint64_t seed)
 {
-  if constexpr (MODE == kKeyFixed || MODE == kKey24) {
-    return xxh64_bytes(keys + i * stride, stride, seed);
-  } else {
-    const uint64_t b = offs[i];
-    return xxh64_bytes(keys + b, offs[i + 1] - b, seed);
-  }
+  uint32_t len;
+  const uint8_t* p = key_at<MODE>(keys, offs, stride, i, len);
+  if (len < 32) return XxhShort(p, len).finish(seed + kP5);
+  return xxh64_bytes(p, len, seed);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -90,6 +105,31 @@ __device__ inline void lds_set_bit(uint32_t* blk, uint32_t bit)
   uint32_t word;
   asm("v_bfe_u32 %0, %1, 5, 4" : "=v"(word) : "v"(bit));
   atomicOr(blk + word, 1u << (bit & 31));
+}
+
+// Bloom insert of one fixed/variable-length key: keys under 32 bytes share the seed-independent
+// lane rounds over all k hashes (XxhShort); longer keys hash from scratch per seed.
+template <int K, int MODE>
+__device__ inline void bloom_insert_any(uint32_t* s_bits, uint32_t nb, uint32_t k,
+                                        const uint8_t* p, uint32_t len)
+{
+  if (len < 32) {
+    const XxhShort x(p, len);
+    const uint64_t h0 = x.finish(c_bloom.seed_p5[0]);
+    uint32_t* blk = s_bits + 16 * (uint32_t)__umul64hi(h0, (uint64_t)nb);
+    lds_set_bit(blk, (uint32_t)h0 & 511u);
+    if constexpr (K != 0) {
+#pragma unroll
+      for (uint32_t j = 1; j < (uint32_t)K; ++j) lds_set_bit(blk, x.finish_lo9(c_bloom.seed_p5[j]));
+    } else {
+      for (uint32_t j = 1; j < k; ++j) lds_set_bit(blk, x.finish_lo9(c_bloom.seed_p5[j]));
+    }
+  } else {
+    const uint64_t h0 = xxh64_bytes(p, len, c_bloom.seed[0]);
+    uint32_t* blk = s_bits + 16 * (uint32_t)__umul64hi(h0, (uint64_t)nb);
+    lds_set_bit(blk, (uint32_t)h0 & 511u);
+    for (uint32_t j = 1; j < k; ++j) lds_set_bit(blk, (uint32_t)xxh64_bytes(p, len, c_bloom.seed[j]) & 511u);
+  }
 }
 
 __device__ inline void write_bloom_header(uint8_t* payload, const tkv_amq_segment& sg, int part)
@@ -214,13 +254,14 @@ __global__ __launch_bounds__(256) void bloom_build_lds(const uint8_t* __restrict
       else bloom_keysL_lds<0, 24>(kp, n, nb, k, s_bits);
     }
   } else {
+    // one key per thread per iteration (two in flight measured 2% slower: the loop is
+    // VALU-bound, every lane paying for the longest key of its wave)
     for (uint32_t i = tid; i < n; i += 256) {
-      const uint64_t gi = sg.key_begin + i;
-      const uint64_t h0 = hash_key<MODE>(keys, offs, stride, gi, c_bloom.seed[0]);
-      uint32_t* blk = s_bits + 16 * (uint32_t)__umul64hi(h0, (uint64_t)nb);
-      lds_set_bit(blk, (uint32_t)h0 & 511u);
-      for (uint32_t j = 1; j < k; ++j)
-        lds_set_bit(blk, (uint32_t)hash_key<MODE>(keys, offs, stride, gi, c_bloom.seed[j]) & 511u);
+      uint32_t len;
+      const uint8_t* p = key_at<MODE>(keys, offs, stride, sg.key_begin + i, len);
+      if (k == 7) bloom_insert_any<7, MODE>(s_bits, nb, k, p, len);
+      else if (k == 8) bloom_insert_any<8, MODE>(s_bits, nb, k, p, len);
+      else bloom_insert_any<0, MODE>(s_bits, nb, k, p, len);
     }
   }
   __syncthreads();
@@ -711,13 +752,27 @@ __global__ __launch_bounds__(256) void bloom_probe(const uint8_t* __restrict__ f
     const ProbeDesc d = load_probe_desc(segs, sidx);
     if (d.hash_count != 0) {
       const uint8_t* words = filters + d.out_offset + kBloomHeader;
-      const uint64_t h0 = hash_key<MODE>(q, qoffs, stride, i, c_bloom.seed[0]);
-      const uint64_t* blk = reinterpret_cast<const uint64_t*>(words + 64 * __umul64hi(h0, (uint64_t)d.n_blocks));
-      uint32_t b = (uint32_t)h0 & 511u;
-      ok &= (uint32_t)(blk[b >> 6] >> (b & 63));
-      for (uint32_t j = 1; j < d.hash_count; ++j) {
-        b = (uint32_t)hash_key<MODE>(q, qoffs, stride, i, c_bloom.seed[j]) & 511u;
+      uint32_t len;
+      const uint8_t* p = key_at<MODE>(q, qoffs, stride, i, len);
+      if (len < 32) {  // seed-independent lane rounds shared by the k hashes
+        const XxhShort x(p, len);
+        const uint64_t h0 = x.finish(c_bloom.seed_p5[0]);
+        const uint64_t* blk = reinterpret_cast<const uint64_t*>(words + 64 * __umul64hi(h0, (uint64_t)d.n_blocks));
+        uint32_t b = (uint32_t)h0 & 511u;
         ok &= (uint32_t)(blk[b >> 6] >> (b & 63));
+        for (uint32_t j = 1; j < d.hash_count; ++j) {
+          b = x.finish_lo9(c_bloom.seed_p5[j]) & 511u;
+          ok &= (uint32_t)(blk[b >> 6] >> (b & 63));
+        }
+      } else {
+        const uint64_t h0 = xxh64_bytes(p, len, c_bloom.seed[0]);
+        const uint64_t* blk = reinterpret_cast<const uint64_t*>(words + 64 * __umul64hi(h0, (uint64_t)d.n_blocks));
+        uint32_t b = (uint32_t)h0 & 511u;
+        ok &= (uint32_t)(blk[b >> 6] >> (b & 63));
+        for (uint32_t j = 1; j < d.hash_count; ++j) {
+          b = (uint32_t)xxh64_bytes(p, len, c_bloom.seed[j]) & 511u;
+          ok &= (uint32_t)(blk[b >> 6] >> (b & 63));
+        }
       }
     }
   }
@@ -1720,9 +1775,17 @@ __global__ __launch_bounds__(256) void bloom_hash_kernel(const uint8_t* __restri
     *reinterpret_cast<uint64_t*>(rec) = x.finish(c_bloom.rhinit16[0]);
     for (uint32_t j = 1; j < k_max; ++j) bits[j - 1] = (uint16_t)(x.finish_lo9(c_bloom.rhinit16[j]) & 511u);
   } else {
-    *reinterpret_cast<uint64_t*>(rec) = hash_key<MODE>(q, qoffs, stride, i, c_bloom.seed[0]);
-    for (uint32_t j = 1; j < k_max; ++j)
-      bits[j - 1] = (uint16_t)(hash_key<MODE>(q, qoffs, stride, i, c_bloom.seed[j]) & 511u);
+    uint32_t len;
+    const uint8_t* p = key_at<MODE>(q, qoffs, stride, i, len);
+    if (len < 32) {
+      const XxhShort x(p, len);
+      *reinterpret_cast<uint64_t*>(rec) = x.finish(c_bloom.seed_p5[0]);
+      for (uint32_t j = 1; j < k_max; ++j) bits[j - 1] = (uint16_t)(x.finish_lo9(c_bloom.seed_p5[j]) & 511u);
+    } else {
+      *reinterpret_cast<uint64_t*>(rec) = xxh64_bytes(p, len, c_bloom.seed[0]);
+      for (uint32_t j = 1; j < k_max; ++j)
+        bits[j - 1] = (uint16_t)(xxh64_bytes(p, len, c_bloom.seed[j]) & 511u);
+    }
   }
 }
 
