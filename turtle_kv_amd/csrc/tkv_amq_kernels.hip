@@ -2,18 +2,24 @@
 //
 // Hot path:
 //   bloom_build_lds      one workgroup per leaf filter ("segment"); 16-byte keys streamed with
-//                        global_load_dwordx4, k XXH64 hashes in registers, bits set in an LDS
-//                        image of the whole filter with ds_or_b32, image written out with
-//                        16-byte coalesced stores.  No MFMA: this is hashing and bit-set.
+//                        global_load_dwordx4, k XXH64 hashes in registers (seed-independent
+//                        lane rounds shared), bits set in an LDS image of the whole filter with
+//                        ds_or_b32, image written out with 16-byte coalesced stores.  Other key
+//                        shapes: 24-byte lanes, or XxhShort for any key under 32 bytes.
+//   bloom_part_* / bloom_tile_build
+//                        one filter larger than LDS: keys partitioned by 64 KiB tile (count,
+//                        scans, LDS-staged scatter), then each tile built in LDS.
 //   vqf_decide           one wave per segment replays the reference's insert order exactly
-//                        (power-of-two-choice decisions depend only on per-block counts);
-//                        per 64-key chunk: bit-sliced ballot matches give every lane its
-//                        all-primary counts, then one ballot round per key that takes its
-//                        alternate block.  Emits (block, rank) -> (bucket, tag) records.
-//   vqf_place            one wave per 64-byte VQF block: stable rank by bucket offset with
-//                        ballots, metadata zeros at rank+offset, block image in LDS, 16-byte
-//                        stores.
-//   *_probe              one lane per (query, segment) test.
+//                        (power-of-two-choice decisions depend only on per-block counts, kept
+//                        in LDS); per 64-key chunk every conflict-free lane decides in the same
+//                        round.  Emits one coalesced (block, rank, bucket, tag) record per key.
+//   vqf_place_fused      one workgroup per segment: the records land at [block][rank] of an LDS
+//                        image, then one thread per 64-byte block runs the stable counting sort
+//                        by bucket offset and writes the block (vqf_scatter + vqf_place: the
+//                        same through HBM for segments whose image does not fit LDS).
+//   *_probe              one lane per (query, segment) test; *_hash + *_probe_hashed hash each
+//                        query once for many segments.
+// No MFMA anywhere: this is hashing and bit-set, not a contraction.
 #include <hip/hip_runtime.h>
 
 #include <mutex>
