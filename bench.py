@@ -2,7 +2,8 @@
 16-byte keys @ 10 bits/key, bit-exact).
 
   python bench.py [--gpus N] [--steps K] [--warmup W]
-                  [--workload bloom10|bloom12|vqf12|probe10|probe_vqf12|bloom10k24] [--total-keys T]
+                  [--workload bloom10|bloom12|vqf12|probe10|probe_vqf12|bloom10k24|bloom10var|
+                              bloom10mono] [--total-keys T]
 
 One step = one pass of the hot path over one batch: build every leaf filter of
 `--keys-per-gpu` (default 100M, BASELINE config 2) 16-byte keys held in HBM, S = 16,384 keys
