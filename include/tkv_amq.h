@@ -131,7 +131,8 @@ int tkv_amq_build_check(int kind, const void* d_workspace, uint64_t workspace_by
                         void* stream);
 
 /* Batched probe: query i tests the filter of segment d_query_seg[i].  d_result[i] = 1 if
- * the key may be present, 0 if the filter rejects it (reject_page == kTrue). */
+ * the key may be present, 0 if the filter rejects it (reject_page == kTrue).  A segment index
+ * >= n_segs, like a segment without a filter, answers 1 (kUnknown: cannot reject). */
 int tkv_amq_probe(int kind, const uint8_t* d_filters, const tkv_amq_segment* d_segs,
                   uint32_t n_segs, const uint8_t* queries, const uint64_t* query_offsets,
                   uint32_t query_stride, uint64_t n_queries, const uint32_t* d_query_seg,

@@ -191,3 +191,26 @@ def test_build_records_reference_metrics(oracle, amq, torch):
         assert m.build_page_latency.count == l0 + 2 and m.build_page_latency.total_usec > 0
         amq.build_all_filters(plan, kb, check=False)   # unchecked launches record nothing
         assert m.item_count_stats.count == c0 + 2
+
+
+@pytest.mark.parametrize("kind", [0, 1])
+def test_probe_leaf_index_out_of_range(oracle, amq, torch, kind):
+    """A query naming a leaf outside the plan answers "maybe" (reject_page's kUnknown) on every
+    probe path, and nothing outside the plan is read."""
+    counts = [4096, 100]
+    keys = oracle.gen_keys16(8, 0, sum(counts))
+    oracle.sort_segments(keys, np.concatenate([[0], np.cumsum(counts)]).astype(np.uint64))
+    kb = amq.KeyBatch.fixed(torch.from_numpy(keys).cuda())
+    plan = amq.plan_filters(kind, counts, 12, payload_capacity=32704)
+    filt = amq.build_all_filters(plan, kb)
+    miss = amq.KeyBatch.fixed(amq.gen_keys16(9, 0, 1000))
+    bad = torch.tensor([2, 3, 1 << 20, 0x7FFFFFF0] * 250, dtype=torch.int32, device="cuda")
+    assert bool(amq.probe_filters(plan, filt, miss, bad).all())
+    if kind == 0:
+        qh = amq.bloom_query_hashes(miss, 32)
+        assert bool(amq.bloom_probe_hashed(plan, filt, qh, 32, bad).all())
+    else:
+        assert bool(amq.vqf_probe_hashed(plan, filt, amq.vqf_hash_val(miss), bad).all())
+    # in range, the same misses are mostly rejected
+    good = torch.zeros(1000, dtype=torch.int32, device="cuda")
+    assert int(amq.probe_filters(plan, filt, miss, good).sum()) < 100

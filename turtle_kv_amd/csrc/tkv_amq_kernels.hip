@@ -670,14 +670,18 @@ struct ProbeDesc {
   uint32_t hash_count, tag_bits, hash_val_shift;
 };
 
-__device__ inline ProbeDesc load_probe_desc(const tkv_amq_segment* segs, uint32_t s)
+// A leaf index outside the plan reads as "no filter" (the probe answers "maybe", like
+// reject_page's kUnknown for a page it cannot check, tree/key_query.hpp:156-159): nothing is
+// read out of bounds.
+__device__ inline ProbeDesc load_probe_desc(const tkv_amq_segment* segs, uint32_t s, uint32_t n_segs)
 {
-  const uint4 v = reinterpret_cast<const uint4*>(segs + s)[0];
+  const bool in = s < n_segs;
+  const uint4 v = reinterpret_cast<const uint4*>(segs + (in ? s : 0u))[0];
   ProbeDesc d;
   d.out_offset = (uint64_t)v.x | ((uint64_t)v.y << 32);
   d.n_blocks = v.z;
-  d.hash_count = v.w & 0xffffu;
-  d.tag_bits = (v.w >> 16) & 0xffu;
+  d.hash_count = in ? v.w & 0xffffu : 0u;
+  d.tag_bits = in ? (v.w >> 16) & 0xffu : 0u;
   d.hash_val_shift = v.w >> 24;
   return d;
 }
@@ -728,7 +732,7 @@ __device__ inline uint32_t probe_block16(const Xxh16& x, uint64_t h0, const uint
 
 template <int MODE>
 __global__ __launch_bounds__(256) void bloom_probe(const uint8_t* __restrict__ filters,
-                                                   const tkv_amq_segment* __restrict__ segs,
+                                                   const tkv_amq_segment* __restrict__ segs, uint32_t n_segs,
                                                    const uint8_t* __restrict__ q,
                                                    const uint64_t* __restrict__ qoffs,
                                                    uint32_t stride, uint64_t n,
@@ -744,7 +748,7 @@ __global__ __launch_bounds__(256) void bloom_probe(const uint8_t* __restrict__ f
     // the key load, the descriptor and the first hash do not depend on the "has a filter"
     // test, so they are issued before it: one dependent chain qseg -> descriptor -> block
     const uint4 kv = load_nt16(q + 16 * i);
-    const ProbeDesc d = load_probe_desc(segs, sidx);
+    const ProbeDesc d = load_probe_desc(segs, sidx, n_segs);
     const Xxh16 x((uint64_t)kv.x | ((uint64_t)kv.y << 32), (uint64_t)kv.z | ((uint64_t)kv.w << 32));
     const uint64_t h0 = x.finish(c_bloom.rhinit16[0]);
     const uint4* blk = reinterpret_cast<const uint4*>(filters + d.out_offset + kBloomHeader +
@@ -755,7 +759,7 @@ __global__ __launch_bounds__(256) void bloom_probe(const uint8_t* __restrict__ f
     else if (d.hash_count == 8) ok = probe_block16<8>(x, h0, blk, slot);
     else if (d.hash_count != 0) ok = probe_block16<0>(x, h0, blk, slot, d.hash_count);
   } else {
-    const ProbeDesc d = load_probe_desc(segs, sidx);
+    const ProbeDesc d = load_probe_desc(segs, sidx, n_segs);
     if (d.hash_count != 0) {
       const uint8_t* words = filters + d.out_offset + kBloomHeader;
       uint32_t len;
@@ -1712,9 +1716,9 @@ __device__ inline bool vqf_present(const uint8_t* payload, uint32_t n_blocks, ui
 }
 
 __device__ inline uint8_t vqf_probe_one(const uint8_t* filters, const tkv_amq_segment* segs,
-                                        uint32_t s, uint64_t h)
+                                        uint32_t n_segs, uint32_t s, uint64_t h)
 {
-  const ProbeDesc d = load_probe_desc(segs, s);
+  const ProbeDesc d = load_probe_desc(segs, s, n_segs);
   if (d.tag_bits == 0) return 1;  // no filter: cannot reject
   const uint8_t* payload = filters + d.out_offset;
   const uint64_t mask = ~0ull << d.hash_val_shift;  // == PackedVqfFilter::hash_mask
@@ -1726,7 +1730,7 @@ __device__ inline uint8_t vqf_probe_one(const uint8_t* filters, const tkv_amq_se
 
 template <int MODE>
 __global__ __launch_bounds__(256) void vqf_probe(const uint8_t* __restrict__ filters,
-                                                 const tkv_amq_segment* __restrict__ segs,
+                                                 const tkv_amq_segment* __restrict__ segs, uint32_t n_segs,
                                                  const uint8_t* __restrict__ q,
                                                  const uint64_t* __restrict__ qoffs, uint32_t stride,
                                                  uint64_t n, const uint32_t* __restrict__ qseg,
@@ -1742,12 +1746,12 @@ __global__ __launch_bounds__(256) void vqf_probe(const uint8_t* __restrict__ fil
   } else {
     h = hash_key<MODE>(q, qoffs, stride, i, kVqfHashSeed);
   }
-  __builtin_nontemporal_store(vqf_probe_one(filters, segs, __builtin_nontemporal_load(qseg + i), h),
+  __builtin_nontemporal_store(vqf_probe_one(filters, segs, n_segs, __builtin_nontemporal_load(qseg + i), h),
                               result + i);
 }
 
 __global__ __launch_bounds__(256) void vqf_probe_hashed(const uint8_t* __restrict__ filters,
-                                                        const tkv_amq_segment* __restrict__ segs,
+                                                        const tkv_amq_segment* __restrict__ segs, uint32_t n_segs,
                                                         const uint64_t* __restrict__ hashes,
                                                         const uint32_t* __restrict__ pair_query,
                                                         uint64_t n, const uint32_t* __restrict__ qseg,
@@ -1756,7 +1760,7 @@ __global__ __launch_bounds__(256) void vqf_probe_hashed(const uint8_t* __restric
   const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
   const uint64_t qi = pair_query ? pair_query[i] : i;
-  result[i] = vqf_probe_one(filters, segs, qseg[i], hashes[qi]);
+  result[i] = vqf_probe_one(filters, segs, n_segs, qseg[i], hashes[qi]);
 }
 
 // ---- Bloom query hash cache (BloomFilterQuery<KeyView>) ----
@@ -1796,7 +1800,7 @@ __global__ __launch_bounds__(256) void bloom_hash_kernel(const uint8_t* __restri
 }
 
 __global__ __launch_bounds__(256) void bloom_probe_hashed(const uint8_t* __restrict__ filters,
-                                                          const tkv_amq_segment* __restrict__ segs,
+                                                          const tkv_amq_segment* __restrict__ segs, uint32_t n_segs,
                                                           const uint8_t* __restrict__ qrec,
                                                           uint32_t k_max,
                                                           const uint32_t* __restrict__ pair_query,
@@ -1811,7 +1815,7 @@ __global__ __launch_bounds__(256) void bloom_probe_hashed(const uint8_t* __restr
   const uint32_t sidx = qseg[i];
   const uint64_t qi = pair_query ? pair_query[i] : i;
   const uint8_t* rec = qrec + qi * bloom_query_stride(k_max);
-  const ProbeDesc d = load_probe_desc(segs, sidx);
+  const ProbeDesc d = load_probe_desc(segs, sidx, n_segs);
   const uint64_t h0 = *reinterpret_cast<const uint64_t*>(rec);
   uint32_t ok = 1;
   if (d.hash_count != 0 && d.hash_count <= k_max) {
@@ -2223,23 +2227,23 @@ int tkv_amq_probe(int kind, const uint8_t* d_filters, const tkv_amq_segment* d_s
   const dim3 grid((uint32_t)div_up(n, 256)), block(256);
   if (kind == TKV_AMQ_BLOOM) {
     if (mode == kKey16)
-      hipLaunchKernelGGL(bloom_probe<kKey16>, grid, block, 0, s, d_filters, d_segs, q, qoffs,
+      hipLaunchKernelGGL(bloom_probe<kKey16>, grid, block, 0, s, d_filters, d_segs, n_segs, q, qoffs,
                          stride, n, d_qseg, d_result);
     else if (mode == kKeyFixed)
-      hipLaunchKernelGGL(bloom_probe<kKeyFixed>, grid, block, 0, s, d_filters, d_segs, q, qoffs,
+      hipLaunchKernelGGL(bloom_probe<kKeyFixed>, grid, block, 0, s, d_filters, d_segs, n_segs, q, qoffs,
                          stride, n, d_qseg, d_result);
     else
-      hipLaunchKernelGGL(bloom_probe<kKeyVar>, grid, block, 0, s, d_filters, d_segs, q, qoffs,
+      hipLaunchKernelGGL(bloom_probe<kKeyVar>, grid, block, 0, s, d_filters, d_segs, n_segs, q, qoffs,
                          stride, n, d_qseg, d_result);
   } else if (kind == TKV_AMQ_VQF) {
     if (mode == kKey16)
-      hipLaunchKernelGGL(vqf_probe<kKey16>, grid, block, 0, s, d_filters, d_segs, q, qoffs, stride,
+      hipLaunchKernelGGL(vqf_probe<kKey16>, grid, block, 0, s, d_filters, d_segs, n_segs, q, qoffs, stride,
                          n, d_qseg, d_result);
     else if (mode == kKeyFixed)
-      hipLaunchKernelGGL(vqf_probe<kKeyFixed>, grid, block, 0, s, d_filters, d_segs, q, qoffs,
+      hipLaunchKernelGGL(vqf_probe<kKeyFixed>, grid, block, 0, s, d_filters, d_segs, n_segs, q, qoffs,
                          stride, n, d_qseg, d_result);
     else
-      hipLaunchKernelGGL(vqf_probe<kKeyVar>, grid, block, 0, s, d_filters, d_segs, q, qoffs, stride,
+      hipLaunchKernelGGL(vqf_probe<kKeyVar>, grid, block, 0, s, d_filters, d_segs, n_segs, q, qoffs, stride,
                          n, d_qseg, d_result);
   } else {
     return TKV_AMQ_INVALID_ARGUMENT;
@@ -2275,7 +2279,7 @@ int tkv_amq_vqf_probe_hashed(const uint8_t* d_filters, const tkv_amq_segment* d_
   if (!d_filters || !d_segs || !d_hash || !d_qseg || !d_result || n_segs == 0)
     return TKV_AMQ_INVALID_ARGUMENT;
   hipLaunchKernelGGL(vqf_probe_hashed, dim3((uint32_t)div_up(n, 256)), dim3(256), 0,
-                     as_stream(stream), d_filters, d_segs, d_hash, d_pair_query, n, d_qseg, d_result);
+                     as_stream(stream), d_filters, d_segs, n_segs, d_hash, d_pair_query, n, d_qseg, d_result);
   return hipGetLastError() == hipSuccess ? TKV_AMQ_OK : TKV_AMQ_INTERNAL;
 }
 
@@ -2312,7 +2316,7 @@ int tkv_amq_bloom_probe_hashed(const uint8_t* d_filters, const tkv_amq_segment* 
       k_max > kMaxBloomHashes)
     return TKV_AMQ_INVALID_ARGUMENT;
   hipLaunchKernelGGL(bloom_probe_hashed, dim3((uint32_t)div_up(n, 256)), dim3(256), 0,
-                     as_stream(stream), d_filters, d_segs, d_query, k_max, d_pair_query, n, d_qseg,
+                     as_stream(stream), d_filters, d_segs, n_segs, d_query, k_max, d_pair_query, n, d_qseg,
                      d_result);
   return hipGetLastError() == hipSuccess ? TKV_AMQ_OK : TKV_AMQ_INTERNAL;
 }
