@@ -17,6 +17,7 @@ timeout -k 10 300 python bench.py --workload bloom12 --no-e2e > $O/bench_bloom12
 timeout -k 10 300 python bench.py --workload bloom10k24 > $O/bench_bloom10k24.log 2>&1 || exit 8
 timeout -k 10 300 python bench.py --workload bloom12 --total-keys 1000000000 --steps 10 --no-e2e > $O/bench_bloom12_1B.log 2>&1 || exit 9
 timeout -k 10 300 python bench.py --workload bloom10mono > $O/bench_bloom10mono.log 2>&1 || exit 10
+timeout -k 10 300 python bench.py --workload bloom10var --no-e2e > $O/bench_bloom10var.log 2>&1 || exit 10
 cd /tmp
 # kernel-trace stats of the exact default bench command, and of the other workloads
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -T -d $O/prof_bloom10 -o run --output-format csv -- python3 $R/bench.py --no-cpu-baseline --no-e2e > $O/prof_bloom10.log 2>&1 || exit 11
