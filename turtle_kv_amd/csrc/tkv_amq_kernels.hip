@@ -1531,8 +1531,6 @@ __device__ void vqf_place_fused_body(const tkv_amq_segment& sg, uint32_t seg_ind
                                      VqfWorkspace ws, const uint64_t* __restrict__ recs,
                                      uint8_t* __restrict__ out, uint32_t* lds)
 {
-  using C = Vqf<T>;
-  using E = typename C::Entry;
   const uint32_t tid = threadIdx.x;
   const uint32_t nb = sg.n_blocks, n = sg.n_keys;
   for (uint32_t b = tid; b < nb; b += kFusedThreads) lds[b * kFusedRegionWords + kFusedCountWord] = 0;
@@ -1712,7 +1710,8 @@ __device__ inline bool vqf_present(const uint8_t* payload, uint32_t n_blocks, ui
   // primary-then-alternate order only matters for the answer, which is an OR)
   const VqfBucketRef<T> rp = vqf_bucket_ref<T>(blocks, pi);
   const VqfBucketRef<T> ra = vqf_bucket_ref<T>(blocks, ai);
-  return vqf_bucket_has<T>(rp, tag) | vqf_bucket_has<T>(ra, tag);
+  // both buckets are scanned (no short-circuit: the two tests are independent work)
+  return (int)vqf_bucket_has<T>(rp, tag) | (int)vqf_bucket_has<T>(ra, tag);
 }
 
 __device__ inline uint8_t vqf_probe_one(const uint8_t* filters, const tkv_amq_segment* segs,
