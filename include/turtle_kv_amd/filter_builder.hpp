@@ -289,27 +289,117 @@ inline Status stage_keys(const std::vector<std::string_view>& items, DeviceBuffe
   return OkStatus();
 }
 
+// Per-thread scratch for the single-leaf entry points, which the reference calls once per
+// leaf from its worker threads (tree/tree_serialize_context.cpp:71-75): a stream of the
+// thread's own and grow-only device / pinned host buffers, so a call makes no hipMalloc /
+// hipFree (hipFree synchronises the whole device, which would serialise the workers) and
+// only waits for its own stream.
+struct LeafScratch {
+  hipStream_t stream = nullptr;
+  DeviceBuffer d_keys, d_offs, d_segs, d_ws, d_out;
+  u8* h_keys = nullptr;
+  usize h_keys_cap = 0;
+  u64* h_offs = nullptr;
+  usize h_offs_cap = 0;
+  u8* h_io = nullptr;  // pinned: [segment 64 B][status 4 B .. 64 B][payload]
+  usize h_io_cap = 0;
+  std::vector<tkv_amq_key_view> views;
+
+  ~LeafScratch()
+  {
+    if (h_keys) (void)hipHostFree(h_keys);
+    if (h_offs) (void)hipHostFree(h_offs);
+    if (h_io) (void)hipHostFree(h_io);
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+  bool ensure_stream() { return stream || hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) == hipSuccess; }
+  template <typename T>
+  static bool grow_pinned(T*& p, usize& cap, usize n)
+  {
+    if (n <= cap) return true;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    if (hipHostMalloc(reinterpret_cast<void**>(&p), n * sizeof(T)) != hipSuccess) return false;
+    cap = n;
+    return true;
+  }
+};
+
+inline LeafScratch& leaf_scratch()
+{
+  thread_local LeafScratch s;
+  return s;
+}
+
 inline Status build_one(FilterKind kind, usize bpk, u64 leaf_page_id,
                         const std::vector<std::string_view>& items,
                         std::vector<u8>& page_payload, u64 page_payload_bytes)
 {
   if (bpk == 0) return OkStatus();  // filter_builder.hpp:115-117, :227-229
   if (tkv_amq_device_count() == 0) return Status::from(TKV_AMQ_UNAVAILABLE, "no HIP device");
-  FilterBatchBuilder b{kind, bpk, page_payload_bytes};
-  b.add_leaf(leaf_page_id, items.size());
-  TKV_AMQ_REQUIRE_OK(b.plan());
-  DeviceBuffer d_keys, d_offs;
-  bool fixed = false;
-  u32 stride = 16;
-  TKV_AMQ_REQUIRE_OK(stage_keys(items, d_keys, d_offs, fixed, stride));
-  DeviceBuffer d_out(b.total_out_bytes());
-  TKV_AMQ_REQUIRE_OK(b.build_all(d_keys.get(), fixed ? stride : 0,
-                                 fixed ? nullptr : d_offs.get<u64>(), d_out.get()));
-  TKV_AMQ_REQUIRE_OK(b.check());
-  const u32 used = b.segments()[0].payload_bytes;
+  LeafScratch& sc = leaf_scratch();
+  if (!sc.ensure_stream()) return Status::from(TKV_AMQ_INTERNAL, "hipStreamCreate");
+  const u64 n = items.size();
+  tkv_amq_segment seg{};
+  u64 total_out = 0, ws_bytes = 0;
+  u32 max_blocks = 0;
+  int st = tkv_amq_plan((int)kind, &n, &leaf_page_id, 1, (u32)bpk, page_payload_bytes, 0, &seg,
+                        &total_out, &ws_bytes, &max_blocks);
+  if (st != TKV_AMQ_OK) return Status::from(st, "tkv_amq_plan");
+
+  // stage the keys (the EditView key range) into pinned memory: one fixed stride if every key
+  // has the same length, else bytes + offsets
+  u64 bytes = 0;
+  bool fixed = n > 0;
+  const u32 stride = n ? (u32)items[0].size() : 16;
+  for (const auto& k : items) {
+    bytes += k.size();
+    fixed = fixed && k.size() == stride;
+  }
+  fixed = fixed && stride != 0;
+  const void* views = items.data();
+  if (!string_view_is_key_view()) {
+    sc.views.resize(n);
+    for (u64 i = 0; i < n; ++i)
+      sc.views[i] = tkv_amq_key_view{items[i].size(), reinterpret_cast<const u8*>(items[i].data())};
+    views = sc.views.data();
+  }
+  if (!LeafScratch::grow_pinned(sc.h_keys, sc.h_keys_cap, bytes ? bytes : 1) ||
+      !LeafScratch::grow_pinned(sc.h_offs, sc.h_offs_cap, n + 1))
+    return Status::from(TKV_AMQ_RESOURCE_EXHAUSTED, "hipHostMalloc");
+  st = tkv_amq_stage_keys(views, sizeof(tkv_amq_key_view), n, fixed ? stride : 0, sc.h_keys,
+                          sc.h_keys_cap, fixed ? nullptr : sc.h_offs, 1);
+  if (st != TKV_AMQ_OK) return Status::from(st, "tkv_amq_stage_keys");
+  if (!sc.d_keys.resize(bytes ? bytes : 1) || !sc.d_offs.resize(8 * (n + 1)) ||
+      !sc.d_segs.resize(sizeof(seg)) || !sc.d_ws.resize(ws_bytes) || !sc.d_out.resize(total_out) ||
+      !LeafScratch::grow_pinned(sc.h_io, sc.h_io_cap, 128 + (usize)seg.payload_bytes))
+    return Status::from(TKV_AMQ_RESOURCE_EXHAUSTED, "hipMalloc");
+  // everything below is asynchronous on the thread's stream, from and to pinned memory, with
+  // one synchronisation at the end (the VQF failure word comes back with the payload)
+  std::memcpy(sc.h_io, &seg, sizeof(seg));
+  u32* h_status = reinterpret_cast<u32*>(sc.h_io + 64);
+  *h_status = 0;
+  u8* h_payload = sc.h_io + 128;
+  hipStream_t s = sc.stream;
+  const u32 used = seg.payload_bytes;
+  if (hipMemcpyAsync(sc.d_keys.get(), sc.h_keys, bytes, hipMemcpyHostToDevice, s) != hipSuccess ||
+      (!fixed && hipMemcpyAsync(sc.d_offs.get(), sc.h_offs, 8 * (n + 1), hipMemcpyHostToDevice, s) != hipSuccess) ||
+      hipMemcpyAsync(sc.d_segs.get(), sc.h_io, sizeof(seg), hipMemcpyHostToDevice, s) != hipSuccess)
+    return Status::from(TKV_AMQ_INTERNAL, "hipMemcpyAsync keys");
+  st = tkv_amq_build((int)kind, sc.d_keys.get(), fixed ? nullptr : sc.d_offs.get<u64>(),
+                     fixed ? stride : 0, n, sc.d_segs.get<tkv_amq_segment>(), 1, max_blocks,
+                     sc.d_out.get(), sc.d_ws.get(), ws_bytes, s);
+  if (st != TKV_AMQ_OK) return Status::from(st, "tkv_amq_build");
+  if (hipMemcpyAsync(h_payload, sc.d_out.get(), used, hipMemcpyDeviceToHost, s) != hipSuccess)
+    return Status::from(TKV_AMQ_INTERNAL, "hipMemcpyAsync payload");
+  if ((kind == FilterKind::kQuotient && ws_bytes >= 4 &&
+       hipMemcpyAsync(h_status, sc.d_ws.get(), 4, hipMemcpyDeviceToHost, s) != hipSuccess) ||
+      hipStreamSynchronize(s) != hipSuccess)
+    return Status::from(TKV_AMQ_INTERNAL, "hipStreamSynchronize");
+  if (*h_status != 0) return Status::from(TKV_AMQ_INTERNAL, "vqf_insert (filter_builder.hpp:211)");
   page_payload.assign(page_payload_bytes ? page_payload_bytes : used, 0);
-  if (hipMemcpy(page_payload.data(), d_out.get(), used, hipMemcpyDeviceToHost) != hipSuccess)
-    return Status::from(TKV_AMQ_INTERNAL, "hipMemcpy payload");
+  std::memcpy(page_payload.data(), h_payload, used);
   return OkStatus();
 }
 

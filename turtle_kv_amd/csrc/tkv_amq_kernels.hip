@@ -1947,8 +1947,12 @@ const char* tkv_amq_status_string(int s)
 
 int tkv_amq_device_count(void)
 {
-  int n = 0;
-  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  // the visible device set is fixed for the life of the process: ask the runtime once (every
+  // entry point checks it, and the per-leaf path calls several entry points per leaf)
+  static const int n = [] {
+    int c = 0;
+    return hipGetDeviceCount(&c) == hipSuccess ? c : 0;
+  }();
   return n;
 }
 
