@@ -22,9 +22,12 @@
 
 #include <hip/hip_runtime_api.h>
 
+#include <chrono>
 #include <cmath>
+#include <condition_variable>
 #include <cstdint>
 #include <cstring>
+#include <mutex>
 #include <optional>
 #include <string>
 #include <string_view>
@@ -439,6 +442,347 @@ inline Status build_filter_for_leaf_in_job(usize filter_bits_per_key, u64 leaf_p
                                                   page_payload, page_payload_bytes);
   if (!s.ok()) page_payload.clear();
   return s;
+}
+
+// ---------------------------------------------------------------------------------------
+// LeafBatcher: the reference's per-leaf call pattern, built in batches
+// ---------------------------------------------------------------------------------------
+// build_all_pages runs build_filter_for_leaf_in_job once per leaf on its worker threads
+// (tree/tree_serialize_context.cpp:71-75).  One GPU call per leaf pays a copy in, a build, a
+// copy out and a synchronisation for one leaf.  LeafBatcher keeps that call site and batches
+// the calls that arrive together:
+//   - a call reserves its leaf's place in the open batch's pinned arena (keys, offsets) and
+//     stages its keys there itself, in parallel with the other callers;
+//   - the call that opened the batch (its leader) closes it after `linger`, or as soon as
+//     `max_batch` leaves have joined or the arena is full, and the next call opens another
+//     batch, which fills while this one is on the GPU;
+//   - the leader waits for every member's keys, then builds the batch on its thread's stream:
+//     one copy of the arena in, one plan, one build, one copy of the pages out;
+//   - each caller copies its own page out of the batch's pinned output.
+// A batch holds leaves of one kind, bits/key, page size and key stride (0 = variable length);
+// other calls open their own batch.  A leaf larger than the arena is built on its own.  If a
+// batch's VQF build reports an insert failure, its leaves are rebuilt one by one so that only
+// the failing leaf goes without a filter (filter_builder.hpp:323-325).
+class LeafBatcher
+{
+ public:
+  struct Options {
+    usize max_batch;
+    std::chrono::microseconds linger;
+    usize arena_bytes;  // pinned key bytes per batch (and as many bytes of offsets)
+  };
+
+  LeafBatcher() : LeafBatcher(Options{8, std::chrono::microseconds{20}, usize{8} << 20}) {}
+  explicit LeafBatcher(Options o) : opt_{o}
+  {
+    if (opt_.max_batch == 0) opt_.max_batch = 1;
+  }
+  LeafBatcher(const LeafBatcher&) = delete;
+  LeafBatcher& operator=(const LeafBatcher&) = delete;
+  ~LeafBatcher()
+  {
+    for (Batch* b : all_) destroy(b);
+  }
+
+  Status build(FilterKind kind, usize bpk, u64 leaf_page_id, const std::vector<std::string_view>& items,
+               std::vector<u8>& page_payload, u64 page_payload_bytes)
+  {
+    if (bpk == 0) {  // filter_builder.hpp:115-117, :227-229
+      page_payload.clear();
+      return OkStatus();
+    }
+    if (tkv_amq_device_count() == 0) return Status::from(TKV_AMQ_UNAVAILABLE, "no HIP device");
+    const u64 n = items.size();
+    u64 bytes = 0;
+    bool fixed = n > 0;
+    const u32 len0 = n ? (u32)items[0].size() : 0;
+    for (const auto& k : items) {
+      bytes += k.size();
+      fixed = fixed && k.size() == len0;
+    }
+    const u32 stride = fixed && len0 ? len0 : 0;
+    if (bytes > opt_.arena_bytes || n + 1 > key_cap()) {
+      Status st = detail::build_one(kind, bpk, leaf_page_id, items, page_payload, page_payload_bytes);
+      if (!st.ok()) page_payload.clear();
+      return st;
+    }
+
+    Req r{&items, leaf_page_id, n, bytes};
+    std::unique_lock<std::mutex> lk{mu_};
+    ++active_;
+    Batch* b = nullptr;
+    bool leader = false;
+    for (;;) {
+      for (Batch* o : open_)
+        if (o->kind == kind && o->bpk == bpk && o->cap == page_payload_bytes && o->stride == stride) b = o;
+      if (b && (b->bytes + bytes > opt_.arena_bytes || b->n + n + 1 > key_cap())) {
+        close(b);
+        b = nullptr;
+      }
+      if (b || !free_.empty()) break;
+      // a new batch's pinned arenas, stream and device buffers, allocated outside the lock
+      lk.unlock();
+      Batch* nb = create();
+      lk.lock();
+      if (!nb) {
+        --active_;
+        lk.unlock();
+        Status st = detail::build_one(kind, bpk, leaf_page_id, items, page_payload, page_payload_bytes);
+        if (!st.ok()) page_payload.clear();
+        return st;
+      }
+      all_.push_back(nb);
+      free_.push_back(nb);
+    }
+    if (!b) {
+      leader = true;
+      b = free_.back();
+      free_.pop_back();
+      b->kind = kind;
+      b->bpk = bpk;
+      b->cap = page_payload_bytes;
+      b->stride = stride;
+      open_.push_back(b);
+    }
+    r.key_off = b->n;
+    r.byte_off = b->bytes;
+    b->n += n;
+    b->bytes += bytes;
+    b->reqs.push_back(&r);
+    ++b->users;
+    if (b->reqs.size() >= opt_.max_batch) close(b);
+    lk.unlock();
+
+    const Status staged = stage(r, *b);
+
+    lk.lock();
+    ++b->staged;
+    cv_.notify_all();
+    if (leader) {
+      const auto deadline = std::chrono::steady_clock::now() + opt_.linger;
+      // no lingering once every caller inside build() has joined this batch (one thread alone
+      // never waits)
+      cv_.wait_until(lk, deadline, [&] { return b->closed || b->reqs.size() >= active_; });
+      if (!b->closed) close(b);
+      cv_.wait(lk, [&] { return b->staged == b->reqs.size(); });
+      lk.unlock();
+      run(*b);
+      lk.lock();
+      for (Req* q : b->reqs) q->done = true;
+      cv_.notify_all();
+    } else {
+      cv_.wait(lk, [&] { return r.done; });
+    }
+    lk.unlock();
+
+    // this leaf's page, from the batch's pinned output (or the per-leaf rebuild)
+    Status st = staged.ok() ? r.st : staged;
+    if (st.ok() && r.page) {
+      page_payload.assign(page_payload_bytes ? page_payload_bytes : r.page_bytes, 0);
+      std::memcpy(page_payload.data(), r.page, r.page_bytes);
+    } else if (st.ok() && r.rebuilt) {
+      page_payload.swap(r.rebuilt_page);
+    } else {
+      page_payload.clear();
+    }
+    lk.lock();
+    if (--b->users == 0) release(b);
+    --active_;
+    cv_.notify_all();
+    return st;
+  }
+
+ private:
+  struct Req {
+    const std::vector<std::string_view>* items;
+    u64 page_id;
+    u64 n, bytes;
+    u64 key_off = 0, byte_off = 0;  // this leaf's place in the batch arena
+    Status st{};
+    const u8* page = nullptr;  // into the batch's pinned output
+    u64 page_bytes = 0;
+    bool rebuilt = false;
+    std::vector<u8> rebuilt_page;
+    bool done = false;
+  };
+
+  struct Batch {
+    FilterKind kind{};
+    usize bpk = 0;
+    u64 cap = 0;
+    u32 stride = 0;
+    u8* h_keys = nullptr;   // [arena_bytes]
+    u64* h_offs = nullptr;  // [arena_bytes / 8]
+    u8* h_io = nullptr;     // [segments][status 64 B][pages]
+    usize h_io_cap = 0;
+    hipStream_t stream = nullptr;
+    DeviceBuffer d_keys, d_offs, d_segs, d_ws, d_out;
+    u64 n = 0, bytes = 0;
+    usize staged = 0, users = 0;
+    bool closed = false;
+    std::vector<Req*> reqs;
+  };
+
+  usize key_cap() const { return opt_.arena_bytes / 8; }
+
+  // under mu_
+  void close(Batch* b)
+  {
+    b->closed = true;
+    for (usize i = 0; i < open_.size(); ++i)
+      if (open_[i] == b) {
+        open_.erase(open_.begin() + i);
+        break;
+      }
+    cv_.notify_all();
+  }
+
+  Batch* create()
+  {
+    Batch* b = new Batch;
+    const usize seg_bytes = opt_.max_batch * sizeof(tkv_amq_segment);
+    if (hipHostMalloc(reinterpret_cast<void**>(&b->h_keys), opt_.arena_bytes ? opt_.arena_bytes : 1) != hipSuccess ||
+        hipHostMalloc(reinterpret_cast<void**>(&b->h_offs), 8 * key_cap() + 8) != hipSuccess ||
+        hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking) != hipSuccess ||
+        !b->d_keys.resize(opt_.arena_bytes ? opt_.arena_bytes : 1) || !b->d_offs.resize(8 * key_cap() + 8) ||
+        !b->d_segs.resize(seg_bytes)) {
+      destroy(b);
+      return nullptr;
+    }
+    return b;
+  }
+
+  static void destroy(Batch* b)
+  {
+    if (b->h_keys) (void)hipHostFree(b->h_keys);
+    if (b->h_offs) (void)hipHostFree(b->h_offs);
+    if (b->h_io) (void)hipHostFree(b->h_io);
+    if (b->stream) (void)hipStreamDestroy(b->stream);
+    delete b;
+  }
+
+  // grow-only, with headroom, so that steady state allocates nothing
+  static bool reserve_device(DeviceBuffer& d, usize n) { return n <= d.size() || d.resize(n + n / 2); }
+
+  void release(Batch* b)
+  {
+    b->reqs.clear();
+    b->n = b->bytes = 0;
+    b->staged = 0;
+    b->closed = false;
+    free_.push_back(b);
+  }
+
+  // the caller's keys into its reserved place in the arena; variable-length offsets are
+  // staged leaf-relative into the thread's pinned scratch, then rebased into the arena
+  static Status stage(const Req& r, Batch& b)
+  {
+    const auto& items = *r.items;
+    const void* views = items.data();
+    detail::LeafScratch& sc = detail::leaf_scratch();
+    if (!detail::string_view_is_key_view()) {
+      sc.views.resize(r.n);
+      for (u64 i = 0; i < r.n; ++i)
+        sc.views[i] = tkv_amq_key_view{items[i].size(), reinterpret_cast<const u8*>(items[i].data())};
+      views = sc.views.data();
+    }
+    if (r.n == 0) return OkStatus();
+    if (b.stride) {
+      const int st = tkv_amq_stage_keys(views, sizeof(tkv_amq_key_view), r.n, b.stride,
+                                        b.h_keys + r.byte_off, r.bytes, nullptr, 1);
+      return st == TKV_AMQ_OK ? OkStatus() : Status::from(st, "tkv_amq_stage_keys");
+    }
+    if (!detail::LeafScratch::grow_pinned(sc.h_offs, sc.h_offs_cap, r.n + 1))
+      return Status::from(TKV_AMQ_RESOURCE_EXHAUSTED, "hipHostMalloc");
+    const int st = tkv_amq_stage_keys(views, sizeof(tkv_amq_key_view), r.n, 0, b.h_keys + r.byte_off,
+                                      r.bytes, sc.h_offs, 1);
+    if (st != TKV_AMQ_OK) return Status::from(st, "tkv_amq_stage_keys");
+    u64* dst = b.h_offs + r.key_off;
+    for (u64 j = 0; j < r.n; ++j) dst[j] = sc.h_offs[j] + r.byte_off;
+    return OkStatus();
+  }
+
+  // on the leader's thread: every member staged, nothing else touches the batch
+  void run(Batch& b)
+  {
+    Status st = build_batch(b);
+    if (!st.ok() && b.reqs.size() > 1 && st.code == TKV_AMQ_INTERNAL) {
+      for (Req* q : b.reqs) {
+        q->st = detail::build_one(b.kind, b.bpk, q->page_id, *q->items, q->rebuilt_page, b.cap);
+        q->rebuilt = q->st.ok();
+      }
+    } else {
+      for (Req* q : b.reqs) q->st = st;
+    }
+  }
+
+  Status build_batch(Batch& b)
+  {
+    const usize n_segs = b.reqs.size();
+    std::vector<u64> counts(n_segs), ids(n_segs);
+    for (usize i = 0; i < n_segs; ++i) {
+      counts[i] = b.reqs[i]->n;
+      ids[i] = b.reqs[i]->page_id;
+    }
+    std::vector<tkv_amq_segment> segs(n_segs);
+    u64 total_out = 0, ws_bytes = 0;
+    u32 max_blocks = 0;
+    int st = tkv_amq_plan((int)b.kind, counts.data(), ids.data(), (u32)n_segs, (u32)b.bpk, b.cap, 0,
+                          segs.data(), &total_out, &ws_bytes, &max_blocks);
+    if (st != TKV_AMQ_OK) return Status::from(st, "tkv_amq_plan");
+    const usize seg_bytes = n_segs * sizeof(tkv_amq_segment);
+    const usize io_bytes = seg_bytes + 64 + total_out;
+    if (!detail::LeafScratch::grow_pinned(b.h_io, b.h_io_cap, io_bytes <= b.h_io_cap ? io_bytes : io_bytes + io_bytes / 2))
+      return Status::from(TKV_AMQ_RESOURCE_EXHAUSTED, "hipHostMalloc");
+    const u64 n = b.n, bytes = b.bytes;
+    if (!reserve_device(b.d_segs, seg_bytes) || !reserve_device(b.d_ws, ws_bytes) ||
+        !reserve_device(b.d_out, total_out))
+      return Status::from(TKV_AMQ_RESOURCE_EXHAUSTED, "hipMalloc");
+    std::memcpy(b.h_io, segs.data(), seg_bytes);
+    u32* h_status = reinterpret_cast<u32*>(b.h_io + seg_bytes);
+    *h_status = 0;
+    u8* h_out = b.h_io + seg_bytes + 64;
+    if (b.stride == 0) b.h_offs[n] = bytes;
+    hipStream_t s = b.stream;
+    if ((bytes && hipMemcpyAsync(b.d_keys.get(), b.h_keys, bytes, hipMemcpyHostToDevice, s) != hipSuccess) ||
+        (b.stride == 0 && hipMemcpyAsync(b.d_offs.get(), b.h_offs, 8 * (n + 1), hipMemcpyHostToDevice, s) != hipSuccess) ||
+        hipMemcpyAsync(b.d_segs.get(), b.h_io, seg_bytes, hipMemcpyHostToDevice, s) != hipSuccess)
+      return Status::from(TKV_AMQ_INTERNAL, "hipMemcpyAsync keys");
+    st = tkv_amq_build((int)b.kind, b.d_keys.get(), b.stride ? nullptr : b.d_offs.get<u64>(), b.stride, n,
+                       b.d_segs.get<tkv_amq_segment>(), (u32)n_segs, max_blocks, b.d_out.get(),
+                       b.d_ws.get(), ws_bytes, s);
+    if (st != TKV_AMQ_OK) return Status::from(st, "tkv_amq_build");
+    if (hipMemcpyAsync(h_out, b.d_out.get(), total_out, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        (b.kind == FilterKind::kQuotient && ws_bytes >= 4 &&
+         hipMemcpyAsync(h_status, b.d_ws.get(), 4, hipMemcpyDeviceToHost, s) != hipSuccess) ||
+        hipStreamSynchronize(s) != hipSuccess)
+      return Status::from(TKV_AMQ_INTERNAL, "hipMemcpyAsync pages");
+    if (*h_status != 0) return Status::from(TKV_AMQ_INTERNAL, "vqf_insert (filter_builder.hpp:211)");
+    for (usize i = 0; i < n_segs; ++i) {
+      b.reqs[i]->page = h_out + segs[i].out_offset;
+      b.reqs[i]->page_bytes = segs[i].payload_bytes;
+    }
+    return OkStatus();
+  }
+
+  Options opt_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::vector<Batch*> open_, free_, all_;
+  usize active_ = 0;  // callers inside build() past their size check
+};
+
+// build_filter_for_leaf_in_job through a process-wide LeafBatcher: the reference's per-leaf
+// call site, built in batches across the worker threads that call it concurrently.  The
+// batcher is never destroyed, so no pinned memory is freed after the HIP runtime shuts down.
+inline Status build_filter_for_leaf_in_job_batched(usize filter_bits_per_key, u64 leaf_page_id,
+                                                   const std::vector<std::string_view>& items,
+                                                   std::vector<u8>& page_payload,
+                                                   u64 page_payload_bytes = 32768 - kPackedPageHeaderSize,
+                                                   FilterKind kind = kDefaultFilterKind)
+{
+  static LeafBatcher* batcher = new LeafBatcher;
+  return batcher->build(kind, filter_bits_per_key, leaf_page_id, items, page_payload, page_payload_bytes);
 }
 
 // ---------------------------------------------------------------------------------------

@@ -3,10 +3,12 @@
 // Usage: test_mirror <tests/golden dir>
 #include <turtle_kv_amd/filter_builder.hpp>
 
+#include <algorithm>
 #include <cstdio>
 #include <fstream>
 #include <iterator>
 #include <string>
+#include <thread>
 #include <vector>
 
 using namespace turtle_kv_amd;
@@ -104,6 +106,55 @@ int main(int argc, char** argv)
     std::vector<u8> out(want_vqf.size());
     (void)hipMemcpy(out.data(), d_out.get(), out.size(), hipMemcpyDeviceToHost);
     EXPECT(out == want_vqf);
+  }
+  // LeafBatcher: the per-leaf call site from 16 worker threads, built in batches.  Every page
+  // equals the unbatched per-leaf build; leaves mix 24-byte and variable-length keys (one
+  // batch then stages offsets), kinds and sizes, and include an empty leaf.
+  {
+    const int n_leaves = 96;
+    std::vector<std::vector<std::string>> leaf_keys(n_leaves);
+    uint64_t st = 12345;
+    auto rnd = [&st] {
+      st ^= st << 13;
+      st ^= st >> 7;
+      st ^= st << 17;
+      return st;
+    };
+    for (int l = 0; l < n_leaves; ++l) {
+      const int n = l == 5 ? 0 : 500 + (int)(rnd() % 4000);
+      for (int i = 0; i < n; ++i) {
+        const int len = (l % 3 == 0) ? 24 : 4 + (int)(rnd() % 40);
+        std::string k(len, '\0');
+        for (auto& c : k) c = (char)rnd();
+        leaf_keys[l].push_back(k);
+      }
+      std::sort(leaf_keys[l].begin(), leaf_keys[l].end());
+      leaf_keys[l].erase(std::unique(leaf_keys[l].begin(), leaf_keys[l].end()), leaf_keys[l].end());
+    }
+    std::vector<std::vector<std::string_view>> views(n_leaves);
+    for (int l = 0; l < n_leaves; ++l) views[l].assign(leaf_keys[l].begin(), leaf_keys[l].end());
+    for (FilterKind kind : {FilterKind::kQuotient, FilterKind::kBloom}) {
+      const usize bpk = kind == FilterKind::kBloom ? 10 : 12;
+      std::vector<std::vector<u8>> got(n_leaves), want(n_leaves);
+      std::vector<Status> got_st(n_leaves);
+      std::vector<std::thread> pool;
+      for (int t = 0; t < 16; ++t)
+        pool.emplace_back([&, t] {
+          for (int l = t; l < n_leaves; l += 16)
+            got_st[l] = build_filter_for_leaf_in_job_batched(bpk, 500 + l, views[l], got[l],
+                                                             32768 - 64, kind);
+        });
+      for (auto& th : pool) th.join();
+      for (int l = 0; l < n_leaves; ++l) {
+        EXPECT(got_st[l].ok());
+        EXPECT(build_filter_for_leaf_in_job(bpk, 500 + l, views[l], want[l], 32768 - 64, kind).ok());
+        EXPECT(got[l] == want[l]);
+      }
+      // one caller alone: its batch closes at once
+      std::vector<u8> solo;
+      EXPECT(build_filter_for_leaf_in_job_batched(bpk, 501, views[1], solo, 32768 - 64, kind).ok());
+      EXPECT(solo == want[1]);
+    }
   }
   std::printf("%s (%d failures)\n", failures ? "FAIL" : "OK", failures);
   return failures ? 1 : 0;

@@ -2,7 +2,7 @@
 // worker threads, as TreeSerializeContext::build_all_pages does (tree/tree_serialize_context.cpp
 // :71-75, tree/filter_builder.hpp:307-331).  Host keys in, host filter pages out (PCIe
 // included); the batched host pipeline's rate is bench.py's e2e_pcie_inclusive.
-//   leaf_bench <threads> <leaves> [keys_per_leaf=16384] [kind: 0 bloom | 1 vqf]
+//   leaf_bench <threads> <leaves> [keys_per_leaf=16384] [kind: 0 bloom | 1 vqf] [batched: 0 | 1] [max_batch=8] [linger_us=20]
 #include <turtle_kv_amd/filter_builder.hpp>
 
 #include <algorithm>
@@ -30,6 +30,9 @@ int main(int argc, char** argv)
   const int leaves = argc > 2 ? std::atoi(argv[2]) : 512;
   const u64 per = argc > 3 ? std::strtoull(argv[3], nullptr, 10) : 16384;
   const FilterKind kind = (argc > 4 && std::atoi(argv[4]) == 1) ? FilterKind::kQuotient : FilterKind::kBloom;
+  const bool batched = argc > 5 && std::atoi(argv[5]) == 1;
+  LeafBatcher batcher{LeafBatcher::Options{(usize)(argc > 6 ? std::atoi(argv[6]) : 8),
+                                           std::chrono::microseconds{argc > 7 ? std::atoi(argv[7]) : 20}, usize{8} << 20}};
   const usize bpk = kind == FilterKind::kBloom ? 10 : 12;
   const u64 page = 32768 - kPackedPageHeaderSize;
   if (tkv_amq_device_count() == 0) {
@@ -53,26 +56,37 @@ int main(int argc, char** argv)
   }
   std::vector<std::vector<u8>> pages(leaves);
 
+  // each worker builds every leaf once untimed (its thread-local stream and buffers are
+  // created then), waits for the others, then the timed pass builds every leaf again
   auto run = [&](int t_count) {
-    std::atomic<int> next{0}, failed{0};
-    const auto t0 = std::chrono::steady_clock::now();
+    std::atomic<int> next_warm{0}, next{0}, failed{0}, ready{0};
+    std::atomic<bool> go{false};
+    auto build = [&](int l) {
+      return batched ? batcher.build(kind, bpk, 1000 + l, items[l], pages[l], page)
+                     : build_filter_for_leaf_in_job(bpk, 1000 + l, items[l], pages[l], page, kind);
+    };
     std::vector<std::thread> pool;
     for (int t = 0; t < t_count; ++t)
       pool.emplace_back([&] {
+        for (int l; (l = next_warm.fetch_add(1)) < leaves;) (void)build(l);
+        ready.fetch_add(1);
+        while (!go.load()) std::this_thread::yield();
         for (int l; (l = next.fetch_add(1)) < leaves;)
-          if (!build_filter_for_leaf_in_job(bpk, 1000 + l, items[l], pages[l], page, kind).ok())
-            failed.fetch_add(1);
+          if (!build(l).ok()) failed.fetch_add(1);
       });
+    while (ready.load() < t_count) std::this_thread::yield();
+    const auto t0 = std::chrono::steady_clock::now();
+    go.store(true);
     for (auto& th : pool) th.join();
     const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     return std::make_pair(dt, failed.load());
   };
-  run(threads);  // warm-up: per-thread streams and buffers
   for (int t : {1, threads}) {
     auto [dt, failed] = run(t);
-    std::printf("per-leaf drop-in: %2d threads  %d leaves x %llu keys  %.2f ms  %.0f leaves/s  %.1f Mkeys/s%s\n",
-                t, leaves, (unsigned long long)per, dt * 1e3, leaves / dt, leaves * per / dt / 1e6,
+    std::printf("per-leaf %s: %2d threads  %d leaves x %llu keys  %.2f ms  %.0f leaves/s  %.1f Mkeys/s%s\n",
+                batched ? "batched " : "drop-in", t, leaves, (unsigned long long)per, dt * 1e3, leaves / dt, leaves * per / dt / 1e6,
                 failed ? "  FAILED" : "");
+    if (batched) std::printf("  (max_batch %s, linger %s us)\n", argc > 6 ? argv[6] : "8", argc > 7 ? argv[7] : "20");
   }
   return 0;
 }

@@ -1878,6 +1878,10 @@ using namespace tkv;
 namespace {
 
 constexpr uint32_t kBloomLdsBudget = 64 * 1024;
+// The LDS build runs one workgroup per leaf, so a batch of a few leaves (the per-leaf call
+// site, or a small LeafBatcher batch) keeps a few CUs busy for the whole leaf.  Below this many
+// leaves the keys are spread over n_keys/256 workgroups that set bits with device atomics.
+constexpr uint32_t kBloomSpreadSegs = 64;
 
 inline uint32_t vqf_slots(int t) { return t == 8 ? 48u : 28u; }
 inline uint32_t vqf_buckets(int t) { return t == 8 ? 80u : 36u; }
@@ -2090,7 +2094,7 @@ int tkv_amq_build(int kind, const uint8_t* keys, const uint64_t* offs, uint32_t 
   if (kind == TKV_AMQ_BLOOM) {
     const uint64_t lds = 64ull * max_blocks;
     if (max_blocks == 0) return TKV_AMQ_OK;
-    if (lds <= kBloomLdsBudget) {
+    if (lds <= kBloomLdsBudget && n_segs >= kBloomSpreadSegs) {
       const dim3 grid(n_segs), block(256);
       const int bmode = build_key_mode(keys, offs, stride);
       if (bmode == kKey24)
@@ -2146,8 +2150,8 @@ int tkv_amq_build(int kind, const uint8_t* keys, const uint64_t* offs, uint32_t 
                          dim3(kBloomTileThreads), 64ull * kBloomTileBlocks, s, d_segs, w, pg.P,
                          pg.n_tiles, pg.part_off, d_out);
     } else {
-      // leaves beyond the LDS budget in a multi-leaf batch, or keys that are not 16 bytes:
-      // device atomics
+      // fewer than kBloomSpreadSegs leaves, leaves beyond the LDS budget in a multi-leaf batch,
+      // or a monolithic filter whose keys are not 16 bytes: device atomics
       const dim3 g1(n_segs), b(256);
       hipLaunchKernelGGL(bloom_global_init, g1, b, 0, s, d_segs, d_out);
       const uint32_t g2 = (uint32_t)(div_up(n_keys, 256) < 8192 ? div_up(n_keys, 256) : 8192);
