@@ -133,6 +133,24 @@ def test_variable_length_keys(oracle, amq, torch, kind):
     assert_same(plan, out, ref)
 
 
+def test_variable_length_keys_many_leaves(oracle, amq, torch):
+    """Batches of >= 64 leaves take the per-leaf LDS build (bloom_build_lds<kKeyVar>; fewer
+    leaves take the spread atomic path): empty and large leaves, every short length, keys of
+    >= 32 bytes, and the generic-k loop (5 bits/key -> k = 3)."""
+    rng = np.random.default_rng(12)
+    counts = [int(c) for c in rng.integers(0, 700, 70)]
+    counts[3], counts[10], counts[11], counts[40] = 0, 4096, 9000, 4097
+    lens = rng.integers(0, 72, sum(counts))
+    blob = rng.integers(0, 256, int(lens.sum()), dtype=np.uint8)
+    offs = np.zeros(len(lens) + 1, np.int64)
+    offs[1:] = np.cumsum(lens)
+    for bpk in (10, 12, 5):
+        ref = oracle_per_segment(oracle, 0, blob, counts, bpk, offsets=offs.astype(np.uint64))
+        plan, out = gpu_build(amq, torch, 0, torch.from_numpy(blob).cuda(), counts, bpk,
+                              offsets_t=torch.from_numpy(offs).cuda())
+        assert_same(plan, out, ref)
+
+
 def sorted_keys(oracle, seed, counts):
     keys = oracle.gen_keys16(seed, 0, sum(counts))
     oracle.sort_segments(keys, seg_bounds(counts))
