@@ -1706,12 +1706,18 @@ __device__ inline bool vqf_present(const uint8_t* payload, uint32_t n_blocks, ui
   const uint32_t pi = (uint32_t)mod_by_magic(h >> T, R, magic);
   const uint32_t ai = (uint32_t)mod_by_magic((h ^ ((uint64_t)tag * kVqfAltMul)) >> T, R, magic);
   const uint8_t* blocks = payload + kVqfHeader + kVqfMetadata;
+#if TKV_VQF_PROBE_BOTH
   // both blocks' metadata loads are issued before either bucket is scanned (the reference's
   // primary-then-alternate order only matters for the answer, which is an OR)
   const VqfBucketRef<T> rp = vqf_bucket_ref<T>(blocks, pi);
   const VqfBucketRef<T> ra = vqf_bucket_ref<T>(blocks, ai);
-  // both buckets are scanned (no short-circuit: the two tests are independent work)
   return (int)vqf_bucket_has<T>(rp, tag) | (int)vqf_bucket_has<T>(ra, tag);
+#else
+  // primary bucket first; only the lanes that did not find the tag there read the alternate
+  // block (vqf_is_present's order, vqf_filter_page_view.hpp:120-124)
+  if (vqf_bucket_has<T>(vqf_bucket_ref<T>(blocks, pi), tag)) return true;
+  return vqf_bucket_has<T>(vqf_bucket_ref<T>(blocks, ai), tag);
+#endif
 }
 
 __device__ inline uint8_t vqf_probe_one(const uint8_t* filters, const tkv_amq_segment* segs,
