@@ -133,13 +133,17 @@ def test_variable_length_keys(oracle, amq, torch, kind):
     assert_same(plan, out, ref)
 
 
-def test_variable_length_keys_many_leaves(oracle, amq, torch):
-    """Batches of >= 64 leaves take the per-leaf LDS build (bloom_build_lds<kKeyVar>; fewer
-    leaves take the spread atomic path): empty and large leaves, every short length, keys of
-    >= 32 bytes, and the generic-k loop (5 bits/key -> k = 3)."""
+@pytest.mark.parametrize("big_leaf", [False, True])
+def test_variable_length_keys_many_leaves(oracle, amq, torch, big_leaf):
+    """Batches of >= 64 leaves take the per-leaf LDS build, bloom_build_lds<kKeyVar> (fewer
+    leaves take the spread atomic path).  Empty leaves, a 45000-key leaf (big_leaf: a 56 KiB
+    image), every short length, keys of >= 32 bytes, and the generic-k loop (5 bits/key ->
+    k = 3)."""
     rng = np.random.default_rng(12)
     counts = [int(c) for c in rng.integers(0, 700, 70)]
-    counts[3], counts[10], counts[11], counts[40] = 0, 4096, 9000, 4097
+    counts[3], counts[10], counts[11], counts[40] = 0, 4096, 9000, 513
+    if big_leaf:
+        counts[50] = 45000
     lens = rng.integers(0, 72, sum(counts))
     blob = rng.integers(0, 256, int(lens.sum()), dtype=np.uint8)
     offs = np.zeros(len(lens) + 1, np.int64)
