@@ -9,19 +9,28 @@ One step = one pass of the hot path over one batch: build every leaf filter of
 `--keys-per-gpu` (default 100M, BASELINE config 2) 16-byte keys held in HBM, S = 16,384 keys
 per leaf (6,103 full leaves + 8,448), into one device filter array.  Multi-GPU: one process
 per GPU (torch.distributed, RCCL); each rank builds its own contiguous range of leaves (weak
-scaling, no data-path collective).  The RCCL all-gather of the filter array (north star) is
-timed separately after the timed region and reported as `allgather_ms` (`--allgather` puts
-it inside the timed step instead).
+scaling, no data-path collective).  `--gpus N` without a launcher starts the N rank
+processes itself (before anything touches a GPU); under torch.distributed.run the world size
+must equal --gpus.  The RCCL all-gather of the filter array (north star) is timed separately
+after the timed region and reported as `allgather_ms` (`--allgather` puts it inside the
+timed step instead); rank 0 then checks the gathered array against a single-process build.
+
+After the timed region every rank byte-compares a sample of its leaves (first, last, the
+partial leaf, 8 seeded-random ones) with the CPU oracle built from independently generated
+keys ("verified"); probe workloads compare all 200M answers with the oracle's ("fpr_oracle").
 
 The printed JSON line carries `roofline` (dominant kernel, HIP events on the build stream,
 algorithmic bytes) and `cpu_baseline` (the C oracle -- a restatement of the reference's CPU
-path -- timed on this host's cores on rank 0, N = 1 only).
+path, -O3 -march=native -mbmi2 -mavx2 on this host -- timed on this host's cores on rank 0,
+N = 1 only).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -35,20 +44,21 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s peak (spec)
 FABRIC_LINES_G_PER_S = 61.7  # MI355X_MICROARCH.md: random rows of a 151 MB table, 7.9 TB/s / 128 B
 
 WORKLOADS = {
-    # name: (kind, bits_per_key, payload_capacity, metric label)
-    "bloom10": (0, 10, 0, "Bloom @10 bits/key"),
-    "bloom12": (0, 12, 0, "Bloom @12 bits/key"),
-    "vqf12": (1, 12, 32704, "VQF @12 bits/key (reference clamp of 10 -> 12)"),
-    "probe10": (0, 10, 0, "Bloom @10 probe, 50% hits"),
-    "probe_vqf12": (1, 12, 32704, "VQF @12 probe, 50% hits"),
-    "bloom10k24": (0, 10, 0, "Bloom @10 bits/key, 24-byte keys (TurtleKV default key size)"),
-    "bloom10mono": (0, 10, 0, "Bloom @10 bits/key, one monolithic filter per GPU"),
-    "bloom10var": (0, 10, 0, "Bloom @10 bits/key, variable-length keys (8-31 B)"),
+    # name: (kind, bits_per_key, metric label); VQF payload capacity comes from TreeOptions
+    "bloom10": (0, 10, "Bloom @10 bits/key"),
+    "bloom12": (0, 12, "Bloom @12 bits/key"),
+    "vqf12": (1, 12, "VQF @12 bits/key (reference clamp of 10 -> 12)"),
+    "probe10": (0, 10, "Bloom @10 probe, 50% hits"),
+    "probe_vqf12": (1, 12, "VQF @12 probe, 50% hits"),
+    "bloom10k24": (0, 10, "Bloom @10 bits/key, 24-byte keys (TurtleKV default key size)"),
+    "bloom10mono": (0, 10, "Bloom @10 bits/key, one monolithic filter per GPU"),
+    "bloom10var": (0, 10, "Bloom @10 bits/key, variable-length keys (8-31 B)"),
 }
 # workloads whose one filter spans every key of the GPU (the monolithic
 # single-filter Bloom variant)
 MONOLITHIC = {"bloom10mono"}
 KEY_BYTES = {"bloom10k24": 24, "bloom10var": 0}  # 0: variable length (offsets)
+SWEEP_LEAVES = (64, 256, 1024)                   # + the whole batch
 
 
 def parse():
@@ -75,8 +85,69 @@ def parse():
                          "steady clock; 0 disables)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-verify", action="store_true",
+                    help="skip the post-timing oracle comparison (kernel experiments only)")
+    ap.add_argument("--no-sweep", action="store_true",
+                    help="skip the batch-size sweep (64 / 256 / 1024 / all leaves)")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU baseline threads (0: every core this process may use)")
     return ap.parse_args()
+
+
+# ---------------------------------------------------------------------------------------
+# --gpus N without a launcher: start the ranks (this process never touches a GPU)
+# ---------------------------------------------------------------------------------------
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(n: int) -> int:
+    """One child process per rank, as torch.distributed.run would start them; rank 0's
+    stdout carries the JSON line.  Returns the first non-zero exit code, else 0."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]],
+                                      env=env))
+    rc = 0
+    pending = list(procs)
+    while pending:
+        for p in list(pending):
+            code = p.poll()
+            if code is None:
+                continue
+            pending.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in pending:  # a failed rank leaves the others waiting in a collective
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
+# ---------------------------------------------------------------------------------------
+# host CPU share (the CPU baseline's core count)
+# ---------------------------------------------------------------------------------------
+def host_cpu_share():
+    """CPUs this process may use: the affinity mask, capped by a cgroup CPU quota if one is
+    set (the GPU box runs each job with a 16-CPU quota on a 256-thread host)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    cores = aff if quota is None else max(1, min(aff, int(quota)))
+    return cores, {"affinity_cpus": aff, "cgroup_cpu_quota": quota,
+                   "host_cpus": os.cpu_count()}
 
 
 def segment_counts(n_keys, leaf_keys=SEG_KEYS):
@@ -84,15 +155,21 @@ def segment_counts(n_keys, leaf_keys=SEG_KEYS):
     return [leaf_keys] * full + ([rem] if rem else [])
 
 
-def cpu_baseline(kind, bpk, cap, keys_host, counts, threads, leaf_keys=SEG_KEYS):
-    """Oracle (C, -O3, one filter per thread at a time, leaves spread over `threads` workers
-    like TreeSerializeContext::build_all_pages) over the same keys; bounded to <= ~20 s."""
+def _oracle_libs():
+    """(native-march oracle or None, portable oracle) -- loaded only for the baseline leg"""
     from oracle import oracle as O
     O.build_oracle()
+    return O, O.native_lib(), O.lib()
+
+
+def cpu_baseline(kind, bpk, cap, keys_host, counts, threads, leaf_keys=SEG_KEYS):
+    """The C oracle (one filter per thread at a time, leaves spread over `threads` workers
+    like TreeSerializeContext::build_all_pages) over the same keys, bounded to ~10 s."""
+    O, native, portable = _oracle_libs()
     n_segs = len(counts)
-    # bound the sample: estimate from a small run, then size to ~10 s wall
-    probe_segs = min(n_segs, 4 * threads)
-    def run(ns):
+    cores, share = host_cpu_share()
+
+    def run(L, ns, nthr):
         c = counts[:ns]
         sb = np.concatenate([[0], np.cumsum(c)]).astype(np.uint64)
         if kind == 0:
@@ -102,39 +179,64 @@ def cpu_baseline(kind, bpk, cap, keys_host, counts, threads, leaf_keys=SEG_KEYS)
         offs = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.uint64)
         out = np.empty(int(sizes.sum()), np.uint8)
         t0 = time.perf_counter()
-        st, _ = O.build_segments(kind, keys_host, sb, bpk, offs, sizes, 0, n_threads=threads,
-                                 out=out)
+        st, _ = O.build_segments(kind, keys_host, sb, bpk, offs, sizes, 0, n_threads=nthr,
+                                 out=out, L=L)
         dt = time.perf_counter() - t0
         assert st == 0, st
         return int(sb[-1]), dt
-    n0, t0 = run(probe_segs)
-    rate = n0 / max(t0, 1e-9)
-    target_keys = min(int(sum(counts)), int(rate * 10.0))
-    ns = n_segs if target_keys >= sum(counts) else max(probe_segs, target_keys // leaf_keys)
-    if ns == probe_segs:
-        nk, dt = n0, t0
-    else:
-        nk, dt = run(ns)
+
+    def timed(L, nthr):
+        probe_segs = min(n_segs, 4 * nthr)
+        n0, t0 = run(L, probe_segs, nthr)
+        rate = n0 / max(t0, 1e-9)
+        target = min(int(sum(counts)), int(rate * 8.0))
+        ns = n_segs if target >= sum(counts) else max(probe_segs, target // leaf_keys)
+        nk, dt = (n0, t0) if ns == probe_segs else run(L, ns, nthr)
+        return ns, nk, dt
+
+    L = native or portable
+    ns, nk, dt = timed(L, threads)
     used = min(threads, ns)  # one filter per thread at a time
-    return {"value": round(nk / dt / 1e6, 2), "unit": "Mkeys/s", "cores": used,
-            "kind": "port",
-            "sample": f"{ns} leaves x {leaf_keys} keys ({nk} keys) of the same workload, C oracle "
-                      f"(oracle/tkv_amq_oracle.c, -O3 -march=x86-64-v3), {used} threads, "
-                      f"{dt:.2f} s wall"}
+    res = {"value": round(nk / dt / 1e6, 2), "unit": "Mkeys/s", "cores": used,
+           "kind": "port",
+           "sample": f"{ns} leaves x {leaf_keys} keys ({nk} keys) of the same workload, C oracle "
+                     f"(oracle/tkv_amq_oracle.c, "
+                     f"{'-O3 -march=native -mbmi2 -mavx2' if native else '-O3 -march=x86-64-v3 (native build failed)'}), "
+                     f"{used} threads, {dt:.2f} s wall",
+           "host": share,
+           "per_core_mkeys_s": round(nk / dt / 1e6 / used, 2)}
+    if native:
+        ns2, nk2, dt2 = timed(portable, threads)
+        res["portable_x86_64_v3"] = {"value": round(nk2 / dt2 / 1e6, 2), "threads": min(threads, ns2)}
+    return res
 
 
+# ---------------------------------------------------------------------------------------
+# main
+# ---------------------------------------------------------------------------------------
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; launch with "
+                         f"torch.distributed.run --nproc-per-node {args.gpus}, or without a "
+                         "launcher (bench.py starts the ranks itself)")
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+
     import torch
     import torch.distributed as dist
 
     import turtle_kv_amd as amq
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    # one process per GPU (rehearsals with more ranks than GPUs share devices round-robin)
-    local = local % max(1, torch.cuda.device_count())
+    n_dev = torch.cuda.device_count()
+    if world > 1 and args.backend == "nccl" and world > n_dev:
+        raise SystemExit(f"bench.py: {world} ranks over RCCL need {world} GPUs, {n_dev} visible "
+                         "(--backend gloo rehearses the multi-rank logic with shared devices)")
+    # one process per GPU (gloo rehearsals with more ranks than GPUs share devices round-robin)
+    local = local % max(1, n_dev)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
@@ -143,7 +245,11 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(args.backend)
-    kind, bpk, cap, label = WORKLOADS[args.workload]
+    kind, bpk, label = WORKLOADS[args.workload]
+    # the VQF payload capacity is the default TreeOptions' filter page at this bits/key
+    # (tree/tree_options.hpp:177-220): 32 KiB pages, 32,704 payload bytes at 12 bits/key
+    cap = (amq.TreeOptions(kind).set_filter_bits_per_key(bpk).filter_page_payload_size()
+           if kind == amq.VQF else 0)
     from turtle_kv_amd import dist as tdist
     strong = args.total_keys is not None
     leaf_keys = args.leaf_keys or SEG_KEYS
@@ -164,7 +270,7 @@ def main():
     n = shard.key_end - shard.key_begin
     total_keys = sum(all_counts)
     key_bytes = KEY_BYTES.get(args.workload, 16)
-    var_lens = None
+    offsets = None
     if key_bytes == 16:
         keys = amq.gen_keys16(42, shard.key_begin, n, device=dev)
     elif key_bytes == 0:
@@ -176,6 +282,7 @@ def main():
         torch.cumsum(var_lens, 0, out=offsets[1:])
         keys = torch.randint(0, 256, (int(offsets[-1].item()),), dtype=torch.uint8, device=dev,
                              generator=g)
+        del var_lens
     else:
         g = torch.Generator(device=dev)
         g.manual_seed(42 + rank)
@@ -183,8 +290,10 @@ def main():
     if kind == 1:
         # VQF inserts in leaf key order: sort each leaf's keys (memcmp order) on the device
         keys = sort_segments_device(torch, keys, counts)
-    kb = amq.KeyBatch.variable(keys, offsets) if var_lens is not None else amq.KeyBatch.fixed(keys)
-    out = torch.empty(plan.total_out_bytes, dtype=torch.uint8, device=dev)
+    kb = amq.KeyBatch.variable(keys, offsets) if offsets is not None else amq.KeyBatch.fixed(keys)
+    # zeroed once: the build never writes past a leaf's payload, so the slack bytes of every
+    # fixed-stride slot stay 0 and the gathered array is comparable byte for byte
+    out = torch.zeros(plan.total_out_bytes, dtype=torch.uint8, device=dev)
     ws = torch.empty(max(plan.workspace_bytes, 1), dtype=torch.uint8, device=dev)
     gathered = (torch.empty(plan.total_out_bytes * world, dtype=torch.uint8, device=dev)
                 if world > 1 else None)
@@ -219,7 +328,7 @@ def main():
     torch.cuda.synchronize()
     if not probe and kind == 1 and not os.environ.get("TKV_AMQ_LIB"):  # (experiment libs skip it)
         amq.abi.check(amq.abi.lib().tkv_amq_build_check(kind, amq.filters._ptr(ws),
-                                                        plan.workspace_bytes,
+                                                        ws.numel(),
                                                         amq.filters._stream_handle()), "vqf build")
 
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -247,6 +356,29 @@ def main():
     ms_per_step = wall / args.steps * 1e3
     value = units * args.steps / wall / 1e6
 
+    # ---- the timed output, checked (untimed) ----
+    verified = None
+    probe_check = None
+    if not args.no_verify:
+        if probe:
+            probe_check = verify_probe(torch, kind, plan, out, q, qseg, is_hit, res,
+                                       baseline=(rank == 0 and world == 1
+                                                 and not args.no_cpu_baseline))
+            ok = True
+        else:
+            verified = verify_sample(torch, kind, bpk, cap, plan, keys, offsets, out, key_bytes,
+                                     shard, rank, leaf_keys)
+            ok = verified["ok"]
+        if world > 1:
+            flag = torch.tensor([1 if ok else 0], dtype=torch.int32,
+                                device=dev if args.backend == "nccl" else "cpu")
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+            ok = bool(flag.item())
+            if verified is not None:
+                verified["all_ranks_ok"] = ok
+        if not ok:
+            raise SystemExit(f"bench.py: timed output differs from the oracle: {verified}")
+
     # algorithmic bytes per launch: build = 16 B/key in + filter payload out;
     # probe = 16 B key + 4 B leaf id + 1 B result per lookup
     fpr = None
@@ -259,7 +391,7 @@ def main():
                              f"hits, first indices {bad[:8].tolist()}")
         fpr = float(res[~is_hit].float().mean())
     else:
-        key_in = n * key_bytes if var_lens is None else keys.numel() + 8 * (n + 1)
+        key_in = n * key_bytes if offsets is None else keys.numel() + 8 * (n + 1)
         alg_bytes = key_in + int(plan.segs["payload_bytes"].astype(np.int64).sum())
     achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
     prof = load_profile(args.workload)
@@ -288,14 +420,26 @@ def main():
                                "7.9 TB/s / 128 B, the guide's random-row gather rate"}
 
     allgather_ms = None
-    if world > 1 and not args.allgather:
-        torch.cuda.synchronize()
-        dist.barrier()
-        g0 = time.perf_counter()
-        for _ in range(3):
+    gather_ok = None
+    if world > 1:
+        if not args.allgather:
+            torch.cuda.synchronize()
+            dist.barrier()
+            g0 = time.perf_counter()
+            for _ in range(3):
+                tdist.allgather_filters(out, gathered)
+            torch.cuda.synchronize()
+            allgather_ms = (time.perf_counter() - g0) / 3 * 1e3
+        else:
             tdist.allgather_filters(out, gathered)
-        torch.cuda.synchronize()
-        allgather_ms = (time.perf_counter() - g0) / 3 * 1e3
+        if rank == 0 and not args.no_verify and not probe:
+            gather_ok = verify_gather(torch, amq, kind, bpk, cap, all_counts, stride, gathered,
+                                      key_bytes, dev)
+
+    sweep = None
+    if rank == 0 and world == 1 and not probe and not args.no_sweep and \
+            args.workload not in MONOLITHIC and len(counts) > SWEEP_LEAVES[0]:
+        sweep = batch_sweep(torch, amq, kind, bpk, cap, counts, kb, ws, plan, kernel_ms)
 
     e2e = None
     if (rank == 0 and world == 1 and not args.no_e2e and not probe and key_bytes == 16
@@ -309,16 +453,18 @@ def main():
         return
 
     base = None
+    cores, _ = host_cpu_share()
+    threads = args.cpu_threads or cores
     if world == 1 and not args.no_cpu_baseline:
-        if probe or key_bytes != 16:
-            base = None
-        else:
-            # the CPU sample is bounded (~10 s); copy at most the first 100M keys to the host
+        if probe:
+            base = probe_check.get("cpu_baseline") if probe_check else None
+        elif key_bytes == 16:
+            # the CPU sample is bounded (~8 s); copy at most the first 100M keys to the host
             lim = max(1, 100_000_000 // leaf_keys)
             nk_host = sum(counts[:lim]) if n > 100_000_000 else n
             base = cpu_baseline(kind, bpk, cap, keys[:nk_host].cpu().numpy(),
                                 counts[:lim] if n > 100_000_000 else counts,
-                                args.cpu_threads, leaf_keys)
+                                threads, leaf_keys)
 
     kdesc = f"{key_bytes}B" if key_bytes else "8-31B (mean %.1f B)" % (keys.numel() / max(n, 1))
     line = {
@@ -339,15 +485,21 @@ def main():
         "config": {"workload": (f"{label}: {total_keys} x {kdesc} keys over {world} GPU(s)"
                                 if strong else f"{label}: {n} x {kdesc} keys per GPU")
                                + f", {leaf_keys}-key leaves ({len(counts)} filters on rank 0)",
-                   "keys_per_gpu": n, "total_keys": total_keys, "key_bytes": key_bytes, "leaf_keys": leaf_keys, "bits_per_key": bpk,
+                   "keys_per_gpu": n, "total_keys": total_keys, "key_bytes": key_bytes,
+                   "leaf_keys": leaf_keys, "bits_per_key": bpk,
                    "filter": "bloom-blocked512" if kind == 0 else "vqf",
-                   "parallelism": f"leaf-sharded x{world}"},
+                   "payload_capacity": cap or None,
+                   "parallelism": f"leaf-sharded x{world}",
+                   "backend": args.backend if world > 1 else None},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "kernel_ms": round(kernel_ms, 4),
                      "alg_bytes_per_launch": alg_bytes},
         "cpu_baseline": base,
     }
+    if verified is not None:
+        line["verified"] = verified["ok"] and verified.get("all_ranks_ok", True)
+        line["verify"] = verified
     if valu_roof is not None:
         line["valu_roofline"] = valu_roof
     if fabric_roof is not None:
@@ -355,14 +507,168 @@ def main():
     if allgather_ms is not None:
         line["allgather_ms"] = round(allgather_ms, 3)
         line["build_plus_allgather_mkeys_s"] = round(units / ((ms_per_step + allgather_ms) * 1e-3) / 1e6, 2)
+    if gather_ok is not None:
+        line["gather_verified"] = gather_ok
+    if sweep is not None:
+        line["batch_sweep"] = sweep
     if e2e is not None:
         line["e2e_pcie_inclusive"] = e2e
     if fpr is not None:
         line["probe"] = {"lookups": int(q.shape[0]), "hits_all_true": True,
                          "false_positive_rate": round(fpr, 6)}
+        if probe_check is not None:
+            line["probe"].update({k: v for k, v in probe_check.items() if k != "cpu_baseline"})
+            line["verified"] = probe_check["results_equal_oracle"]
     print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+# ---------------------------------------------------------------------------------------
+# verification of the timed output (untimed, oracle = the checker)
+# ---------------------------------------------------------------------------------------
+def sample_leaves(n_leaves, counts, rank, leaf_keys):
+    rng = np.random.default_rng(45 + rank)
+    pick = {0, n_leaves - 1}
+    partial = [i for i, c in enumerate(counts) if c != leaf_keys]
+    pick.update(partial[:1])
+    pick.update(int(x) for x in rng.integers(0, n_leaves, min(8, n_leaves)))
+    return sorted(pick)
+
+
+def verify_sample(torch, kind, bpk, cap, plan, keys, offsets, out, key_bytes, shard, rank,
+                  leaf_keys):
+    """Byte-compare a sample of this rank's leaves with the CPU oracle.  16-byte keys are
+    regenerated on the host by the oracle (so the device key generator and, for VQF, the
+    device sort are checked too); other key shapes are copied from the device."""
+    from oracle import oracle as O
+    O.build_oracle()
+    counts = plan.segs["n_keys"].astype(np.int64)
+    leaves = sample_leaves(len(counts), counts, rank, leaf_keys)
+    bad = []
+    keys_checked = 0
+    for s in leaves:
+        seg = plan.segs[s]
+        kb0, c = int(seg["key_begin"]), int(seg["n_keys"])
+        src = int(seg["src_page_id"])
+        o_off = None
+        if key_bytes == 16:
+            kh = O.gen_keys16(42, shard.key_begin + kb0, c)
+            if kind == 1:
+                O.sort_segments(kh, np.array([0, c], dtype=np.uint64), n_threads=1)
+            if not np.array_equal(kh, keys[kb0:kb0 + c].cpu().numpy()):
+                bad.append({"leaf": s, "what": "device keys differ from the oracle's"})
+                continue
+            stride = 16
+        elif key_bytes == 0:
+            o = offsets[kb0:kb0 + c + 1].cpu().numpy()
+            kh = keys[int(o[0]):int(o[-1])].cpu().numpy() if c else np.zeros(1, np.uint8)
+            o_off = (o - o[0]).astype(np.uint64)
+            stride = 0
+        else:
+            kh = keys[kb0:kb0 + c].cpu().numpy()
+            stride = key_bytes
+        if kind == 0:
+            st, ref = O.bloom_build(kh, c, bpk, src_page_id=src, offsets=o_off, stride=stride)
+            ref = ref.tobytes()
+        else:
+            st, ref, pl = O.vqf_build(kh, c, bpk, cap, src_page_id=src, offsets=o_off, stride=stride)
+            ref = ref[:pl.payload_used].tobytes()
+        if st != 0:
+            bad.append({"leaf": s, "what": f"oracle status {st}"})
+            continue
+        off, nbytes = int(seg["out_offset"]), int(seg["payload_bytes"])
+        got = out[off:off + nbytes].cpu().numpy().tobytes()
+        keys_checked += c
+        if got != ref:
+            bad.append({"leaf": s, "what": "filter bytes differ"})
+    return {"ok": not bad, "leaves": leaves, "keys": keys_checked,
+            "against": "CPU oracle (oracle/tkv_amq_oracle.c) on oracle-generated keys"
+                       if key_bytes == 16 else "CPU oracle on the device keys", "mismatches": bad}
+
+
+def verify_gather(torch, amq, kind, bpk, cap, all_counts, stride, gathered, key_bytes, dev):
+    """Rank 0: the all-gathered array equals a single-process build of every leaf at the same
+    stride (16-byte keys; other key shapes are generated per rank and are not regenerable)."""
+    if key_bytes != 16 or sum(all_counts) > 1_200_000_000:
+        return None
+    full_plan = amq.plan_filters(kind, all_counts, bpk, payload_capacity=cap, out_stride=stride)
+    allk = amq.gen_keys16(42, 0, sum(all_counts), device=dev)
+    if kind == 1:
+        allk = sort_segments_device(torch, allk, all_counts)
+    full = torch.zeros(gathered.numel(), dtype=torch.uint8, device=dev)
+    amq.build_all_filters(full_plan, amq.KeyBatch.fixed(allk), out=full[:full_plan.total_out_bytes])
+    ok = bool(torch.equal(full, gathered))
+    del full, allk
+    return ok
+
+
+def verify_probe(torch, kind, plan, filters, q, qseg, is_hit, res, baseline):
+    """All lookups of the timed probe through the CPU oracle over the GPU-built filter bytes:
+    the answers (and so the FPR) must be identical.  Timed, this is also the probe's CPU
+    baseline (the oracle's reject_page loop over `cores` host threads)."""
+    from oracle import oracle as O
+    O.build_oracle()
+    native = O.native_lib() if baseline else None
+    cores, share = host_cpu_share()
+    f = filters.cpu().numpy()
+    qh = q.cpu().numpy()
+    qs = qseg.cpu().numpy().astype(np.uint32)
+    got = res.cpu().numpy()
+    hit = is_hit.cpu().numpy()
+    offs = plan.segs["out_offset"]
+    t0 = time.perf_counter()
+    st, ref = O.probe_segments(kind, f, offs, qh, qs, n_threads=cores, L=native)
+    dt = time.perf_counter() - t0
+    if st != 0:
+        raise SystemExit(f"bench.py: oracle probe failed ({st})")
+    equal = bool(np.array_equal(got, ref))
+    if not equal:
+        raise SystemExit(f"bench.py: probe answers differ from the oracle's at "
+                         f"{np.nonzero(got != ref)[0][:8].tolist()}")
+    out = {"results_equal_oracle": equal,
+           "fpr_oracle": round(float(ref[~hit].mean()), 6),
+           "false_positives": int(ref[~hit].sum())}
+    if baseline:
+        out["cpu_baseline"] = {
+            "value": round(len(qs) / dt / 1e6, 2), "unit": "Mkeys/s", "cores": cores,
+            "kind": "port",
+            "sample": f"all {len(qs)} lookups of the timed probe, C oracle probe "
+                      f"(tkvo_probe_segments: hash + {'Bloom query' if kind == 0 else 'vqf_is_present'}"
+                      f" per lookup, {'-O3 -march=native -mbmi2 -mavx2' if native else '-O3 -march=x86-64-v3'}), "
+                      f"{cores} threads, {dt:.2f} s wall",
+            "host": share, "per_core_mkeys_s": round(len(qs) / dt / 1e6 / cores, 2)}
+    return out
+
+
+def batch_sweep(torch, amq, kind, bpk, cap, counts, kb, ws, plan_all, kernel_ms_all, steps=20):
+    """Build rate against the number of leaves per batch (a checkpoint's build_all_pages
+    queue holds tens to thousands of leaves): the first L leaves of the same keys."""
+    rows = []
+    stream = torch.cuda.current_stream()
+    for L in SWEEP_LEAVES:
+        if L >= len(counts):
+            continue
+        c = counts[:L]
+        nk = sum(c)
+        p = amq.plan_filters(kind, c, bpk, payload_capacity=cap)
+        sub = (amq.KeyBatch.fixed(kb.data[:nk]) if kb.offsets is None else
+               amq.KeyBatch.variable(kb.data, kb.offsets[:nk + 1]))
+        o = torch.empty(max(p.total_out_bytes, 1), dtype=torch.uint8, device=kb.data.device)
+        for _ in range(5):
+            amq.build_all_filters(p, sub, out=o, workspace=ws, check=False)
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(steps)]
+        for a, b in ev:
+            a.record(stream)
+            amq.build_all_filters(p, sub, out=o, workspace=ws, check=False)
+            b.record(stream)
+        torch.cuda.synchronize()
+        ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+        rows.append({"leaves": L, "keys": nk, "ms": round(ms, 4), "mkeys_s": round(nk / ms / 1e3, 1)})
+    rows.append({"leaves": len(counts), "keys": int(sum(counts)), "ms": round(kernel_ms_all, 4),
+                 "mkeys_s": round(sum(counts) / kernel_ms_all / 1e3, 1)})
+    return rows
 
 
 def sort_segments_device(torch, keys, counts, chunk_keys=1 << 23):
@@ -372,7 +678,8 @@ def sort_segments_device(torch, keys, counts, chunk_keys=1 << 23):
     applied to all 100M keys at once returned rows that were not a permutation of the input
     past leaf ~2007 on this ROCm build (argsort and repeat_interleave alone check out at
     100M, tools/gpu/diag_torch_sort.py; the failing op was not isolated).  Chunked, the
-    result equals the oracle's sort at full size (tests/test_gpu_scale.py)."""
+    result equals the oracle's sort at full size (tests/test_gpu_scale.py), and the bench
+    re-checks sampled leaves against oracle-generated keys after every run (verify_sample)."""
     out = torch.empty_like(keys)
     b = 0
     i = 0

@@ -24,6 +24,17 @@
  *   tkv_amq_vqf_*sizing     vqf_filter_load_factor<T> (vqf_filter_page_view.hpp:39-59),
  *                           vqf_required_size<T> / vqf_nslots_for_size (vqf 0.2.4, used at
  *                           tree/filter_builder.hpp:243-244,270,274)
+ *   tkv_amq_filter_page_size_log2, tkv_amq_expected_items_per_leaf, tkv_amq_leaf_data_size
+ *                           TreeOptions::filter_page_size_log2 / expected_items_per_leaf /
+ *                           leaf_data_size (tree/tree_options.hpp:177-258, tree_options.cpp:57-60,
+ *                           tree/packed_leaf_page.hpp:307-311, core/packed_sizeof_edit.hpp:13-15)
+ *   tkv_amq_plan_pages      FilterPageAlloc + the page header fields the builders set:
+ *                           layout_id (filter_builder.hpp:237), unused_begin / unused_end
+ *                           (:293-296), in one page-sized slot per leaf
+ *   tkv_amq_probe_ex / tkv_amq_*_probe_hashed_ex
+ *                           the same probes with KeyQuery::reject_page's page-id check
+ *                           (tree/key_query.hpp:205-212,227-232) and KeyQuery::Metrics counters
+ *                           (:36-60, updated at :154,157,210,231,243 and key_query.cpp:41,77)
  *   tkv_amq_stage_keys      the EditView key range build_filter_for_leaf_in_job iterates
  *                           (core/merge_compactor.hpp:107-139) gathered into one contiguous
  *                           host key buffer for the H2D copy (host only)
@@ -50,7 +61,7 @@
 extern "C" {
 #endif
 
-#define TKV_AMQ_ABI_VERSION 1
+#define TKV_AMQ_ABI_VERSION 2
 
 /* status codes (batt::StatusCode values) */
 #define TKV_AMQ_OK 0
@@ -79,8 +90,12 @@ typedef struct tkv_amq_segment {
   uint32_t n_keys;        /* items in the leaf (tombstones included) */
   uint32_t payload_bytes; /* bytes of payload the build writes (header + filter) */
   uint32_t bits_per_key;  /* effective bits/key after the TreeOptions clamp */
-  uint32_t reserved;
+  uint32_t page_flags;    /* TKV_AMQ_PAGE_IMAGE | page_size_log2 << 8 (tkv_amq_plan_pages); 0 */
 } tkv_amq_segment;
+
+/* page_flags bit: the build also writes the 64-byte llfs PackedPageHeader fields the filter
+ * builders set, at out_offset - 64 (the page starts there) */
+#define TKV_AMQ_PAGE_IMAGE 0x1u
 
 const char* tkv_amq_version(void);
 const char* tkv_amq_status_string(int status);
@@ -93,6 +108,19 @@ uint64_t tkv_amq_filter_bits_per_key(int kind, uint64_t requested_bits_per_key);
 double tkv_amq_vqf_load_factor(int tag_bits, uint64_t bits_per_key);
 uint64_t tkv_amq_vqf_required_size(int tag_bits, uint64_t nslots);
 uint64_t tkv_amq_vqf_nslots_for_size(int tag_bits, uint64_t bytes);
+
+/* TreeOptions filter page sizing (tree/tree_options.hpp:177-258).
+ *  leaf_size              TreeOptions::leaf_size() (default 2 MiB)
+ *  key/value_size_hint    defaults 24 / 100 (tree_options.hpp:58-59)
+ *  bits_per_key           as set (the VQF clamp of filter_bits_per_key() is applied here)
+ * tkv_amq_filter_page_size_log2 returns the derived log2 page size (0 for VQF with bpk 0, where
+ * the reference would divide by a zero load factor).  The filter page payload capacity the
+ * builders see is (1 << log2) - 64 (the llfs PackedPageHeader). */
+uint64_t tkv_amq_leaf_data_size(uint64_t leaf_size);
+uint64_t tkv_amq_expected_items_per_leaf(uint64_t leaf_size, uint32_t key_size_hint,
+                                         uint32_t value_size_hint);
+uint32_t tkv_amq_filter_page_size_log2(int kind, uint64_t leaf_size, uint32_t key_size_hint,
+                                       uint32_t value_size_hint, uint64_t bits_per_key);
 
 /* Host-side plan for a batch of n_segs leaves.
  *  seg_key_counts[n_segs]  items per leaf (keys are laid out leaf after leaf)
@@ -110,6 +138,20 @@ int tkv_amq_plan(int kind, const uint64_t* seg_key_counts, const uint64_t* src_p
                  uint32_t n_segs, uint32_t bits_per_key, uint64_t payload_capacity,
                  uint64_t out_stride, tkv_amq_segment* segs, uint64_t* total_out_bytes,
                  uint64_t* workspace_bytes, uint32_t* max_seg_blocks);
+
+/* Plan whole filter pages: leaf s owns bytes [s << page_size_log2, (s+1) << page_size_log2) of
+ * the output array, laid out as the page buffer FilterPageAlloc hands the builder
+ * (filter_builder.hpp:70-88): a 64-byte PackedPageHeader, then the payload (capacity =
+ * page size - 64, which drives the VQF sizing).  tkv_amq_build then also writes the header
+ * fields the filter builders set -- layout_id ("vqf_filt", :237 / vqf_filter_page_view.hpp:142;
+ * Bloom "bloomflt"), unused_begin = 64 + payload bytes, unused_end = page size (:293-296) --
+ * and the page size.  Magic, page id and crc are the PageCache's (llfs) and are written as 0.
+ * Header field offsets follow llfs 0.42's PackedPageHeader and are UNPINNED (llfs is absent).
+ * Bytes between unused_begin and unused_end are not written. */
+int tkv_amq_plan_pages(int kind, const uint64_t* seg_key_counts, const uint64_t* src_page_ids,
+                       uint32_t n_segs, uint32_t bits_per_key, uint32_t page_size_log2,
+                       tkv_amq_segment* segs, uint64_t* total_out_bytes, uint64_t* workspace_bytes,
+                       uint32_t* max_seg_blocks);
 
 /* Device build of every planned filter.
  *  keys         device; fixed-length keys (key_offsets == NULL: key i at keys + i*key_stride,
@@ -138,6 +180,34 @@ int tkv_amq_probe(int kind, const uint8_t* d_filters, const tkv_amq_segment* d_s
                   uint32_t query_stride, uint64_t n_queries, const uint32_t* d_query_seg,
                   uint8_t* d_result, void* stream);
 
+/* KeyQuery::Metrics counters (tree/key_query.hpp:36-60) a probe launch adds to (device
+ * memory, u64 each, accumulated with atomics across launches; zero them to reset). */
+typedef struct tkv_amq_probe_metrics {
+  uint64_t total_filter_query_count;    /* every (query, leaf) test (:154) */
+  uint64_t no_filter_page_count;        /* leaf without a filter / outside the plan (:157) */
+  uint64_t page_id_mismatch_count;      /* filter's src_page_id != the leaf asked about (:210,231) */
+  uint64_t filter_reject_count;         /* definitely absent, kTrue (:243) */
+  uint64_t filter_positive_count;       /* filter says maybe, kFalse (key_query.cpp:41) */
+  uint64_t filter_false_positive_count; /* positive, but ground truth says absent (:77) */
+} tkv_amq_probe_metrics;
+
+/* Optional per-query inputs and outputs of the _ex probes (any field may be NULL):
+ *  d_query_page_id[i]  the leaf page id query i asks about (reject_page's page_id_to_reject);
+ *                      if it differs from the filter's src_page_id the answer is 1 (kUnknown)
+ *  d_truth[i]          1 if the key is in the leaf (the leaf search's answer), for the
+ *                      false-positive count; NULL => filter_false_positive_count untouched
+ *  d_metrics           counters to add to */
+typedef struct tkv_amq_probe_opts {
+  const uint64_t* d_query_page_id;
+  const uint8_t* d_truth;
+  tkv_amq_probe_metrics* d_metrics;
+} tkv_amq_probe_opts;
+
+int tkv_amq_probe_ex(int kind, const uint8_t* d_filters, const tkv_amq_segment* d_segs,
+                     uint32_t n_segs, const uint8_t* queries, const uint64_t* query_offsets,
+                     uint32_t query_stride, uint64_t n_queries, const uint32_t* d_query_seg,
+                     uint8_t* d_result, const tkv_amq_probe_opts* opts, void* stream);
+
 /* vqf_hash_val for n keys -> d_hash[n] (device) */
 int tkv_amq_vqf_hash(const uint8_t* keys, const uint64_t* key_offsets, uint32_t key_stride,
                      uint64_t n_keys, uint64_t* d_hash, void* stream);
@@ -149,6 +219,12 @@ int tkv_amq_vqf_probe_hashed(const uint8_t* d_filters, const tkv_amq_segment* d_
                              uint32_t n_segs, const uint64_t* d_hash,
                              const uint32_t* d_pair_query, uint64_t n_pairs,
                              const uint32_t* d_pair_leaf, uint8_t* d_result, void* stream);
+/* opts fields are indexed by pair i */
+int tkv_amq_vqf_probe_hashed_ex(const uint8_t* d_filters, const tkv_amq_segment* d_segs,
+                                uint32_t n_segs, const uint64_t* d_hash,
+                                const uint32_t* d_pair_query, uint64_t n_pairs,
+                                const uint32_t* d_pair_leaf, uint8_t* d_result,
+                                const tkv_amq_probe_opts* opts, void* stream);
 
 /* BloomFilterQuery<KeyView> (tree/key_query.hpp:78,97,219): the hashes one query needs,
  * computed once and reused for every Bloom filter it is tested against.  Record i lives at
@@ -162,6 +238,11 @@ int tkv_amq_bloom_probe_hashed(const uint8_t* d_filters, const tkv_amq_segment* 
                                uint32_t n_segs, const uint8_t* d_query, uint32_t k_max,
                                const uint32_t* d_pair_query, uint64_t n_pairs,
                                const uint32_t* d_pair_leaf, uint8_t* d_result, void* stream);
+int tkv_amq_bloom_probe_hashed_ex(const uint8_t* d_filters, const tkv_amq_segment* d_segs,
+                                  uint32_t n_segs, const uint8_t* d_query, uint32_t k_max,
+                                  const uint32_t* d_pair_query, uint64_t n_pairs,
+                                  const uint32_t* d_pair_leaf, uint8_t* d_result,
+                                  const tkv_amq_probe_opts* opts, void* stream);
 
 /* Key staging, host only (no device needed): the H2D front end.  The reference passes the
  * build a flattened range of EditView whose keys are KeyView = std::string_view into leaf /

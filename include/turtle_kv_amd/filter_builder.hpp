@@ -12,6 +12,10 @@
 //   TreeSerializeContext::build_all_pages tree/tree_serialize_context.cpp:62-115 (filter half)
 //                                                                          FilterBatchBuilder
 //   KeyQuery::reject_page                 tree/key_query.hpp:149-247       KeyQuery::reject_page
+//   KeyQuery::Metrics                     tree/key_query.hpp:36-60         KeyQuery::Metrics
+//   TreeOptions (filter sizing)           tree/tree_options.hpp:149-258    TreeOptions
+//   FilterPageAlloc page image            tree/filter_builder.hpp:58-105,231-237,293-296
+//                                                                          FilterBatchBuilder::plan_pages
 //
 // The single-leaf functions take the leaf's keys as host string views (the reference's
 // `items` range of EditView keys, tombstones included) and fill a host page payload
@@ -22,6 +26,7 @@
 
 #include <hip/hip_runtime_api.h>
 
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <condition_variable>
@@ -86,6 +91,60 @@ inline usize filter_bits_per_key(std::optional<u16> requested,
                                  FilterKind kind = kDefaultFilterKind)
 {
   return (usize)tkv_amq_filter_bits_per_key((int)kind, requested.value_or(kDefaultFilterBitsPerKey));
+}
+
+// The filter part of TreeOptions (tree/tree_options.hpp:43-395): bits per key with the VQF
+// clamp, and the filter page size from the leaf size and key/value size hints.  `kind` stands
+// for the compile-time filter switch (config.hpp:20-24).
+class TreeOptions
+{
+ public:
+  static constexpr u32 kDefaultKeySizeHint = 24;     // :58
+  static constexpr u32 kDefaultValueSizeHint = 100;  // :59
+
+  explicit TreeOptions(FilterKind kind = kDefaultFilterKind) : kind_{kind} {}
+  static TreeOptions with_default_values(FilterKind kind = kDefaultFilterKind) { return TreeOptions{kind}; }
+
+  u64 leaf_size() const { return u64{1} << leaf_size_log2_; }
+  TreeOptions& set_leaf_size_log2(u8 size_log2) { leaf_size_log2_ = size_log2; return *this; }
+  usize leaf_data_size() const { return (usize)tkv_amq_leaf_data_size(leaf_size()); }
+
+  TreeOptions& set_filter_bits_per_key(std::optional<u16> bpk) { filter_bits_per_key_ = bpk; return *this; }
+  usize filter_bits_per_key() const { return turtle_kv_amd::filter_bits_per_key(filter_bits_per_key_, kind_); }
+
+  TreeOptions& set_key_size_hint(u32 n) { key_size_hint_ = n; return *this; }
+  TreeOptions& set_value_size_hint(u32 n) { value_size_hint_ = n; return *this; }
+  u32 key_size_hint() const { return key_size_hint_; }
+  u32 value_size_hint() const { return value_size_hint_; }
+  usize expected_items_per_leaf() const
+  {
+    return (usize)tkv_amq_expected_items_per_leaf(leaf_size(), key_size_hint_, value_size_hint_);
+  }
+
+  TreeOptions& set_filter_page_size_log2(u8 size_log2) { filter_page_size_log2_ = size_log2; return *this; }
+  u32 filter_page_size_log2() const
+  {
+    if (filter_page_size_log2_) return *filter_page_size_log2_;
+    return tkv_amq_filter_page_size_log2((int)kind_, leaf_size(), key_size_hint_, value_size_hint_,
+                                         filter_bits_per_key_.value_or(kDefaultFilterBitsPerKey));
+  }
+  u64 filter_page_size() const { return u64{1} << filter_page_size_log2(); }
+  // the payload the filter builders size against: the page minus the llfs PackedPageHeader
+  u64 filter_page_payload_size() const { return filter_page_size() - kPackedPageHeaderSize; }
+
+ private:
+  FilterKind kind_;
+  u8 leaf_size_log2_ = 21;  // 2 MiB (tree_options.cpp:20-21)
+  std::optional<u16> filter_bits_per_key_;
+  std::optional<u8> filter_page_size_log2_;
+  u32 key_size_hint_ = kDefaultKeySizeHint;
+  u32 value_size_hint_ = kDefaultValueSizeHint;
+};
+
+// payload capacity of the default TreeOptions' filter page at this bits/key
+inline u64 default_filter_page_payload_size(usize bits_per_key, FilterKind kind)
+{
+  return TreeOptions{kind}.set_filter_bits_per_key((u16)bits_per_key).filter_page_payload_size();
 }
 
 // vqf_metadata + PackedVqfFilter on-page layout (little-endian)
@@ -171,6 +230,16 @@ class FilterBatchBuilder
   {
   }
 
+  // Whole filter pages of 2^page_size_log2 bytes, leaf s at s << log2: the PackedPageHeader
+  // fields the builders set, then the payload (tkv_amq_plan_pages).
+  static FilterBatchBuilder pages(FilterKind kind, usize bits_per_key, u32 page_size_log2)
+  {
+    FilterBatchBuilder b{kind, bits_per_key, (u64{1} << page_size_log2) - kPackedPageHeaderSize,
+                         u64{1} << page_size_log2};
+    b.page_log2_ = page_size_log2;
+    return b;
+  }
+
   // Queue one leaf whose keys occupy the next n_keys slots of the device key array.
   u32 add_leaf(u64 leaf_page_id, u64 n_keys)
   {
@@ -182,9 +251,13 @@ class FilterBatchBuilder
   Status plan()
   {
     segs_.resize(counts_.size());
-    const int st = tkv_amq_plan((int)kind_, counts_.data(), page_ids_.data(), (u32)counts_.size(),
-                                (u32)bpk_, cap_, stride_, segs_.data(), &total_out_, &ws_bytes_,
-                                &max_blocks_);
+    const int st =
+        page_log2_ ? tkv_amq_plan_pages((int)kind_, counts_.data(), page_ids_.data(), (u32)counts_.size(),
+                                        (u32)bpk_, page_log2_, segs_.data(), &total_out_, &ws_bytes_,
+                                        &max_blocks_)
+                   : tkv_amq_plan((int)kind_, counts_.data(), page_ids_.data(), (u32)counts_.size(),
+                                  (u32)bpk_, cap_, stride_, segs_.data(), &total_out_, &ws_bytes_,
+                                  &max_blocks_);
     if (st != TKV_AMQ_OK) return Status::from(st, "tkv_amq_plan");
     if (!d_segs_.resize(segs_.size() * sizeof(tkv_amq_segment)) || !d_ws_.resize(ws_bytes_))
       return Status::from(TKV_AMQ_RESOURCE_EXHAUSTED, "hipMalloc");
@@ -237,6 +310,7 @@ class FilterBatchBuilder
   std::vector<tkv_amq_segment> segs_;
   u64 total_out_ = 0, ws_bytes_ = 0;
   u32 max_blocks_ = 0;
+  u32 page_log2_ = 0;
   bool planned_ = false;
   DeviceBuffer d_segs_, d_ws_;
 };
@@ -428,13 +502,17 @@ inline Status build_quotient_filter_for_leaf(usize filter_bits_per_key, u64 leaf
 
 // Like the reference: a failed build is logged by the caller and the leaf gets no filter
 // (filter_builder.hpp:323-325); the returned Status carries the reason.
+// page_payload_bytes 0: the default TreeOptions' filter page payload at this bits/key
+// (TreeOptions::filter_page_size(), tree/tree_options.hpp:177-220; 32,704 bytes at 12 bits/key)
 inline Status build_filter_for_leaf_in_job(usize filter_bits_per_key, u64 leaf_page_id,
                                            const std::vector<std::string_view>& items,
                                            std::vector<u8>& page_payload,
-                                           u64 page_payload_bytes = 32768 - kPackedPageHeaderSize,
+                                           u64 page_payload_bytes = 0,
                                            FilterKind kind = kDefaultFilterKind)
 {
   page_payload.clear();
+  if (page_payload_bytes == 0 && filter_bits_per_key != 0)
+    page_payload_bytes = default_filter_page_payload_size(filter_bits_per_key, kind);
   Status s = kind == FilterKind::kBloom
                  ? build_bloom_filter_for_leaf(filter_bits_per_key, leaf_page_id, items,
                                                page_payload, page_payload_bytes)
@@ -692,12 +770,18 @@ class LeafBatcher
                                         b.h_keys + r.byte_off, r.bytes, nullptr, 1);
       return st == TKV_AMQ_OK ? OkStatus() : Status::from(st, "tkv_amq_stage_keys");
     }
+    u64* dst = b.h_offs + r.key_off;
+    // on failure this leaf's slice of the batch offsets must not keep an earlier batch's
+    // values (the batch is built anyway): zero-length keys at the leaf's own byte offset
+    auto fail = [&](int code, const char* what) {
+      for (u64 j = 0; j < r.n; ++j) dst[j] = r.byte_off;
+      return Status::from(code, what);
+    };
     if (!detail::LeafScratch::grow_pinned(sc.h_offs, sc.h_offs_cap, r.n + 1))
-      return Status::from(TKV_AMQ_RESOURCE_EXHAUSTED, "hipHostMalloc");
+      return fail(TKV_AMQ_RESOURCE_EXHAUSTED, "hipHostMalloc");
     const int st = tkv_amq_stage_keys(views, sizeof(tkv_amq_key_view), r.n, 0, b.h_keys + r.byte_off,
                                       r.bytes, sc.h_offs, 1);
-    if (st != TKV_AMQ_OK) return Status::from(st, "tkv_amq_stage_keys");
-    u64* dst = b.h_offs + r.key_off;
+    if (st != TKV_AMQ_OK) return fail(st, "tkv_amq_stage_keys");
     for (u64 j = 0; j < r.n; ++j) dst[j] = sc.h_offs[j] + r.byte_off;
     return OkStatus();
   }
@@ -778,9 +862,11 @@ class LeafBatcher
 inline Status build_filter_for_leaf_in_job_batched(usize filter_bits_per_key, u64 leaf_page_id,
                                                    const std::vector<std::string_view>& items,
                                                    std::vector<u8>& page_payload,
-                                                   u64 page_payload_bytes = 32768 - kPackedPageHeaderSize,
+                                                   u64 page_payload_bytes = 0,
                                                    FilterKind kind = kDefaultFilterKind)
 {
+  if (page_payload_bytes == 0 && filter_bits_per_key != 0)
+    page_payload_bytes = default_filter_page_payload_size(filter_bits_per_key, kind);
   static LeafBatcher* batcher = new LeafBatcher;
   return batcher->build(kind, filter_bits_per_key, leaf_page_id, items, page_payload, page_payload_bytes);
 }
@@ -790,24 +876,74 @@ inline Status build_filter_for_leaf_in_job_batched(usize filter_bits_per_key, u6
 // ---------------------------------------------------------------------------------------
 enum class BoolStatus : int { kFalse = 0, kTrue = 1, kUnknown = 2 };
 
+// FastCountMetric<u64>
+struct CountMetric {
+  std::atomic<u64> value{0};
+  void add(u64 n) { value.fetch_add(n, std::memory_order_relaxed); }
+  u64 get() const { return value.load(std::memory_order_relaxed); }
+};
+
 class KeyQuery
 {
  public:
+  // KeyQuery::Metrics, the filter counters (tree/key_query.hpp:36-60).  reject_page updates
+  // total / no-filter / load-failed / page-id-mismatch / reject (:154,157,183,210,231,243);
+  // positive / false positive are the caller's leaf search's (key_query.cpp:41,77):
+  // reject_page counts them when the caller passes the ground truth.
+  struct Metrics {
+    CountMetric total_filter_query_count;
+    CountMetric no_filter_page_count;
+    CountMetric filter_page_load_failed_count;
+    CountMetric page_id_mismatch_count;
+    CountMetric filter_reject_count;
+    CountMetric filter_positive_count;
+    CountMetric filter_false_positive_count;
+
+    double filter_false_positive_rate() const noexcept
+    {
+      const double positives = (double)filter_positive_count.get();
+      if (positives == 0) return -1;
+      return (double)filter_false_positive_count.get() / positives;
+    }
+  };
+
+  static Metrics& metrics()
+  {
+    static Metrics metrics_;
+    return metrics_;
+  }
+
   explicit KeyQuery(std::vector<std::string_view> keys) : keys_{std::move(keys)} {}
 
   // per key: kTrue = definitely absent; kFalse = maybe present; kUnknown = no filter or the
-  // filter belongs to another page (key_query.hpp:156-159, 207-212, 227-232)
+  // filter belongs to another page (key_query.hpp:156-159, 207-212, 227-232).
+  // truth (optional, one per key: 1 = the key is in the leaf) feeds the positive /
+  // false-positive counters the reference's leaf search keeps (key_query.cpp:41,77).
   Status reject_page(u64 page_id_to_reject, const std::vector<u8>* filter_payload,
-                     FilterKind kind, std::vector<BoolStatus>& out)
+                     FilterKind kind, std::vector<BoolStatus>& out,
+                     const std::vector<u8>* truth = nullptr)
   {
-    out.assign(keys_.size(), BoolStatus::kUnknown);
-    if (!filter_payload || filter_payload->size() < 64) return OkStatus();
+    Metrics& m = metrics();
+    const u64 n = keys_.size();
+    out.assign(n, BoolStatus::kUnknown);
+    m.total_filter_query_count.add(n);
+    if (!filter_payload) {
+      m.no_filter_page_count.add(n);
+      return OkStatus();
+    }
+    if (filter_payload->size() < 64) {  // cannot be read as a filter page: cannot reject
+      m.filter_page_load_failed_count.add(n);
+      return OkStatus();
+    }
     u64 magic, src;
     std::memcpy(&magic, filter_payload->data(), 8);
     std::memcpy(&src, filter_payload->data() + (kind == FilterKind::kBloom ? 16 : 8), 8);
     const u64 want = kind == FilterKind::kBloom ? PackedBloomFilterPage::kMagic : PackedVqfFilter::kMagic;
     if (magic != want) return Status::from(TKV_AMQ_INTERNAL, "filter page magic");
-    if (src != page_id_to_reject) return OkStatus();
+    if (src != page_id_to_reject) {
+      m.page_id_mismatch_count.add(n);
+      return OkStatus();
+    }
     if (keys_.empty()) return OkStatus();
     if (tkv_amq_device_count() == 0) return Status::from(TKV_AMQ_UNAVAILABLE, "no HIP device");
 
@@ -819,31 +955,53 @@ class KeyQuery
       seg.n_blocks = h.block_count;
       seg.hash_count = h.hash_count;
     } else {
+      if (filter_payload->size() < sizeof(PackedVqfFilter)) {
+        m.filter_page_load_failed_count.add(n);
+        return OkStatus();
+      }
       PackedVqfFilter h;
       std::memcpy(&h, filter_payload->data(), sizeof(h));
-      const u64 buckets = h.metadata.key_remainder_bits == 8 ? 80 : 36;
+      const u64 tb = h.metadata.key_remainder_bits;
+      if ((tb != 8 && tb != 16) || h.metadata.nblocks == 0 || h.hash_mask == 0)
+        return Status::from(TKV_AMQ_INTERNAL, "PackedVqfFilter metadata");
+      // hash_mask = ~0 << hash_val_shift (filter_builder.hpp:187): truncated leaves answer
+      // "maybe" for every hash with a low bit set (vqf_filter_page_view.hpp:115-117)
+      const u32 shift = (u32)__builtin_ctzll(h.hash_mask);
+      if (h.hash_mask != (~u64{0} << shift)) return Status::from(TKV_AMQ_INTERNAL, "hash_mask");
+      const u64 buckets = tb == 8 ? 80 : 36;
       seg.n_blocks = (u32)h.metadata.nblocks;
-      seg.tag_bits = (u8)h.metadata.key_remainder_bits;
+      seg.tag_bits = (u8)tb;
+      seg.hash_val_shift = (u8)shift;
       seg.mod_magic = ~0ull / (h.metadata.nblocks * buckets);
     }
     seg.out_offset = 0;
-    DeviceBuffer d_keys, d_offs, d_page(filter_payload->size()), d_seg(sizeof(seg)),
-        d_leaf(4 * keys_.size()), d_res(keys_.size());
+    DeviceBuffer d_keys, d_offs, d_page, d_seg, d_leaf, d_res;
+    if (!d_page.resize(filter_payload->size()) || !d_seg.resize(sizeof(seg)) ||
+        !d_leaf.resize(4 * n) || !d_res.resize(n))
+      return Status::from(TKV_AMQ_RESOURCE_EXHAUSTED, "hipMalloc");
     bool fixed = false;
     u32 stride = 16;
     TKV_AMQ_REQUIRE_OK(detail::stage_keys(keys_, d_keys, d_offs, fixed, stride));
-    (void)hipMemcpy(d_page.get(), filter_payload->data(), filter_payload->size(), hipMemcpyHostToDevice);
-    (void)hipMemcpy(d_seg.get(), &seg, sizeof(seg), hipMemcpyHostToDevice);
-    (void)hipMemset(d_leaf.get(), 0, 4 * keys_.size());
+    if (hipMemcpy(d_page.get(), filter_payload->data(), filter_payload->size(), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(d_seg.get(), &seg, sizeof(seg), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemset(d_leaf.get(), 0, 4 * n) != hipSuccess)
+      return Status::from(TKV_AMQ_INTERNAL, "hipMemcpy page");
     const int st = tkv_amq_probe((int)kind, d_page.get(), d_seg.get<tkv_amq_segment>(), 1,
                                  d_keys.get(), fixed ? nullptr : d_offs.get<u64>(),
-                                 fixed ? stride : 0, keys_.size(), d_leaf.get<u32>(),
-                                 d_res.get(), nullptr);
+                                 fixed ? stride : 0, n, d_leaf.get<u32>(), d_res.get(), nullptr);
     if (st != TKV_AMQ_OK) return Status::from(st, "tkv_amq_probe");
-    std::vector<u8> res(keys_.size());
+    std::vector<u8> res(n);
     if (hipMemcpy(res.data(), d_res.get(), res.size(), hipMemcpyDeviceToHost) != hipSuccess)
       return Status::from(TKV_AMQ_INTERNAL, "hipMemcpy result");
-    for (usize i = 0; i < res.size(); ++i) out[i] = res[i] ? BoolStatus::kFalse : BoolStatus::kTrue;
+    u64 rejects = 0, fps = 0;
+    for (usize i = 0; i < res.size(); ++i) {
+      out[i] = res[i] ? BoolStatus::kFalse : BoolStatus::kTrue;
+      rejects += res[i] == 0;
+      if (truth && i < truth->size()) fps += res[i] != 0 && (*truth)[i] == 0;
+    }
+    m.filter_reject_count.add(rejects);
+    m.filter_positive_count.add(n - rejects);
+    if (truth) m.filter_false_positive_count.add(fps);
     return OkStatus();
   }
 

@@ -18,7 +18,9 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB_PATH = os.path.join(_HERE, "build", "libtkv_amq_oracle.so")
+_NATIVE_PATH = os.path.join(_HERE, "build", "native", "libtkv_amq_oracle.so")
 _lib = None
+_native = None
 
 VQF_HASH_SEED = 0x9D0924DC03E79A75
 BLOOM, VQF = 0, 1
@@ -40,52 +42,76 @@ def build_oracle() -> str:
     return _LIB_PATH
 
 
+def build_native() -> str:
+    """The reference's own flags (-O3 -march=native -mbmi2 -mavx2, CMakeLists.txt:46-48),
+    compiled for the CPU this runs on (bench.py's cpu_baseline leg, on the GPU box's host)."""
+    subprocess.run(["make", "-s", "-C", _HERE, "native"], check=True)
+    return _NATIVE_PATH
+
+
 def lib():
     global _lib
     if _lib is None:
         if not os.path.exists(_LIB_PATH):
             build_oracle()
-        L = ctypes.CDLL(_LIB_PATH)
-        u64, u32, vp, i32 = ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_int
-        L.tkvo_xxh64.restype = u64
-        L.tkvo_xxh64.argtypes = [vp, ctypes.c_size_t, u64]
-        L.tkvo_splitmix64_at.restype = u64
-        L.tkvo_splitmix64_at.argtypes = [u64, u64]
-        L.tkvo_gen_keys16.argtypes = [u64, u64, u64, vp]
-        L.tkvo_sort_keys16_segments.argtypes = [vp, vp, u32, i32]
-        L.tkvo_bloom_hash_count.restype = u32
-        L.tkvo_bloom_hash_count.argtypes = [u32]
-        L.tkvo_bloom_seed.restype = u64
-        L.tkvo_bloom_seed.argtypes = [u32]
-        L.tkvo_bloom_block_count.restype = u32
-        L.tkvo_bloom_block_count.argtypes = [u64, u32]
-        L.tkvo_bloom_payload_size.restype = u64
-        L.tkvo_bloom_payload_size.argtypes = [u64, u32]
-        L.tkvo_bloom_build_payload.restype = i32
-        L.tkvo_bloom_build_payload.argtypes = [vp, vp, u32, u64, u32, u64, vp, u64]
-        L.tkvo_bloom_query_payload.restype = i32
-        L.tkvo_bloom_query_payload.argtypes = [vp, vp, ctypes.c_size_t]
-        L.tkvo_vqf_load_factor.restype = ctypes.c_double
-        L.tkvo_vqf_load_factor.argtypes = [i32, u64]
-        L.tkvo_vqf_required_size.restype = u64
-        L.tkvo_vqf_required_size.argtypes = [i32, u64]
-        L.tkvo_vqf_nslots_for_size.restype = u64
-        L.tkvo_vqf_nslots_for_size.argtypes = [i32, u64]
-        L.tkvo_vqf_plan_segment.restype = i32
-        L.tkvo_vqf_plan_segment.argtypes = [u64, u64, u64, ctypes.POINTER(VqfPlan)]
-        L.tkvo_vqf_build_payload.restype = i32
-        L.tkvo_vqf_build_payload.argtypes = [vp, vp, u32, u64, u64, u64, vp, u64,
-                                             ctypes.POINTER(VqfPlan)]
-        L.tkvo_vqf_is_present_payload.restype = i32
-        L.tkvo_vqf_is_present_payload.argtypes = [vp, u64]
-        L.tkvo_tree_filter_bits_per_key.restype = u64
-        L.tkvo_tree_filter_bits_per_key.argtypes = [u64, i32]
-        L.tkvo_build_segments.restype = i32
-        L.tkvo_build_segments.argtypes = [i32, vp, vp, u32, u32, vp, vp, vp, vp, i32]
-        L.tkvo_probe_segments.restype = i32
-        L.tkvo_probe_segments.argtypes = [i32, vp, vp, vp, vp, u64, vp, i32]
-        _lib = L
+        _lib = _load(_LIB_PATH)
     return _lib
+
+
+def native_lib():
+    """The oracle built with -march=native on this host (None if that build fails: the
+    portable build is then the baseline, and bench.py says so)."""
+    global _native
+    if _native is None:
+        try:
+            build_native()
+            _native = _load(_NATIVE_PATH)
+        except (OSError, subprocess.CalledProcessError):
+            return None
+    return _native
+
+
+def _load(path):
+    L = ctypes.CDLL(path)
+    u64, u32, vp, i32 = ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_int
+    L.tkvo_xxh64.restype = u64
+    L.tkvo_xxh64.argtypes = [vp, ctypes.c_size_t, u64]
+    L.tkvo_splitmix64_at.restype = u64
+    L.tkvo_splitmix64_at.argtypes = [u64, u64]
+    L.tkvo_gen_keys16.argtypes = [u64, u64, u64, vp]
+    L.tkvo_sort_keys16_segments.argtypes = [vp, vp, u32, i32]
+    L.tkvo_bloom_hash_count.restype = u32
+    L.tkvo_bloom_hash_count.argtypes = [u32]
+    L.tkvo_bloom_seed.restype = u64
+    L.tkvo_bloom_seed.argtypes = [u32]
+    L.tkvo_bloom_block_count.restype = u32
+    L.tkvo_bloom_block_count.argtypes = [u64, u32]
+    L.tkvo_bloom_payload_size.restype = u64
+    L.tkvo_bloom_payload_size.argtypes = [u64, u32]
+    L.tkvo_bloom_build_payload.restype = i32
+    L.tkvo_bloom_build_payload.argtypes = [vp, vp, u32, u64, u32, u64, vp, u64]
+    L.tkvo_bloom_query_payload.restype = i32
+    L.tkvo_bloom_query_payload.argtypes = [vp, vp, ctypes.c_size_t]
+    L.tkvo_vqf_load_factor.restype = ctypes.c_double
+    L.tkvo_vqf_load_factor.argtypes = [i32, u64]
+    L.tkvo_vqf_required_size.restype = u64
+    L.tkvo_vqf_required_size.argtypes = [i32, u64]
+    L.tkvo_vqf_nslots_for_size.restype = u64
+    L.tkvo_vqf_nslots_for_size.argtypes = [i32, u64]
+    L.tkvo_vqf_plan_segment.restype = i32
+    L.tkvo_vqf_plan_segment.argtypes = [u64, u64, u64, ctypes.POINTER(VqfPlan)]
+    L.tkvo_vqf_build_payload.restype = i32
+    L.tkvo_vqf_build_payload.argtypes = [vp, vp, u32, u64, u64, u64, vp, u64,
+                                         ctypes.POINTER(VqfPlan)]
+    L.tkvo_vqf_is_present_payload.restype = i32
+    L.tkvo_vqf_is_present_payload.argtypes = [vp, u64]
+    L.tkvo_tree_filter_bits_per_key.restype = u64
+    L.tkvo_tree_filter_bits_per_key.argtypes = [u64, i32]
+    L.tkvo_build_segments.restype = i32
+    L.tkvo_build_segments.argtypes = [i32, vp, vp, u32, u32, vp, vp, vp, vp, i32]
+    L.tkvo_probe_segments.restype = i32
+    L.tkvo_probe_segments.argtypes = [i32, vp, vp, vp, vp, u64, vp, i32]
+    return L
 
 
 def _p(a: np.ndarray | None):
@@ -143,23 +169,24 @@ def vqf_is_present(payload: np.ndarray, hash_val: int) -> int:
 def build_segments(kind: int, keys16: np.ndarray, seg_begin: np.ndarray, bpk: int,
                    out_offset: np.ndarray, out_capacity: np.ndarray, total_bytes: int,
                    src_page_id: np.ndarray | None = None, n_threads: int = 8,
-                   out: np.ndarray | None = None):
+                   out: np.ndarray | None = None, L=None):
     seg_begin = np.ascontiguousarray(seg_begin, dtype=np.uint64)
     out_offset = np.ascontiguousarray(out_offset, dtype=np.uint64)
     out_capacity = np.ascontiguousarray(out_capacity, dtype=np.uint64)
     if out is None:
         out = np.zeros(total_bytes, dtype=np.uint8)
-    st = lib().tkvo_build_segments(kind, _p(keys16), _p(seg_begin), len(seg_begin) - 1, bpk,
+    st = (L or lib()).tkvo_build_segments(kind, _p(keys16), _p(seg_begin), len(seg_begin) - 1, bpk,
                                    _p(src_page_id), _p(out), _p(out_offset), _p(out_capacity),
                                    n_threads)
     return st, out
 
 
 def probe_segments(kind: int, filters: np.ndarray, out_offset: np.ndarray,
-                   queries16: np.ndarray, query_seg: np.ndarray, n_threads: int = 8):
+                   queries16: np.ndarray, query_seg: np.ndarray, n_threads: int = 8, L=None,
+                   out: np.ndarray | None = None):
     out_offset = np.ascontiguousarray(out_offset, dtype=np.uint64)
     query_seg = np.ascontiguousarray(query_seg, dtype=np.uint32)
-    res = np.zeros(len(query_seg), dtype=np.uint8)
-    st = lib().tkvo_probe_segments(kind, _p(filters), _p(out_offset), _p(queries16),
+    res = np.zeros(len(query_seg), dtype=np.uint8) if out is None else out
+    st = (L or lib()).tkvo_probe_segments(kind, _p(filters), _p(out_offset), _p(queries16),
                                    _p(query_seg), len(query_seg), _p(res), n_threads)
     return st, res

@@ -43,6 +43,16 @@ int main(int argc, char** argv)
   EXPECT(filter_bits_per_key(10) == 12);
   EXPECT(filter_bits_per_key(10, FilterKind::kBloom) == 10);
   EXPECT(vqf_filter_load_factor<8>(12) == 10.2 / 12.0);
+  // TreeOptions filter page sizing (host only): defaults -> 32 KiB pages, 32,704 payload bytes
+  {
+    TreeOptions t = TreeOptions::with_default_values();
+    EXPECT(t.leaf_size() == (u64{2} << 20) && t.leaf_data_size() == (usize{2} << 20) - 104);
+    EXPECT(t.expected_items_per_leaf() == 15767);
+    EXPECT(t.filter_page_size_log2() == 15 && t.filter_page_payload_size() == 32704);
+    EXPECT(TreeOptions{FilterKind::kBloom}.set_filter_bits_per_key(10).filter_bits_per_key() == 10);
+    EXPECT(TreeOptions{}.set_filter_bits_per_key(10).filter_bits_per_key() == 12);
+    EXPECT(default_filter_page_payload_size(12, FilterKind::kQuotient) == 32704);
+  }
 
   // build_filter_for_leaf_in_job, default kind = VQF (config.hpp:24)
   std::vector<u8> vqf_page;
@@ -155,6 +165,63 @@ int main(int argc, char** argv)
       EXPECT(build_filter_for_leaf_in_job_batched(bpk, 501, views[1], solo, 32768 - 64, kind).ok());
       EXPECT(solo == want[1]);
     }
+  }
+  // reject_page on a leaf whose hashes were truncated to fit the page (hash_val_shift > 0,
+  // filter_builder.hpp:277-290): no inserted key may be rejected (the shift must
+  // come from the page's hash_mask)
+  {
+    std::vector<u8> small;
+    EXPECT(build_quotient_filter_for_leaf(12, 9, items, small, 4096 - 64).ok());
+    PackedVqfFilter h;
+    std::memcpy(&h, small.data(), sizeof(h));
+    EXPECT(h.hash_mask == (~u64{0} << 1));
+    KeyQuery qt(items);
+    std::vector<BoolStatus> rt;
+    EXPECT(qt.reject_page(9, &small, FilterKind::kQuotient, rt).ok());
+    size_t rejected = 0;
+    for (auto v : rt) rejected += v == BoolStatus::kTrue;
+    EXPECT(rejected == 0);
+  }
+  // KeyQuery::Metrics (tree/key_query.hpp:36-60)
+  {
+    auto& m = KeyQuery::metrics();
+    const u64 t0 = m.total_filter_query_count.get(), r0 = m.filter_reject_count.get(),
+              p0 = m.filter_positive_count.get(), f0 = m.filter_false_positive_count.get(),
+              x0 = m.page_id_mismatch_count.get(), z0 = m.no_filter_page_count.get();
+    std::vector<u8> truth(miss.size(), 0);
+    EXPECT(qm.reject_page(7, &vqf_page, FilterKind::kQuotient, r, &truth).ok());
+    size_t rej = 0;
+    for (auto v : r) rej += v == BoolStatus::kTrue;
+    EXPECT(qm.reject_page(8, &vqf_page, FilterKind::kQuotient, r).ok());
+    EXPECT(qm.reject_page(7, nullptr, FilterKind::kQuotient, r).ok());
+    EXPECT(m.total_filter_query_count.get() - t0 == 3 * miss.size());
+    EXPECT(m.filter_reject_count.get() - r0 == rej);
+    EXPECT(m.filter_positive_count.get() - p0 == miss.size() - rej);
+    EXPECT(m.filter_false_positive_count.get() - f0 == miss.size() - rej);
+    EXPECT(m.page_id_mismatch_count.get() - x0 == miss.size());
+    EXPECT(m.no_filter_page_count.get() - z0 == miss.size());
+    EXPECT(m.filter_false_positive_rate() > 0);
+  }
+  // whole filter pages (tkv_amq_plan_pages): header fields the builders set, then the payload
+  {
+    FilterBatchBuilder b = FilterBatchBuilder::pages(FilterKind::kQuotient, 12, 15);
+    b.add_leaf(7, 4096);
+    EXPECT(b.plan().ok() && b.total_out_bytes() == 32768);
+    DeviceBuffer d_keys(4096 * 24), d_out(b.total_out_bytes());
+    std::string blob;
+    for (auto& k : keys) blob += k;
+    (void)hipMemcpy(d_keys.get(), blob.data(), blob.size(), hipMemcpyHostToDevice);
+    EXPECT(b.build_all(d_keys.get(), 24, nullptr, d_out.get()).ok());
+    EXPECT(b.check().ok());
+    std::vector<u8> page(32768);
+    (void)hipMemcpy(page.data(), d_out.get(), page.size(), hipMemcpyDeviceToHost);
+    EXPECT(std::memcmp(page.data() + 16, "vqf_filt", 8) == 0);
+    u32 ub, ue, sz;
+    std::memcpy(&ub, page.data() + 28, 4);
+    std::memcpy(&ue, page.data() + 32, 4);
+    std::memcpy(&sz, page.data() + 60, 4);
+    EXPECT(ub == 64 + want_vqf.size() && ue == 32768 && sz == 32768);
+    EXPECT(std::equal(want_vqf.begin(), want_vqf.end(), page.begin() + 64));
   }
   std::printf("%s (%d failures)\n", failures ? "FAIL" : "OK", failures);
   return failures ? 1 : 0;

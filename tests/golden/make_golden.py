@@ -7,6 +7,10 @@ Sources, in decreasing order of independence from this repo's code:
                       (tree/filter_builder.hpp:241-290, vqf_filter_page_view.hpp:39-59,
                       tree/tree_options.hpp:155-164) -- Python floats are IEEE doubles, so the
                       floor(n / load_factor) results are the reference's
+  page_sizing.json    the same pure-Python restatement of TreeOptions filter page sizing
+                      (tree/tree_options.hpp:177-258, tree_options.cpp:57-60,
+                      tree/packed_leaf_page.hpp:307-311, core/packed_sizeof_edit.hpp:13-15);
+                      sizeof(llfs::PackedArray<T>) = 8 is UNPINNED (llfs absent)
   workload_e_keys.txt the first 4096 distinct `user<20 digits>` keys of the reference's own
                       data/workloads/workload-e.txt (a data fixture, read once at generation
                       time; nothing reads /root/reference at test time)
@@ -124,6 +128,51 @@ def sizing():
     return {"vqf": vqf, "bloom": bloom, "clamp": clamp}
 
 
+# ---- TreeOptions filter page sizing, restated -------------------------------------------
+PAGE_HEADER, LEAF_HEADER, PACKED_ARRAY = 64, 32, 8   # llfs::PackedPageHeader, PackedLeafPage, PackedArray
+BLOOM_PAGE_HEADER, VQF_PAGE_HEADER = 64, 32 + 48     # tkv-amq v1 PackedBloomFilterPage; PackedVqfFilter
+
+
+def log2_ceil(x):
+    k = 0
+    while (1 << k) < x:
+        k += 1
+    return k
+
+
+def expected_items_per_leaf(leaf_size, key_hint, value_hint):
+    leaf_data = leaf_size - (PAGE_HEADER + LEAF_HEADER + PACKED_ARRAY)
+    return leaf_data // (4 + key_hint + 4 + 1 + value_hint)
+
+
+def filter_page_size_log2(kind, leaf_size, key_hint, value_hint, bpk_set):
+    bpk = bpk_set if kind == 0 else (0 if bpk_set == 0 else max(12, bpk_set))
+    items = expected_items_per_leaf(leaf_size, key_hint, value_hint)
+    if kind == 0:
+        bits = -(-(items * bpk) // 512) * 512
+        return log2_ceil(PAGE_HEADER + BLOOM_PAGE_HEADER + bits // 8)
+    if bpk == 0:
+        return 0
+    s8 = int(math.ceil(float(items) / load_factor(8, bpk)))
+    s16 = int(math.ceil(float(items) / load_factor(16, bpk)))
+    return log2_ceil(max(required_size(8, s8), required_size(16, s16)) + PAGE_HEADER + VQF_PAGE_HEADER)
+
+
+def page_sizing():
+    rows = []
+    for kind in (0, 1):
+        for leaf_log2 in (12, 16, 18, 20, 21, 22, 24, 26):
+            for kh, vh in ((24, 100), (16, 0), (8, 8), (64, 1000), (16, 16), (100, 4000)):
+                for b in (0, 1, 8, 10, 12, 13, 16, 22, 32):
+                    L = 1 << leaf_log2
+                    rows.append({"kind": kind, "leaf_size": L, "key_size_hint": kh,
+                                 "value_size_hint": vh, "bits_per_key": b,
+                                 "leaf_data_size": L - (PAGE_HEADER + LEAF_HEADER + PACKED_ARRAY),
+                                 "expected_items_per_leaf": expected_items_per_leaf(L, kh, vh),
+                                 "filter_page_size_log2": filter_page_size_log2(kind, L, kh, vh, b)})
+    return rows
+
+
 def segments(n_keys, seg=S):
     b = list(range(0, n_keys, seg)) + [n_keys]
     return np.array(b, dtype=np.uint64)
@@ -200,6 +249,8 @@ def main():
         json.dump(xxh_vectors(), f)
     with open(os.path.join(HERE, "sizing.json"), "w") as f:
         json.dump(sizing(), f)
+    with open(os.path.join(HERE, "page_sizing.json"), "w") as f:
+        json.dump(page_sizing(), f)
     with open(os.path.join(HERE, "filters.json"), "w") as f:
         json.dump(filter_digests(wkeys), f, indent=1)
     print("golden fixtures written to", HERE)

@@ -1,0 +1,108 @@
+"""bench.py end to end at small sizes: the multi-rank launcher (--gpus N without a launcher
+starts the ranks itself), the post-timing oracle checks of the timed output, the gathered
+array check, and the probe's full oracle comparison.  The GPU tests run bench.py as a child
+process on the one-GPU box (two gloo ranks share the device)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def run_bench(*args, env=None, timeout=400):
+    e = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        e.pop(k, None)
+    e.update(env or {})
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], capture_output=True,
+                       text=True, timeout=timeout, env=e, cwd=ROOT)
+    return r
+
+
+def last_json(r):
+    lines = [ln for ln in r.stdout.strip().splitlines() if ln.startswith("{")]
+    assert lines, r.stdout[-2000:] + r.stderr[-4000:]
+    return json.loads(lines[-1])
+
+
+def test_bench_refuses_world_mismatch():
+    """Under a launcher the world size must equal --gpus (a mislaunched scaling run must not
+    report n_gpus: 1)."""
+    r = run_bench("--gpus", "2", env={"WORLD_SIZE": "1"}, timeout=120)
+    assert r.returncode != 0
+    assert "--gpus 2 but WORLD_SIZE=1" in r.stderr
+
+
+SMALL = ["--steps", "3", "--warmup", "1", "--ramp-ms", "0", "--no-e2e", "--no-cpu-baseline"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("workload", ["bloom10", "vqf12"])
+def test_bench_two_ranks_gloo(workload):
+    """--gpus 2 with no launcher: two ranks (sharing the box's one GPU over gloo), n_gpus 2,
+    every rank's sampled leaves equal the oracle, and rank 0 finds the all-gathered array
+    equal to a single-process build of all leaves."""
+    r = run_bench("--gpus", "2", "--backend", "gloo", "--keys-per-gpu", "2000000",
+                  "--workload", workload, *SMALL)
+    assert r.returncode == 0, r.stderr[-4000:]
+    d = last_json(r)
+    assert d["n_gpus"] == 2 and d["scaling"] == "weak"
+    assert d["config"]["total_keys"] == 4_000_000
+    assert d["verified"] is True and d["verify"]["all_ranks_ok"] is True
+    assert d["gather_verified"] is True
+    assert d["allgather_ms"] > 0
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_nccl():
+    import torch
+    if torch.cuda.device_count() < 2:
+        pytest.skip("RCCL needs one GPU per rank")
+    r = run_bench("--gpus", "2", "--keys-per-gpu", "2000000", *SMALL)
+    assert r.returncode == 0, r.stderr[-4000:]
+    d = last_json(r)
+    assert d["n_gpus"] == 2 and d["gather_verified"] is True and d["verified"] is True
+
+
+@pytest.mark.gpu
+def test_bench_strong_scaling_two_ranks():
+    """--total-keys (config 5's form): one checkpoint split by leaf range; the last rank
+    holds fewer leaves, the gathered array still equals the single-process build."""
+    r = run_bench("--gpus", "2", "--backend", "gloo", "--workload", "bloom12",
+                  "--total-keys", "3000001", *SMALL)
+    assert r.returncode == 0, r.stderr[-4000:]
+    d = last_json(r)
+    assert d["scaling"] == "strong" and d["n_gpus"] == 2
+    assert d["gather_verified"] is True and d["verified"] is True
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("workload", ["probe10", "probe_vqf12"])
+def test_bench_probe_matches_oracle(workload):
+    """Config 4's check at a small size: every answer equals the oracle's over the GPU-built
+    filter, so the FPRs are equal; the probe line carries a CPU baseline."""
+    r = run_bench("--workload", workload, "--keys-per-gpu", "1000000", "--steps", "3",
+                  "--warmup", "1", "--ramp-ms", "0", "--no-e2e")
+    assert r.returncode == 0, r.stderr[-4000:]
+    d = last_json(r)
+    p = d["probe"]
+    assert p["results_equal_oracle"] is True and d["verified"] is True
+    assert p["fpr_oracle"] == p["false_positive_rate"]
+    assert d["cpu_baseline"] and d["cpu_baseline"]["value"] > 0
+
+
+@pytest.mark.gpu
+def test_bench_single_gpu_line():
+    """The default line's shape at a small size: verified sample, batch-size sweep, a CPU
+    baseline with the host's CPU share stated."""
+    r = run_bench("--keys-per-gpu", "3000000", "--steps", "3", "--warmup", "1", "--ramp-ms", "0",
+                  "--no-e2e")
+    assert r.returncode == 0, r.stderr[-4000:]
+    d = last_json(r)
+    assert d["n_gpus"] == 1 and d["verified"] is True
+    assert [row["leaves"] for row in d["batch_sweep"]] == [64, 256, 1024, 184]
+    b = d["cpu_baseline"]
+    assert b["cores"] >= 1 and "host" in b and b["value"] > 0

@@ -10,7 +10,8 @@ from .filters import (BoolStatus, FilterPage, FilterPlan, KeyBatch, KeyQuery, Pa
                       plan_filters, probe_filters, vqf_filter_load_factor, vqf_hash_val,
                       vqf_nslots_for_size, vqf_probe_hashed, vqf_required_size, key_views,
                       stage_keys, BloomFilterMetrics, QuotientFilterMetrics,
-                      plan_filter_stats, record_filter_metrics)
+                      plan_filter_stats, record_filter_metrics, TreeOptions, plan_filter_pages,
+                      page_header_fields, ProbeMetrics, KeyQueryMetrics)
 
 __all__ = [
     "abi", "BLOOM", "VQF", "TkvAmqError", "BoolStatus", "FilterPage", "FilterPlan", "KeyBatch",
@@ -20,4 +21,5 @@ __all__ = [
     "vqf_nslots_for_size", "vqf_probe_hashed", "vqf_required_size", "bloom_query_hashes",
     "bloom_probe_hashed", "HostFilterPipeline", "key_views", "stage_keys",
     "BloomFilterMetrics", "QuotientFilterMetrics", "plan_filter_stats", "record_filter_metrics",
+    "TreeOptions", "plan_filter_pages", "page_header_fields", "ProbeMetrics", "KeyQueryMetrics",
 ]

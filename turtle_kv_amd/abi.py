@@ -49,7 +49,7 @@ class Segment(ctypes.Structure):
         ("n_keys", ctypes.c_uint32),
         ("payload_bytes", ctypes.c_uint32),
         ("bits_per_key", ctypes.c_uint32),
-        ("reserved", ctypes.c_uint32),
+        ("page_flags", ctypes.c_uint32),
     ]
 
 
@@ -59,7 +59,20 @@ SEGMENT_DTYPE = np.dtype([
     ("out_offset", "<u8"), ("n_blocks", "<u4"), ("hash_count", "<u2"), ("tag_bits", "u1"),
     ("hash_val_shift", "u1"), ("mod_magic", "<u8"), ("key_begin", "<u8"), ("src_page_id", "<u8"),
     ("block_base", "<u8"), ("n_keys", "<u4"), ("payload_bytes", "<u4"), ("bits_per_key", "<u4"),
-    ("reserved", "<u4")])
+    ("page_flags", "<u4")])
+PAGE_IMAGE = 0x1  # TKV_AMQ_PAGE_IMAGE
+
+
+class ProbeOpts(ctypes.Structure):
+    """tkv_amq_probe_opts (device pointers, any may be NULL)."""
+    _fields_ = [("d_query_page_id", ctypes.c_void_p), ("d_truth", ctypes.c_void_p),
+                ("d_metrics", ctypes.c_void_p)]
+
+
+# tkv_amq_probe_metrics: KeyQuery::Metrics counters (tree/key_query.hpp:36-60), u64 each
+PROBE_METRICS_FIELDS = ("total_filter_query_count", "no_filter_page_count",
+                        "page_id_mismatch_count", "filter_reject_count", "filter_positive_count",
+                        "filter_false_positive_count")
 assert SEGMENT_DTYPE.itemsize == 64
 
 # every symbol include/tkv_amq.h declares
@@ -69,7 +82,9 @@ EXPORTS = [
     "tkv_amq_vqf_nslots_for_size", "tkv_amq_plan", "tkv_amq_build", "tkv_amq_build_check",
     "tkv_amq_probe", "tkv_amq_vqf_hash", "tkv_amq_vqf_probe_hashed", "tkv_amq_gen_keys16",
     "tkv_amq_bloom_query_stride", "tkv_amq_bloom_hash", "tkv_amq_bloom_probe_hashed",
-    "tkv_amq_stage_keys",
+    "tkv_amq_stage_keys", "tkv_amq_leaf_data_size", "tkv_amq_expected_items_per_leaf",
+    "tkv_amq_filter_page_size_log2", "tkv_amq_plan_pages", "tkv_amq_probe_ex",
+    "tkv_amq_vqf_probe_hashed_ex", "tkv_amq_bloom_probe_hashed_ex",
 ]
 
 # tkv_amq_key_view (libstdc++ std::string_view layout)
@@ -128,6 +143,22 @@ def lib(build_if_missing: bool = True):
     L.tkv_amq_gen_keys16.argtypes = [u64, u64, u64, vp, vp]
     L.tkv_amq_stage_keys.restype = i32
     L.tkv_amq_stage_keys.argtypes = [vp, u64, u64, u32, vp, u64, vp, i32]
+    L.tkv_amq_leaf_data_size.restype = u64
+    L.tkv_amq_leaf_data_size.argtypes = [u64]
+    L.tkv_amq_expected_items_per_leaf.restype = u64
+    L.tkv_amq_expected_items_per_leaf.argtypes = [u64, u32, u32]
+    L.tkv_amq_filter_page_size_log2.restype = u32
+    L.tkv_amq_filter_page_size_log2.argtypes = [i32, u64, u32, u32, u64]
+    L.tkv_amq_plan_pages.restype = i32
+    L.tkv_amq_plan_pages.argtypes = [i32, vp, vp, u32, u32, u32, vp,
+                                     ctypes.POINTER(u64), ctypes.POINTER(u64), ctypes.POINTER(u32)]
+    popts = ctypes.POINTER(ProbeOpts)
+    L.tkv_amq_probe_ex.restype = i32
+    L.tkv_amq_probe_ex.argtypes = [i32, vp, vp, u32, vp, vp, u32, u64, vp, vp, popts, vp]
+    L.tkv_amq_vqf_probe_hashed_ex.restype = i32
+    L.tkv_amq_vqf_probe_hashed_ex.argtypes = [vp, vp, u32, vp, vp, u64, vp, vp, popts, vp]
+    L.tkv_amq_bloom_probe_hashed_ex.restype = i32
+    L.tkv_amq_bloom_probe_hashed_ex.argtypes = [vp, vp, u32, vp, u32, vp, u64, vp, vp, popts, vp]
     _lib = L
     return L
 

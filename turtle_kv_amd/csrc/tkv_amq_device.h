@@ -28,6 +28,12 @@ constexpr uint32_t kBloomHeader = 64;
 constexpr uint32_t kVqfHeader = 32;   // sizeof(PackedVqfFilter) - sizeof(vqf_metadata)
 constexpr uint32_t kVqfMetadata = 48; // sizeof(vqf_metadata)
 constexpr uint32_t kMaxBloomHashes = 32;
+// page framing (TreeOptions sizing, tree/tree_options.hpp:177-258; filter page image):
+constexpr uint64_t kPackedPageHeaderBytes = 64;  // sizeof(llfs::PackedPageHeader), pinned by
+                                                 // tree/packed_node_page.hpp:472
+constexpr uint64_t kPackedLeafPageBytes = 32;    // sizeof(PackedLeafPage), packed_leaf_page.hpp:303
+constexpr uint64_t kPackedArrayBytes = 8;        // sizeof(llfs::PackedArray<T>): UNPINNED (llfs
+                                                 // absent; u32 item_count + 4 reserved bytes)
 
 __host__ __device__ constexpr inline uint64_t rotl64(uint64_t x, int r)
 {

@@ -155,6 +155,34 @@ __device__ inline void write_bloom_header(uint8_t* payload, const tkv_amq_segmen
   reinterpret_cast<ulonglong2*>(payload)[part] = v;
 }
 
+// The llfs PackedPageHeader fields the filter builders set, for segments planned by
+// tkv_amq_plan_pages (page_flags & TKV_AMQ_PAGE_IMAGE): layout_id @16 (filter_builder.hpp:237),
+// unused_begin @28 = 64 + payload bytes and unused_end @32 = page size (:293-296), size @60.
+// The PageCache's own fields (magic, page_id, crc32, user slot) are written as 0.  Offsets
+// follow llfs 0.42's PackedPageHeader and are UNPINNED (llfs is absent).
+// part = 0..3: one 16-byte piece each.
+constexpr uint64_t kLayoutVqf = 0x746c69665f667176ull;    // "vqf_filt" (vqf_filter_page_view.hpp:142)
+constexpr uint64_t kLayoutBloom = 0x746c666d6f6f6c62ull;  // "bloomflt" (tkv-amq v1; llfs's unpinned)
+
+__device__ inline void write_page_header(uint8_t* out, const tkv_amq_segment& sg, uint64_t layout,
+                                         uint32_t part)
+{
+  if (!(sg.page_flags & TKV_AMQ_PAGE_IMAGE)) return;
+  uint8_t* page = out + sg.out_offset - kPackedPageHeaderBytes;
+  const uint32_t size = 1u << ((sg.page_flags >> 8) & 31u);
+  uint4 v = {0, 0, 0, 0};
+  if (part == 1) {
+    v.x = (uint32_t)layout;
+    v.y = (uint32_t)(layout >> 32);
+    v.w = (uint32_t)kPackedPageHeaderBytes + sg.payload_bytes;  // unused_begin
+  } else if (part == 2) {
+    v.x = size;  // unused_end
+  } else if (part == 3) {
+    v.w = size;  // size
+  }
+  reinterpret_cast<uint4*>(page)[part] = v;
+}
+
 // `first`: block index of s_bits[0] (0 for a whole leaf image; a tile's first block for the
 // monolithic build's tile images)
 template <int K>
@@ -274,6 +302,7 @@ __global__ __launch_bounds__(256) void bloom_build_lds(const uint8_t* __restrict
 
   uint8_t* payload = out + sg.out_offset;
   if (tid < 4) write_bloom_header(payload, sg, tid);
+  else if (tid < 8) write_page_header(out, sg, kLayoutBloom, tid - 4);
   uint4* dst = reinterpret_cast<uint4*>(payload + kBloomHeader);
   const uint4* src = reinterpret_cast<const uint4*>(s_bits);
   for (uint32_t q = tid; q < nb * 4; q += 256) dst[q] = src[q];
@@ -291,6 +320,7 @@ __global__ __launch_bounds__(256) void bloom_global_init(const tkv_amq_segment* 
   uint8_t* payload = out + sg.out_offset;
   const uint32_t tid = threadIdx.x;
   if (tid < 4) write_bloom_header(payload, sg, tid);
+  else if (tid < 8) write_page_header(out, sg, kLayoutBloom, tid - 4);
   uint4* dst = reinterpret_cast<uint4*>(payload + kBloomHeader);
   const uint4 z = {0, 0, 0, 0};
   for (uint64_t q = tid; q < 4ull * sg.n_blocks; q += 256) dst[q] = z;
@@ -378,9 +408,7 @@ constexpr uint32_t kStageKeys = 4;
 constexpr uint32_t kStageThreads = 1024;
 constexpr uint32_t kStageMaxWgs = 256;
 constexpr uint32_t kStageMaxTiles = 2048;  // 2048 x (64 + 8) B = 144 KiB of LDS
-#ifndef TKV_STAGE_R
-#define TKV_STAGE_R 2  // keys staged per thread per round
-#endif
+constexpr uint32_t kStageRound = 2;        // keys staged per thread per round
 
 __host__ __device__ constexpr inline uint32_t bloom_stage_lds_bytes(uint32_t n_tiles)
 {
@@ -498,7 +526,7 @@ __global__ __launch_bounds__(kStageThreads) void bloom_part_scatter_staged(
   const uint4* kp = keys + sg.key_begin;
   uint4* part = reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(ws) + part_off);
   // each round, every thread stages kR keys (prefetched one round ahead)
-  constexpr uint32_t kR = TKV_STAGE_R;
+  constexpr uint32_t kR = kStageRound;
   constexpr uint32_t kRound = kR * kStageThreads;
   uint4 ring[kR];
 #pragma unroll
@@ -655,6 +683,7 @@ __global__ __launch_bounds__(NT) void bloom_tile_build(
   __syncthreads();
   uint8_t* payload = out + sg.out_offset;
   if (t == 0 && tid < 4) write_bloom_header(payload, sg, tid);
+  else if (t == 0 && tid < 8) write_page_header(out, sg, kLayoutBloom, tid - 4);
   uint4* dst = reinterpret_cast<uint4*>(payload + kBloomHeader + 64ull * first);
   const uint4* src = reinterpret_cast<const uint4*>(s_bits);
   for (uint32_t q = tid; q < tb * 4; q += NT) dst[q] = src[q];
@@ -691,10 +720,6 @@ __device__ inline ProbeDesc load_probe_desc(const tkv_amq_segment* segs, uint32_
 // are then LDS reads.  Stride 20 dwords keeps the slots 16-byte aligned and spreads banks.
 constexpr uint32_t kProbeSlotWords = 20;
 
-#ifndef TKV_EXP
-#define TKV_EXP 0  // kernel experiments only (tools/exp_variants.sh); 0 = the product build
-#endif
-
 // The block's four 16-byte loads are issued first and the remaining k-1 bit indices are
 // hashed while they are in flight; only then is the block staged in the lane's LDS slot.
 template <int K>
@@ -730,19 +755,68 @@ __device__ inline uint32_t probe_block16(const Xxh16& x, uint64_t h0, const uint
   return ok;
 }
 
-template <int MODE>
-__global__ __launch_bounds__(256) void bloom_probe(const uint8_t* __restrict__ filters,
-                                                   const tkv_amq_segment* __restrict__ segs, uint32_t n_segs,
-                                                   const uint8_t* __restrict__ q,
-                                                   const uint64_t* __restrict__ qoffs,
-                                                   uint32_t stride, uint64_t n,
-                                                   const uint32_t* __restrict__ qseg,
-                                                   uint8_t* __restrict__ result)
+// KeyQuery::Metrics tallies of one lane (tkv_amq_probe_ex): per query, the class of its
+// reject_page answer (tree/key_query.hpp:149-247).  Reduced over the wave with shuffles and
+// added to the caller's counters with one atomic per counter per wave.
+enum ProbeClass : uint32_t { kNoFilter = 0, kIdMismatch = 1, kChecked = 2 };
+
+struct ProbeTally {
+  uint32_t total = 0, no_filter = 0, mismatch = 0, reject = 0, positive = 0, false_pos = 0;
+  // r: result bit (1 = maybe present) | class << 1
+  __device__ inline void add(uint32_t r, const uint8_t* truth, uint64_t i)
+  {
+    const uint32_t cls = r >> 1;
+    ++total;
+    no_filter += cls == kNoFilter;
+    mismatch += cls == kIdMismatch;
+    const bool checked = cls == kChecked;
+    reject += checked && !(r & 1u);
+    const bool pos = checked && (r & 1u);
+    positive += pos;
+    if (pos && truth) false_pos += truth[i] == 0;
+  }
+};
+
+__device__ inline uint32_t wave_sum(uint32_t v)
 {
-  __shared__ uint4 s_blk[256 * kProbeSlotWords / 4];
-  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= n) return;
-  const uint32_t sidx = __builtin_nontemporal_load(qseg + i);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ inline void flush_tally(const ProbeTally& t, tkv_amq_probe_metrics* m, bool has_truth)
+{
+  const uint32_t v[6] = {wave_sum(t.total), wave_sum(t.no_filter), wave_sum(t.mismatch),
+                         wave_sum(t.reject), wave_sum(t.positive), wave_sum(t.false_pos)};
+  if (__lane_id() == 0 && m) {
+    unsigned long long* c = reinterpret_cast<unsigned long long*>(m);
+    if (v[0]) atomicAdd(&c[0], (unsigned long long)v[0]);
+    if (v[1]) atomicAdd(&c[1], (unsigned long long)v[1]);
+    if (v[2]) atomicAdd(&c[2], (unsigned long long)v[2]);
+    if (v[3]) atomicAdd(&c[3], (unsigned long long)v[3]);
+    if (v[4]) atomicAdd(&c[4], (unsigned long long)v[4]);
+    if (has_truth && v[5]) atomicAdd(&c[5], (unsigned long long)v[5]);
+  }
+}
+
+// filter header's src_page_id (PackedBloomFilterPage / PackedVqfFilter) vs the leaf the query
+// asks about (reject_page, tree/key_query.hpp:205-212,227-232): the filter bytes decide, as in
+// the reference
+__device__ inline bool page_id_matches(const uint8_t* payload, uint32_t id_off, const uint64_t* ids,
+                                       uint64_t i)
+{
+  return ids == nullptr || *reinterpret_cast<const uint64_t*>(payload + id_off) == ids[i];
+}
+
+// One Bloom (query, leaf) test: result bit | class << 1.
+template <int MODE>
+__device__ inline uint32_t bloom_probe_item(const uint8_t* __restrict__ filters,
+                                            const tkv_amq_segment* __restrict__ segs, uint32_t n_segs,
+                                            const uint8_t* __restrict__ q,
+                                            const uint64_t* __restrict__ qoffs, uint32_t stride,
+                                            uint64_t i, uint32_t sidx, uint4* slot,
+                                            const uint64_t* page_ids)
+{
   uint32_t ok = 1;
   if constexpr (MODE == kKey16) {
     // the key load, the descriptor and the first hash do not depend on the "has a filter"
@@ -753,40 +827,72 @@ __global__ __launch_bounds__(256) void bloom_probe(const uint8_t* __restrict__ f
     const uint64_t h0 = x.finish(c_bloom.rhinit16[0]);
     const uint4* blk = reinterpret_cast<const uint4*>(filters + d.out_offset + kBloomHeader +
                                                       64 * __umul64hi(h0, (uint64_t)d.n_blocks));
-    uint4* slot = s_blk + threadIdx.x * (kProbeSlotWords / 4);
     // hash_count 0: no filter page => reject_page returns kUnknown => cannot reject
+    if (d.hash_count == 0) return 1u | (kNoFilter << 1);
+    if (!page_id_matches(filters + d.out_offset, 16, page_ids, i)) return 1u | (kIdMismatch << 1);
     if (d.hash_count == 7) ok = probe_block16<7>(x, h0, blk, slot);
     else if (d.hash_count == 8) ok = probe_block16<8>(x, h0, blk, slot);
-    else if (d.hash_count != 0) ok = probe_block16<0>(x, h0, blk, slot, d.hash_count);
+    else ok = probe_block16<0>(x, h0, blk, slot, d.hash_count);
   } else {
     const ProbeDesc d = load_probe_desc(segs, sidx, n_segs);
-    if (d.hash_count != 0) {
-      const uint8_t* words = filters + d.out_offset + kBloomHeader;
-      uint32_t len;
-      const uint8_t* p = key_at<MODE>(q, qoffs, stride, i, len);
-      if (len < 32) {  // seed-independent lane rounds shared by the k hashes
-        const XxhShort x(p, len);
-        const uint64_t h0 = x.finish(c_bloom.seed_p5[0]);
-        const uint64_t* blk = reinterpret_cast<const uint64_t*>(words + 64 * __umul64hi(h0, (uint64_t)d.n_blocks));
-        uint32_t b = (uint32_t)h0 & 511u;
+    if (d.hash_count == 0) return 1u | (kNoFilter << 1);
+    if (!page_id_matches(filters + d.out_offset, 16, page_ids, i)) return 1u | (kIdMismatch << 1);
+    const uint8_t* words = filters + d.out_offset + kBloomHeader;
+    uint32_t len;
+    const uint8_t* p = key_at<MODE>(q, qoffs, stride, i, len);
+    if (len < 32) {  // seed-independent lane rounds shared by the k hashes
+      const XxhShort x(p, len);
+      const uint64_t h0 = x.finish(c_bloom.seed_p5[0]);
+      const uint64_t* blk = reinterpret_cast<const uint64_t*>(words + 64 * __umul64hi(h0, (uint64_t)d.n_blocks));
+      uint32_t b = (uint32_t)h0 & 511u;
+      ok &= (uint32_t)(blk[b >> 6] >> (b & 63));
+      for (uint32_t j = 1; j < d.hash_count; ++j) {
+        b = x.finish_lo9(c_bloom.seed_p5[j]) & 511u;
         ok &= (uint32_t)(blk[b >> 6] >> (b & 63));
-        for (uint32_t j = 1; j < d.hash_count; ++j) {
-          b = x.finish_lo9(c_bloom.seed_p5[j]) & 511u;
-          ok &= (uint32_t)(blk[b >> 6] >> (b & 63));
-        }
-      } else {
-        const uint64_t h0 = xxh64_bytes(p, len, c_bloom.seed[0]);
-        const uint64_t* blk = reinterpret_cast<const uint64_t*>(words + 64 * __umul64hi(h0, (uint64_t)d.n_blocks));
-        uint32_t b = (uint32_t)h0 & 511u;
+      }
+    } else {
+      const uint64_t h0 = xxh64_bytes(p, len, c_bloom.seed[0]);
+      const uint64_t* blk = reinterpret_cast<const uint64_t*>(words + 64 * __umul64hi(h0, (uint64_t)d.n_blocks));
+      uint32_t b = (uint32_t)h0 & 511u;
+      ok &= (uint32_t)(blk[b >> 6] >> (b & 63));
+      for (uint32_t j = 1; j < d.hash_count; ++j) {
+        b = (uint32_t)xxh64_bytes(p, len, c_bloom.seed[j]) & 511u;
         ok &= (uint32_t)(blk[b >> 6] >> (b & 63));
-        for (uint32_t j = 1; j < d.hash_count; ++j) {
-          b = (uint32_t)xxh64_bytes(p, len, c_bloom.seed[j]) & 511u;
-          ok &= (uint32_t)(blk[b >> 6] >> (b & 63));
-        }
       }
     }
   }
-  __builtin_nontemporal_store((uint8_t)(ok & 1u), result + i);
+  return (ok & 1u) | (kChecked << 1);
+}
+
+// kOpts = false: one lane per query (the plain probe).  kOpts = true (tkv_amq_probe_ex): a
+// grid-stride loop over a bounded grid with the page-id check and the metrics tallies.
+template <int MODE, bool kOpts>
+__global__ __launch_bounds__(256) void bloom_probe(const uint8_t* __restrict__ filters,
+                                                   const tkv_amq_segment* __restrict__ segs, uint32_t n_segs,
+                                                   const uint8_t* __restrict__ q,
+                                                   const uint64_t* __restrict__ qoffs,
+                                                   uint32_t stride, uint64_t n,
+                                                   const uint32_t* __restrict__ qseg,
+                                                   uint8_t* __restrict__ result, tkv_amq_probe_opts opts)
+{
+  __shared__ uint4 s_blk[256 * kProbeSlotWords / 4];
+  uint4* slot = s_blk + threadIdx.x * (kProbeSlotWords / 4);
+  if constexpr (!kOpts) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t r = bloom_probe_item<MODE>(filters, segs, n_segs, q, qoffs, stride, i,
+                                              __builtin_nontemporal_load(qseg + i), slot, nullptr);
+    __builtin_nontemporal_store((uint8_t)(r & 1u), result + i);
+  } else {
+    ProbeTally t;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+      const uint32_t r = bloom_probe_item<MODE>(filters, segs, n_segs, q, qoffs, stride, i, qseg[i],
+                                                slot, opts.d_query_page_id);
+      result[i] = (uint8_t)(r & 1u);
+      t.add(r, opts.d_truth, i);
+    }
+    flush_tally(t, opts.d_metrics, opts.d_truth != nullptr);
+  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -846,6 +952,23 @@ __device__ inline uint64_t* vqf_records(VqfWorkspace ws, const tkv_amq_segment* 
 {
   const tkv_amq_segment& last = segs[n_segs - 1];
   return reinterpret_cast<uint64_t*>(ws.temp + kVqfTempStride * (last.block_base + last.n_blocks));
+}
+
+// Bytes of workspace the plan's VQF kernels touch (tkv_amq_plan's workspace_bytes minus the
+// tail pad).  Every VQF kernel checks it against the size the caller passed and, if the
+// workspace is too small, records kVqfStatusWorkspace and writes nothing else.
+constexpr uint32_t kVqfStatusOverflow = 1u;   // a block overflowed (vqf_insert failed)
+constexpr uint32_t kVqfStatusWorkspace = 2u;  // workspace smaller than the plan needs
+
+__device__ inline bool vqf_ws_ok(const tkv_amq_segment* segs, uint32_t n_segs, uint64_t ws_bytes,
+                                 VqfWorkspace ws)
+{
+  const tkv_amq_segment& last = segs[n_segs - 1];
+  const uint64_t need = vqf_temp_offset(n_segs) + kVqfTempStride * (last.block_base + last.n_blocks) +
+                        8 * (last.key_begin + last.n_keys);
+  if (need <= ws_bytes) return true;
+  if (threadIdx.x == 0) atomicOr(ws.status, kVqfStatusWorkspace);
+  return false;
 }
 
 __device__ inline uint32_t& vqf_count(VqfWorkspace ws, uint64_t block)
@@ -967,19 +1090,9 @@ __device__ void vqf_decide_body(const uint8_t* __restrict__ keys, const uint64_t
     if constexpr (MODE == kKey16) {
       // branch-free (clamped index, select on the result): straight-line code lets the
       // compiler count vmcnt exactly instead of draining every outstanding access
-#if TKV_EXP == 2
-      kv_load = make_uint4(inext * 0x9e3779b9u, inext ^ sg.key_begin, inext + 77u, (uint32_t)sg.key_begin);
-#else
       kv_load = kp[min(inext + 64, n - 1)];
-#endif
-#if TKV_EXP != 1
       if (pend) *pend_ptr = pend_val;
-#endif
-#if TKV_EXP == 5
-      const uint64_t hh = ((uint64_t)kv_hash.x << 32 | kv_hash.y) * 0x9e3779b97f4a7c15ull ^ kv_hash.z;
-#else
       const uint64_t hh = vqf_key_hash<MODE>(keys, offs, stride, 0, kv_hash);
-#endif
       hn = vnext ? hh : 0;
     } else {
       if (pend) *pend_ptr = pend_val;
@@ -1051,7 +1164,7 @@ __device__ void vqf_decide_body(const uint8_t* __restrict__ keys, const uint64_t
       // popcounts.
       uint64_t U = __ballot(L.kept && pb != ab);  // blocks differ (vqf_insert alt test)
       uint64_t F = __ballot((cp >= C::kThreshold) & (ca < cp)) & U;
-      if (TKV_EXP != 4 && F != 0) {
+      if (F != 0) {
         // lanes whose alternate block is my primary / my alternate
         uint32_t map_lo = (uint32_t)keptmask, map_hi = (uint32_t)(keptmask >> 32);
         uint32_t maa_lo = map_lo, maa_hi = map_hi;
@@ -1140,7 +1253,7 @@ __device__ void vqf_decide_body(const uint8_t* __restrict__ keys, const uint64_t
   }
   if (lane == 0) {
     ws.nelts[seg_index] = nelts;
-    if (fail) atomicOr(ws.status, 1u);
+    if (fail) atomicOr(ws.status, kVqfStatusOverflow);
   }
 }
 
@@ -1169,12 +1282,14 @@ template <int MODE>
 __global__ __launch_bounds__(64) void vqf_decide(const uint8_t* __restrict__ keys,
                                                  const uint64_t* __restrict__ offs, uint32_t stride,
                                                  const tkv_amq_segment* __restrict__ segs,
-                                                 void* ws_base, uint32_t n_segs, int flags)
+                                                 void* ws_base, uint64_t ws_bytes, uint32_t n_segs,
+                                                 int flags)
 {
   const bool match_lds = flags & 1, compact_ok = flags & 2;
   extern __shared__ __attribute__((aligned(16))) uint32_t s_cnt[];
   const tkv_amq_segment sg = segs[blockIdx.x];
   const VqfWorkspace ws = vqf_workspace(ws_base, n_segs);
+  if (!vqf_ws_ok(segs, n_segs, ws_bytes, ws)) return;
   uint64_t* recs = vqf_records(ws, segs, n_segs);
   if (sg.tag_bits == 8)
     vqf_decide_dispatch<8, MODE>(keys, offs, stride, sg, blockIdx.x, ws, recs, s_cnt, match_lds, compact_ok);
@@ -1185,12 +1300,14 @@ __global__ __launch_bounds__(64) void vqf_decide(const uint8_t* __restrict__ key
 // One thread per key: moves the key's entry from its coalesced placement record into the
 // block record (insertion rank = slot).  Fully parallel, so the partial-line writes overlap.
 __global__ __launch_bounds__(256) void vqf_scatter(const tkv_amq_segment* __restrict__ segs,
-                                                   void* ws_base, uint32_t n_segs, uint64_t n_keys)
+                                                   void* ws_base, uint64_t ws_bytes, uint32_t n_segs,
+                                                   uint64_t n_keys)
 {
   const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   const tkv_amq_segment& last = segs[n_segs - 1];
-  if (i >= n_keys || i >= last.key_begin + last.n_keys) return;
   const VqfWorkspace ws = vqf_workspace(ws_base, n_segs);
+  if (!vqf_ws_ok(segs, n_segs, ws_bytes, ws)) return;
+  if (i >= n_keys || i >= last.key_begin + last.n_keys) return;
   const uint64_t r = __builtin_nontemporal_load(vqf_records(ws, segs, n_segs) + i);
   const uint32_t hi = (uint32_t)(r >> 32), lo = (uint32_t)r;
   if (hi == 0xffffffffu) return;
@@ -1235,6 +1352,8 @@ __device__ void vqf_place_body(const tkv_amq_segment& sg, uint32_t seg_index, Vq
     v.x = w0;
     v.y = w1;
     reinterpret_cast<ulonglong2*>(payload)[tid] = v;
+  } else if (tid < 9) {
+    write_page_header(out, sg, kLayoutVqf, tid - 5);
   }
 
   uint32_t* cnt = s_cnt + tid * kCntStride;
@@ -1323,13 +1442,14 @@ __device__ void vqf_place_body(const tkv_amq_segment& sg, uint32_t seg_index, Vq
 }
 
 __global__ __launch_bounds__(kPlaceThreads) void vqf_place(const tkv_amq_segment* __restrict__ segs,
-                                                           void* ws_base, uint32_t n_segs,
-                                                           uint8_t* __restrict__ out)
+                                                           void* ws_base, uint64_t ws_bytes,
+                                                           uint32_t n_segs, uint8_t* __restrict__ out)
 {
   __shared__ uint32_t s_cnt[kPlaceThreads * 21];
   __shared__ uint32_t s_img[kPlaceThreads * 17];
   const tkv_amq_segment sg = segs[blockIdx.x];
   const VqfWorkspace ws = vqf_workspace(ws_base, n_segs);
+  if (!vqf_ws_ok(segs, n_segs, ws_bytes, ws)) return;
   if (sg.tag_bits == 8) vqf_place_body<8>(sg, blockIdx.x, ws, out, s_cnt, s_img);
   else if (sg.tag_bits == 16) vqf_place_body<16>(sg, blockIdx.x, ws, out, s_cnt, s_img);
 }
@@ -1397,6 +1517,8 @@ __device__ void vqf_place_fused_sort(const tkv_amq_segment& sg, uint32_t seg_ind
     v.x = w0;
     v.y = w1;
     reinterpret_cast<ulonglong2*>(payload)[tid] = v;
+  } else if (tid < 9) {
+    write_page_header(out, sg, kLayoutVqf, tid - 5);
   }
   uint4* dst_blocks = reinterpret_cast<uint4*>(payload + kVqfHeader + kVqfMetadata);
 
@@ -1595,16 +1717,18 @@ __device__ void vqf_place_fused_body(const tkv_amq_segment& sg, uint32_t seg_ind
     }
   }
   __syncthreads();
-  if (TKV_EXP != 6) vqf_place_fused_sort<T, 1>(sg, seg_index, ws, out, lds);
+  vqf_place_fused_sort<T, 1>(sg, seg_index, ws, out, lds);
 }
 
 __global__ __launch_bounds__(kFusedThreads) void vqf_place_fused(const tkv_amq_segment* __restrict__ segs,
-                                                                 void* ws_base, uint32_t n_segs,
+                                                                 void* ws_base, uint64_t ws_bytes,
+                                                                 uint32_t n_segs,
                                                                  uint8_t* __restrict__ out)
 {
   extern __shared__ __attribute__((aligned(16))) uint32_t s_lds[];
   const tkv_amq_segment sg = segs[blockIdx.x];
   const VqfWorkspace ws = vqf_workspace(ws_base, n_segs);
+  if (!vqf_ws_ok(segs, n_segs, ws_bytes, ws)) return;
   const uint64_t* recs = vqf_records(ws, segs, n_segs);
   if (sg.tag_bits == 8) vqf_place_fused_body<8>(sg, blockIdx.x, ws, recs, out, s_lds);
   else if (sg.tag_bits == 16) vqf_place_fused_body<16>(sg, blockIdx.x, ws, recs, out, s_lds);
@@ -1706,66 +1830,89 @@ __device__ inline bool vqf_present(const uint8_t* payload, uint32_t n_blocks, ui
   const uint32_t pi = (uint32_t)mod_by_magic(h >> T, R, magic);
   const uint32_t ai = (uint32_t)mod_by_magic((h ^ ((uint64_t)tag * kVqfAltMul)) >> T, R, magic);
   const uint8_t* blocks = payload + kVqfHeader + kVqfMetadata;
-#if TKV_VQF_PROBE_BOTH
-  // both blocks' metadata loads are issued before either bucket is scanned (the reference's
-  // primary-then-alternate order only matters for the answer, which is an OR)
-  const VqfBucketRef<T> rp = vqf_bucket_ref<T>(blocks, pi);
-  const VqfBucketRef<T> ra = vqf_bucket_ref<T>(blocks, ai);
-  return (int)vqf_bucket_has<T>(rp, tag) | (int)vqf_bucket_has<T>(ra, tag);
-#else
   // primary bucket first; only the lanes that did not find the tag there read the alternate
-  // block (vqf_is_present's order, vqf_filter_page_view.hpp:120-124)
+  // block (vqf_is_present's order, vqf_filter_page_view.hpp:120-124; loading both blocks up
+  // front measured slower)
   if (vqf_bucket_has<T>(vqf_bucket_ref<T>(blocks, pi), tag)) return true;
   return vqf_bucket_has<T>(vqf_bucket_ref<T>(blocks, ai), tag);
-#endif
 }
 
-__device__ inline uint8_t vqf_probe_one(const uint8_t* filters, const tkv_amq_segment* segs,
-                                        uint32_t n_segs, uint32_t s, uint64_t h)
+// One VQF (hash, leaf) test: result bit | class << 1.
+__device__ inline uint32_t vqf_probe_one(const uint8_t* filters, const tkv_amq_segment* segs,
+                                         uint32_t n_segs, uint32_t s, uint64_t h,
+                                         const uint64_t* page_ids = nullptr, uint64_t i = 0)
 {
   const ProbeDesc d = load_probe_desc(segs, s, n_segs);
-  if (d.tag_bits == 0) return 1;  // no filter: cannot reject
+  if (d.tag_bits == 0) return 1u | (kNoFilter << 1);  // no filter: cannot reject
   const uint8_t* payload = filters + d.out_offset;
+  if (!page_id_matches(payload, 8, page_ids, i)) return 1u | (kIdMismatch << 1);
   const uint64_t mask = ~0ull << d.hash_val_shift;  // == PackedVqfFilter::hash_mask
-  if ((h & mask) != h) return 1;  // dropped hash values are always "maybe" (:115-117)
+  // dropped hash values are always "maybe" (:115-117)
+  if ((h & mask) != h) return 1u | (kChecked << 1);
   const uint64_t magic = segs[s].mod_magic;
-  return d.tag_bits == 8 ? (uint8_t)vqf_present<8>(payload, d.n_blocks, magic, h)
-                         : (uint8_t)vqf_present<16>(payload, d.n_blocks, magic, h);
+  const bool p = d.tag_bits == 8 ? vqf_present<8>(payload, d.n_blocks, magic, h)
+                                 : vqf_present<16>(payload, d.n_blocks, magic, h);
+  return (uint32_t)p | (kChecked << 1);
 }
 
 template <int MODE>
+__device__ inline uint64_t vqf_query_hash(const uint8_t* __restrict__ q, const uint64_t* __restrict__ qoffs,
+                                          uint32_t stride, uint64_t i)
+{
+  if constexpr (MODE == kKey16) {
+    const uint4 kv = load_nt16(q + 16 * i);
+    const Xxh16 x((uint64_t)kv.x | ((uint64_t)kv.y << 32), (uint64_t)kv.z | ((uint64_t)kv.w << 32));
+    return x.finish(xxh16_rhinit(kVqfHashSeed));
+  } else {
+    return hash_key<MODE>(q, qoffs, stride, i, kVqfHashSeed);
+  }
+}
+
+template <int MODE, bool kOpts>
 __global__ __launch_bounds__(256) void vqf_probe(const uint8_t* __restrict__ filters,
                                                  const tkv_amq_segment* __restrict__ segs, uint32_t n_segs,
                                                  const uint8_t* __restrict__ q,
                                                  const uint64_t* __restrict__ qoffs, uint32_t stride,
                                                  uint64_t n, const uint32_t* __restrict__ qseg,
-                                                 uint8_t* __restrict__ result)
+                                                 uint8_t* __restrict__ result, tkv_amq_probe_opts opts)
 {
-  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= n) return;
-  uint64_t h;
-  if constexpr (MODE == kKey16) {
-    const uint4 kv = load_nt16(q + 16 * i);
-    const Xxh16 x((uint64_t)kv.x | ((uint64_t)kv.y << 32), (uint64_t)kv.z | ((uint64_t)kv.w << 32));
-    h = x.finish(xxh16_rhinit(kVqfHashSeed));
+  if constexpr (!kOpts) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t h = vqf_query_hash<MODE>(q, qoffs, stride, i);
+    __builtin_nontemporal_store(
+        (uint8_t)(vqf_probe_one(filters, segs, n_segs, __builtin_nontemporal_load(qseg + i), h) & 1u),
+        result + i);
   } else {
-    h = hash_key<MODE>(q, qoffs, stride, i, kVqfHashSeed);
+    ProbeTally t;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+      const uint32_t r = vqf_probe_one(filters, segs, n_segs, qseg[i],
+                                       vqf_query_hash<MODE>(q, qoffs, stride, i), opts.d_query_page_id, i);
+      result[i] = (uint8_t)(r & 1u);
+      t.add(r, opts.d_truth, i);
+    }
+    flush_tally(t, opts.d_metrics, opts.d_truth != nullptr);
   }
-  __builtin_nontemporal_store(vqf_probe_one(filters, segs, n_segs, __builtin_nontemporal_load(qseg + i), h),
-                              result + i);
 }
 
+template <bool kOpts>
 __global__ __launch_bounds__(256) void vqf_probe_hashed(const uint8_t* __restrict__ filters,
                                                         const tkv_amq_segment* __restrict__ segs, uint32_t n_segs,
                                                         const uint64_t* __restrict__ hashes,
                                                         const uint32_t* __restrict__ pair_query,
                                                         uint64_t n, const uint32_t* __restrict__ qseg,
-                                                        uint8_t* __restrict__ result)
+                                                        uint8_t* __restrict__ result, tkv_amq_probe_opts opts)
 {
-  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= n) return;
-  const uint64_t qi = pair_query ? pair_query[i] : i;
-  result[i] = vqf_probe_one(filters, segs, n_segs, qseg[i], hashes[qi]);
+  ProbeTally t;
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+    const uint64_t qi = pair_query ? pair_query[i] : i;
+    const uint32_t r = vqf_probe_one(filters, segs, n_segs, qseg[i], hashes[qi],
+                                     kOpts ? opts.d_query_page_id : nullptr, i);
+    result[i] = (uint8_t)(r & 1u);
+    if constexpr (kOpts) t.add(r, opts.d_truth, i);
+    else break;
+  }
+  if constexpr (kOpts) flush_tally(t, opts.d_metrics, opts.d_truth != nullptr);
 }
 
 // ---- Bloom query hash cache (BloomFilterQuery<KeyView>) ----
@@ -1804,44 +1951,55 @@ __global__ __launch_bounds__(256) void bloom_hash_kernel(const uint8_t* __restri
   }
 }
 
+template <bool kOpts>
 __global__ __launch_bounds__(256) void bloom_probe_hashed(const uint8_t* __restrict__ filters,
                                                           const tkv_amq_segment* __restrict__ segs, uint32_t n_segs,
                                                           const uint8_t* __restrict__ qrec,
                                                           uint32_t k_max,
                                                           const uint32_t* __restrict__ pair_query,
                                                           uint64_t n, const uint32_t* __restrict__ qseg,
-                                                          uint8_t* __restrict__ result)
+                                                          uint8_t* __restrict__ result, tkv_amq_probe_opts opts)
 {
   __shared__ uint4 s_blk[256 * kProbeSlotWords / 4];
-  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= n) return;
-  // qseg[i] and pair_query[i], then the descriptor and the query record, are independent
-  // loads issued side by side; only the block load waits for both
-  const uint32_t sidx = qseg[i];
-  const uint64_t qi = pair_query ? pair_query[i] : i;
-  const uint8_t* rec = qrec + qi * bloom_query_stride(k_max);
-  const ProbeDesc d = load_probe_desc(segs, sidx, n_segs);
-  const uint64_t h0 = *reinterpret_cast<const uint64_t*>(rec);
-  uint32_t ok = 1;
-  if (d.hash_count != 0 && d.hash_count <= k_max) {
-    const uint16_t* bits = reinterpret_cast<const uint16_t*>(rec + 8);
-    const uint4* blk = reinterpret_cast<const uint4*>(filters + d.out_offset + kBloomHeader +
-                                                      64 * __umul64hi(h0, (uint64_t)d.n_blocks));
-    uint4* slot = s_blk + threadIdx.x * (kProbeSlotWords / 4);
-    const uint32_t* slot32 = reinterpret_cast<const uint32_t*>(slot);
-    const uint4 b0 = blk[0], b1 = blk[1], b2 = blk[2], b3 = blk[3];
-    slot[0] = b0;
-    slot[1] = b1;
-    slot[2] = b2;
-    slot[3] = b3;
-    uint32_t bit = (uint32_t)h0 & 511u;
-    ok &= slot32[bit >> 5] >> (bit & 31);
-    for (uint32_t j = 1; j < d.hash_count; ++j) {
-      bit = bits[j - 1];
-      ok &= slot32[bit >> 5] >> (bit & 31);
+  uint4* slot = s_blk + threadIdx.x * (kProbeSlotWords / 4);
+  const uint32_t* slot32 = reinterpret_cast<const uint32_t*>(slot);
+  ProbeTally t;
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+    // qseg[i] and pair_query[i], then the descriptor and the query record, are independent
+    // loads issued side by side; only the block load waits for both
+    const uint32_t sidx = qseg[i];
+    const uint64_t qi = pair_query ? pair_query[i] : i;
+    const uint8_t* rec = qrec + qi * bloom_query_stride(k_max);
+    const ProbeDesc d = load_probe_desc(segs, sidx, n_segs);
+    const uint64_t h0 = *reinterpret_cast<const uint64_t*>(rec);
+    uint32_t r;
+    // a filter whose hash_count exceeds the cached k_max cannot be tested: cannot reject
+    if (d.hash_count == 0 || d.hash_count > k_max) {
+      r = 1u | (kNoFilter << 1);
+    } else if (kOpts && !page_id_matches(filters + d.out_offset, 16, opts.d_query_page_id, i)) {
+      r = 1u | (kIdMismatch << 1);
+    } else {
+      const uint16_t* bits = reinterpret_cast<const uint16_t*>(rec + 8);
+      const uint4* blk = reinterpret_cast<const uint4*>(filters + d.out_offset + kBloomHeader +
+                                                        64 * __umul64hi(h0, (uint64_t)d.n_blocks));
+      const uint4 b0 = blk[0], b1 = blk[1], b2 = blk[2], b3 = blk[3];
+      slot[0] = b0;
+      slot[1] = b1;
+      slot[2] = b2;
+      slot[3] = b3;
+      uint32_t bit = (uint32_t)h0 & 511u;
+      uint32_t ok = slot32[bit >> 5] >> (bit & 31);
+      for (uint32_t j = 1; j < d.hash_count; ++j) {
+        bit = bits[j - 1];
+        ok &= slot32[bit >> 5] >> (bit & 31);
+      }
+      r = (ok & 1u) | (kChecked << 1);
     }
+    result[i] = (uint8_t)(r & 1u);
+    if constexpr (kOpts) t.add(r, opts.d_truth, i);
+    else break;
   }
-  result[i] = (uint8_t)(ok & 1u);
+  if constexpr (kOpts) flush_tally(t, opts.d_metrics, opts.d_truth != nullptr);
 }
 
 template <int MODE>
@@ -1912,6 +2070,26 @@ inline int build_key_mode(const uint8_t* keys, const uint64_t* offs, uint32_t st
 }
 
 inline hipStream_t as_stream(void* s) { return static_cast<hipStream_t>(s); }
+
+inline tkv_amq_probe_opts probe_opts(const tkv_amq_probe_opts* o)
+{
+  tkv_amq_probe_opts r{nullptr, nullptr, nullptr};
+  return o ? *o : r;
+}
+
+inline bool probe_opts_used(const tkv_amq_probe_opts& o)
+{
+  return o.d_query_page_id || o.d_truth || o.d_metrics;
+}
+
+// plain probes: one lane per query; with options: a grid-stride loop over a bounded grid, so
+// the metrics take one atomic per counter per wave (8 waves per SIMD)
+inline uint32_t probe_grid(uint64_t n, bool ex)
+{
+  const uint64_t g = (n + 255) / 256;
+  const uint64_t cap = ex ? 8192 : 0xffffffffull;
+  return (uint32_t)(g < cap ? g : cap);
+}
 
 inline uint64_t div_up(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
 
@@ -1991,6 +2169,54 @@ uint64_t tkv_amq_vqf_nslots_for_size(int tag_bits, uint64_t bytes)
 {
   if (bytes < kVqfMetadata + 64) return 0;
   return (bytes - kVqfMetadata) / 64 * vqf_slots(tag_bits) - 1;
+}
+
+// ---- TreeOptions filter page sizing (tree/tree_options.hpp:177-258) ----
+uint64_t tkv_amq_leaf_data_size(uint64_t leaf_size)
+{
+  // leaf_max_space_from_size (tree/packed_leaf_page.hpp:307-311)
+  constexpr uint64_t kOverhead = kPackedPageHeaderBytes + kPackedLeafPageBytes + kPackedArrayBytes;
+  return leaf_size > kOverhead ? leaf_size - kOverhead : 0;
+}
+
+uint64_t tkv_amq_expected_items_per_leaf(uint64_t leaf_size, uint32_t key_size_hint,
+                                         uint32_t value_size_hint)
+{
+  // expected_item_size (:246-253), PackedSizeOfEdit (core/packed_sizeof_edit.hpp:13-15):
+  // u32 key length + key + u32 value offset + 1 op byte + value
+  const uint64_t item = 4ull + key_size_hint + 4ull + 1ull + value_size_hint;
+  return tkv_amq_leaf_data_size(leaf_size) / item;
+}
+
+static uint32_t log2_ceil_u64(uint64_t x)
+{
+  uint32_t k = 0;
+  while (k < 64 && (1ull << k) < x) ++k;
+  return k;
+}
+
+uint32_t tkv_amq_filter_page_size_log2(int kind, uint64_t leaf_size, uint32_t key_size_hint,
+                                       uint32_t value_size_hint, uint64_t bits_per_key)
+{
+  const uint64_t bpk = tkv_amq_filter_bits_per_key(kind, bits_per_key);
+  const uint64_t items = tkv_amq_expected_items_per_leaf(leaf_size, key_size_hint, value_size_hint);
+  uint64_t page;
+  if (kind == TKV_AMQ_BLOOM) {
+    // round_up_bits(9, items * bpk) / 8 + page header + PackedBloomFilterPage (:184-191)
+    const uint64_t bits = (items * bpk + 511) & ~511ull;
+    page = kPackedPageHeaderBytes + kBloomHeader + bits / 8;
+  } else if (kind == TKV_AMQ_VQF) {
+    if (bpk == 0) return 0;  // no filter pages (the reference would take ceil(n / 0.0))
+    // (:195-209): ceil(items / load factor) slots at 8 and 16 tag bits, the larger size
+    const double n = (double)items;
+    const uint64_t s8 = (uint64_t)ceil(n / tkv_amq_vqf_load_factor(8, bpk));
+    const uint64_t s16 = (uint64_t)ceil(n / tkv_amq_vqf_load_factor(16, bpk));
+    const uint64_t f8 = tkv_amq_vqf_required_size(8, s8), f16 = tkv_amq_vqf_required_size(16, s16);
+    page = (f8 > f16 ? f8 : f16) + kPackedPageHeaderBytes + kVqfHeader + kVqfMetadata;
+  } else {
+    return 0;
+  }
+  return log2_ceil_u64(page);
 }
 
 int tkv_amq_plan(int kind, const uint64_t* counts, const uint64_t* src_ids, uint32_t n_segs,
@@ -2082,6 +2308,24 @@ int tkv_amq_plan(int kind, const uint64_t* counts, const uint64_t* src_ids, uint
       *ws_bytes = bloom_part_geom(key_begin, max_blocks).bytes;  // 16-byte keys
   }
   if (max_blocks_out) *max_blocks_out = max_blocks;
+  return TKV_AMQ_OK;
+}
+
+int tkv_amq_plan_pages(int kind, const uint64_t* counts, const uint64_t* src_ids, uint32_t n_segs,
+                       uint32_t bpk, uint32_t page_log2, tkv_amq_segment* segs, uint64_t* total_out,
+                       uint64_t* ws_bytes, uint32_t* max_blocks_out)
+{
+  // FilterPageAlloc's page buffer: a 64-byte PackedPageHeader, then the payload the builders
+  // size against (filter_builder.hpp:231-244)
+  if (page_log2 < 7 || page_log2 > 31) return TKV_AMQ_INVALID_ARGUMENT;
+  const uint64_t page = 1ull << page_log2;
+  const int st = tkv_amq_plan(kind, counts, src_ids, n_segs, bpk, page - kPackedPageHeaderBytes,
+                              page, segs, total_out, ws_bytes, max_blocks_out);
+  if (st != TKV_AMQ_OK) return st;
+  for (uint32_t s = 0; s < n_segs; ++s) {
+    segs[s].out_offset += kPackedPageHeaderBytes;
+    segs[s].page_flags = TKV_AMQ_PAGE_IMAGE | (page_log2 << 8);
+  }
   return TKV_AMQ_OK;
 }
 
@@ -2180,7 +2424,10 @@ int tkv_amq_build(int kind, const uint8_t* keys, const uint64_t* offs, uint32_t 
   if (max_blocks == 0) return TKV_AMQ_OK;
   if (max_blocks > kVqfMaxLdsBlocks) return TKV_AMQ_RESOURCE_EXHAUSTED;
   if (!d_ws) return TKV_AMQ_INVALID_ARGUMENT;
-  if (ws_bytes < vqf_temp_offset(n_segs)) return TKV_AMQ_INVALID_ARGUMENT;
+  // the status word and leaf counts must be writable; the rest is checked on the device
+  // against the plan (every leaf with a filter has >= 1 block record, every key one record)
+  if (ws_bytes < vqf_temp_offset(n_segs) + kVqfTempStride * (uint64_t)max_blocks + 8 * n_keys)
+    return TKV_AMQ_INVALID_ARGUMENT;
   if (hipMemsetAsync(d_ws, 0, 64, s) != hipSuccess) return TKV_AMQ_INTERNAL;
   // LDS: u32 block counts (+ the u64 lane-mask table when every leaf is small enough)
   const int match_lds = max_blocks <= kVqfMatchLdsBlocks;
@@ -2190,13 +2437,13 @@ int tkv_amq_build(int kind, const uint8_t* keys, const uint64_t* offs, uint32_t 
   const size_t lds = 4ull * ((max_blocks + 1) & ~1u) + (match_lds ? 8ull * max_blocks : 0);
   if (mode == kKey16)
     hipLaunchKernelGGL(vqf_decide<kKey16>, dim3(n_segs), dim3(64), lds, s, keys, offs, stride,
-                       d_segs, d_ws, n_segs, flags);
+                       d_segs, d_ws, ws_bytes, n_segs, flags);
   else if (mode == kKeyFixed)
     hipLaunchKernelGGL(vqf_decide<kKeyFixed>, dim3(n_segs), dim3(64), lds, s, keys, offs, stride,
-                       d_segs, d_ws, n_segs, flags);
+                       d_segs, d_ws, ws_bytes, n_segs, flags);
   else
     hipLaunchKernelGGL(vqf_decide<kKeyVar>, dim3(n_segs), dim3(64), lds, s, keys, offs, stride,
-                       d_segs, d_ws, n_segs, flags);
+                       d_segs, d_ws, ws_bytes, n_segs, flags);
   if (fused) {
     static std::once_flag lds_attr[kMaxDevices];
     once_per_device(lds_attr, [] {
@@ -2204,13 +2451,13 @@ int tkv_amq_build(int kind, const uint8_t* keys, const uint64_t* offs, uint32_t 
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)kFusedLdsBudget);
     });
     hipLaunchKernelGGL(vqf_place_fused, dim3(n_segs), dim3(kFusedThreads), fused_lds, s, d_segs,
-                       d_ws, n_segs, d_out);
+                       d_ws, ws_bytes, n_segs, d_out);
   } else {
     if (n_keys)
       hipLaunchKernelGGL(vqf_scatter, dim3((uint32_t)div_up(n_keys, 256)), dim3(256), 0, s,
-                         d_segs, d_ws, n_segs, n_keys);
-    hipLaunchKernelGGL(vqf_place, dim3(n_segs), dim3(kPlaceThreads), 0, s, d_segs, d_ws, n_segs,
-                       d_out);
+                         d_segs, d_ws, ws_bytes, n_segs, n_keys);
+    hipLaunchKernelGGL(vqf_place, dim3(n_segs), dim3(kPlaceThreads), 0, s, d_segs, d_ws, ws_bytes,
+                       n_segs, d_out);
   }
   return hipGetLastError() == hipSuccess ? TKV_AMQ_OK : TKV_AMQ_INTERNAL;
 }
@@ -2223,6 +2470,7 @@ int tkv_amq_build_check(int kind, const void* d_ws, uint64_t ws_bytes, void* str
   if (kind != TKV_AMQ_VQF || !d_ws || ws_bytes < 64) return TKV_AMQ_OK;
   uint32_t status = 0;
   if (hipMemcpy(&status, d_ws, 4, hipMemcpyDeviceToHost) != hipSuccess) return TKV_AMQ_INTERNAL;
+  if (status & kVqfStatusWorkspace) return TKV_AMQ_INVALID_ARGUMENT;
   return status ? TKV_AMQ_INTERNAL : TKV_AMQ_OK;
 }
 
@@ -2230,37 +2478,45 @@ int tkv_amq_probe(int kind, const uint8_t* d_filters, const tkv_amq_segment* d_s
                   uint32_t n_segs, const uint8_t* q, const uint64_t* qoffs, uint32_t stride,
                   uint64_t n, const uint32_t* d_qseg, uint8_t* d_result, void* stream)
 {
+  return tkv_amq_probe_ex(kind, d_filters, d_segs, n_segs, q, qoffs, stride, n, d_qseg, d_result,
+                          nullptr, stream);
+}
+
+int tkv_amq_probe_ex(int kind, const uint8_t* d_filters, const tkv_amq_segment* d_segs,
+                     uint32_t n_segs, const uint8_t* q, const uint64_t* qoffs, uint32_t stride,
+                     uint64_t n, const uint32_t* d_qseg, uint8_t* d_result,
+                     const tkv_amq_probe_opts* opts, void* stream)
+{
   if (tkv_amq_device_count() == 0) return TKV_AMQ_UNAVAILABLE;
   if (n == 0) return TKV_AMQ_OK;
   if (!d_filters || !d_segs || !q || !d_qseg || !d_result || n_segs == 0 || (!qoffs && !stride))
     return TKV_AMQ_INVALID_ARGUMENT;
+  if (kind != TKV_AMQ_BLOOM && kind != TKV_AMQ_VQF) return TKV_AMQ_INVALID_ARGUMENT;
   const hipStream_t s = as_stream(stream);
   const int mode = key_mode(qoffs, stride);
   if (mode == kKey16 && (reinterpret_cast<uintptr_t>(q) & 15)) return TKV_AMQ_INVALID_ARGUMENT;
-  const dim3 grid((uint32_t)div_up(n, 256)), block(256);
+  const tkv_amq_probe_opts o = probe_opts(opts);
+  const bool ex = probe_opts_used(o);
+  const dim3 grid(probe_grid(n, ex)), block(256);
+#define TKV_PROBE_LAUNCH(KERNEL, MODE)                                                         \
+  do {                                                                                         \
+    if (ex)                                                                                    \
+      hipLaunchKernelGGL((KERNEL<MODE, true>), grid, block, 0, s, d_filters, d_segs, n_segs, q, \
+                         qoffs, stride, n, d_qseg, d_result, o);                               \
+    else                                                                                       \
+      hipLaunchKernelGGL((KERNEL<MODE, false>), grid, block, 0, s, d_filters, d_segs, n_segs,  \
+                         q, qoffs, stride, n, d_qseg, d_result, o);                            \
+  } while (0)
   if (kind == TKV_AMQ_BLOOM) {
-    if (mode == kKey16)
-      hipLaunchKernelGGL(bloom_probe<kKey16>, grid, block, 0, s, d_filters, d_segs, n_segs, q, qoffs,
-                         stride, n, d_qseg, d_result);
-    else if (mode == kKeyFixed)
-      hipLaunchKernelGGL(bloom_probe<kKeyFixed>, grid, block, 0, s, d_filters, d_segs, n_segs, q, qoffs,
-                         stride, n, d_qseg, d_result);
-    else
-      hipLaunchKernelGGL(bloom_probe<kKeyVar>, grid, block, 0, s, d_filters, d_segs, n_segs, q, qoffs,
-                         stride, n, d_qseg, d_result);
-  } else if (kind == TKV_AMQ_VQF) {
-    if (mode == kKey16)
-      hipLaunchKernelGGL(vqf_probe<kKey16>, grid, block, 0, s, d_filters, d_segs, n_segs, q, qoffs, stride,
-                         n, d_qseg, d_result);
-    else if (mode == kKeyFixed)
-      hipLaunchKernelGGL(vqf_probe<kKeyFixed>, grid, block, 0, s, d_filters, d_segs, n_segs, q, qoffs,
-                         stride, n, d_qseg, d_result);
-    else
-      hipLaunchKernelGGL(vqf_probe<kKeyVar>, grid, block, 0, s, d_filters, d_segs, n_segs, q, qoffs, stride,
-                         n, d_qseg, d_result);
+    if (mode == kKey16) TKV_PROBE_LAUNCH(bloom_probe, kKey16);
+    else if (mode == kKeyFixed) TKV_PROBE_LAUNCH(bloom_probe, kKeyFixed);
+    else TKV_PROBE_LAUNCH(bloom_probe, kKeyVar);
   } else {
-    return TKV_AMQ_INVALID_ARGUMENT;
+    if (mode == kKey16) TKV_PROBE_LAUNCH(vqf_probe, kKey16);
+    else if (mode == kKeyFixed) TKV_PROBE_LAUNCH(vqf_probe, kKeyFixed);
+    else TKV_PROBE_LAUNCH(vqf_probe, kKeyVar);
   }
+#undef TKV_PROBE_LAUNCH
   return hipGetLastError() == hipSuccess ? TKV_AMQ_OK : TKV_AMQ_INTERNAL;
 }
 
@@ -2287,12 +2543,29 @@ int tkv_amq_vqf_probe_hashed(const uint8_t* d_filters, const tkv_amq_segment* d_
                              uint32_t n_segs, const uint64_t* d_hash, const uint32_t* d_pair_query,
                              uint64_t n, const uint32_t* d_qseg, uint8_t* d_result, void* stream)
 {
+  return tkv_amq_vqf_probe_hashed_ex(d_filters, d_segs, n_segs, d_hash, d_pair_query, n, d_qseg,
+                                     d_result, nullptr, stream);
+}
+
+int tkv_amq_vqf_probe_hashed_ex(const uint8_t* d_filters, const tkv_amq_segment* d_segs,
+                                uint32_t n_segs, const uint64_t* d_hash,
+                                const uint32_t* d_pair_query, uint64_t n, const uint32_t* d_qseg,
+                                uint8_t* d_result, const tkv_amq_probe_opts* opts, void* stream)
+{
   if (tkv_amq_device_count() == 0) return TKV_AMQ_UNAVAILABLE;
   if (n == 0) return TKV_AMQ_OK;
   if (!d_filters || !d_segs || !d_hash || !d_qseg || !d_result || n_segs == 0)
     return TKV_AMQ_INVALID_ARGUMENT;
-  hipLaunchKernelGGL(vqf_probe_hashed, dim3((uint32_t)div_up(n, 256)), dim3(256), 0,
-                     as_stream(stream), d_filters, d_segs, n_segs, d_hash, d_pair_query, n, d_qseg, d_result);
+  const tkv_amq_probe_opts o = probe_opts(opts);
+  const bool ex = probe_opts_used(o);
+  if (ex)
+    hipLaunchKernelGGL(vqf_probe_hashed<true>, dim3(probe_grid(n, true)), dim3(256), 0,
+                       as_stream(stream), d_filters, d_segs, n_segs, d_hash, d_pair_query, n, d_qseg,
+                       d_result, o);
+  else
+    hipLaunchKernelGGL(vqf_probe_hashed<false>, dim3(probe_grid(n, false)), dim3(256), 0,
+                       as_stream(stream), d_filters, d_segs, n_segs, d_hash, d_pair_query, n, d_qseg,
+                       d_result, o);
   return hipGetLastError() == hipSuccess ? TKV_AMQ_OK : TKV_AMQ_INTERNAL;
 }
 
@@ -2323,14 +2596,30 @@ int tkv_amq_bloom_probe_hashed(const uint8_t* d_filters, const tkv_amq_segment* 
                                const uint32_t* d_pair_query, uint64_t n, const uint32_t* d_qseg,
                                uint8_t* d_result, void* stream)
 {
+  return tkv_amq_bloom_probe_hashed_ex(d_filters, d_segs, n_segs, d_query, k_max, d_pair_query, n,
+                                       d_qseg, d_result, nullptr, stream);
+}
+
+int tkv_amq_bloom_probe_hashed_ex(const uint8_t* d_filters, const tkv_amq_segment* d_segs,
+                                  uint32_t n_segs, const uint8_t* d_query, uint32_t k_max,
+                                  const uint32_t* d_pair_query, uint64_t n, const uint32_t* d_qseg,
+                                  uint8_t* d_result, const tkv_amq_probe_opts* opts, void* stream)
+{
   if (tkv_amq_device_count() == 0) return TKV_AMQ_UNAVAILABLE;
   if (n == 0) return TKV_AMQ_OK;
   if (!d_filters || !d_segs || !d_query || !d_qseg || !d_result || n_segs == 0 || k_max == 0 ||
       k_max > kMaxBloomHashes)
     return TKV_AMQ_INVALID_ARGUMENT;
-  hipLaunchKernelGGL(bloom_probe_hashed, dim3((uint32_t)div_up(n, 256)), dim3(256), 0,
-                     as_stream(stream), d_filters, d_segs, n_segs, d_query, k_max, d_pair_query, n, d_qseg,
-                     d_result);
+  const tkv_amq_probe_opts o = probe_opts(opts);
+  const bool ex = probe_opts_used(o);
+  if (ex)
+    hipLaunchKernelGGL(bloom_probe_hashed<true>, dim3(probe_grid(n, true)), dim3(256), 0,
+                       as_stream(stream), d_filters, d_segs, n_segs, d_query, k_max, d_pair_query, n,
+                       d_qseg, d_result, o);
+  else
+    hipLaunchKernelGGL(bloom_probe_hashed<false>, dim3(probe_grid(n, false)), dim3(256), 0,
+                       as_stream(stream), d_filters, d_segs, n_segs, d_query, k_max, d_pair_query, n,
+                       d_qseg, d_result, o);
   return hipGetLastError() == hipSuccess ? TKV_AMQ_OK : TKV_AMQ_INTERNAL;
 }
 

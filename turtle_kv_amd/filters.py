@@ -4,6 +4,7 @@ Reference interface (mathworks/turtle_kv, src/turtle_kv/...) and the function he
 replaces it:
 
   TreeOptions::filter_bits_per_key        tree/tree_options.hpp:155-164  -> filter_bits_per_key
+  TreeOptions filter page sizing          tree/tree_options.hpp:166-258  -> TreeOptions
   vqf_hash_val                            vqf_filter_page_view.hpp:32-35 -> vqf_hash_val
   vqf_filter_load_factor<T>               vqf_filter_page_view.hpp:39-59 -> vqf_filter_load_factor
   build_bloom_filter_for_leaf             tree/filter_builder.hpp:109-152 -> build_bloom_filter_for_leaf
@@ -13,6 +14,9 @@ replaces it:
                                           half of it)                     -> build_all_filters
   PackedVqfFilter::is_present             vqf_filter_page_view.hpp:113-125 -> PackedVqfFilter.is_present
   KeyQuery::reject_page                   tree/key_query.hpp:149-247      -> KeyQuery.reject_page
+  KeyQuery::Metrics                       tree/key_query.hpp:36-60        -> KeyQueryMetrics
+  FilterPageAlloc page + header fields    tree/filter_builder.hpp:58-105,231-237,293-296
+                                                                          -> plan_filter_pages
 
 Device memory, streams and multi-GPU plumbing come from PyTorch-ROCm; every filter
 computation runs in the HIP kernels of libtkv_amq.so.  There is no CPU fallback: with no
@@ -96,6 +100,105 @@ def vqf_filter_load_factor(tag_bits: int, bits_per_key: int) -> float:
     return float(abi.lib().tkv_amq_vqf_load_factor(tag_bits, bits_per_key))
 
 
+def _log2_ceil(x: int) -> int:
+    return max(0, (int(x) - 1).bit_length())
+
+
+class TreeOptions:
+    """The filter part of TreeOptions (tree/tree_options.hpp:43-395, tree_options.cpp:17-60):
+    bits per key with the VQF clamp, and the filter page size derived from the leaf size and
+    the key/value size hints.  `kind` stands for the compile-time filter switch (config.hpp:20-24)."""
+
+    kDefaultFilterBitsPerKey = 12   # :57
+    kDefaultKeySizeHint = 24        # :58
+    kDefaultValueSizeHint = 100     # :59
+
+    def __init__(self, kind: int = DEFAULT_FILTER_KIND):
+        self.kind = kind
+        self.leaf_size_log2_ = 21                  # 2 MiB (:384, with_default_values)
+        self.filter_bits_per_key_ = None
+        self.filter_page_size_log2_ = None
+        self.key_size_hint_ = self.kDefaultKeySizeHint
+        self.value_size_hint_ = self.kDefaultValueSizeHint
+
+    @classmethod
+    def with_default_values(cls, kind: int = DEFAULT_FILTER_KIND) -> "TreeOptions":
+        return cls(kind)
+
+    # leaf size
+    def leaf_size(self) -> int:
+        return 1 << self.leaf_size_log2_
+
+    def set_leaf_size(self, size: int) -> "TreeOptions":
+        self.leaf_size_log2_ = _log2_ceil(size)
+        if self.leaf_size() != size:
+            raise TkvAmqError(abi.INVALID_ARGUMENT, "leaf_size must be a power of 2")  # :106
+        return self
+
+    def set_leaf_size_log2(self, size_log2: int) -> "TreeOptions":
+        self.leaf_size_log2_ = int(size_log2)
+        return self
+
+    def leaf_data_size(self) -> int:
+        """leaf_max_space_from_size (tree/packed_leaf_page.hpp:307-311)."""
+        return int(abi.lib().tkv_amq_leaf_data_size(self.leaf_size()))
+
+    # bits per key
+    def set_filter_bits_per_key(self, bits_per_key: int | None) -> "TreeOptions":
+        self.filter_bits_per_key_ = bits_per_key
+        return self
+
+    def filter_bits_per_key(self) -> int:
+        return filter_bits_per_key(self.filter_bits_per_key_, self.kind)
+
+    # item size hints
+    def key_size_hint(self) -> int:
+        return self.key_size_hint_
+
+    def set_key_size_hint(self, n_bytes: int) -> "TreeOptions":
+        self.key_size_hint_ = int(n_bytes)
+        return self
+
+    def value_size_hint(self) -> int:
+        return self.value_size_hint_
+
+    def set_value_size_hint(self, n_bytes: int) -> "TreeOptions":
+        self.value_size_hint_ = int(n_bytes)
+        return self
+
+    def expected_item_size(self) -> int:
+        """PackedSizeOfEdit (core/packed_sizeof_edit.hpp:13-15) of a hint-sized edit."""
+        return 4 + self.key_size_hint_ + 4 + 1 + self.value_size_hint_
+
+    def expected_items_per_leaf(self) -> int:
+        return int(abi.lib().tkv_amq_expected_items_per_leaf(self.leaf_size(), self.key_size_hint_,
+                                                             self.value_size_hint_))
+
+    # filter page size
+    def set_filter_page_size_log2(self, size_log2: int) -> "TreeOptions":
+        self.filter_page_size_log2_ = int(size_log2)
+        return self
+
+    def set_filter_page_size(self, size: int) -> "TreeOptions":
+        return self.set_filter_page_size_log2(_log2_ceil(size))
+
+    def filter_page_size_log2(self) -> int:
+        if self.filter_page_size_log2_ is not None:
+            return self.filter_page_size_log2_
+        return int(abi.lib().tkv_amq_filter_page_size_log2(
+            self.kind, self.leaf_size(), self.key_size_hint_, self.value_size_hint_,
+            K_DEFAULT_FILTER_BITS_PER_KEY if self.filter_bits_per_key_ is None
+            else int(self.filter_bits_per_key_)))
+
+    def filter_page_size(self) -> int:
+        return 1 << self.filter_page_size_log2()
+
+    def filter_page_payload_size(self) -> int:
+        """The payload buffer the filter builders size against: page size minus the llfs
+        PackedPageHeader (filter_builder.hpp:231-244)."""
+        return self.filter_page_size() - PACKED_PAGE_HEADER_BYTES
+
+
 def vqf_required_size(tag_bits: int, nslots: int) -> int:
     return int(abi.lib().tkv_amq_vqf_required_size(tag_bits, nslots))
 
@@ -146,6 +249,34 @@ def plan_filters(kind: int, seg_key_counts, bits_per_key: int, payload_capacity:
     abi.check(st, "tkv_amq_plan")
     return FilterPlan(kind, int(bits_per_key), segs, int(tot.value), int(ws.value), int(mb.value),
                       int(counts.sum()) if n else 0)
+
+
+def plan_filter_pages(kind: int, seg_key_counts, bits_per_key: int, page_size_log2: int,
+                      src_page_ids=None) -> FilterPlan:
+    """One whole filter page per leaf (tkv_amq_plan_pages): leaf s's page is bytes
+    [s << log2, (s+1) << log2) of the output, a 64-byte page header then the payload, the
+    buffer FilterPageAlloc hands the builder (filter_builder.hpp:70-88).  The build writes the
+    header fields the builders set (layout_id, unused_begin, unused_end) and the page size."""
+    counts = np.ascontiguousarray(np.asarray(seg_key_counts, dtype=np.uint64))
+    n = len(counts)
+    segs = np.zeros(n, dtype=abi.SEGMENT_DTYPE)
+    src = None if src_page_ids is None else np.ascontiguousarray(np.asarray(src_page_ids, dtype=np.uint64))
+    tot, ws, mb = ctypes.c_uint64(0), ctypes.c_uint64(0), ctypes.c_uint32(0)
+    st = abi.lib().tkv_amq_plan_pages(kind, _ptr(counts), _ptr(src), n, int(bits_per_key),
+                                      int(page_size_log2), _ptr(segs), ctypes.byref(tot),
+                                      ctypes.byref(ws), ctypes.byref(mb))
+    abi.check(st, "tkv_amq_plan_pages")
+    return FilterPlan(kind, int(bits_per_key), segs, int(tot.value), int(ws.value), int(mb.value),
+                      int(counts.sum()) if n else 0)
+
+
+def page_header_fields(page: np.ndarray) -> dict:
+    """The PackedPageHeader fields of one filter page image (offsets as in tkv_amq_plan_pages,
+    llfs 0.42's layout: UNPINNED)."""
+    b = np.asarray(page, dtype=np.uint8)
+    u32 = b[:64].view("<u4")
+    return {"layout_id": bytes(b[16:24]).rstrip(b"\0").decode("ascii", "replace"),
+            "unused_begin": int(u32[7]), "unused_end": int(u32[8]), "size": int(u32[15])}
 
 
 # ---------------------------------------------------------------------------------------
@@ -385,36 +516,90 @@ def build_all_filters(plan: FilterPlan, keys: KeyBatch, out=None, workspace=None
     dev = keys.data.device
     if out is None:
         out = torch.empty(max(plan.total_out_bytes, 1), dtype=torch.uint8, device=dev)
+    elif out.numel() < plan.total_out_bytes:
+        raise TkvAmqError(abi.INVALID_ARGUMENT,
+                          f"output holds {out.numel()} bytes, the plan needs {plan.total_out_bytes}")
     if plan.workspace_bytes and workspace is None:
         workspace = torch.empty(plan.workspace_bytes, dtype=torch.uint8, device=dev)
+    ws_bytes = 0 if workspace is None else workspace.numel() * workspace.element_size()
+    if ws_bytes < plan.workspace_bytes:
+        raise TkvAmqError(abi.INVALID_ARGUMENT,
+                          f"workspace holds {ws_bytes} bytes, the plan needs {plan.workspace_bytes}")
     sh = _stream_handle(stream)
     t0 = time.perf_counter()
     st = abi.lib().tkv_amq_build(plan.kind, _ptr(keys.data), _ptr(keys.offsets), keys.stride,
                                  keys.n, _ptr(plan.device_segs(dev)), plan.n_segs,
-                                 plan.max_seg_blocks, _ptr(out), _ptr(workspace),
-                                 plan.workspace_bytes, sh)
+                                 plan.max_seg_blocks, _ptr(out), _ptr(workspace), ws_bytes, sh)
     abi.check(st, "tkv_amq_build")
     if check:
         # synchronous: the batch is known good, record its metrics with the build latency
-        abi.check(abi.lib().tkv_amq_build_check(plan.kind, _ptr(workspace), plan.workspace_bytes,
-                                                sh), "vqf_insert (filter_builder.hpp:211)")
+        abi.check(abi.lib().tkv_amq_build_check(plan.kind, _ptr(workspace), ws_bytes, sh),
+                  "vqf_insert (filter_builder.hpp:211)")
         record_filter_metrics(plan, (time.perf_counter() - t0) * 1e6)
     return out
 
 
-def probe_filters(plan: FilterPlan, filters, queries: KeyBatch, query_seg, out=None, stream=None):
+class ProbeMetrics:
+    """Device-side KeyQuery::Metrics counters (tkv_amq_probe_metrics) that probe launches add
+    to; `collect()` reads them, `fold_into()` adds them to a host KeyQueryMetrics."""
+
+    def __init__(self, device=None):
+        torch = _torch()
+        self.counts = torch.zeros(len(abi.PROBE_METRICS_FIELDS), dtype=torch.int64,
+                                  device=device or "cuda")
+
+    def reset(self) -> None:
+        self.counts.zero_()
+
+    def collect(self) -> dict:
+        return dict(zip(abi.PROBE_METRICS_FIELDS, (int(v) for v in self.counts.cpu().tolist())))
+
+    def fold_into(self, m: "KeyQueryMetrics", reset: bool = True) -> None:
+        for k, v in self.collect().items():
+            getattr(m, k).add(v)
+        if reset:
+            self.reset()
+
+
+def _probe_opts(query_page_ids, truth, metrics):
+    torch = _torch()
+    keep = []
+    pid = None
+    if query_page_ids is not None:
+        pid = query_page_ids.to(dtype=torch.int64).contiguous()
+        keep.append(pid)
+    tr = None
+    if truth is not None:
+        tr = truth.to(dtype=torch.uint8).contiguous()
+        keep.append(tr)
+    o = abi.ProbeOpts(None if pid is None else pid.data_ptr(), None if tr is None else tr.data_ptr(),
+                      None if metrics is None else metrics.counts.data_ptr())
+    return o, keep
+
+
+def probe_filters(plan: FilterPlan, filters, queries: KeyBatch, query_seg, out=None, stream=None,
+                  query_page_ids=None, truth=None, metrics: ProbeMetrics | None = None):
     """Batched KeyQuery filter test: result[i] = 0 iff the filter of segment query_seg[i]
-    rejects queries[i] (reject_page == kTrue)."""
+    rejects queries[i] (reject_page == kTrue).  Optional, per query: the leaf page id asked
+    about (a filter built for another page answers 1, kUnknown), the ground truth (1 = key is
+    in the leaf) for the false-positive count, and device KeyQuery::Metrics counters."""
     torch = _torch()
     _require_device()
     dev = filters.device
     if out is None:
         out = torch.empty(queries.n, dtype=torch.uint8, device=dev)
     qs = query_seg.to(dtype=torch.int32)
-    st = abi.lib().tkv_amq_probe(plan.kind, _ptr(filters), _ptr(plan.device_segs(dev)),
-                                 plan.n_segs, _ptr(queries.data), _ptr(queries.offsets),
-                                 queries.stride, queries.n, _ptr(qs), _ptr(out),
-                                 _stream_handle(stream))
+    sh = _stream_handle(stream)
+    if query_page_ids is None and truth is None and metrics is None:
+        st = abi.lib().tkv_amq_probe(plan.kind, _ptr(filters), _ptr(plan.device_segs(dev)),
+                                     plan.n_segs, _ptr(queries.data), _ptr(queries.offsets),
+                                     queries.stride, queries.n, _ptr(qs), _ptr(out), sh)
+    else:
+        o, _keep = _probe_opts(query_page_ids, truth, metrics)
+        st = abi.lib().tkv_amq_probe_ex(plan.kind, _ptr(filters), _ptr(plan.device_segs(dev)),
+                                        plan.n_segs, _ptr(queries.data), _ptr(queries.offsets),
+                                        queries.stride, queries.n, _ptr(qs), _ptr(out),
+                                        ctypes.byref(o), sh)
     abi.check(st, "tkv_amq_probe")
     return out
 
@@ -430,9 +615,11 @@ def vqf_hash_val(keys: KeyBatch, stream=None):
 
 
 def vqf_probe_hashed(plan: FilterPlan, filters, hash_vals, query_seg, out=None, stream=None,
-                     pair_query=None):
+                     pair_query=None, query_page_ids=None, truth=None,
+                     metrics: ProbeMetrics | None = None):
     """PackedVqfFilter::is_present for pre-hashed queries; pair i tests leaf query_seg[i]
-    with hash_vals[pair_query[i]] (identity when pair_query is None)."""
+    with hash_vals[pair_query[i]] (identity when pair_query is None).  The optional inputs
+    are per pair, as in probe_filters."""
     torch = _torch()
     _require_device()
     dev = filters.device
@@ -441,9 +628,11 @@ def vqf_probe_hashed(plan: FilterPlan, filters, hash_vals, query_seg, out=None, 
         out = torch.empty(n, dtype=torch.uint8, device=dev)
     qs = query_seg.to(dtype=torch.int32)
     pq = None if pair_query is None else pair_query.to(dtype=torch.int32)
-    abi.check(abi.lib().tkv_amq_vqf_probe_hashed(_ptr(filters), _ptr(plan.device_segs(dev)),
-                                                 plan.n_segs, _ptr(hash_vals), _ptr(pq), n,
-                                                 _ptr(qs), _ptr(out), _stream_handle(stream)),
+    o, _keep = _probe_opts(query_page_ids, truth, metrics)
+    abi.check(abi.lib().tkv_amq_vqf_probe_hashed_ex(_ptr(filters), _ptr(plan.device_segs(dev)),
+                                                    plan.n_segs, _ptr(hash_vals), _ptr(pq), n,
+                                                    _ptr(qs), _ptr(out), ctypes.byref(o),
+                                                    _stream_handle(stream)),
               "tkv_amq_vqf_probe_hashed")
     return out
 
@@ -462,7 +651,8 @@ def bloom_query_hashes(keys: KeyBatch, k_max: int, stream=None):
 
 
 def bloom_probe_hashed(plan: FilterPlan, filters, query_hashes, k_max: int, query_seg, out=None,
-                       stream=None, pair_query=None):
+                       stream=None, pair_query=None, query_page_ids=None, truth=None,
+                       metrics: ProbeMetrics | None = None):
     """PackedBloomFilter::query(BloomFilterQuery) for (query, leaf) pairs."""
     torch = _torch()
     _require_device()
@@ -472,9 +662,11 @@ def bloom_probe_hashed(plan: FilterPlan, filters, query_hashes, k_max: int, quer
         out = torch.empty(n, dtype=torch.uint8, device=dev)
     qs = query_seg.to(dtype=torch.int32)
     pq = None if pair_query is None else pair_query.to(dtype=torch.int32)
-    abi.check(abi.lib().tkv_amq_bloom_probe_hashed(_ptr(filters), _ptr(plan.device_segs(dev)),
-                                                   plan.n_segs, _ptr(query_hashes), k_max, _ptr(pq),
-                                                   n, _ptr(qs), _ptr(out), _stream_handle(stream)),
+    o, _keep = _probe_opts(query_page_ids, truth, metrics)
+    abi.check(abi.lib().tkv_amq_bloom_probe_hashed_ex(_ptr(filters), _ptr(plan.device_segs(dev)),
+                                                      plan.n_segs, _ptr(query_hashes), k_max,
+                                                      _ptr(pq), n, _ptr(qs), _ptr(out),
+                                                      ctypes.byref(o), _stream_handle(stream)),
               "tkv_amq_bloom_probe_hashed")
     return out
 
@@ -520,10 +712,14 @@ def build_quotient_filter_for_leaf(filter_bits_per_key: int, leaf_page_id: int, 
 
 
 def build_filter_for_leaf_in_job(filter_bits_per_key: int, leaf_page_id: int, keys: KeyBatch,
-                                 page_payload_bytes: int = 32768 - PACKED_PAGE_HEADER_BYTES,
+                                 page_payload_bytes: int | None = None,
                                  kind: int = DEFAULT_FILTER_KIND) -> FilterPage | None:
     """Like the reference: a failed build is logged and the leaf gets no filter
-    (filter_builder.hpp:323-325)."""
+    (filter_builder.hpp:323-325).  The payload capacity defaults to the filter page of the
+    default TreeOptions for this bits/key (TreeOptions.filter_page_payload_size)."""
+    if page_payload_bytes is None:
+        page_payload_bytes = (TreeOptions(kind).set_filter_bits_per_key(filter_bits_per_key)
+                              .filter_page_payload_size())
     try:
         if kind == BLOOM:
             return build_bloom_filter_for_leaf(filter_bits_per_key, leaf_page_id, keys,
@@ -561,37 +757,104 @@ class PackedVqfFilter:
         return vqf_probe_hashed(self.page.plan, self.page.payload, hv, qs)
 
 
+class _Count:
+    """FastCountMetric<u64>."""
+
+    def __init__(self):
+        self._lock = threading.Lock()
+        self.value = 0
+
+    def add(self, n: int) -> None:
+        with self._lock:
+            self.value += int(n)
+
+    def get(self) -> int:
+        return self.value
+
+    def __repr__(self):
+        return str(self.value)
+
+
+class KeyQueryMetrics:
+    """KeyQuery::Metrics, the filter counters (tree/key_query.hpp:36-60).  reject_page updates
+    total / no-filter / load-failed / page-id-mismatch / reject (:154,157,183,210,231,243);
+    the caller's leaf search updates positive / false positive (key_query.cpp:41,77): the
+    batched device probes count those when given a ProbeMetrics (and ground truth)."""
+
+    def __init__(self):
+        self.total_filter_query_count = _Count()
+        self.no_filter_page_count = _Count()
+        self.filter_page_load_failed_count = _Count()
+        self.page_id_mismatch_count = _Count()
+        self.filter_reject_count = _Count()
+        self.filter_positive_count = _Count()
+        self.filter_false_positive_count = _Count()
+
+    def filter_false_positive_rate(self) -> float:
+        positives = self.filter_positive_count.get()
+        if positives == 0:
+            return -1.0
+        return self.filter_false_positive_count.get() / positives
+
+    def as_dict(self) -> dict:
+        return {k: v.get() for k, v in vars(self).items() if isinstance(v, _Count)}
+
+
 class KeyQuery:
     """KeyQuery (tree/key_query.hpp:33-253) for a batch of point-query keys.  The hashes are
     computed once per query and reused for every filter probed: the VQF hash_val
     (key_query.hpp:82) and the Bloom BloomFilterQuery cache (:78,97)."""
 
     BLOOM_K_MAX = 32
+    _metrics = KeyQueryMetrics()
+
+    @classmethod
+    def metrics(cls) -> KeyQueryMetrics:
+        """The process-wide counters (KeyQuery::metrics(), :64-68)."""
+        return cls._metrics
 
     def __init__(self, keys: KeyBatch):
         self.keys = keys
         self.hash_val = vqf_hash_val(keys)
         self.bloom_query = bloom_query_hashes(keys, self.BLOOM_K_MAX)
 
-    def reject_page(self, page_id_to_reject: int, filter_page: FilterPage | None) -> list:
+    def reject_page(self, page_id_to_reject: int, filter_page: FilterPage | None,
+                    truth=None) -> list:
         """Per key: kTrue = filter says definitely absent; kFalse = maybe present;
-        kUnknown = no filter page or it belongs to another leaf (key_query.hpp:156-159,207-232)."""
+        kUnknown = no filter page, or it belongs to another leaf (key_query.hpp:156-159,207-232).
+        `truth` (optional, 1 = key is in the leaf): counts the positives that are false, as the
+        caller's leaf search does (key_query.cpp:41,77)."""
         torch = _torch()
+        m = self.metrics()
+        n = self.keys.n
+        m.total_filter_query_count.add(n)
         if filter_page is None:
-            return [BoolStatus.kUnknown] * self.keys.n
+            m.no_filter_page_count.add(n)
+            return [BoolStatus.kUnknown] * n
         hdr = filter_page.payload[:32].cpu().numpy().view("<u8")
         magic = int(hdr[0])
-        src = int(hdr[2]) if filter_page.kind == BLOOM else int(hdr[1])
-        if magic not in (VQF_MAGIC, BLOOM_MAGIC):
+        want = VQF_MAGIC if filter_page.kind == VQF else BLOOM_MAGIC
+        if magic != want:  # check_magic (:194, vqf_filter_page_view.hpp:97-100)
             raise TkvAmqError(abi.INTERNAL, "filter page magic mismatch")
+        src = int(hdr[2]) if filter_page.kind == BLOOM else int(hdr[1])
         if src != page_id_to_reject:
-            return [BoolStatus.kUnknown] * self.keys.n
-        qs = torch.zeros(self.keys.n, dtype=torch.int32, device=filter_page.payload.device)
+            m.page_id_mismatch_count.add(n)
+            return [BoolStatus.kUnknown] * n
+        dev = filter_page.payload.device
+        qs = torch.zeros(n, dtype=torch.int32, device=dev)
+        pm = ProbeMetrics(dev)
+        tr = None if truth is None else torch.as_tensor(np.asarray(truth, dtype=np.uint8), device=dev)
         if filter_page.kind == VQF:
-            present = vqf_probe_hashed(filter_page.plan, filter_page.payload, self.hash_val, qs)
+            present = vqf_probe_hashed(filter_page.plan, filter_page.payload, self.hash_val, qs,
+                                       truth=tr, metrics=pm)
         else:
             present = bloom_probe_hashed(filter_page.plan, filter_page.payload, self.bloom_query,
-                                         self.BLOOM_K_MAX, qs)
+                                         self.BLOOM_K_MAX, qs, truth=tr, metrics=pm)
+        c = pm.collect()
+        m.filter_reject_count.add(c["filter_reject_count"])
+        m.filter_positive_count.add(c["filter_positive_count"])
+        if truth is not None:
+            m.filter_false_positive_count.add(c["filter_false_positive_count"])
         return [BoolStatus.kFalse if p else BoolStatus.kTrue for p in present.cpu().tolist()]
 
 
