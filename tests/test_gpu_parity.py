@@ -155,6 +155,39 @@ def test_variable_length_keys_many_leaves(oracle, amq, torch, big_leaf):
         assert_same(plan, out, ref)
 
 
+@pytest.mark.parametrize("n_leaves", [64, 300, 1023, 1024])
+@pytest.mark.parametrize("shape", ["k16", "k24", "var"])
+def test_bloom_leaf_kernel_widths(oracle, amq, torch, n_leaves, shape):
+    """The leaf kernel runs 1024 threads per leaf below 1024 leaves and 256 from there: both
+    widths, every key shape, ragged leaves, against the oracle (sampled leaves)."""
+    rng = np.random.default_rng(n_leaves)
+    counts = [int(c) for c in rng.integers(0, 3000, n_leaves)]
+    counts[0], counts[1], counts[-1] = 0, 16384, 1
+    n = sum(counts)
+    offs = None
+    if shape == "k16":
+        keys, stride = oracle.gen_keys16(42, 0, n), 16
+    elif shape == "k24":
+        keys, stride = rng.integers(0, 256, (n, 24), dtype=np.uint8), 24
+    else:
+        lens = rng.integers(0, 40, n)
+        keys, stride = rng.integers(0, 256, int(lens.sum()), dtype=np.uint8), 0
+        offs = np.zeros(n + 1, np.int64)
+        offs[1:] = np.cumsum(lens)
+    plan, out = gpu_build(amq, torch, 0, torch.from_numpy(keys).cuda(), counts, 10,
+                          offsets_t=None if offs is None else torch.from_numpy(offs).cuda())
+    sb = seg_bounds(counts)
+    for s in sorted({0, 1, n_leaves - 1, *rng.integers(0, n_leaves, 12).tolist()}):
+        b, c = int(sb[s]), counts[s]
+        if offs is None:
+            st, ref = oracle.bloom_build(keys[b:], c, 10, src_page_id=s, stride=stride)
+        else:
+            o = (offs[b:b + c + 1] - offs[b]).astype(np.uint64)
+            st, ref = oracle.bloom_build(keys[int(offs[b]):], c, 10, src_page_id=s, offsets=o, stride=0)
+        assert st == 0
+        assert segment_bytes(plan, out, s) == ref.tobytes(), f"leaf {s}"
+
+
 def sorted_keys(oracle, seed, counts):
     keys = oracle.gen_keys16(seed, 0, sum(counts))
     oracle.sort_segments(keys, seg_bounds(counts))

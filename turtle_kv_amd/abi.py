@@ -143,6 +143,9 @@ def lib(build_if_missing: bool = True):
     L.tkv_amq_gen_keys16.argtypes = [u64, u64, u64, vp, vp]
     L.tkv_amq_stage_keys.restype = i32
     L.tkv_amq_stage_keys.argtypes = [vp, u64, u64, u32, vp, u64, vp, i32]
+    if os.environ.get("TKV_AMQ_LIB") and not hasattr(L, "tkv_amq_probe_ex"):
+        _lib = L  # an older experiment build (A/B timing): the round-1 entry points only
+        return L
     L.tkv_amq_leaf_data_size.restype = u64
     L.tkv_amq_leaf_data_size.argtypes = [u64]
     L.tkv_amq_expected_items_per_leaf.restype = u64

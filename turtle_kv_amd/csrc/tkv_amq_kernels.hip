@@ -222,24 +222,24 @@ __device__ inline void bloom_keys16_lds(const uint4* __restrict__ kp, uint32_t n
   }
 }
 
-template <int K, int L>
+template <int K, int L, uint32_t NT>
 __device__ inline void bloom_keysL_lds(const uint64_t* __restrict__ kp, uint32_t n, uint32_t nb,
                                        uint32_t k, uint32_t* s_bits)
 {
   constexpr int N = L / 8;
   const uint32_t tid = threadIdx.x;
   constexpr int U = 2;
-  for (uint32_t base = 0; base < n; base += 256 * U) {
+  for (uint32_t base = 0; base < n; base += NT * U) {
     uint64_t lanes[U][N];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const uint32_t i = min(base + u * 256 + tid, n - 1);
+      const uint32_t i = min(base + u * NT + tid, n - 1);
 #pragma unroll
       for (int w = 0; w < N; ++w) lanes[u][w] = kp[(uint64_t)i * N + w];
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      if (base + u * 256 + tid < n) {
+      if (base + u * NT + tid < n) {
         const XxhFixed<L> x(lanes[u]);
         const uint64_t h0 = x.finish(xxh_fixed_rc<L>(c_bloom.seed[0]));
         uint32_t* blk = s_bits + 16 * (uint32_t)__umul64hi(h0, (uint64_t)nb);
@@ -257,8 +257,10 @@ __device__ inline void bloom_keysL_lds(const uint64_t* __restrict__ kp, uint32_t
   }
 }
 
-template <int MODE>
-__global__ __launch_bounds__(256) void bloom_build_lds(const uint8_t* __restrict__ keys,
+// NT = 256 for large batches (8 workgroups per CU); a batch too small to fill the chip takes
+// NT = 1024 so each leaf's keys spread over 16 waves instead of 4.
+template <int MODE, uint32_t NT>
+__global__ __launch_bounds__(NT) void bloom_build_lds(const uint8_t* __restrict__ keys,
                                                        const uint64_t* __restrict__ offs,
                                                        uint32_t stride,
                                                        const tkv_amq_segment* __restrict__ segs,
@@ -271,26 +273,26 @@ __global__ __launch_bounds__(256) void bloom_build_lds(const uint8_t* __restrict
   const uint32_t tid = threadIdx.x;
   const uint32_t nwords = nb * 16;
 
-  for (uint32_t w = tid; w < nwords; w += 256) s_bits[w] = 0;
+  for (uint32_t w = tid; w < nwords; w += NT) s_bits[w] = 0;
   __syncthreads();
 
   if constexpr (MODE == kKey16) {
     const uint4* kp = reinterpret_cast<const uint4*>(keys) + sg.key_begin;
     // k = 7 / 8 are the hash counts at 10 / 12 bits per key: fully unrolled variants
-    if (k == 7) bloom_keys16_lds<7>(kp, n, nb, k, s_bits);
-    else if (k == 8) bloom_keys16_lds<8>(kp, n, nb, k, s_bits);
-    else bloom_keys16_lds<0>(kp, n, nb, k, s_bits);
+    if (k == 7) bloom_keys16_lds<7, NT>(kp, n, nb, k, s_bits);
+    else if (k == 8) bloom_keys16_lds<8, NT>(kp, n, nb, k, s_bits);
+    else bloom_keys16_lds<0, NT>(kp, n, nb, k, s_bits);
   } else if constexpr (MODE == kKey24) {
     const uint64_t* kp = reinterpret_cast<const uint64_t*>(keys) + 3 * sg.key_begin;
     if (n != 0) {
-      if (k == 7) bloom_keysL_lds<7, 24>(kp, n, nb, k, s_bits);
-      else if (k == 8) bloom_keysL_lds<8, 24>(kp, n, nb, k, s_bits);
-      else bloom_keysL_lds<0, 24>(kp, n, nb, k, s_bits);
+      if (k == 7) bloom_keysL_lds<7, 24, NT>(kp, n, nb, k, s_bits);
+      else if (k == 8) bloom_keysL_lds<8, 24, NT>(kp, n, nb, k, s_bits);
+      else bloom_keysL_lds<0, 24, NT>(kp, n, nb, k, s_bits);
     }
   } else {
     // one key per thread per iteration (two in flight measured 2% slower: the loop is
     // VALU-bound, every lane paying for the longest key of its wave)
-    for (uint32_t i = tid; i < n; i += 256) {
+    for (uint32_t i = tid; i < n; i += NT) {
       uint32_t len;
       const uint8_t* p = key_at<MODE>(keys, offs, stride, sg.key_begin + i, len);
       if (k == 7) bloom_insert_any<7, MODE>(s_bits, nb, k, p, len);
@@ -305,7 +307,7 @@ __global__ __launch_bounds__(256) void bloom_build_lds(const uint8_t* __restrict
   else if (tid < 8) write_page_header(out, sg, kLayoutBloom, tid - 4);
   uint4* dst = reinterpret_cast<uint4*>(payload + kBloomHeader);
   const uint4* src = reinterpret_cast<const uint4*>(s_bits);
-  for (uint32_t q = tid; q < nb * 4; q += 256) dst[q] = src[q];
+  for (uint32_t q = tid; q < nb * 4; q += NT) dst[q] = src[q];
 }
 
 // ---------------------------------------------------------------------------------------
@@ -808,8 +810,11 @@ __device__ inline bool page_id_matches(const uint8_t* payload, uint32_t id_off, 
   return ids == nullptr || *reinterpret_cast<const uint64_t*>(payload + id_off) == ids[i];
 }
 
-// One Bloom (query, leaf) test: result bit | class << 1.
-template <int MODE>
+// One Bloom (query, leaf) test: result bit | class << 1 (the class only with kOpts).  Without
+// kOpts the control flow is the plain probe's: no early exit, so the key load is issued
+// side by side with the segment index and descriptor loads (an early "no filter" return
+// made the compiler sink it behind them: 11% slower).
+template <int MODE, bool kOpts>
 __device__ inline uint32_t bloom_probe_item(const uint8_t* __restrict__ filters,
                                             const tkv_amq_segment* __restrict__ segs, uint32_t n_segs,
                                             const uint8_t* __restrict__ q,
@@ -828,11 +833,16 @@ __device__ inline uint32_t bloom_probe_item(const uint8_t* __restrict__ filters,
     const uint4* blk = reinterpret_cast<const uint4*>(filters + d.out_offset + kBloomHeader +
                                                       64 * __umul64hi(h0, (uint64_t)d.n_blocks));
     // hash_count 0: no filter page => reject_page returns kUnknown => cannot reject
-    if (d.hash_count == 0) return 1u | (kNoFilter << 1);
-    if (!page_id_matches(filters + d.out_offset, 16, page_ids, i)) return 1u | (kIdMismatch << 1);
-    if (d.hash_count == 7) ok = probe_block16<7>(x, h0, blk, slot);
-    else if (d.hash_count == 8) ok = probe_block16<8>(x, h0, blk, slot);
-    else ok = probe_block16<0>(x, h0, blk, slot, d.hash_count);
+    uint32_t cls = d.hash_count == 0 ? kNoFilter : kChecked;
+    if constexpr (kOpts) {
+      if (cls == kChecked && !page_id_matches(filters + d.out_offset, 16, page_ids, i)) cls = kIdMismatch;
+    }
+    if (!kOpts || cls == kChecked) {
+      if (d.hash_count == 7) ok = probe_block16<7>(x, h0, blk, slot);
+      else if (d.hash_count == 8) ok = probe_block16<8>(x, h0, blk, slot);
+      else if (d.hash_count != 0) ok = probe_block16<0>(x, h0, blk, slot, d.hash_count);
+    }
+    return (ok & 1u) | (cls << 1);
   } else {
     const ProbeDesc d = load_probe_desc(segs, sidx, n_segs);
     if (d.hash_count == 0) return 1u | (kNoFilter << 1);
@@ -880,14 +890,14 @@ __global__ __launch_bounds__(256) void bloom_probe(const uint8_t* __restrict__ f
   if constexpr (!kOpts) {
     const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
-    const uint32_t r = bloom_probe_item<MODE>(filters, segs, n_segs, q, qoffs, stride, i,
-                                              __builtin_nontemporal_load(qseg + i), slot, nullptr);
+    const uint32_t r = bloom_probe_item<MODE, false>(filters, segs, n_segs, q, qoffs, stride, i,
+                                                     __builtin_nontemporal_load(qseg + i), slot, nullptr);
     __builtin_nontemporal_store((uint8_t)(r & 1u), result + i);
   } else {
     ProbeTally t;
     for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
-      const uint32_t r = bloom_probe_item<MODE>(filters, segs, n_segs, q, qoffs, stride, i, qseg[i],
-                                                slot, opts.d_query_page_id);
+      const uint32_t r = bloom_probe_item<MODE, true>(filters, segs, n_segs, q, qoffs, stride, i,
+                                                      qseg[i], slot, opts.d_query_page_id);
       result[i] = (uint8_t)(r & 1u);
       t.add(r, opts.d_truth, i);
     }
@@ -1838,6 +1848,7 @@ __device__ inline bool vqf_present(const uint8_t* payload, uint32_t n_blocks, ui
 }
 
 // One VQF (hash, leaf) test: result bit | class << 1.
+template <bool kOpts>
 __device__ inline uint32_t vqf_probe_one(const uint8_t* filters, const tkv_amq_segment* segs,
                                          uint32_t n_segs, uint32_t s, uint64_t h,
                                          const uint64_t* page_ids = nullptr, uint64_t i = 0)
@@ -1845,7 +1856,9 @@ __device__ inline uint32_t vqf_probe_one(const uint8_t* filters, const tkv_amq_s
   const ProbeDesc d = load_probe_desc(segs, s, n_segs);
   if (d.tag_bits == 0) return 1u | (kNoFilter << 1);  // no filter: cannot reject
   const uint8_t* payload = filters + d.out_offset;
-  if (!page_id_matches(payload, 8, page_ids, i)) return 1u | (kIdMismatch << 1);
+  if constexpr (kOpts) {
+    if (!page_id_matches(payload, 8, page_ids, i)) return 1u | (kIdMismatch << 1);
+  }
   const uint64_t mask = ~0ull << d.hash_val_shift;  // == PackedVqfFilter::hash_mask
   // dropped hash values are always "maybe" (:115-117)
   if ((h & mask) != h) return 1u | (kChecked << 1);
@@ -1881,13 +1894,13 @@ __global__ __launch_bounds__(256) void vqf_probe(const uint8_t* __restrict__ fil
     if (i >= n) return;
     const uint64_t h = vqf_query_hash<MODE>(q, qoffs, stride, i);
     __builtin_nontemporal_store(
-        (uint8_t)(vqf_probe_one(filters, segs, n_segs, __builtin_nontemporal_load(qseg + i), h) & 1u),
+        (uint8_t)(vqf_probe_one<false>(filters, segs, n_segs, __builtin_nontemporal_load(qseg + i), h) & 1u),
         result + i);
   } else {
     ProbeTally t;
     for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
-      const uint32_t r = vqf_probe_one(filters, segs, n_segs, qseg[i],
-                                       vqf_query_hash<MODE>(q, qoffs, stride, i), opts.d_query_page_id, i);
+      const uint32_t r = vqf_probe_one<true>(filters, segs, n_segs, qseg[i],
+                                             vqf_query_hash<MODE>(q, qoffs, stride, i), opts.d_query_page_id, i);
       result[i] = (uint8_t)(r & 1u);
       t.add(r, opts.d_truth, i);
     }
@@ -1906,8 +1919,8 @@ __global__ __launch_bounds__(256) void vqf_probe_hashed(const uint8_t* __restric
   ProbeTally t;
   for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
     const uint64_t qi = pair_query ? pair_query[i] : i;
-    const uint32_t r = vqf_probe_one(filters, segs, n_segs, qseg[i], hashes[qi],
-                                     kOpts ? opts.d_query_page_id : nullptr, i);
+    const uint32_t r = vqf_probe_one<kOpts>(filters, segs, n_segs, qseg[i], hashes[qi],
+                                            opts.d_query_page_id, i);
     result[i] = (uint8_t)(r & 1u);
     if constexpr (kOpts) t.add(r, opts.d_truth, i);
     else break;
@@ -2046,6 +2059,25 @@ constexpr uint32_t kBloomLdsBudget = 64 * 1024;
 // site, or a small LeafBatcher batch) keeps a few CUs busy for the whole leaf.  Below this many
 // leaves the keys are spread over n_keys/256 workgroups that set bits with device atomics.
 constexpr uint32_t kBloomSpreadSegs = 64;
+// Below this many leaves one 256-thread workgroup per leaf leaves most of the chip idle: the
+// leaf kernel runs 1024 threads per leaf instead.
+constexpr uint32_t kBloomWideSegs = 1024;
+
+template <uint32_t NT>
+void launch_bloom_lds(int bmode, int mode, uint32_t n_segs, size_t lds, hipStream_t s,
+                      const uint8_t* keys, const uint64_t* offs, uint32_t stride,
+                      const tkv_amq_segment* d_segs, uint8_t* d_out)
+{
+  const dim3 grid(n_segs), block(NT);
+  if (bmode == kKey24)
+    hipLaunchKernelGGL((bloom_build_lds<kKey24, NT>), grid, block, lds, s, keys, offs, stride, d_segs, d_out);
+  else if (mode == kKey16)
+    hipLaunchKernelGGL((bloom_build_lds<kKey16, NT>), grid, block, lds, s, keys, offs, stride, d_segs, d_out);
+  else if (mode == kKeyFixed)
+    hipLaunchKernelGGL((bloom_build_lds<kKeyFixed, NT>), grid, block, lds, s, keys, offs, stride, d_segs, d_out);
+  else
+    hipLaunchKernelGGL((bloom_build_lds<kKeyVar, NT>), grid, block, lds, s, keys, offs, stride, d_segs, d_out);
+}
 
 inline uint32_t vqf_slots(int t) { return t == 8 ? 48u : 28u; }
 inline uint32_t vqf_buckets(int t) { return t == 8 ? 80u : 36u; }
@@ -2345,20 +2377,12 @@ int tkv_amq_build(int kind, const uint8_t* keys, const uint64_t* offs, uint32_t 
     const uint64_t lds = 64ull * max_blocks;
     if (max_blocks == 0) return TKV_AMQ_OK;
     if (lds <= kBloomLdsBudget && n_segs >= kBloomSpreadSegs) {
-      const dim3 grid(n_segs), block(256);
       const int bmode = build_key_mode(keys, offs, stride);
-      if (bmode == kKey24)
-        hipLaunchKernelGGL(bloom_build_lds<kKey24>, grid, block, lds, s, keys, offs, stride, d_segs,
-                           d_out);
-      else if (mode == kKey16)
-        hipLaunchKernelGGL(bloom_build_lds<kKey16>, grid, block, lds, s, keys, offs, stride, d_segs,
-                           d_out);
-      else if (mode == kKeyFixed)
-        hipLaunchKernelGGL(bloom_build_lds<kKeyFixed>, grid, block, lds, s, keys, offs, stride,
-                           d_segs, d_out);
-      else
-        hipLaunchKernelGGL(bloom_build_lds<kKeyVar>, grid, block, lds, s, keys, offs, stride, d_segs,
-                           d_out);
+      if (n_segs < kBloomWideSegs) {
+        launch_bloom_lds<1024>(bmode, mode, n_segs, lds, s, keys, offs, stride, d_segs, d_out);
+      } else {
+        launch_bloom_lds<256>(bmode, mode, n_segs, lds, s, keys, offs, stride, d_segs, d_out);
+      }
       return hipGetLastError() == hipSuccess ? TKV_AMQ_OK : TKV_AMQ_INTERNAL;
     }
     const BloomPartGeom pg = bloom_part_geom(n_keys, max_blocks);
