@@ -655,6 +655,8 @@ def batch_sweep(torch, amq, kind, bpk, cap, counts, kb, ws, plan_all, kernel_ms_
         sub = (amq.KeyBatch.fixed(kb.data[:nk]) if kb.offsets is None else
                amq.KeyBatch.variable(kb.data, kb.offsets[:nk + 1]))
         o = torch.empty(max(p.total_out_bytes, 1), dtype=torch.uint8, device=kb.data.device)
+        if p.workspace_bytes > ws.numel():  # (small Bloom batches split leaves over workgroups)
+            ws = torch.empty(p.workspace_bytes, dtype=torch.uint8, device=kb.data.device)
         for _ in range(5):
             amq.build_all_filters(p, sub, out=o, workspace=ws, check=False)
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))

@@ -158,8 +158,9 @@ def test_variable_length_keys_many_leaves(oracle, amq, torch, big_leaf):
 @pytest.mark.parametrize("n_leaves", [64, 300, 1023, 1024])
 @pytest.mark.parametrize("shape", ["k16", "k24", "var"])
 def test_bloom_leaf_kernel_widths(oracle, amq, torch, n_leaves, shape):
-    """The leaf kernel runs 1024 threads per leaf below 1024 leaves and 256 from there: both
-    widths, every key shape, ragged leaves, against the oracle (sampled leaves)."""
+    """Below 1024 leaves each leaf's keys are split over several workgroups whose images are
+    ORed by the last one (bloom_build_split); from 1024 leaves one workgroup per leaf
+    (bloom_build_lds).  Both, every key shape, ragged leaves, against the oracle (sampled)."""
     rng = np.random.default_rng(n_leaves)
     counts = [int(c) for c in rng.integers(0, 3000, n_leaves)]
     counts[0], counts[1], counts[-1] = 0, 16384, 1
@@ -186,6 +187,30 @@ def test_bloom_leaf_kernel_widths(oracle, amq, torch, n_leaves, shape):
             st, ref = oracle.bloom_build(keys[int(offs[b]):], c, 10, src_page_id=s, offsets=o, stride=0)
         assert st == 0
         assert segment_bytes(plan, out, s) == ref.tobytes(), f"leaf {s}"
+
+
+@pytest.mark.parametrize("counts", [[16384], [16384, 9000, 1, 0, 52000], [3000] * 200])
+def test_bloom_split_matches_unsplit(oracle, amq, torch, counts):
+    """The split build (workspace given) and the one-workgroup / atomic builds (no workspace)
+    write the same bytes; the split one also equals the oracle (a 52K-key leaf: a 64 KiB
+    image, the largest the LDS paths take)."""
+    keys = oracle.gen_keys16(9, 0, sum(counts))
+    kt = torch.from_numpy(keys).cuda()
+    plan = amq.plan_filters(0, counts, 10)
+    assert plan.workspace_bytes > 0
+    a = amq.build_all_filters(plan, amq.KeyBatch.fixed(kt))
+    L, F = amq.abi.lib(), amq.filters
+    b = torch.zeros_like(a)
+    st = L.tkv_amq_build(0, F._ptr(kt), None, 16, kt.shape[0], F._ptr(plan.device_segs()), plan.n_segs,
+                         plan.max_seg_blocks, F._ptr(b), None, 0, F._stream_handle())
+    assert st == 0
+    torch.cuda.synchronize()
+    an, bn = a.cpu().numpy(), b.cpu().numpy()
+    sb = seg_bounds(counts)
+    for s in range(len(counts)):
+        assert segment_bytes(plan, an, s) == segment_bytes(plan, bn, s), f"leaf {s}"
+        st, ref = oracle.bloom_build(keys[int(sb[s]):], counts[s], 10, src_page_id=s)
+        assert segment_bytes(plan, an, s) == ref.tobytes(), f"leaf {s}"
 
 
 def sorted_keys(oracle, seed, counts):

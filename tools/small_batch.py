@@ -1,0 +1,53 @@
+"""Time builds of the first L leaves of the bench layout (16,384-key leaves, 16-byte keys) for
+several L: the small-batch curve (a checkpoint's build_all_pages queue holds tens to
+thousands of leaves).  Run under rocprofv3 --kernel-trace --stats for per-kernel times.
+
+  python tools/small_batch.py [--kind 0|1] [--leaves 1,8,64,256,1024] [--reps 50]
+"""
+import argparse
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import turtle_kv_amd as amq  # noqa: E402
+from bench import sort_segments_device  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--kind", type=int, default=0)
+    ap.add_argument("--bpk", type=int, default=0)
+    ap.add_argument("--leaves", default="1,8,64,256,1024")
+    ap.add_argument("--reps", type=int, default=50)
+    a = ap.parse_args()
+    bpk = a.bpk or (10 if a.kind == 0 else 12)
+    cap = amq.TreeOptions(a.kind).set_filter_bits_per_key(bpk).filter_page_payload_size() if a.kind else 0
+    for L in [int(x) for x in a.leaves.split(",")]:
+        counts = [16384] * L
+        keys = amq.gen_keys16(42, 0, 16384 * L)
+        if a.kind == 1:
+            keys = sort_segments_device(torch, keys, counts)
+        kb = amq.KeyBatch.fixed(keys)
+        plan = amq.plan_filters(a.kind, counts, bpk, payload_capacity=cap)
+        out = torch.empty(plan.total_out_bytes, dtype=torch.uint8, device="cuda")
+        ws = torch.empty(max(plan.workspace_bytes, 1), dtype=torch.uint8, device="cuda")
+        for _ in range(5):
+            amq.build_all_filters(plan, kb, out=out, workspace=ws, check=False)
+        torch.cuda.synchronize()
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(a.reps)]
+        for e0, e1 in ev:
+            e0.record()
+            amq.build_all_filters(plan, kb, out=out, workspace=ws, check=False)
+            e1.record()
+        torch.cuda.synchronize()
+        ms = float(np.median([e0.elapsed_time(e1) for e0, e1 in ev]))
+        print(f"kind {a.kind} leaves {L:5d} keys {16384 * L:9d} median {ms * 1e3:8.1f} us "
+              f"{16384 * L / ms / 1e3:9.1f} Mkeys/s ws {plan.workspace_bytes}", flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -257,8 +257,41 @@ __device__ inline void bloom_keysL_lds(const uint64_t* __restrict__ kp, uint32_t
   }
 }
 
-// NT = 256 for large batches (8 workgroups per CU); a batch too small to fill the chip takes
-// NT = 1024 so each leaf's keys spread over 16 waves instead of 4.
+// Keys [kb, ke) of one leaf into its LDS image s_bits (NT threads).
+template <int MODE, uint32_t NT>
+__device__ inline void bloom_leaf_image(const uint8_t* __restrict__ keys,
+                                        const uint64_t* __restrict__ offs, uint32_t stride,
+                                        const tkv_amq_segment& sg, uint32_t kb, uint32_t ke,
+                                        uint32_t* s_bits)
+{
+  const uint32_t n = ke - kb, nb = sg.n_blocks, k = sg.hash_count;
+  if constexpr (MODE == kKey16) {
+    const uint4* kp = reinterpret_cast<const uint4*>(keys) + sg.key_begin + kb;
+    // k = 7 / 8 are the hash counts at 10 / 12 bits per key: fully unrolled variants
+    if (k == 7) bloom_keys16_lds<7, NT>(kp, n, nb, k, s_bits);
+    else if (k == 8) bloom_keys16_lds<8, NT>(kp, n, nb, k, s_bits);
+    else bloom_keys16_lds<0, NT>(kp, n, nb, k, s_bits);
+  } else if constexpr (MODE == kKey24) {
+    const uint64_t* kp = reinterpret_cast<const uint64_t*>(keys) + 3 * (sg.key_begin + kb);
+    if (n != 0) {
+      if (k == 7) bloom_keysL_lds<7, 24, NT>(kp, n, nb, k, s_bits);
+      else if (k == 8) bloom_keysL_lds<8, 24, NT>(kp, n, nb, k, s_bits);
+      else bloom_keysL_lds<0, 24, NT>(kp, n, nb, k, s_bits);
+    }
+  } else {
+    // one key per thread per iteration (two in flight measured 2% slower: the loop is
+    // VALU-bound, every lane paying for the longest key of its wave)
+    for (uint32_t i = kb + threadIdx.x; i < ke; i += NT) {
+      uint32_t len;
+      const uint8_t* p = key_at<MODE>(keys, offs, stride, sg.key_begin + i, len);
+      if (k == 7) bloom_insert_any<7, MODE>(s_bits, nb, k, p, len);
+      else if (k == 8) bloom_insert_any<8, MODE>(s_bits, nb, k, p, len);
+      else bloom_insert_any<0, MODE>(s_bits, nb, k, p, len);
+    }
+  }
+}
+
+// One workgroup per leaf filter (batches of >= kBloomSplitSegs leaves).
 template <int MODE, uint32_t NT>
 __global__ __launch_bounds__(NT) void bloom_build_lds(const uint8_t* __restrict__ keys,
                                                        const uint64_t* __restrict__ offs,
@@ -275,31 +308,7 @@ __global__ __launch_bounds__(NT) void bloom_build_lds(const uint8_t* __restrict_
 
   for (uint32_t w = tid; w < nwords; w += NT) s_bits[w] = 0;
   __syncthreads();
-
-  if constexpr (MODE == kKey16) {
-    const uint4* kp = reinterpret_cast<const uint4*>(keys) + sg.key_begin;
-    // k = 7 / 8 are the hash counts at 10 / 12 bits per key: fully unrolled variants
-    if (k == 7) bloom_keys16_lds<7, NT>(kp, n, nb, k, s_bits);
-    else if (k == 8) bloom_keys16_lds<8, NT>(kp, n, nb, k, s_bits);
-    else bloom_keys16_lds<0, NT>(kp, n, nb, k, s_bits);
-  } else if constexpr (MODE == kKey24) {
-    const uint64_t* kp = reinterpret_cast<const uint64_t*>(keys) + 3 * sg.key_begin;
-    if (n != 0) {
-      if (k == 7) bloom_keysL_lds<7, 24, NT>(kp, n, nb, k, s_bits);
-      else if (k == 8) bloom_keysL_lds<8, 24, NT>(kp, n, nb, k, s_bits);
-      else bloom_keysL_lds<0, 24, NT>(kp, n, nb, k, s_bits);
-    }
-  } else {
-    // one key per thread per iteration (two in flight measured 2% slower: the loop is
-    // VALU-bound, every lane paying for the longest key of its wave)
-    for (uint32_t i = tid; i < n; i += NT) {
-      uint32_t len;
-      const uint8_t* p = key_at<MODE>(keys, offs, stride, sg.key_begin + i, len);
-      if (k == 7) bloom_insert_any<7, MODE>(s_bits, nb, k, p, len);
-      else if (k == 8) bloom_insert_any<8, MODE>(s_bits, nb, k, p, len);
-      else bloom_insert_any<0, MODE>(s_bits, nb, k, p, len);
-    }
-  }
+  bloom_leaf_image<MODE, NT>(keys, offs, stride, sg, 0, n, s_bits);
   __syncthreads();
 
   uint8_t* payload = out + sg.out_offset;
@@ -308,6 +317,74 @@ __global__ __launch_bounds__(NT) void bloom_build_lds(const uint8_t* __restrict_
   uint4* dst = reinterpret_cast<uint4*>(payload + kBloomHeader);
   const uint4* src = reinterpret_cast<const uint4*>(s_bits);
   for (uint32_t q = tid; q < nb * 4; q += NT) dst[q] = src[q];
+}
+
+// Batches too small to fill the chip with one workgroup per leaf (one leaf per call, or a
+// checkpoint of a few hundred leaves): each leaf's keys are split over `parts` workgroups,
+// each building the image of its key range in LDS and writing it to the workspace
+// (bloom_build_split); bloom_split_merge then ORs a leaf's part images into the filter.  The
+// bits set do not depend on which workgroup set them, so the filter equals the one-workgroup
+// build.  Two kernels, not a last-workgroup merge: the parts of a leaf run on different XCDs,
+// and an agent-scope fence per workgroup (an L2 writeback plus invalidate on each XCD) made
+// the merge pattern 4-9x slower than this.  Workspace: image (s, p) at
+// ((s * parts) + p) * img_stride.
+constexpr uint32_t kSplitThreads = 512;
+constexpr uint32_t kSplitMaxParts = 16;
+constexpr uint32_t kMergeThreads = 256;
+
+template <int MODE>
+__global__ __launch_bounds__(kSplitThreads) void bloom_build_split(
+    const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint32_t stride,
+    const tkv_amq_segment* __restrict__ segs, uint32_t parts, uint8_t* __restrict__ ws,
+    uint64_t img_stride)
+{
+  constexpr uint32_t NT = kSplitThreads;
+  extern __shared__ uint32_t s_bits[];
+  const uint32_t seg = blockIdx.x / parts, part = blockIdx.x - seg * parts;
+  const tkv_amq_segment sg = segs[seg];
+  const uint32_t n = sg.n_keys, nb = sg.n_blocks;
+  if (sg.hash_count == 0) return;  // no filter
+  const uint32_t tid = threadIdx.x;
+  for (uint32_t w = tid; w < nb * 16; w += NT) s_bits[w] = 0;
+  __syncthreads();
+  const uint32_t chunk = (n + parts - 1) / parts;
+  const uint32_t kb = min(n, part * chunk), ke = min(n, kb + chunk);
+  bloom_leaf_image<MODE, NT>(keys, offs, stride, sg, kb, ke, s_bits);
+  __syncthreads();
+  const uint4* img = reinterpret_cast<const uint4*>(s_bits);
+  uint4* dst = reinterpret_cast<uint4*>(ws + (uint64_t)blockIdx.x * img_stride);
+  for (uint32_t q = tid; q < nb * 4; q += NT) dst[q] = img[q];
+}
+
+// one thread per 16-byte word of a leaf's image, kMergeThreads words per workgroup: all the
+// parts' loads are issued together (up to kSplitMaxParts, predicated), then ORed
+__global__ __launch_bounds__(kMergeThreads) void bloom_split_merge(
+    const tkv_amq_segment* __restrict__ segs, uint32_t parts, uint32_t chunks,
+    const uint8_t* __restrict__ ws, uint64_t img_stride, uint8_t* __restrict__ out)
+{
+  const uint32_t seg = blockIdx.x / chunks, c = blockIdx.x - seg * chunks;
+  const tkv_amq_segment sg = segs[seg];
+  if (sg.hash_count == 0) return;
+  const uint32_t tid = threadIdx.x, nq = sg.n_blocks * 4;
+  uint8_t* payload = out + sg.out_offset;
+  if (c == 0 && tid < 4) write_bloom_header(payload, sg, tid);
+  else if (c == 0 && tid < 8) write_page_header(out, sg, kLayoutBloom, tid - 4);
+  const uint32_t q = c * kMergeThreads + tid;
+  if (q >= nq) return;
+  const uint8_t* base = ws + (uint64_t)seg * parts * img_stride + 16ull * q;
+  uint4 o[kSplitMaxParts];
+#pragma unroll
+  for (uint32_t p = 0; p < kSplitMaxParts; ++p)
+    o[p] = p < parts ? load_nt16(base + (uint64_t)p * img_stride) : make_uint4(0, 0, 0, 0);
+  uint4 v = o[0];
+#pragma unroll
+  for (uint32_t p = 1; p < kSplitMaxParts; ++p) {
+    v.x |= o[p].x;
+    v.y |= o[p].y;
+    v.z |= o[p].z;
+    v.w |= o[p].w;
+  }
+  reinterpret_cast<uint4*>(payload + kBloomHeader)[q] = v;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -2059,9 +2136,32 @@ constexpr uint32_t kBloomLdsBudget = 64 * 1024;
 // site, or a small LeafBatcher batch) keeps a few CUs busy for the whole leaf.  Below this many
 // leaves the keys are spread over n_keys/256 workgroups that set bits with device atomics.
 constexpr uint32_t kBloomSpreadSegs = 64;
-// Below this many leaves one 256-thread workgroup per leaf leaves most of the chip idle: the
-// leaf kernel runs 1024 threads per leaf instead.
-constexpr uint32_t kBloomWideSegs = 1024;
+// Below this many leaves (and with the workspace tkv_amq_plan sizes for it) each leaf's keys
+// are split over several workgroups (bloom_build_split): about kSplitTargetWgs workgroups in
+// all, at most kSplitMaxParts per leaf, at least kSplitMinKeys keys each.
+constexpr uint32_t kBloomSplitSegs = 256;
+constexpr uint32_t kSplitTargetWgs = 1024;
+constexpr uint32_t kSplitMinKeys = 1024;
+// From kBloomSplitSegs up to kBloomWideSegs leaves, one 1024-thread workgroup per leaf; from
+// there one 256-thread workgroup per leaf (8 per CU).
+constexpr uint32_t kBloomWideSegs = 2048;
+
+// parts per leaf for a batch of n_segs leaves holding n_keys keys (1: no split)
+inline uint32_t bloom_split_parts(uint32_t n_segs, uint64_t n_keys, uint64_t max_blocks)
+{
+  if (n_segs == 0 || n_segs >= kBloomSplitSegs || 64 * max_blocks > kBloomLdsBudget) return 1;
+  uint64_t p = (kSplitTargetWgs + n_segs - 1) / n_segs;
+  const uint64_t per_leaf = n_keys / n_segs;
+  const uint64_t by_keys = per_leaf / kSplitMinKeys;
+  if (p > by_keys) p = by_keys;
+  if (p > kSplitMaxParts) p = kSplitMaxParts;
+  return p < 2 ? 1u : (uint32_t)p;
+}
+
+inline uint64_t bloom_split_ws_bytes(uint32_t n_segs, uint32_t parts, uint64_t max_blocks)
+{
+  return parts < 2 ? 0 : (uint64_t)n_segs * parts * 64 * max_blocks;
+}
 
 template <uint32_t NT>
 void launch_bloom_lds(int bmode, int mode, uint32_t n_segs, size_t lds, hipStream_t s,
@@ -2338,6 +2438,9 @@ int tkv_amq_plan(int kind, const uint64_t* counts, const uint64_t* src_ids, uint
       *ws_bytes = vqf_temp_offset(n_segs) + kVqfTempStride * block_base + 8 * key_begin + 64;
     if (kind == TKV_AMQ_BLOOM && bloom_partitioned(n_segs, max_blocks, key_begin))
       *ws_bytes = bloom_part_geom(key_begin, max_blocks).bytes;  // 16-byte keys
+    else if (kind == TKV_AMQ_BLOOM)
+      *ws_bytes = bloom_split_ws_bytes(n_segs, bloom_split_parts(n_segs, key_begin, max_blocks),
+                                       max_blocks);
   }
   if (max_blocks_out) *max_blocks_out = max_blocks;
   return TKV_AMQ_OK;
@@ -2376,13 +2479,49 @@ int tkv_amq_build(int kind, const uint8_t* keys, const uint64_t* offs, uint32_t 
   if (kind == TKV_AMQ_BLOOM) {
     const uint64_t lds = 64ull * max_blocks;
     if (max_blocks == 0) return TKV_AMQ_OK;
+    const uint32_t parts = bloom_split_parts(n_segs, n_keys, max_blocks);
+    const uint64_t split_ws = bloom_split_ws_bytes(n_segs, parts, max_blocks);
+    if (parts > 1 && d_ws && ws_bytes >= split_ws) {
+      // a small batch: each leaf's keys over `parts` workgroups, then their images ORed
+      static std::once_flag split_attr[kMaxDevices];
+      once_per_device(split_attr, [] {
+        const int cap = (int)kBloomLdsBudget;
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&bloom_build_split<kKey16>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, cap);
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&bloom_build_split<kKey24>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, cap);
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&bloom_build_split<kKeyFixed>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, cap);
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&bloom_build_split<kKeyVar>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, cap);
+      });
+      const int bmode = build_key_mode(keys, offs, stride);
+      const dim3 grid(n_segs * parts), block(kSplitThreads);
+      uint8_t* w = static_cast<uint8_t*>(d_ws);
+      const uint64_t img = 64ull * max_blocks;
+      if (bmode == kKey24)
+        hipLaunchKernelGGL(bloom_build_split<kKey24>, grid, block, lds, s, keys, offs, stride, d_segs,
+                           parts, w, img);
+      else if (mode == kKey16)
+        hipLaunchKernelGGL(bloom_build_split<kKey16>, grid, block, lds, s, keys, offs, stride, d_segs,
+                           parts, w, img);
+      else if (mode == kKeyFixed)
+        hipLaunchKernelGGL(bloom_build_split<kKeyFixed>, grid, block, lds, s, keys, offs, stride,
+                           d_segs, parts, w, img);
+      else
+        hipLaunchKernelGGL(bloom_build_split<kKeyVar>, grid, block, lds, s, keys, offs, stride, d_segs,
+                           parts, w, img);
+      const uint32_t chunks = (uint32_t)div_up(4ull * max_blocks, kMergeThreads);
+      hipLaunchKernelGGL(bloom_split_merge, dim3(n_segs * chunks), dim3(kMergeThreads), 0, s, d_segs,
+                         parts, chunks, w, img, d_out);
+      return hipGetLastError() == hipSuccess ? TKV_AMQ_OK : TKV_AMQ_INTERNAL;
+    }
     if (lds <= kBloomLdsBudget && n_segs >= kBloomSpreadSegs) {
       const int bmode = build_key_mode(keys, offs, stride);
-      if (n_segs < kBloomWideSegs) {
+      if (n_segs < kBloomWideSegs)
         launch_bloom_lds<1024>(bmode, mode, n_segs, lds, s, keys, offs, stride, d_segs, d_out);
-      } else {
+      else
         launch_bloom_lds<256>(bmode, mode, n_segs, lds, s, keys, offs, stride, d_segs, d_out);
-      }
       return hipGetLastError() == hipSuccess ? TKV_AMQ_OK : TKV_AMQ_INTERNAL;
     }
     const BloomPartGeom pg = bloom_part_geom(n_keys, max_blocks);
