@@ -5,10 +5,10 @@
 #   gpurun -- ./tools/gpu/profile_round.sh
 set -o pipefail
 R=$GRAFT_REPO_ROOT; cd $R
-O=$R/gpurun_out/round
+O=$R/gpurun_out/${O:-round}
 mkdir -p $O
 export TMPDIR=/tmp
-timeout -k 10 400 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread > $O/gpu_tests.log 2>&1 || exit 2
+timeout -k 10 900 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1 || exit 2
 timeout -k 10 300 python bench.py > $O/bench_bloom10.log 2>&1 || exit 3
 timeout -k 10 300 python bench.py --workload vqf12 --no-e2e > $O/bench_vqf12.log 2>&1 || exit 4
 timeout -k 10 300 python bench.py --workload probe10 > $O/bench_probe10.log 2>&1 || exit 5
