@@ -87,8 +87,10 @@ def parse():
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-verify", action="store_true",
                     help="skip the post-timing oracle comparison (kernel experiments only)")
-    ap.add_argument("--no-sweep", action="store_true",
-                    help="skip the batch-size sweep (64 / 256 / 1024 / all leaves)")
+    ap.add_argument("--sweep", action="store_true",
+                    help="also time the build over the first 64 / 256 / 1024 leaves (batch-size "
+                         "curve; off by default so that a kernel-trace profile of the default "
+                         "command averages the timed launches only)")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="CPU baseline threads (0: every core this process may use)")
     return ap.parse_args()
@@ -437,7 +439,7 @@ def main():
                                       key_bytes, dev)
 
     sweep = None
-    if rank == 0 and world == 1 and not probe and not args.no_sweep and \
+    if rank == 0 and world == 1 and not probe and args.sweep and \
             args.workload not in MONOLITHIC and len(counts) > SWEEP_LEAVES[0]:
         sweep = batch_sweep(torch, amq, kind, bpk, cap, counts, kb, ws, plan, kernel_ms)
 

@@ -99,7 +99,7 @@ def test_bench_single_gpu_line():
     """The default line's shape at a small size: verified sample, batch-size sweep, a CPU
     baseline with the host's CPU share stated."""
     r = run_bench("--keys-per-gpu", "3000000", "--steps", "3", "--warmup", "1", "--ramp-ms", "0",
-                  "--no-e2e")
+                  "--no-e2e", "--sweep")
     assert r.returncode == 0, r.stderr[-4000:]
     d = last_json(r)
     assert d["n_gpus"] == 1 and d["verified"] is True
