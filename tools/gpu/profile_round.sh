@@ -35,9 +35,9 @@ fi
 cd /tmp
 if has prof; then
   # kernel-trace stats of the exact default bench command, and of the other workloads
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -T -d $O/prof_bloom10 -o run --output-format csv -- python3 $R/bench.py > $O/prof_bloom10.log 2>&1 || exit 11
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_bloom10 -o run --output-format csv -- python3 $R/bench.py > $O/prof_bloom10.log 2>&1 || exit 11
   for W in vqf12 probe10 probe_vqf12 bloom10mono; do
-    timeout -k 10 300 rocprofv3 --kernel-trace --stats -T -d $O/prof_$W -o run --output-format csv -- python3 $R/bench.py --workload $W --no-cpu-baseline --no-e2e > $O/prof_$W.log 2>&1 || exit 12
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_$W -o run --output-format csv -- python3 $R/bench.py --workload $W --no-cpu-baseline --no-e2e > $O/prof_$W.log 2>&1 || exit 12
   done
 fi
 if has pmc; then

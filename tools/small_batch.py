@@ -22,6 +22,8 @@ def main():
     ap.add_argument("--bpk", type=int, default=0)
     ap.add_argument("--leaves", default="1,8,64,256,1024")
     ap.add_argument("--reps", type=int, default=50)
+    ap.add_argument("--no-ws", action="store_true",
+                    help="call the ABI without a workspace (Bloom: the unsplit paths)")
     a = ap.parse_args()
     bpk = a.bpk or (10 if a.kind == 0 else 12)
     cap = amq.TreeOptions(a.kind).set_filter_bits_per_key(bpk).filter_page_payload_size() if a.kind else 0
@@ -34,14 +36,24 @@ def main():
         plan = amq.plan_filters(a.kind, counts, bpk, payload_capacity=cap)
         out = torch.empty(plan.total_out_bytes, dtype=torch.uint8, device="cuda")
         ws = torch.empty(max(plan.workspace_bytes, 1), dtype=torch.uint8, device="cuda")
+        lib, F = amq.abi.lib(), amq.filters
+        segs = plan.device_segs()
+
+        def build():
+            if a.no_ws:
+                amq.abi.check(lib.tkv_amq_build(a.kind, F._ptr(kb.data), None, 16, kb.n, F._ptr(segs),
+                                              plan.n_segs, plan.max_seg_blocks, F._ptr(out), None, 0,
+                                              F._stream_handle()), "build")
+            else:
+                amq.build_all_filters(plan, kb, out=out, workspace=ws, check=False)
         for _ in range(5):
-            amq.build_all_filters(plan, kb, out=out, workspace=ws, check=False)
+            build()
         torch.cuda.synchronize()
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
               for _ in range(a.reps)]
         for e0, e1 in ev:
             e0.record()
-            amq.build_all_filters(plan, kb, out=out, workspace=ws, check=False)
+            build()
             e1.record()
         torch.cuda.synchronize()
         ms = float(np.median([e0.elapsed_time(e1) for e0, e1 in ev]))
