@@ -272,6 +272,49 @@ def test_vqf_unsorted_and_duplicate_keys(oracle, amq, torch):
     assert_same(plan, out, ref)
 
 
+@pytest.mark.parametrize("n_leaves", [40, 512, 513])
+@pytest.mark.parametrize("shape", ["k16", "k24", "var"])
+def test_vqf_decide_paths(oracle, amq, torch, n_leaves, shape):
+    """Batches of up to 512 leaves take vqf_decide_resident (the leaf's key locations in LDS,
+    one decider wave), larger ones vqf_decide (one wave per leaf).  Inside the resident
+    kernel a leaf whose locations do not fit (30000 keys) runs vqf_decide's body, without
+    the LDS match table (> 512 blocks).  8- and 16-bit tags (12 / 22 bits per key; at 22 a
+    16384-key leaf has > 512 blocks and stays resident), ragged leaves, sampled against the
+    oracle."""
+    rng = np.random.default_rng(1000 + n_leaves)
+    counts = [int(c) for c in rng.integers(0, 3000, n_leaves)]
+    counts[0], counts[1], counts[2], counts[-1] = 0, 16384, 30000, 1
+    n = sum(counts)
+    offs = None
+    if shape == "k16":
+        keys, stride = oracle.gen_keys16(5, 0, n), 16
+    elif shape == "k24":
+        keys, stride = rng.integers(0, 256, (n, 24), dtype=np.uint8), 24
+    else:  # >= 6 bytes: duplicates of very short keys would overflow a block (as in the oracle)
+        lens = rng.integers(6, 40, n)
+        keys, stride = rng.integers(0, 256, int(lens.sum()), dtype=np.uint8), 0
+        offs = np.zeros(n + 1, np.int64)
+        offs[1:] = np.cumsum(lens)
+    sb = seg_bounds(counts)
+    for bpk in (12, 22):
+        plan, out = gpu_build(amq, torch, 1, torch.from_numpy(keys).cuda(), counts, bpk, cap=65472,
+                              offsets_t=None if offs is None else torch.from_numpy(offs).cuda())
+        if bpk == 12:
+            assert plan.segs["n_blocks"][2] > 512 and plan.segs["n_blocks"][1] <= 512
+        else:
+            assert plan.segs["n_blocks"][1] > 512 and 16 in set(plan.segs["tag_bits"].tolist())
+        for s in sorted({0, 1, 2, n_leaves - 1, *rng.integers(0, n_leaves, 10).tolist()}):
+            b, c = int(sb[s]), counts[s]
+            if offs is None:
+                st, ref, p = oracle.vqf_build(keys[b:], c, bpk, 65472, src_page_id=s, stride=stride)
+            else:
+                o = (offs[b:b + c + 1] - offs[b]).astype(np.uint64)
+                st, ref, p = oracle.vqf_build(keys[int(offs[b]):], c, bpk, 65472, src_page_id=s,
+                                              offsets=o, stride=0)
+            assert st == 0
+            assert segment_bytes(plan, out, s) == ref[:p.payload_used].tobytes(), f"bpk {bpk} leaf {s}"
+
+
 def probe_inputs(oracle, n_keys, counts, n_miss):
     hits = np.arange(n_keys)
     seg_of = np.repeat(np.arange(len(counts)), counts)

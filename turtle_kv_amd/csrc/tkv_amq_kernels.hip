@@ -1006,7 +1006,8 @@ constexpr uint32_t kVqfTempStride = 128;  // workspace bytes per block (>= slots
 constexpr uint32_t kVqfMaxLdsBlocks = 16384;
 constexpr uint32_t kVqfMatchLdsBlocks = 512;  // vqf_decide's LDS lane-mask table (8 B/block)
 
-// workspace: [status u32 x16][nelts u32 x n_segs][pad to 256][128-byte record per block]
+// workspace: [status u32 x8][record sink u64 x4][nelts u32 x n_segs][pad to 256]
+//            [128-byte record per block]
 //            [u64 placement record per key]
 // block record = slots x Entry (insertion order) ... u32 final count at byte 124
 // key record (written by vqf_decide in key order, coalesced; scattered by vqf_scatter):
@@ -1016,6 +1017,7 @@ struct VqfWorkspace {
   uint32_t* status;
   uint32_t* nelts;
   uint8_t* temp;
+  uint64_t* sink;  // write-only target of vqf_decide's stores for lanes with no record
 };
 constexpr uint32_t kVqfCountByte = 124;
 
@@ -1030,6 +1032,7 @@ __host__ __device__ inline VqfWorkspace vqf_workspace(void* base, uint32_t n_seg
   VqfWorkspace w;
   w.status = reinterpret_cast<uint32_t*>(p);
   w.nelts = reinterpret_cast<uint32_t*>(p + 64);
+  w.sink = reinterpret_cast<uint64_t*>(p + 32);
   w.temp = p + vqf_temp_offset(n_segs);
   return w;
 }
@@ -1149,7 +1152,9 @@ __device__ void vqf_decide_body(const uint8_t* __restrict__ keys, const uint64_t
     cnt[b] = 0;
     if constexpr (kLdsMatch) mt[b] = 0;
   }
-  __syncthreads();
+  // one wave: its LDS operations execute in order, so no workgroup barrier (the body also
+  // runs in wave 0 of vqf_decide_ring's workgroup after the other waves have left)
+  asm volatile("" ::: "memory");
   const unsigned long long mybit = 1ull << lane;
 
   uint32_t nelts = 0;
@@ -1164,9 +1169,13 @@ __device__ void vqf_decide_body(const uint8_t* __restrict__ keys, const uint64_t
   // the next step (after that step's loads), so a wait for the key prefetch never waits
   // for a store issued just before it.  (Scattering each tag straight into its block's
   // record from here made every step wait on partial-line writes: 2.1x slower.)
-  Rec* pend_ptr = rec;
+  // The store is unconditional (lanes with nothing to write hit a sink word), so the number
+  // of memory operations issued after each key load is fixed and the compiler's wait for
+  // that load (s_waitcnt vmcnt counts loads and stores in issue order) lets the later load
+  // and the stores stay in flight; a skippable store made it wait for the newest load too.
+  Rec* const sink = reinterpret_cast<Rec*>(ws.sink);
+  Rec* pend_ptr = sink;
   Rec pend_val = 0;
-  bool pend = false;
   auto step = [&](uint32_t base, VqfLoc& cur, const uint4& kv_hash, uint4& kv_load) {
     const VqfLoc L = cur;
     // primary block counts before this chunk (every lane reads: an invalid lane's block is 0)
@@ -1178,11 +1187,11 @@ __device__ void vqf_decide_body(const uint8_t* __restrict__ keys, const uint64_t
       // branch-free (clamped index, select on the result): straight-line code lets the
       // compiler count vmcnt exactly instead of draining every outstanding access
       kv_load = kp[min(inext + 64, n - 1)];
-      if (pend) *pend_ptr = pend_val;
+      *pend_ptr = pend_val;
       const uint64_t hh = vqf_key_hash<MODE>(keys, offs, stride, 0, kv_hash);
       hn = vnext ? hh : 0;
     } else {
-      if (pend) *pend_ptr = pend_val;
+      *pend_ptr = pend_val;
       hn = vnext ? vqf_key_hash<MODE>(keys, offs, stride, sg.key_begin + inext, kv_hash) : 0;
     }
 
@@ -1301,8 +1310,7 @@ __device__ void vqf_decide_body(const uint8_t* __restrict__ keys, const uint64_t
     const uint32_t cho = alt ? ao : L.po;
     const uint32_t r = alt ? ca : cp;  // count of the chosen block when this key is inserted
     fail |= (uint32_t)(__ballot(L.kept && r >= C::kSlots) != 0);
-    pend = base + lane < n;
-    pend_ptr = rec + base + lane;
+    pend_ptr = base + lane < n ? rec + base + lane : sink;
     if constexpr (kCompact) {
       pend_val = (L.kept && r < C::kSlots) ? (chosen << 21) | (r << 15) | (cho << T) | L.tag
                                            : 0xffffffffu;
@@ -1328,8 +1336,8 @@ __device__ void vqf_decide_body(const uint8_t* __restrict__ keys, const uint64_t
     if (base + 64 >= n) break;
     step(base + 64, cur, kvB, kvA);
   }
-  if (pend) *pend_ptr = pend_val;
-  __syncthreads();
+  if (pend_ptr != sink) *pend_ptr = pend_val;
+  asm volatile("" ::: "memory");
   // the final per-block counts feed only the unfused place path (the fused one recounts in
   // LDS): 4 bytes per 128-byte block record, so skip them when they are not read
   if (!fused) {
@@ -1382,6 +1390,298 @@ __global__ __launch_bounds__(64) void vqf_decide(const uint8_t* __restrict__ key
     vqf_decide_dispatch<8, MODE>(keys, offs, stride, sg, blockIdx.x, ws, recs, s_cnt, match_lds, compact_ok);
   else if (sg.tag_bits == 16)
     vqf_decide_dispatch<16, MODE>(keys, offs, stride, sg, blockIdx.x, ws, recs, s_cnt, match_lds, compact_ok);
+}
+
+// ---------------------------------------------------------------------------------------
+// Small batches: vqf_decide_ring.  A lone leaf's decide is a serial chain of 64-key steps, so
+// a batch too small to fill the chip is bound by that chain's latency.  Here one 512-thread
+// workgroup per leaf splits the work: waves 1..7 (producers) hash and locate the leaf's
+// chunks of 64 keys in order and compute every chunk's four lane-match masks (lanes with
+// my primary as primary / as alternate, with my alternate as primary / as alternate) with
+// ballots; wave 0 (the decider) replays the insertion order from them.  Per step the
+// decider reads the chunk's slot and the two block counts in one LDS round trip and runs
+// only the decision logic of vqf_decide_body.  Chunks pass through a ring of kRingSlots slots:
+// a producer fills a slot when the decider has freed it and then publishes it (ready word =
+// chunk + 1); the decider frees a slot once its words are in registers.  LDS operations of
+// a CU take effect in issue order per wave, so a decider that sees the ready word written
+// after the slot's words reads those words.  ~70 KB of LDS: two workgroups per CU.
+// A leaf with more than kRingMaxBlocks blocks runs vqf_decide_body in wave 0.
+// Same decisions, same key records as vqf_decide (test_gpu_parity: small and large batches).
+constexpr uint32_t kRingThreads = 512;
+constexpr uint32_t kRingProducers = kRingThreads / 64 - 1;
+constexpr uint32_t kRingSlots = 16;
+constexpr uint32_t kRingSlotWords = 5 * 64;  // u64: location, Mpp, Mpa, Map, Maa per lane
+constexpr uint32_t kRingMaxBlocks = 2048;
+constexpr uint32_t kRingLdsBytes = kRingSlots * kRingSlotWords * 8 + 4 * kRingSlots + 8 +
+                                   4 * kRingMaxBlocks;
+constexpr uint32_t kVqfRingMaxSegs = 768;
+static_assert(kRingLdsBytes <= 160 * 1024 / 3, "three workgroups per CU");
+// (a batch with a leaf beyond kRingMaxBlocks is launched with the LDS vqf_decide_body needs)
+
+// Ring hand-off words: relaxed workgroup-scope atomics, so they stay LDS operations (a
+// volatile access through a generic pointer is compiled as a system-coherent flat access).
+__device__ inline uint32_t lds_load_relaxed(uint32_t* p)
+{
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ inline void lds_store_relaxed(uint32_t* p, uint32_t v)
+{
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// location word: tag | po << T | pb << (T + 7) | ao << (T + 21) | ab << (T + 28) | kept << 63
+template <int T>
+__device__ inline uint64_t vqf_pack_loc(const VqfLoc& l, uint32_t ab, uint32_t ao)
+{
+  return (uint64_t)l.tag | ((uint64_t)l.po << T) | ((uint64_t)l.pb << (T + 7)) |
+         ((uint64_t)ao << (T + 21)) | ((uint64_t)ab << (T + 28)) | ((uint64_t)l.kept << 63);
+}
+
+template <int T, int MODE, int NBITS>
+__device__ void vqf_ring_produce(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs,
+                                 uint32_t stride, const tkv_amq_segment& sg, uint64_t* ring,
+                                 uint32_t* ready, uint32_t* freed)
+{
+  using C = Vqf<T>;
+  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x / 64 - 1;
+  const uint32_t n = sg.n_keys, nb = sg.n_blocks;
+  const uint32_t n_chunks = (n + 63) / 64;
+  const uint64_t R = (uint64_t)nb * C::kBuckets;
+  const uint64_t magic = sg.mod_magic;
+  const uint64_t mask = ~0ull << sg.hash_val_shift;  // filter_builder.hpp:187
+  const uint4* kp = reinterpret_cast<const uint4*>(keys) + sg.key_begin;
+  // a producer's next three chunks of keys are in flight (one chunk's load latency is longer
+  // than the time to produce it); the loop is unrolled by three so the buffers rotate
+  constexpr uint32_t kDepth = 3, kStep = kRingProducers;
+  auto load = [&](uint32_t q, uint4& kv) {  // clamped, not skipped: a fixed count in flight
+    if constexpr (MODE == kKey16) kv = kp[min(q * 64 + lane, n - 1)];
+  };
+  auto produce = [&](uint32_t q, uint4& kv) {
+    const uint32_t i = q * 64 + lane;
+    const bool valid = i < n;
+    const uint64_t h = valid ? vqf_key_hash<MODE>(keys, offs, stride, sg.key_begin + i, kv) : 0;
+    load(q + kDepth * kStep, kv);
+    const VqfLoc l = vqf_locate<T>(h, valid, mask, R, magic);
+    uint32_t ab, ao;
+    vqf_locate_alt<T>(l, R, magic, ab, ao);
+    const uint64_t keptmask = __ballot(l.kept);
+    uint32_t pp_lo = (uint32_t)keptmask, pp_hi = (uint32_t)(keptmask >> 32);
+    uint32_t pa_lo = pp_lo, pa_hi = pp_hi, ap_lo = pp_lo, ap_hi = pp_hi, aa_lo = pp_lo, aa_hi = pp_hi;
+#pragma unroll
+    for (int j = 0; j < NBITS; ++j) {
+      const uint32_t xp = (uint32_t)__builtin_amdgcn_sbfe((int32_t)l.pb, j, 1);  // 0 or ~0
+      const uint32_t xa = (uint32_t)__builtin_amdgcn_sbfe((int32_t)ab, j, 1);
+      const uint64_t bp = __ballot(xp != 0), ba = __ballot(xa != 0);
+      const uint32_t bpl = (uint32_t)bp, bph = (uint32_t)(bp >> 32);
+      const uint32_t bal = (uint32_t)ba, bah = (uint32_t)(ba >> 32);
+      pp_lo &= ~(bpl ^ xp);
+      pp_hi &= ~(bph ^ xp);
+      pa_lo &= ~(bpl ^ xa);
+      pa_hi &= ~(bph ^ xa);
+      ap_lo &= ~(bal ^ xp);
+      ap_hi &= ~(bah ^ xp);
+      aa_lo &= ~(bal ^ xa);
+      aa_hi &= ~(bah ^ xa);
+    }
+    // the slot is free once the decider has taken chunk q - kRingSlots
+    while (q >= kRingSlots && lds_load_relaxed(freed) < q - kRingSlots + 1) __builtin_amdgcn_s_sleep(1);
+    asm volatile("" ::: "memory");  // no slot write above the wait, none below the publish
+    uint64_t* slot = ring + (q % kRingSlots) * kRingSlotWords;
+    slot[lane] = vqf_pack_loc<T>(l, ab, ao);
+    slot[64 + lane] = ((uint64_t)pp_hi << 32) | pp_lo;
+    slot[128 + lane] = ((uint64_t)pa_hi << 32) | pa_lo;
+    slot[192 + lane] = ((uint64_t)ap_hi << 32) | ap_lo;
+    slot[256 + lane] = ((uint64_t)aa_hi << 32) | aa_lo;
+    asm volatile("" ::: "memory");
+    if (lane == 0) lds_store_relaxed(ready + q % kRingSlots, q + 1);
+  };
+  if (w >= n_chunks) return;
+  uint4 kv0 = make_uint4(0, 0, 0, 0), kv1 = kv0, kv2 = kv0;
+  load(w, kv0);
+  load(w + kStep, kv1);
+  load(w + 2 * kStep, kv2);
+  for (uint32_t q = w; q < n_chunks; q += kDepth * kStep) {
+    produce(q, kv0);
+    if (q + kStep >= n_chunks) break;
+    produce(q + kStep, kv1);
+    if (q + 2 * kStep >= n_chunks) break;
+    produce(q + 2 * kStep, kv2);
+  }
+}
+
+template <int T, bool kCompact>
+__device__ void vqf_ring_decide(const tkv_amq_segment& sg, uint32_t seg_index, VqfWorkspace ws,
+                                uint64_t* __restrict__ recs, const uint64_t* ring,
+                                uint32_t* ready, uint32_t* freed, uint32_t* cnt, bool fused)
+{
+  using C = Vqf<T>;
+  const uint32_t lane = threadIdx.x;
+  const uint32_t n = sg.n_keys, nb = sg.n_blocks;
+  const uint32_t n_chunks = (n + 63) / 64;
+  const uint64_t lt = lanemask_lt();
+  using Rec = typename std::conditional<kCompact, uint32_t, uint64_t>::type;
+  Rec* rec = reinterpret_cast<Rec*>(recs + sg.key_begin);
+  Rec* const sink = reinterpret_cast<Rec*>(ws.sink);  // see vqf_decide_body
+  Rec* pend_ptr = sink;
+  Rec pend_val = 0;
+  uint32_t nelts = 0;
+  // The next chunk's ready word and slot are read one step ahead (they do not depend on the
+  // counts), so a step waits for one LDS round trip: the block counts.  Two slot register
+  // sets alternate (the loop is unrolled by two), so no step copies the prefetched words.
+  struct Slot {
+    uint32_t rdy;
+    uint64_t loc, pp, pa, ap, aa;
+  };
+  auto fetch = [&](uint32_t c, Slot& S) {
+    const uint64_t* slot = ring + (c % kRingSlots) * kRingSlotWords;
+    S.rdy = lds_load_relaxed(ready + c % kRingSlots);
+    asm volatile("" ::: "memory");  // the slot words are read after the ready word
+    S.loc = slot[lane];
+    S.pp = slot[64 + lane];
+    S.pa = slot[128 + lane];
+    S.ap = slot[192 + lane];
+    S.aa = slot[256 + lane];
+  };
+  auto step = [&](uint32_t c, Slot& S, Slot& next) {
+    while (S.rdy != c + 1) {
+      __builtin_amdgcn_s_sleep(1);
+      fetch(c, S);
+    }
+    const uint64_t wloc = S.loc, Mpp = S.pp, Mpa = S.pa, Map = S.ap, Maa = S.aa;
+    const uint32_t base = c * 64;
+    const bool kept = wloc >> 63;
+    const uint32_t tag = (uint32_t)wloc & ((1u << T) - 1);
+    const uint32_t po = (uint32_t)(wloc >> T) & 127u;
+    const uint32_t pb = (uint32_t)(wloc >> (T + 7)) & 16383u;
+    const uint32_t ao = (uint32_t)(wloc >> (T + 21)) & 127u;
+    const uint32_t ab = (uint32_t)(wloc >> (T + 28)) & 16383u;
+    const uint32_t cnt_p = cnt[pb], cnt_a = cnt[ab];
+    // LDS operations complete in issue order: the prefetch goes after the count reads, so
+    // waiting for the counts does not wait for it.  Neither the hand-off write nor the
+    // prefetch is skipped (every lane writes the same word; the last step re-reads the last
+    // slot), so the compiler's count of LDS operations in flight is exact on every path.
+    asm volatile("" ::: "memory");
+    lds_store_relaxed(freed, c + 1);  // the slot's words are in registers (LDS order)
+    fetch(min(c + 1, n_chunks - 1), next);
+    *pend_ptr = pend_val;
+    const uint64_t keptmask = __ballot(kept);
+    nelts += __popcll(keptmask);
+    // the decision logic of vqf_decide_body, with every mask at hand
+    uint32_t cp = kept ? cnt_p + __popcll(Mpp & lt) : 0u;
+    uint32_t ca = 0;
+    uint64_t altmask = 0;
+    if (__ballot(kept && cp >= C::kThreshold) != 0) {
+      ca = kept ? cnt_a + __popcll(Mpa & lt) : 0u;
+      uint64_t U = __ballot(kept && pb != ab);
+      uint64_t F = __ballot((cp >= C::kThreshold) & (ca < cp)) & U;
+      if (F != 0) {
+        const uint64_t conf = (Mpp | Mpa | Map | Maa) & lt;
+        U &= __ballot(cp + (uint32_t)__popcll(Map & lt) >= C::kThreshold);
+        F &= U;
+        while (F != 0) {
+          const uint64_t res = __ballot((conf & U) == 0) & U;
+          const uint64_t A = res & F;
+          altmask |= A;
+          U &= ~res;
+          const uint64_t Al = A & lt;
+          cp = cp + (uint32_t)__popcll(Map & Al) - (uint32_t)__popcll(Mpp & Al);
+          ca = ca + (uint32_t)__popcll(Maa & Al) - (uint32_t)__popcll(Mpa & Al);
+          F = __ballot((cp >= C::kThreshold) & (ca < cp)) & U;
+        }
+      }
+    }
+    const bool alt = (altmask >> lane) & 1;
+    const uint32_t chosen = alt ? ab : pb;
+    const uint32_t cho = alt ? ao : po;
+    const uint32_t r = alt ? ca : cp;  // a full block (r >= slots) shows in the final counts
+    pend_ptr = base + lane < n ? rec + base + lane : sink;
+    if constexpr (kCompact) {
+      pend_val = (kept && r < C::kSlots) ? (chosen << 21) | (r << 15) | (cho << T) | tag : 0xffffffffu;
+    } else {
+      const uint32_t slot_hi = (kept && r < C::kSlots)
+                                   ? (uint32_t)((sg.block_base + chosen) * 64 + r) : 0xffffffffu;
+      pend_val = ((uint64_t)slot_hi << 32) | ((cho << T) | tag) | (T == 16 ? 0x80000000u : 0u);
+    }
+    if (kept) atomicAdd(cnt + chosen, 1u);
+  };
+  Slot A, B;
+  if (n_chunks > 0) fetch(0, A);
+  for (uint32_t c = 0; c < n_chunks; c += 2) {
+    step(c, A, B);
+    if (c + 1 >= n_chunks) break;
+    step(c + 1, B, A);
+  }
+  // a key found its block full (vqf_insert fails) iff that block's final count exceeds slots
+  uint32_t fail = 0;
+  for (uint32_t b = lane; b < nb; b += 64) fail |= cnt[b] > C::kSlots;
+  if (pend_ptr != sink) *pend_ptr = pend_val;
+  asm volatile("" ::: "memory");
+  if (!fused) {  // block counts for the unfused place (as vqf_decide_body)
+    for (uint32_t b = lane; b < nb; b += 64) {
+      const uint32_t c = cnt[b];
+      vqf_count(ws, sg.block_base + b) = c < C::kSlots ? c : C::kSlots;
+    }
+  }
+  const bool any_fail = __ballot(fail) != 0;
+  if (lane == 0) {
+    ws.nelts[seg_index] = nelts;
+    if (any_fail) atomicOr(ws.status, kVqfStatusOverflow);
+  }
+}
+
+template <int T, int MODE, bool kCompact, int NBITS>
+__device__ void vqf_ring_body(const uint8_t* keys, const uint64_t* offs, uint32_t stride,
+                              const tkv_amq_segment& sg, uint32_t seg_index, VqfWorkspace ws,
+                              uint64_t* recs, uint32_t* lds, bool fused)
+{
+  uint64_t* ring = reinterpret_cast<uint64_t*>(lds);
+  uint32_t* ready = reinterpret_cast<uint32_t*>(ring + kRingSlots * kRingSlotWords);
+  uint32_t* freed = ready + kRingSlots;
+  uint32_t* cnt = freed + 2;
+  for (uint32_t i = threadIdx.x; i < kRingSlots + 1; i += kRingThreads) ready[i] = 0;  // + freed
+  for (uint32_t b = threadIdx.x; b < sg.n_blocks; b += kRingThreads) cnt[b] = 0;
+  __syncthreads();
+  if (threadIdx.x < 64)
+    vqf_ring_decide<T, kCompact>(sg, seg_index, ws, recs, ring, ready, freed, cnt, fused);
+  else
+    vqf_ring_produce<T, MODE, NBITS>(keys, offs, stride, sg, ring, ready, freed);
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kRingThreads) void vqf_decide_ring(
+    const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint32_t stride,
+    const tkv_amq_segment* __restrict__ segs, void* ws_base, uint64_t ws_bytes, uint32_t n_segs,
+    int flags)
+{
+  const bool match_lds = flags & 1, compact_ok = flags & 2;
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_ring[];
+  const tkv_amq_segment sg = segs[blockIdx.x];
+  const VqfWorkspace ws = vqf_workspace(ws_base, n_segs);
+  if (!vqf_ws_ok(segs, n_segs, ws_bytes, ws)) return;
+  uint64_t* recs = vqf_records(ws, segs, n_segs);
+  const uint32_t nb = sg.n_blocks;
+  if (nb > kRingMaxBlocks) {
+    if (threadIdx.x >= 64) return;
+    if (sg.tag_bits == 8)
+      vqf_decide_dispatch<8, MODE>(keys, offs, stride, sg, blockIdx.x, ws, recs, s_ring, match_lds, compact_ok);
+    else if (sg.tag_bits == 16)
+      vqf_decide_dispatch<16, MODE>(keys, offs, stride, sg, blockIdx.x, ws, recs, s_ring, match_lds, compact_ok);
+    return;
+  }
+  // compact records exactly where vqf_decide_dispatch writes them
+  if (sg.tag_bits == 8) {
+    if (nb <= 512 && compact_ok)
+      vqf_ring_body<8, MODE, true, 9>(keys, offs, stride, sg, blockIdx.x, ws, recs, s_ring, compact_ok);
+    else if (nb <= 512)
+      vqf_ring_body<8, MODE, false, 9>(keys, offs, stride, sg, blockIdx.x, ws, recs, s_ring, compact_ok);
+    else
+      vqf_ring_body<8, MODE, false, 11>(keys, offs, stride, sg, blockIdx.x, ws, recs, s_ring, compact_ok);
+  } else if (sg.tag_bits == 16) {
+    if (nb <= 512)
+      vqf_ring_body<16, MODE, false, 9>(keys, offs, stride, sg, blockIdx.x, ws, recs, s_ring, compact_ok);
+    else
+      vqf_ring_body<16, MODE, false, 11>(keys, offs, stride, sg, blockIdx.x, ws, recs, s_ring, compact_ok);
+  }
 }
 
 // One thread per key: moves the key's entry from its coalesced placement record into the
@@ -2598,7 +2898,26 @@ int tkv_amq_build(int kind, const uint8_t* keys, const uint64_t* offs, uint32_t 
   const bool fused = fused_lds <= kFusedLdsBudget;  // compact records are read only there
   const int flags = match_lds | (fused ? 2 : 0);
   const size_t lds = 4ull * ((max_blocks + 1) & ~1u) + (match_lds ? 8ull * max_blocks : 0);
-  if (mode == kKey16)
+  if (n_segs <= kVqfRingMaxSegs) {
+    static std::once_flag ring_attr[kMaxDevices];
+    once_per_device(ring_attr, [] {
+      for (const void* f : {reinterpret_cast<const void*>(&vqf_decide_ring<kKey16>),
+                            reinterpret_cast<const void*>(&vqf_decide_ring<kKeyFixed>),
+                            reinterpret_cast<const void*>(&vqf_decide_ring<kKeyVar>)})
+        (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    });
+    const dim3 g(n_segs), b(kRingThreads);
+    const size_t rl = lds > kRingLdsBytes ? lds : kRingLdsBytes;
+    if (mode == kKey16)
+      hipLaunchKernelGGL(vqf_decide_ring<kKey16>, g, b, rl, s, keys, offs, stride, d_segs, d_ws,
+                         ws_bytes, n_segs, flags);
+    else if (mode == kKeyFixed)
+      hipLaunchKernelGGL(vqf_decide_ring<kKeyFixed>, g, b, rl, s, keys, offs, stride, d_segs, d_ws,
+                         ws_bytes, n_segs, flags);
+    else
+      hipLaunchKernelGGL(vqf_decide_ring<kKeyVar>, g, b, rl, s, keys, offs, stride, d_segs, d_ws,
+                         ws_bytes, n_segs, flags);
+  } else if (mode == kKey16)
     hipLaunchKernelGGL(vqf_decide<kKey16>, dim3(n_segs), dim3(64), lds, s, keys, offs, stride,
                        d_segs, d_ws, ws_bytes, n_segs, flags);
   else if (mode == kKeyFixed)
