@@ -272,15 +272,14 @@ def test_vqf_unsorted_and_duplicate_keys(oracle, amq, torch):
     assert_same(plan, out, ref)
 
 
-@pytest.mark.parametrize("n_leaves", [40, 512, 513])
+@pytest.mark.parametrize("n_leaves", [40, 768, 769])
 @pytest.mark.parametrize("shape", ["k16", "k24", "var"])
 def test_vqf_decide_paths(oracle, amq, torch, n_leaves, shape):
-    """Batches of up to 512 leaves take vqf_decide_resident (the leaf's key locations in LDS,
-    one decider wave), larger ones vqf_decide (one wave per leaf).  Inside the resident
-    kernel a leaf whose locations do not fit (30000 keys) runs vqf_decide's body, without
-    the LDS match table (> 512 blocks).  8- and 16-bit tags (12 / 22 bits per key; at 22 a
-    16384-key leaf has > 512 blocks and stays resident), ragged leaves, sampled against the
-    oracle."""
+    """Batches of up to 768 leaves take vqf_decide_ring (producer waves locate and match
+    each 64-key chunk, one decider wave replays the insertion order), larger ones vqf_decide
+    (one wave per leaf).  8- and 16-bit tags (12 / 22 bits per key), leaves of <= 512 and
+    > 512 blocks (the producers' 9- and 11-bit matches; a 30000-key leaf), fused and unfused
+    place, ragged leaves, every key shape, sampled against the oracle."""
     rng = np.random.default_rng(1000 + n_leaves)
     counts = [int(c) for c in rng.integers(0, 3000, n_leaves)]
     counts[0], counts[1], counts[2], counts[-1] = 0, 16384, 30000, 1
@@ -313,6 +312,23 @@ def test_vqf_decide_paths(oracle, amq, torch, n_leaves, shape):
                                               offsets=o, stride=0)
             assert st == 0
             assert segment_bytes(plan, out, s) == ref[:p.payload_used].tobytes(), f"bpk {bpk} leaf {s}"
+
+
+@pytest.mark.parametrize("n_leaves", [4, 800])
+def test_vqf_leaf_beyond_ring_blocks(oracle, amq, torch, n_leaves):
+    """A 100000-key leaf in 1 MiB pages has 2451 blocks: more than the ring kernel's count
+    table holds, so its wave 0 runs vqf_decide_body (block-id ballots, no LDS match table);
+    in a batch of 800 leaves vqf_decide does the same.  Unfused place (the image is too big
+    for LDS)."""
+    counts = [100000, 500, 0, 16384] + [300] * (n_leaves - 4)
+    keys = oracle.gen_keys16(6, 0, sum(counts))
+    plan, out = gpu_build(amq, torch, 1, torch.from_numpy(keys).cuda(), counts, 12, cap=1 << 20)
+    assert plan.segs["n_blocks"][0] > 2048
+    sb = seg_bounds(counts)
+    for s in sorted({0, 1, 2, 3, n_leaves - 1}):
+        st, ref, p = oracle.vqf_build(keys[int(sb[s]):], counts[s], 12, 1 << 20, src_page_id=s)
+        assert st == 0
+        assert segment_bytes(plan, out, s) == ref[:p.payload_used].tobytes(), f"leaf {s}"
 
 
 def probe_inputs(oracle, n_keys, counts, n_miss):

@@ -2,7 +2,7 @@
 several L: the small-batch curve (a checkpoint's build_all_pages queue holds tens to
 thousands of leaves).  Run under rocprofv3 --kernel-trace --stats for per-kernel times.
 
-  python tools/small_batch.py [--kind 0|1] [--leaves 1,8,64,256,1024] [--reps 50]
+  python tools/small_batch.py [--kind 0|1] [--leaves 1,8,64,256,512,1024] [--reps 50]
 """
 import argparse
 import os
@@ -20,7 +20,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--kind", type=int, default=0)
     ap.add_argument("--bpk", type=int, default=0)
-    ap.add_argument("--leaves", default="1,8,64,256,1024")
+    ap.add_argument("--leaves", default="1,8,64,256,512,1024")
     ap.add_argument("--reps", type=int, default=50)
     ap.add_argument("--no-ws", action="store_true",
                     help="call the ABI without a workspace (Bloom: the unsplit paths)")

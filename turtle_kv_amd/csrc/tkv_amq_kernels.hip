@@ -1409,8 +1409,9 @@ __global__ __launch_bounds__(64) void vqf_decide(const uint8_t* __restrict__ key
 // Same decisions, same key records as vqf_decide (test_gpu_parity: small and large batches).
 constexpr uint32_t kRingThreads = 512;
 constexpr uint32_t kRingProducers = kRingThreads / 64 - 1;
-constexpr uint32_t kRingSlots = 16;
-constexpr uint32_t kRingSlotWords = 5 * 64;  // u64: location, Mpp, Mpa, Map, Maa per lane
+constexpr uint32_t kRingSlots = 12;
+// u64 per lane: location, Mpp, Mpa, Map, Maa, conflict mask, ranks (kRankPP / PA / AP bytes)
+constexpr uint32_t kRingSlotWords = 7 * 64;
 constexpr uint32_t kRingMaxBlocks = 2048;
 constexpr uint32_t kRingLdsBytes = kRingSlots * kRingSlotWords * 8 + 4 * kRingSlots + 8 +
                                    4 * kRingMaxBlocks;
@@ -1492,6 +1493,15 @@ __device__ void vqf_ring_produce(const uint8_t* __restrict__ keys, const uint64_
     slot[128 + lane] = ((uint64_t)pa_hi << 32) | pa_lo;
     slot[192 + lane] = ((uint64_t)ap_hi << 32) | ap_lo;
     slot[256 + lane] = ((uint64_t)aa_hi << 32) | aa_lo;
+    // what the decider needs of the masks before any lane moves: earlier lanes sharing a
+    // block, and the counts of earlier lanes with my primary as primary / as alternate and
+    // with my alternate as primary
+    const uint64_t lt = lanemask_lt();
+    slot[320 + lane] = ((((uint64_t)(pp_hi | pa_hi | ap_hi | aa_hi)) << 32) | (pp_lo | pa_lo | ap_lo | aa_lo)) & lt;
+    const uint32_t r_pp = __popcll((((uint64_t)pp_hi << 32) | pp_lo) & lt);
+    const uint32_t r_pa = __popcll((((uint64_t)pa_hi << 32) | pa_lo) & lt);
+    const uint32_t r_ap = __popcll((((uint64_t)ap_hi << 32) | ap_lo) & lt);
+    slot[384 + lane] = r_pp | (r_pa << 8) | (r_ap << 16);
     asm volatile("" ::: "memory");
     if (lane == 0) lds_store_relaxed(ready + q % kRingSlots, q + 1);
   };
@@ -1529,8 +1539,8 @@ __device__ void vqf_ring_decide(const tkv_amq_segment& sg, uint32_t seg_index, V
   // counts), so a step waits for one LDS round trip: the block counts.  Two slot register
   // sets alternate (the loop is unrolled by two), so no step copies the prefetched words.
   struct Slot {
-    uint32_t rdy;
-    uint64_t loc, pp, pa, ap, aa;
+    uint32_t rdy, ranks;
+    uint64_t loc, pp, pa, ap, aa, conf;
   };
   auto fetch = [&](uint32_t c, Slot& S) {
     const uint64_t* slot = ring + (c % kRingSlots) * kRingSlotWords;
@@ -1541,6 +1551,8 @@ __device__ void vqf_ring_decide(const tkv_amq_segment& sg, uint32_t seg_index, V
     S.pa = slot[128 + lane];
     S.ap = slot[192 + lane];
     S.aa = slot[256 + lane];
+    S.conf = slot[320 + lane];
+    S.ranks = (uint32_t)slot[384 + lane];
   };
   auto step = [&](uint32_t c, Slot& S, Slot& next) {
     while (S.rdy != c + 1) {
@@ -1548,6 +1560,8 @@ __device__ void vqf_ring_decide(const tkv_amq_segment& sg, uint32_t seg_index, V
       fetch(c, S);
     }
     const uint64_t wloc = S.loc, Mpp = S.pp, Mpa = S.pa, Map = S.ap, Maa = S.aa;
+    const uint64_t conf = S.conf;
+    const uint32_t ranks = S.ranks;
     const uint32_t base = c * 64;
     const bool kept = wloc >> 63;
     const uint32_t tag = (uint32_t)wloc & ((1u << T) - 1);
@@ -1567,16 +1581,15 @@ __device__ void vqf_ring_decide(const tkv_amq_segment& sg, uint32_t seg_index, V
     const uint64_t keptmask = __ballot(kept);
     nelts += __popcll(keptmask);
     // the decision logic of vqf_decide_body, with every mask at hand
-    uint32_t cp = kept ? cnt_p + __popcll(Mpp & lt) : 0u;
+    uint32_t cp = kept ? cnt_p + (ranks & 0xffu) : 0u;
     uint32_t ca = 0;
     uint64_t altmask = 0;
     if (__ballot(kept && cp >= C::kThreshold) != 0) {
-      ca = kept ? cnt_a + __popcll(Mpa & lt) : 0u;
+      ca = kept ? cnt_a + ((ranks >> 8) & 0xffu) : 0u;
       uint64_t U = __ballot(kept && pb != ab);
       uint64_t F = __ballot((cp >= C::kThreshold) & (ca < cp)) & U;
       if (F != 0) {
-        const uint64_t conf = (Mpp | Mpa | Map | Maa) & lt;
-        U &= __ballot(cp + (uint32_t)__popcll(Map & lt) >= C::kThreshold);
+        U &= __ballot(cp + (ranks >> 16) >= C::kThreshold);
         F &= U;
         while (F != 0) {
           const uint64_t res = __ballot((conf & U) == 0) & U;
