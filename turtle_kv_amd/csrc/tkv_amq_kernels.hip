@@ -13,6 +13,9 @@
 //                        (power-of-two-choice decisions depend only on per-block counts, kept
 //                        in LDS); per 64-key chunk every conflict-free lane decides in the same
 //                        round.  Emits one coalesced (block, rank, bucket, tag) record per key.
+//   vqf_decide_ring      batches of <= 768 segments: producer waves hash, locate and match each
+//                        64-key chunk into an LDS ring; one decider wave replays the order from
+//                        it (a lone segment's serial chain, not the VALU rate, sets the time).
 //   vqf_place_fused      one workgroup per segment: the records land at [block][rank] of an LDS
 //                        image, then one thread per 64-byte block runs the stable counting sort
 //                        by bucket offset and writes the block (vqf_scatter + vqf_place: the
