@@ -1204,12 +1204,14 @@ __device__ void vqf_decide_body(const uint8_t* __restrict__ keys, const uint64_t
     // block-id bit, each 32-bit half of the match mask updated with one v_bitop3
     // (m & ~(ballot ^ sext(bit)))
     uint32_t mpp_lo = (uint32_t)keptmask, mpp_hi = (uint32_t)(keptmask >> 32);
+    // LDS operations are never skipped (lanes with no key OR 0, add 0 and clear an entry no
+    // kept lane set in this phase), so the compiler's count of them in flight is exact
     if constexpr (kLdsMatch) {
-      if (L.kept) atomicOr(mt + L.pb, mybit);
+      atomicOr(mt + L.pb, L.kept ? mybit : 0ull);
       asm volatile("" ::: "memory");
       const uint64_t a = mt[L.pb];
       asm volatile("" ::: "memory");
-      if (L.kept) mt[L.pb] = 0;
+      mt[L.pb] = 0;
       mpp_lo &= (uint32_t)a;
       mpp_hi &= (uint32_t)(a >> 32);
     }
@@ -1237,11 +1239,11 @@ __device__ void vqf_decide_body(const uint8_t* __restrict__ keys, const uint64_t
       // lanes with pb_j == my ab
       uint32_t mpa_lo = (uint32_t)keptmask, mpa_hi = (uint32_t)(keptmask >> 32);
       if constexpr (kLdsMatch) {
-        if (L.kept) atomicOr(mt + pb, mybit);
+        atomicOr(mt + pb, L.kept ? mybit : 0ull);
         asm volatile("" ::: "memory");
         const uint64_t b = mt[ab];
         asm volatile("" ::: "memory");
-        if (L.kept) mt[pb] = 0;
+        mt[pb] = 0;
         mpa_lo &= (uint32_t)b;
         mpa_hi &= (uint32_t)(b >> 32);
       }
@@ -1268,11 +1270,11 @@ __device__ void vqf_decide_body(const uint8_t* __restrict__ keys, const uint64_t
         uint32_t map_lo = (uint32_t)keptmask, map_hi = (uint32_t)(keptmask >> 32);
         uint32_t maa_lo = map_lo, maa_hi = map_hi;
         if constexpr (kLdsMatch) {
-          if (L.kept) atomicOr(mt + ab, mybit);
+          atomicOr(mt + ab, L.kept ? mybit : 0ull);
           asm volatile("" ::: "memory");
           const uint64_t a = mt[pb], b = mt[ab];
           asm volatile("" ::: "memory");
-          if (L.kept) mt[ab] = 0;
+          mt[ab] = 0;
           map_lo &= (uint32_t)a;
           map_hi &= (uint32_t)(a >> 32);
           maa_lo &= (uint32_t)b;
@@ -1322,7 +1324,7 @@ __device__ void vqf_decide_body(const uint8_t* __restrict__ keys, const uint64_t
                                    ? (uint32_t)((sg.block_base + chosen) * 64 + r) : 0xffffffffu;
       pend_val = ((uint64_t)slot_hi << 32) | ((cho << T) | L.tag) | (T == 16 ? 0x80000000u : 0u);
     }
-    if (L.kept) atomicAdd(cnt + chosen, 1u);
+    atomicAdd(cnt + chosen, L.kept ? 1u : 0u);
   };
 
   uint4 kv0 = {0, 0, 0, 0}, kvA = {0, 0, 0, 0}, kvB = {0, 0, 0, 0};
@@ -1618,7 +1620,7 @@ __device__ void vqf_ring_decide(const tkv_amq_segment& sg, uint32_t seg_index, V
                                    ? (uint32_t)((sg.block_base + chosen) * 64 + r) : 0xffffffffu;
       pend_val = ((uint64_t)slot_hi << 32) | ((cho << T) | tag) | (T == 16 ? 0x80000000u : 0u);
     }
-    if (kept) atomicAdd(cnt + chosen, 1u);
+    atomicAdd(cnt + chosen, kept ? 1u : 0u);
   };
   Slot A, B;
   if (n_chunks > 0) fetch(0, A);
