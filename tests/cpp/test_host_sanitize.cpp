@@ -8,6 +8,9 @@
 //   bloom <n> <bpk> <seed>                                       -> status fnv negatives
 //   vqf <n> <bpk> <cap> <seed>                                   -> status fnv used negatives
 //   stage <fixed_len> <n> <threads> <seed>                       -> status ok
+//   obuild <kind> <n_segs> <keys_per_seg> <bpk> <threads> <seed>  -> status fnv
+//     (the oracle's threaded checkpoint-level build, tkvo_build_segments; VQF at 32704 B)
+// Built twice by the test: AddressSanitizer + UBSan, and ThreadSanitizer (the threaded paths).
 #include <cinttypes>
 #include <cstdio>
 #include <cstring>
@@ -134,6 +137,30 @@ static void stage_case(std::istringstream& in)
   std::printf("stage %d %d\n", st, ok ? 1 : 0);
 }
 
+static void obuild_case(std::istringstream& in)
+{
+  int kind, threads;
+  uint32_t n_segs, bpk;
+  uint64_t per, seed;
+  in >> kind >> n_segs >> per >> bpk >> threads >> seed;
+  const uint64_t n = per * n_segs;
+  std::vector<uint8_t> keys(16 * n + 1);
+  tkvo_gen_keys16(seed, 0, n, keys.data());
+  std::vector<uint64_t> begin(n_segs + 1), off(n_segs), capv(n_segs);
+  uint64_t total = 0;
+  for (uint32_t s = 0; s <= n_segs; ++s) begin[s] = per * s;
+  for (uint32_t s = 0; s < n_segs; ++s) {
+    capv[s] = kind == 0 ? tkvo_bloom_payload_size(per, bpk) : 32704;
+    off[s] = total;
+    total += capv[s];
+  }
+  if (kind == 1) tkvo_sort_keys16_segments(keys.data(), begin.data(), n_segs, threads);
+  std::vector<uint8_t> out(total + 1);
+  const int st = tkvo_build_segments(kind, keys.data(), begin.data(), n_segs, bpk, nullptr, out.data(),
+                                     off.data(), capv.data(), threads);
+  std::printf("obuild %d %" PRIu64 "\n", st, fnv(out.data(), total));
+}
+
 int main()
 {
   std::string line;
@@ -146,6 +173,7 @@ int main()
     else if (op == "bloom") bloom_case(in);
     else if (op == "vqf") vqf_case(in);
     else if (op == "stage") stage_case(in);
+    else if (op == "obuild") obuild_case(in);
     else if (!op.empty()) {
       std::fprintf(stderr, "unknown case %s\n", op.c_str());
       return 2;

@@ -1,10 +1,12 @@
-"""CPU: the host code under AddressSanitizer + UndefinedBehaviorSanitizer.
+"""CPU: the host code under AddressSanitizer + UndefinedBehaviorSanitizer, and ThreadSanitizer.
 
 tests/cpp/test_host_sanitize.cpp links the host part of tkv_amq_kernels.hip (the plan and
 TreeOptions sizing entry points), tkv_amq_stage.cpp and the C oracle, all built with
 `-fsanitize=address,undefined` (hipcc: host side only, `-Xarch_host`; the oracle with the same
 clang).  The driver runs cases from stdin; every result line must equal the same call through
-the unsanitized libraries (ctypes), and any sanitizer report fails the run.  No device."""
+the unsanitized libraries (ctypes), and any sanitizer report fails the run.  The threaded
+paths (key staging, the oracle's checkpoint-level build) also run under ThreadSanitizer.
+No device."""
 import ctypes
 import os
 import subprocess
@@ -25,11 +27,10 @@ def fnv(b: bytes) -> int:
     return h
 
 
-@pytest.fixture(scope="module")
-def driver(tmp_path_factory):
+def build_driver(d, san):
     if not (os.path.exists(HIPCC) and os.path.exists(CLANG)):
         pytest.skip("ROCm clang / hipcc not installed")
-    d = tmp_path_factory.mktemp("san")
+    SAN = san
     inc = ["-I" + os.path.join(ROOT, "include")]
     host_san = [f for s in SAN for f in ("-Xarch_host", s)]
     steps = [
@@ -52,9 +53,20 @@ def driver(tmp_path_factory):
     return str(d / "test_host_sanitize")
 
 
+@pytest.fixture(scope="module")
+def driver(tmp_path_factory):
+    return build_driver(tmp_path_factory.mktemp("asan"), SAN)
+
+
+@pytest.fixture(scope="module")
+def tsan_driver(tmp_path_factory):
+    return build_driver(tmp_path_factory.mktemp("tsan"), ["-fsanitize=thread"])
+
+
 def run(driver, lines):
     env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0:halt_on_error=1",
-               UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1")
+               UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1",
+               TSAN_OPTIONS="halt_on_error=1")
     r = subprocess.run([driver], input="\n".join(lines) + "\n", capture_output=True, text=True,
                        timeout=300, env=env)
     assert r.returncode == 0 and "Sanitizer" not in r.stderr, r.stderr[-4000:]
@@ -132,4 +144,33 @@ def test_stage_sanitized(driver):
              (0, 300000, 7)]
     got = run(driver, ["stage %d %d %d %d" % (f, n, t, 100 + i) for i, (f, n, t) in enumerate(cases)])
     for c, g in zip(cases, got):
+        assert g == ["stage", "0", "1"], c
+
+
+def oracle_build_expect(oracle, kind, n_segs, per, bpk, threads, seed):
+    n = per * n_segs
+    keys = oracle.gen_keys16(seed, 0, n)
+    begin = np.arange(n_segs + 1, dtype=np.uint64) * per
+    if kind == 1:
+        oracle.sort_segments(keys, begin, threads)
+    cap = oracle.lib().tkvo_bloom_payload_size(per, bpk) if kind == 0 else 32704
+    off = np.arange(n_segs, dtype=np.uint64) * cap
+    capv = np.full(n_segs, cap, np.uint64)
+    out = np.zeros(int(cap) * n_segs + 1, np.uint8)
+    P = oracle._p
+    st = oracle.lib().tkvo_build_segments(kind, P(keys), P(begin), n_segs, bpk, None, P(out), P(off),
+                                          P(capv), threads)
+    return ["obuild", str(st), str(fnv(out[:int(cap) * n_segs].tobytes()))]
+
+
+@pytest.mark.parametrize("which", ["asan", "tsan"])
+def test_threaded_paths_sanitized(driver, tsan_driver, oracle, which):
+    d = driver if which == "asan" else tsan_driver
+    builds = [(0, 16, 3000, 10, 4, 61), (1, 16, 3000, 12, 4, 62), (0, 5, 700, 33, 8, 63)]
+    stages = [(16, 200000, 6), (0, 150000, 5)]
+    got = run(d, ["obuild %d %d %d %d %d %d" % c for c in builds] +
+              ["stage %d %d %d %d" % (f, n, t, 200 + i) for i, (f, n, t) in enumerate(stages)])
+    for c, g in zip(builds, got):
+        assert g == oracle_build_expect(oracle, *c), c
+    for c, g in zip(stages, got[len(builds):]):
         assert g == ["stage", "0", "1"], c
