@@ -3,7 +3,7 @@
 
   python bench.py [--gpus N] [--steps K] [--warmup W]
                   [--workload bloom10|bloom12|vqf12|probe10|probe_vqf12|bloom10k24|bloom10var|
-                              bloom10mono] [--total-keys T]
+                              bloom10mono|bloom12hash] [--total-keys T]
 
 One step = one pass of the hot path over one batch: build every leaf filter of
 `--keys-per-gpu` (default 100M, BASELINE config 2) 16-byte keys held in HBM, S = 16,384 keys
@@ -53,7 +53,11 @@ WORKLOADS = {
     "bloom10k24": (0, 10, "Bloom @10 bits/key, 24-byte keys (TurtleKV default key size)"),
     "bloom10mono": (0, 10, "Bloom @10 bits/key, one monolithic filter per GPU"),
     "bloom10var": (0, 10, "Bloom @10 bits/key, variable-length keys (8-31 B)"),
+    "bloom12hash": (0, 12, "Bloom @12 bits/key, one filter over all GPUs' keys, hash-range sharded"),
 }
+# BASELINE config 5 read literally: one monolithic filter whose bitmap byte ranges are owned by
+# the ranks (route -> RCCL all-to-all of the keys -> range build; turtle_kv_amd.dist)
+HASH_SHARDED = {"bloom12hash"}
 # workloads whose one filter spans every key of the GPU (the monolithic
 # single-filter Bloom variant)
 MONOLITHIC = {"bloom10mono"}
@@ -248,6 +252,8 @@ def main():
         else:
             dist.init_process_group(args.backend)
     kind, bpk, label = WORKLOADS[args.workload]
+    if args.workload in HASH_SHARDED:
+        return bench_hash_sharded(args, torch, dist, amq, world, rank, dev, bpk, label)
     # the VQF payload capacity is the default TreeOptions' filter page at this bits/key
     # (tree/tree_options.hpp:177-220): 32 KiB pages, 32,704 payload bytes at 12 bits/key
     cap = (amq.TreeOptions(kind).set_filter_bits_per_key(bpk).filter_page_payload_size()
@@ -521,6 +527,139 @@ def main():
         if probe_check is not None:
             line["probe"].update({k: v for k, v in probe_check.items() if k != "cpu_baseline"})
             line["verified"] = probe_check["results_equal_oracle"]
+    print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+# ---------------------------------------------------------------------------------------
+# hash-range sharded monolithic Bloom (BASELINE config 5 read literally)
+# ---------------------------------------------------------------------------------------
+def bench_hash_sharded(args, torch, dist, amq, world, rank, dev, bpk, label):
+    """One Bloom filter over every rank's keys; rank r owns a contiguous byte range of its
+    bitmap.  A step = route (tkv_amq_bloom_route) + all-to-all of the keys (RCCL) + the rank's
+    range build (tkv_amq_bloom_build_range); the all-gather of the ranges is timed separately
+    (in-step with --allgather).  Rank 0 checks the gathered filter against a one-GPU build of
+    all keys, and that against the CPU oracle when it holds <= 200M keys."""
+    from turtle_kv_amd import dist as tdist
+    strong = args.total_keys is not None
+    n_local = args.total_keys // world if strong else args.keys_per_gpu
+    total = n_local * world
+    keys = amq.gen_keys16(42, rank * n_local, n_local, device=dev)
+    hs = tdist.HashShardedBloom(total, bpk, world, rank, dev)
+
+    def step():
+        hs.local_build(keys)
+        if args.allgather and world > 1:
+            hs.allgather()
+
+    ramp0 = time.perf_counter()
+    n_ramp = 0
+    while (time.perf_counter() - ramp0) * 1e3 < args.ramp_ms:
+        step()
+        n_ramp += 1
+        torch.cuda.synchronize()
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([wall], dtype=torch.float64, device=dev if args.backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall = float(t.item())
+
+    # untimed breakdown of one step on this rank (HIP events on the current stream)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+    ev[0].record()
+    if world > 1:
+        routed, sc = hs.route(keys)
+        ev[1].record()
+        owned = hs.exchange(routed, sc)
+    else:
+        ev[1].record()
+        owned = keys
+    ev[2].record()
+    hs.build_range(owned)
+    ev[3].record()
+    torch.cuda.synchronize()
+    route_ms, a2a_ms, build_ms = (ev[i].elapsed_time(ev[i + 1]) for i in range(3))
+    n_owned = int(owned.shape[0])
+
+    allgather_ms = None
+    if world > 1:
+        dist.barrier()
+        g0 = time.perf_counter()
+        for _ in range(3):
+            hs.allgather()
+        torch.cuda.synchronize()
+        allgather_ms = (time.perf_counter() - g0) / 3 * 1e3
+    filt = hs.allgather()
+    torch.cuda.synchronize()
+
+    check = None
+    if rank == 0 and not args.no_verify:
+        allk = amq.gen_keys16(42, 0, total, device=dev)
+        ref_plan = amq.plan_filters(0, [total], bpk)
+        ref = amq.build_all_filters(ref_plan, amq.KeyBatch.fixed(allk))
+        check = {"equal_to_one_gpu_build": bool(torch.equal(ref[:filt.numel()], filt))}
+        del allk
+        if total <= 200_000_000:
+            from oracle import oracle as O
+            O.build_oracle()
+            st, oref = O.bloom_build(O.gen_keys16(42, 0, total), total, bpk, src_page_id=0)
+            check["equal_to_oracle"] = st == 0 and oref.tobytes() == filt.cpu().numpy().tobytes()
+        check["ok"] = all(v for k, v in check.items())
+    if world > 1:
+        flag = torch.tensor([1 if (check is None or check["ok"]) else 0], dtype=torch.int32,
+                            device=dev if args.backend == "nccl" else "cpu")
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        ok = bool(flag.item())
+    else:
+        ok = check is None or check["ok"]
+    if not ok:
+        raise SystemExit(f"bench.py: hash-sharded filter differs: {check}")
+    if world > 1:
+        dist.barrier()
+    if rank != 0:
+        dist.destroy_process_group()
+        return
+    ms_per_step = wall / args.steps * 1e3
+    value = total * args.steps / wall / 1e6
+    alg = n_local * 16 + (int(hs.payload_bytes) - 64) // world  # keys in, this rank's bitmap out
+    line = {
+        "metric": f"{label} Mkeys/s (device-resident)",
+        "value": round(value, 2), "unit": "Mkeys/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ramp_steps": n_ramp, "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True, "scaling": "strong" if strong else "weak", "vs_baseline": None,
+        "dtype": "u64", "data": "synthetic (splitmix64 seed 42 keys generated on the device)",
+        "config": {"workload": f"{label}: {total} x 16B keys, {n_local} per GPU, one filter of "
+                               f"{hs.n_blocks} blocks; rank r owns tiles [{hs.tile_begin}, ...)",
+                   "keys_per_gpu": n_local, "total_keys": total, "key_bytes": 16,
+                   "bits_per_key": bpk, "filter": "bloom-blocked512, monolithic",
+                   "parallelism": f"hash-range-sharded x{world}",
+                   "backend": args.backend if world > 1 else None},
+        "roofline": {"bound": "hbm", "achieved": round(alg / (ms_per_step * 1e-3) / 1e9, 1),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(alg / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                     "traffic": None, "kernel_ms": round(build_ms, 4), "alg_bytes_per_launch": alg,
+                     "note": "whole step on rank 0 (route + all-to-all + range build)"},
+        "cpu_baseline": None,
+        "step_breakdown_rank0_ms": {"route": round(route_ms, 4), "all_to_all": round(a2a_ms, 4),
+                                    "range_build": round(build_ms, 4), "keys_owned": n_owned},
+        "verified": check["ok"] if check else None, "verify": check,
+    }
+    if allgather_ms is not None:
+        line["allgather_ms"] = round(allgather_ms, 3)
+        line["build_plus_allgather_mkeys_s"] = round(total / ((ms_per_step + allgather_ms) * 1e-3) / 1e6, 2)
     print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

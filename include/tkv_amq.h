@@ -28,6 +28,10 @@
  *                           TreeOptions::filter_page_size_log2 / expected_items_per_leaf /
  *                           leaf_data_size (tree/tree_options.hpp:177-258, tree_options.cpp:57-60,
  *                           tree/packed_leaf_page.hpp:307-311, core/packed_sizeof_edit.hpp:13-15)
+ *   tkv_amq_bloom_route / tkv_amq_bloom_build_range
+ *                           one monolithic Bloom filter sharded by hash range over GPUs
+ *                           (BASELINE config 5; the llfs build_bloom_filter_page it replaces is
+ *                           called at tree/filter_builder.hpp:126-135)
  *   tkv_amq_plan_pages      FilterPageAlloc + the page header fields the builders set:
  *                           layout_id (filter_builder.hpp:237), unused_begin / unused_end
  *                           (:293-296), in one page-sized slot per leaf
@@ -171,6 +175,34 @@ int tkv_amq_build(int kind, const uint8_t* keys, const uint64_t* key_offsets,
  * Bloom builds cannot fail on the device. */
 int tkv_amq_build_check(int kind, const void* d_workspace, uint64_t workspace_bytes,
                         void* stream);
+
+/* Hash-range sharding of ONE monolithic Bloom filter over several GPUs (BASELINE config 5,
+ * SURVEY.md 8(e); no reference counterpart: the reference builds each filter on one CPU
+ * thread, filter_builder.hpp:126-135).  The filter planned by tkv_amq_plan for the whole key
+ * set (one segment of n_blocks blocks) is cut into T = ceil(n_blocks / 1024) tiles of 1024
+ * blocks; part p of n_parts owns tiles [p*q, min((p+1)*q, T)), q = ceil(T / n_parts), i.e. a
+ * contiguous byte range of the bitmap.  A key belongs to the tile of its block (h0).
+ *
+ * tkv_amq_bloom_route: rank-local step 1.  Reorders this rank's n_keys 16-byte keys by owning
+ * part into d_routed16 (part 0's keys first) and writes the per-part counts
+ * (d_part_counts[n_parts], u32, device) -- the send counts of the all-to-all that follows.
+ * d_seg is the whole filter's segment (device), n_blocks its n_blocks (host copy). */
+uint64_t tkv_amq_bloom_route_ws_bytes(uint64_t n_keys, uint32_t n_parts);
+int tkv_amq_bloom_route(const uint8_t* d_keys16, uint64_t n_keys, const tkv_amq_segment* d_seg,
+                        uint32_t n_blocks, uint32_t n_parts, uint8_t* d_routed16,
+                        uint32_t* d_part_counts, void* d_workspace, uint64_t workspace_bytes,
+                        void* stream);
+
+/* tkv_amq_bloom_build_range: rank-local step 2, after the all-to-all.  Builds tiles
+ * [tile_begin, tile_end) of the filter from the keys this rank received (all of whose tiles
+ * must fall in the range; others are ignored) into d_out at the segment's out_offset, exactly
+ * where tkv_amq_build puts them, and writes the filter header too.  Bytes of other tiles are
+ * not touched, so the ranks' ranges are disjoint and one all-gather of them is the filter. */
+uint64_t tkv_amq_bloom_build_range_ws_bytes(uint64_t n_keys, uint32_t tile_begin, uint32_t tile_end);
+int tkv_amq_bloom_build_range(const uint8_t* d_keys16, uint64_t n_keys, const tkv_amq_segment* d_seg,
+                              uint32_t n_blocks, uint32_t tile_begin, uint32_t tile_end,
+                              uint8_t* d_out, void* d_workspace, uint64_t workspace_bytes,
+                              void* stream);
 
 /* Batched probe: query i tests the filter of segment d_query_seg[i].  d_result[i] = 1 if
  * the key may be present, 0 if the filter rejects it (reject_page == kTrue).  A segment index

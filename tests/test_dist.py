@@ -86,3 +86,18 @@ def test_shard_ranges_cover_all_leaves():
             assert a.leaf_end == b.leaf_begin and a.key_end == b.key_begin
         assert shards[-1].key_end == sum(counts)
         assert all(s.n_leaves <= s.leaves_per_rank for s in shards)
+
+
+def test_hash_shard_tiles_cover_the_filter():
+    """Hash-range sharding (config 5 read literally): the ranks' tile ranges are contiguous,
+    disjoint and cover every tile; a filter with fewer tiles than ranks is refused."""
+    from turtle_kv_amd import abi
+    from turtle_kv_amd.dist import HashShardedBloom, hash_shard_tiles
+    for nb, world in [(1, 1), (1024, 1), (1025, 2), (93750, 8), (2_343_750, 8), (29297, 8)]:
+        T, q = hash_shard_tiles(nb, world)
+        assert T == -(-nb // 1024)
+        ranges = [(min(T, r * q), min(T, (r + 1) * q)) for r in range(world)]
+        assert ranges[0][0] == 0 and ranges[-1][1] == T
+        assert all(a[1] == b[0] for a, b in zip(ranges, ranges[1:]))
+    with pytest.raises(abi.TkvAmqError):
+        HashShardedBloom(100_000, 12, 8, 0, "cpu")   # 3 tiles over 8 ranks

@@ -1,0 +1,108 @@
+"""Hash-range sharding of one monolithic Bloom filter (BASELINE config 5 read literally):
+tkv_amq_bloom_route + tkv_amq_bloom_build_range through the C ABI on one GPU (the parts
+played in turn), the rank-side orchestration (turtle_kv_amd.dist.HashShardedBloom) through
+bench.py with two gloo ranks sharing the box's GPU, and the degenerate one-rank case.  The
+assembled filter must equal the one-GPU monolithic build and the CPU oracle."""
+import numpy as np
+import pytest
+
+from test_gpu_bench import SMALL, last_json, run_bench
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch as t
+    assert t.cuda.is_available(), "GPU tests need a visible MI355X"
+    return t
+
+
+def _route(amq, torch, keys, plan, n_parts):
+    from turtle_kv_amd.filters import _ptr, _stream_handle
+    L = amq.abi.lib()
+    n = keys.shape[0]
+    nb = int(plan.segs[0]["n_blocks"])
+    routed = torch.empty_like(keys)
+    counts = torch.zeros(n_parts, dtype=torch.int32, device="cuda")
+    ws = torch.empty(int(L.tkv_amq_bloom_route_ws_bytes(n, n_parts)), dtype=torch.uint8, device="cuda")
+    amq.abi.check(L.tkv_amq_bloom_route(_ptr(keys), n, _ptr(plan.device_segs()), nb, n_parts,
+                                        _ptr(routed), _ptr(counts), _ptr(ws), ws.numel(),
+                                        _stream_handle()), "route")
+    torch.cuda.synchronize()
+    return routed, counts.cpu().numpy().astype(np.int64)
+
+
+def _build_range(amq, torch, keys, plan, t0, t1, out):
+    from turtle_kv_amd.filters import _ptr, _stream_handle
+    L = amq.abi.lib()
+    n = keys.shape[0]
+    ws = torch.empty(max(1, int(L.tkv_amq_bloom_build_range_ws_bytes(n, t0, t1))), dtype=torch.uint8,
+                     device="cuda")
+    amq.abi.check(L.tkv_amq_bloom_build_range(_ptr(keys), n, _ptr(plan.device_segs()),
+                                              int(plan.segs[0]["n_blocks"]), t0, t1, _ptr(out),
+                                              _ptr(ws), ws.numel(), _stream_handle()), "build_range")
+
+
+@pytest.mark.parametrize("n_keys,bpk,n_parts", [(3_000_000, 12, 3), (1_500_001, 10, 8), (700_000, 12, 1)])
+def test_route_and_range_build_equal_monolithic(oracle, amq, torch, n_keys, bpk, n_parts):
+    from turtle_kv_amd.dist import hash_shard_tiles
+    keys = amq.gen_keys16(11, 0, n_keys)
+    plan = amq.plan_filters(0, [n_keys], bpk)
+    nb = int(plan.segs[0]["n_blocks"])
+    assert 64 * nb > 64 * 1024, "must take the tiled monolithic build"
+    whole = amq.build_all_filters(plan, amq.KeyBatch.fixed(keys))
+    routed, counts = _route(amq, torch, keys, plan, n_parts)
+    assert counts.sum() == n_keys
+    # the route is a permutation of the keys
+    a = np.sort(keys.cpu().numpy().view("<u8").reshape(-1, 2), axis=0)
+    b = np.sort(routed.cpu().numpy().view("<u8").reshape(-1, 2), axis=0)
+    assert np.array_equal(a, b)
+    T, q = hash_shard_tiles(nb, n_parts)
+    out = torch.zeros(plan.total_out_bytes, dtype=torch.uint8, device="cuda")
+    base = np.concatenate([[0], np.cumsum(counts)])
+    for p in range(n_parts):
+        part = routed[int(base[p]):int(base[p + 1])]
+        _build_range(amq, torch, part, plan, min(T, p * q), min(T, (p + 1) * q), out)
+    torch.cuda.synchronize()
+    assert torch.equal(out, whole)
+    st, ref = oracle.bloom_build(keys.cpu().numpy(), n_keys, bpk, src_page_id=0)
+    assert st == 0 and out.cpu().numpy().tobytes() == ref.tobytes()
+
+
+def test_range_build_ignores_keys_outside_its_tiles(amq, torch):
+    """Handing a rank every key (not just the routed ones) builds the same range: keys of
+    other ranks' tiles are skipped."""
+    n = 2_000_000
+    keys = amq.gen_keys16(12, 0, n)
+    plan = amq.plan_filters(0, [n], 12)
+    from turtle_kv_amd.dist import hash_shard_tiles
+    T, q = hash_shard_tiles(int(plan.segs[0]["n_blocks"]), 4)
+    whole = amq.build_all_filters(plan, amq.KeyBatch.fixed(keys))
+    out = torch.zeros(plan.total_out_bytes, dtype=torch.uint8, device="cuda")
+    _build_range(amq, torch, keys, plan, q, 2 * q, out)
+    torch.cuda.synchronize()
+    lo, hi = 64 + 64 * 1024 * q, 64 + 64 * 1024 * 2 * q
+    assert torch.equal(out[lo:hi], whole[lo:hi])
+    assert torch.equal(out[:64], whole[:64])          # the header, from every range
+    assert int(out[64:lo].count_nonzero()) == 0       # other ranges untouched
+    assert int(out[hi:].count_nonzero()) == 0
+
+
+def test_bench_hash_sharded_two_ranks_gloo():
+    r = run_bench("--gpus", "2", "--backend", "gloo", "--workload", "bloom12hash",
+                  "--keys-per-gpu", "2000000", *SMALL)
+    assert r.returncode == 0, r.stderr[-4000:]
+    d = last_json(r)
+    assert d["n_gpus"] == 2 and d["config"]["total_keys"] == 4_000_000
+    assert d["verified"] is True
+    assert d["verify"]["equal_to_one_gpu_build"] and d["verify"]["equal_to_oracle"]
+    assert d["allgather_ms"] > 0
+    assert 0 < d["step_breakdown_rank0_ms"]["keys_owned"] < 4_000_000
+
+
+def test_bench_hash_sharded_one_rank():
+    r = run_bench("--workload", "bloom12hash", "--keys-per-gpu", "3000000", *SMALL)
+    assert r.returncode == 0, r.stderr[-4000:]
+    d = last_json(r)
+    assert d["n_gpus"] == 1 and d["verified"] is True

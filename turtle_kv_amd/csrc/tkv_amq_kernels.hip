@@ -533,13 +533,38 @@ __device__ inline uint32_t bloom_tile_of(const uint4& kv, uint32_t nb)
   return (uint32_t)__umul64hi(h0, (uint64_t)nb) / kBloomTileBlocks;
 }
 
+// The window of a partition pass.  The whole monolithic filter: tile0 = 0, div = 1, keys
+// from the segment.  Hash-range sharding (tkv_amq_bloom_route / _build_range): the route
+// partitions a rank's keys by owner (div = tiles per part, output to `out`); a rank's range
+// build takes its routed keys [0, n) and the tiles [tile0, tile0 + n_tiles).
+struct PartWindow {
+  uint32_t tile0;  // global tile of local tile 0
+  uint32_t div;    // global tiles per local tile
+  uint32_t local;  // keys are [0, n_cap) of the key array, not the segment's range
+  uint32_t hdr;    // the first local tile also writes the filter header (every rank)
+  uint4* out;      // partitioned keys go here instead of the workspace
+};
+
+__host__ __device__ inline PartWindow whole_filter_window()
+{
+  return PartWindow{0u, 1u, 0u, 0u, nullptr};
+}
+
+// local tile of a key, or ~0 outside the window (below tile0 the subtraction wraps)
+__device__ inline uint32_t part_tile(const uint4& kv, uint32_t nb, const PartWindow& pw,
+                                     uint32_t n_tiles)
+{
+  const uint32_t t = (bloom_tile_of(kv, nb) - pw.tile0) / pw.div;
+  return t < n_tiles ? t : ~0u;
+}
+
 // PASS 0: histogram; PASS 1: scatter.  Both walk the same key range in the same way.
 template <int PASS, uint32_t NT>
 __global__ __launch_bounds__(NT) void bloom_part_keys(const uint4* __restrict__ keys,
                                                        const tkv_amq_segment* __restrict__ segs,
                                                        uint32_t* __restrict__ ws, uint32_t n_tiles,
                                                        uint32_t per, uint64_t part_off,
-                                                       uint32_t n_cap)
+                                                       uint32_t n_cap, PartWindow pw)
 {
   extern __shared__ uint32_t s_tile[];
   const tkv_amq_segment sg = segs[0];
@@ -549,10 +574,10 @@ __global__ __launch_bounds__(NT) void bloom_part_keys(const uint4* __restrict__ 
   for (uint32_t t = tid; t < n_tiles; t += NT) s_tile[t] = PASS == 0 ? 0u : base[t] + H[t];
   __syncthreads();
   // n_cap: keys the caller passed (the partition buffer holds that many)
-  const uint32_t n = min(sg.n_keys, n_cap), nb = sg.n_blocks;
+  const uint32_t n = pw.local ? n_cap : min(sg.n_keys, n_cap), nb = sg.n_blocks;
   const uint32_t b = min(n, w * per), e = min(n, b + per);
-  const uint4* kp = keys + sg.key_begin;
-  uint4* part = reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(ws) + part_off);
+  const uint4* kp = keys + (pw.local ? 0 : sg.key_begin);
+  uint4* part = pw.out ? pw.out : reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(ws) + part_off);
   constexpr int U = 4;
   for (uint32_t i0 = b; i0 < e; i0 += NT * U) {
     uint4 kv[U];
@@ -565,7 +590,8 @@ __global__ __launch_bounds__(NT) void bloom_part_keys(const uint4* __restrict__ 
     for (int u = 0; u < U; ++u) {
       const uint32_t i = i0 + u * NT + tid;
       if (i < e) {
-        const uint32_t t = bloom_tile_of(kv[u], nb);
+        const uint32_t t = part_tile(kv[u], nb, pw, n_tiles);
+        if (t == ~0u) continue;
         if constexpr (PASS == 0) {
           atomicAdd(s_tile + t, 1u);
         } else {
@@ -588,7 +614,8 @@ __global__ __launch_bounds__(NT) void bloom_part_keys(const uint4* __restrict__ 
 // reaches every barrier).  The runs start at the padded offsets of bloom_part_scan_cols.
 __global__ __launch_bounds__(kStageThreads) void bloom_part_scatter_staged(
     const uint4* __restrict__ keys, const tkv_amq_segment* __restrict__ segs,
-    uint32_t* __restrict__ ws, uint32_t n_tiles, uint32_t per, uint64_t part_off, uint32_t n_cap)
+    uint32_t* __restrict__ ws, uint32_t n_tiles, uint32_t per, uint64_t part_off, uint32_t n_cap,
+    PartWindow pw)
 {
   extern __shared__ __attribute__((aligned(16))) uint8_t s_stage[];
   uint4* stage = reinterpret_cast<uint4*>(s_stage);                       // [tile][kStageKeys]
@@ -603,9 +630,9 @@ __global__ __launch_bounds__(kStageThreads) void bloom_part_scatter_staged(
     cur[t] = base[t] + H[t];
   }
   __syncthreads();
-  const uint32_t n = min(sg.n_keys, n_cap), nb = sg.n_blocks;
+  const uint32_t n = pw.local ? n_cap : min(sg.n_keys, n_cap), nb = sg.n_blocks;
   const uint32_t b = min(n, w * per), e = min(n, b + per);
-  const uint4* kp = keys + sg.key_begin;
+  const uint4* kp = keys + (pw.local ? 0 : sg.key_begin);
   uint4* part = reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(ws) + part_off);
   // each round, every thread stages kR keys (prefetched one round ahead)
   constexpr uint32_t kR = kStageRound;
@@ -625,8 +652,9 @@ __global__ __launch_bounds__(kStageThreads) void bloom_part_scatter_staged(
       const uint32_t i = c0 + u * kStageThreads + tid;
       kv[u] = ring[u];
       if (i + kRound < e) ring[u] = load_nt16(kp + i + kRound);
-      pend[u] = i < e;
-      t[u] = pend[u] ? bloom_tile_of(kv[u], nb) : 0u;
+      t[u] = i < e ? part_tile(kv[u], nb, pw, n_tiles) : ~0u;
+      pend[u] = t[u] != ~0u;
+      if (!pend[u]) t[u] = 0;
     }
     for (;;) {
       uint32_t slot[kR];
@@ -746,13 +774,13 @@ __global__ __launch_bounds__(256) void bloom_part_scan_tiles(uint32_t* __restric
 template <uint32_t NT>
 __global__ __launch_bounds__(NT) void bloom_tile_build(
     const tkv_amq_segment* __restrict__ segs, const uint32_t* __restrict__ ws, uint32_t P,
-    uint32_t n_tiles, uint64_t part_off, uint8_t* __restrict__ out)
+    uint32_t n_tiles, uint64_t part_off, uint8_t* __restrict__ out, PartWindow pw)
 {
   extern __shared__ uint32_t s_bits[];
   const tkv_amq_segment sg = segs[0];
   const uint32_t t = blockIdx.x, tid = threadIdx.x;
   const uint32_t nb = sg.n_blocks, k = sg.hash_count;
-  const uint32_t first = t * kBloomTileBlocks;
+  const uint32_t first = (pw.tile0 + t) * kBloomTileBlocks;
   const uint32_t tb = min(kBloomTileBlocks, nb - first);
   for (uint32_t w = tid; w < tb * 16; w += NT) s_bits[w] = 0;
   __syncthreads();
@@ -764,8 +792,9 @@ __global__ __launch_bounds__(NT) void bloom_tile_build(
   else bloom_keys16_lds<0, NT>(kp, ke - kb, nb, k, s_bits, first);
   __syncthreads();
   uint8_t* payload = out + sg.out_offset;
-  if (t == 0 && tid < 4) write_bloom_header(payload, sg, tid);
-  else if (t == 0 && tid < 8) write_page_header(out, sg, kLayoutBloom, tid - 4);
+  const bool hdr = t == 0 && (pw.tile0 == 0 || pw.hdr);
+  if (hdr && tid < 4) write_bloom_header(payload, sg, tid);
+  else if (hdr && tid < 8) write_page_header(out, sg, kLayoutBloom, tid - 4);
   uint4* dst = reinterpret_cast<uint4*>(payload + kBloomHeader + 64ull * first);
   const uint4* src = reinterpret_cast<const uint4*>(s_bits);
   for (uint32_t q = tid; q < tb * 4; q += NT) dst[q] = src[q];
@@ -2557,6 +2586,74 @@ inline void once_per_device(std::once_flag (&flags)[kMaxDevices], Fn&& fn)
   std::call_once(flags[dev], fn);
 }
 
+// Kernel attributes of the partitioned monolithic build (dynamic LDS above 64 KiB).
+inline void set_part_attributes()
+{
+  static std::once_flag lds_attr[kMaxDevices];
+  once_per_device(lds_attr, [] {
+    const int cap = (int)(4 * kBloomPartMaxTiles);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&bloom_part_keys<0, 256>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, cap);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&bloom_part_keys<1, 256>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, cap);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&bloom_part_scatter_staged),
+                              hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)bloom_stage_lds_bytes(kStageMaxTiles));
+  });
+}
+
+// count -> scans -> scatter -> tile build over the window `pw` (the whole filter, or one
+// rank's tile range of a hash-range sharded filter)
+inline void launch_partitioned_build(const BloomPartGeom& pg, hipStream_t s, const uint4* k4,
+                                     const tkv_amq_segment* d_segs, uint32_t* w, uint32_t nk,
+                                     const PartWindow& pw, uint8_t* d_out)
+{
+  const size_t hl = 4ull * pg.n_tiles;
+  if (pg.staged)
+    hipLaunchKernelGGL((bloom_part_keys<0, kStageThreads>), dim3(pg.P), dim3(kStageThreads), hl, s,
+                       k4, d_segs, w, pg.n_tiles, pg.per, pg.part_off, nk, pw);
+  else
+    hipLaunchKernelGGL((bloom_part_keys<0, 256>), dim3(pg.P), dim3(256), hl, s, k4, d_segs, w,
+                       pg.n_tiles, pg.per, pg.part_off, nk, pw);
+  hipLaunchKernelGGL(bloom_part_scan_cols, dim3(pg.n_tiles), dim3(256), 0, s, w, pg.P, pg.n_tiles,
+                     (uint32_t)pg.staged);
+  hipLaunchKernelGGL(bloom_part_scan_tiles, dim3(1), dim3(256), 0, s, w, pg.P, pg.n_tiles);
+  if (pg.staged)
+    hipLaunchKernelGGL(bloom_part_scatter_staged, dim3(pg.P), dim3(kStageThreads),
+                       bloom_stage_lds_bytes(pg.n_tiles), s, k4, d_segs, w, pg.n_tiles, pg.per,
+                       pg.part_off, nk, pw);
+  else
+    hipLaunchKernelGGL((bloom_part_keys<1, 256>), dim3(pg.P), dim3(256), hl, s, k4, d_segs, w,
+                       pg.n_tiles, pg.per, pg.part_off, nk, pw);
+  hipLaunchKernelGGL(bloom_tile_build<kBloomTileThreads>, dim3(pg.n_tiles), dim3(kBloomTileThreads),
+                     64ull * kBloomTileBlocks, s, d_segs, w, pg.P, pg.n_tiles, pg.part_off, d_out,
+                     pw);
+}
+
+// Hash-range sharding (BASELINE config 5): T = ceil(n_blocks / tile) tiles, q = ceil(T / parts)
+// per part; part p owns tiles [p * q, min((p + 1) * q, T)).
+inline uint32_t shard_tiles_per_part(uint32_t n_blocks, uint32_t n_parts)
+{
+  const uint32_t T = (uint32_t)div_up(n_blocks, kBloomTileBlocks);
+  return (uint32_t)div_up(T, n_parts);
+}
+
+// the route is an unstaged partition (exact runs, no padding) into n_parts buckets
+inline BloomPartGeom bloom_route_geom(uint64_t n_keys, uint32_t n_parts)
+{
+  BloomPartGeom g;
+  g.n_tiles = n_parts;
+  g.staged = false;
+  const uint64_t p = (n_keys + 4095) / 4096;
+  g.P = (uint32_t)(p < 1 ? 1 : (p > kBloomPartMaxWgs ? kBloomPartMaxWgs : p));
+  g.threads = 256;
+  g.per = (uint32_t)((n_keys + g.P - 1) / g.P);
+  g.h_words = (uint64_t)g.P * n_parts;
+  g.part_off = (4 * (g.h_words + 2ull * n_parts + 1) + 255) & ~255ull;
+  g.bytes = g.part_off;
+  return g;
+}
+
 // a one-filter Bloom batch too large for one LDS image takes the tiled, partitioned build
 // (it needs a workspace of bloom_part_geom(n_keys, n_blocks).bytes and 16-byte keys)
 inline bool bloom_partitioned(uint32_t n_segs, uint64_t max_blocks, uint64_t n_keys)
@@ -2846,40 +2943,10 @@ int tkv_amq_build(int kind, const uint8_t* keys, const uint64_t* offs, uint32_t 
     if (bloom_partitioned(n_segs, max_blocks, n_keys) && mode == kKey16 && d_ws &&
         ws_bytes >= pg.bytes) {
       // one monolithic filter: partition the keys by tile, build every tile in LDS
-      static std::once_flag lds_attr[kMaxDevices];
-      once_per_device(lds_attr, [] {
-        const int cap = (int)(4 * kBloomPartMaxTiles);
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&bloom_part_keys<0, 256>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, cap);
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&bloom_part_keys<1, 256>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, cap);
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&bloom_part_scatter_staged),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)bloom_stage_lds_bytes(kStageMaxTiles));
-      });
-      uint32_t* w = static_cast<uint32_t*>(d_ws);
-      const uint4* k4 = reinterpret_cast<const uint4*>(keys);
-      const size_t hl = 4ull * pg.n_tiles;
-      const uint32_t nk = (uint32_t)n_keys;
-      if (pg.staged)
-        hipLaunchKernelGGL((bloom_part_keys<0, kStageThreads>), dim3(pg.P), dim3(kStageThreads), hl,
-                           s, k4, d_segs, w, pg.n_tiles, pg.per, pg.part_off, nk);
-      else
-        hipLaunchKernelGGL((bloom_part_keys<0, 256>), dim3(pg.P), dim3(256), hl, s, k4, d_segs, w,
-                           pg.n_tiles, pg.per, pg.part_off, nk);
-      hipLaunchKernelGGL(bloom_part_scan_cols, dim3(pg.n_tiles), dim3(256), 0, s, w, pg.P,
-                         pg.n_tiles, (uint32_t)pg.staged);
-      hipLaunchKernelGGL(bloom_part_scan_tiles, dim3(1), dim3(256), 0, s, w, pg.P, pg.n_tiles);
-      if (pg.staged)
-        hipLaunchKernelGGL(bloom_part_scatter_staged, dim3(pg.P), dim3(kStageThreads),
-                           bloom_stage_lds_bytes(pg.n_tiles), s, k4, d_segs, w, pg.n_tiles, pg.per,
-                           pg.part_off, nk);
-      else
-        hipLaunchKernelGGL((bloom_part_keys<1, 256>), dim3(pg.P), dim3(256), hl, s, k4, d_segs, w,
-                           pg.n_tiles, pg.per, pg.part_off, nk);
-      hipLaunchKernelGGL(bloom_tile_build<kBloomTileThreads>, dim3(pg.n_tiles),
-                         dim3(kBloomTileThreads), 64ull * kBloomTileBlocks, s, d_segs, w, pg.P,
-                         pg.n_tiles, pg.part_off, d_out);
+      set_part_attributes();
+      launch_partitioned_build(pg, s, reinterpret_cast<const uint4*>(keys), d_segs,
+                               static_cast<uint32_t*>(d_ws), (uint32_t)n_keys, whole_filter_window(),
+                               d_out);
     } else {
       // fewer than kBloomSpreadSegs leaves, leaves beyond the LDS budget in a multi-leaf batch,
       // or a monolithic filter whose keys are not 16 bytes: device atomics
@@ -2959,6 +3026,73 @@ int tkv_amq_build(int kind, const uint8_t* keys, const uint64_t* offs, uint32_t 
     hipLaunchKernelGGL(vqf_place, dim3(n_segs), dim3(kPlaceThreads), 0, s, d_segs, d_ws, ws_bytes,
                        n_segs, d_out);
   }
+  return hipGetLastError() == hipSuccess ? TKV_AMQ_OK : TKV_AMQ_INTERNAL;
+}
+
+uint64_t tkv_amq_bloom_route_ws_bytes(uint64_t n_keys, uint32_t n_parts)
+{
+  if (n_parts == 0 || n_parts > kStageMaxTiles) return 0;
+  return bloom_route_geom(n_keys, n_parts).bytes;
+}
+
+int tkv_amq_bloom_route(const uint8_t* d_keys16, uint64_t n_keys, const tkv_amq_segment* d_seg,
+                        uint32_t n_blocks, uint32_t n_parts, uint8_t* d_routed16,
+                        uint32_t* d_part_counts, void* d_ws, uint64_t ws_bytes, void* stream)
+{
+  if (tkv_amq_device_count() == 0) return TKV_AMQ_UNAVAILABLE;
+  if (n_parts == 0 || n_parts > kStageMaxTiles || n_blocks == 0 || !d_seg || !d_part_counts ||
+      n_keys > 0xffffffffull)
+    return TKV_AMQ_INVALID_ARGUMENT;
+  if (n_keys && (!d_keys16 || !d_routed16 || (reinterpret_cast<uintptr_t>(d_keys16) & 15) ||
+                 (reinterpret_cast<uintptr_t>(d_routed16) & 15)))
+    return TKV_AMQ_INVALID_ARGUMENT;
+  const BloomPartGeom g = bloom_route_geom(n_keys, n_parts);
+  if (!d_ws || ws_bytes < g.bytes) return TKV_AMQ_INVALID_ARGUMENT;
+  const hipStream_t s = as_stream(stream);
+  uint32_t* w = static_cast<uint32_t*>(d_ws);
+  set_part_attributes();
+  const PartWindow pw{0u, shard_tiles_per_part(n_blocks, n_parts), 1u, 0u,
+                      reinterpret_cast<uint4*>(d_routed16)};
+  const uint4* k4 = reinterpret_cast<const uint4*>(d_keys16);
+  const size_t hl = 4ull * n_parts;
+  const uint32_t nk = (uint32_t)n_keys;
+  hipLaunchKernelGGL((bloom_part_keys<0, 256>), dim3(g.P), dim3(256), hl, s, k4, d_seg, w, n_parts,
+                     g.per, g.part_off, nk, pw);
+  hipLaunchKernelGGL(bloom_part_scan_cols, dim3(n_parts), dim3(256), 0, s, w, g.P, n_parts, 0u);
+  hipLaunchKernelGGL(bloom_part_scan_tiles, dim3(1), dim3(256), 0, s, w, g.P, n_parts);
+  hipLaunchKernelGGL((bloom_part_keys<1, 256>), dim3(g.P), dim3(256), hl, s, k4, d_seg, w, n_parts,
+                     g.per, g.part_off, nk, pw);
+  // the per-part totals bloom_part_scan_cols left after the histogram
+  if (hipMemcpyAsync(d_part_counts, w + g.h_words, 4ull * n_parts, hipMemcpyDeviceToDevice, s) !=
+      hipSuccess)
+    return TKV_AMQ_INTERNAL;
+  return hipGetLastError() == hipSuccess ? TKV_AMQ_OK : TKV_AMQ_INTERNAL;
+}
+
+uint64_t tkv_amq_bloom_build_range_ws_bytes(uint64_t n_keys, uint32_t tile_begin, uint32_t tile_end)
+{
+  if (tile_end <= tile_begin || tile_end - tile_begin > kBloomPartMaxTiles) return 0;
+  return bloom_part_geom(n_keys, (uint64_t)(tile_end - tile_begin) * kBloomTileBlocks).bytes;
+}
+
+int tkv_amq_bloom_build_range(const uint8_t* d_keys16, uint64_t n_keys, const tkv_amq_segment* d_seg,
+                              uint32_t n_blocks, uint32_t tile_begin, uint32_t tile_end,
+                              uint8_t* d_out, void* d_ws, uint64_t ws_bytes, void* stream)
+{
+  if (tkv_amq_device_count() == 0) return TKV_AMQ_UNAVAILABLE;
+  const uint32_t T = (uint32_t)div_up(n_blocks, kBloomTileBlocks);
+  if (!d_seg || !d_out || n_blocks == 0 || tile_begin > tile_end || tile_end > T ||
+      tile_end - tile_begin > kBloomPartMaxTiles || n_keys > 0xffffffffull)
+    return TKV_AMQ_INVALID_ARGUMENT;
+  if (n_keys && (!d_keys16 || (reinterpret_cast<uintptr_t>(d_keys16) & 15)))
+    return TKV_AMQ_INVALID_ARGUMENT;
+  if (tile_begin == tile_end) return TKV_AMQ_OK;
+  const BloomPartGeom pg = bloom_part_geom(n_keys, (uint64_t)(tile_end - tile_begin) * kBloomTileBlocks);
+  if (!d_ws || ws_bytes < pg.bytes) return TKV_AMQ_INVALID_ARGUMENT;
+  set_part_attributes();
+  const PartWindow pw{tile_begin, 1u, 1u, 1u, nullptr};
+  launch_partitioned_build(pg, as_stream(stream), reinterpret_cast<const uint4*>(d_keys16), d_seg,
+                           static_cast<uint32_t*>(d_ws), (uint32_t)n_keys, pw, d_out);
   return hipGetLastError() == hipSuccess ? TKV_AMQ_OK : TKV_AMQ_INTERNAL;
 }
 

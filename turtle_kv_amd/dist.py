@@ -81,3 +81,129 @@ def allgather_filters(local, gathered=None, group=None):
         parts = list(gathered.view(world, -1).unbind(0))
         dist.all_gather(parts, local, group=group)
     return gathered
+
+
+# ---------------------------------------------------------------------------------------
+# Hash-range sharding of ONE monolithic Bloom filter (BASELINE config 5 read literally:
+# "1B keys, Bloom @12, hash-range sharded across 8 GPUs, RCCL all-gather").  Unlike the leaf
+# filters above, keys must move: every key's bits fall in the 64-byte block its h0 selects, so
+# a rank can only build its byte range of the bitmap from the keys whose blocks fall there.
+# Steps per build: route (reorder the rank's keys by owning rank, tkv_amq_bloom_route), one
+# all-to-all of the keys (RCCL over xGMI), the rank's tile range built in LDS
+# (tkv_amq_bloom_build_range), then the all-gather of the bitmap ranges.
+# ---------------------------------------------------------------------------------------
+BLOOM_TILE_BLOCKS = 1024  # blocks per tile, as tkv_amq_bloom_route / _build_range cut them
+
+
+def hash_shard_tiles(n_blocks: int, world: int) -> tuple[int, int]:
+    """(T, q): the filter's tiles and the tiles per rank; rank r owns [r*q, min((r+1)*q, T))."""
+    T = -(-int(n_blocks) // BLOOM_TILE_BLOCKS)
+    return T, -(-T // world)
+
+
+class HashShardedBloom:
+    """One rank's side of a hash-range sharded build of one Bloom filter over the keys of all
+    ranks (n_total_keys in all).  `build(keys)` returns the whole filter payload (header +
+    bitmap, byte-identical to a one-GPU tkv_amq_build of the concatenated keys) on every rank.
+    Buffers are allocated once and grown when a rank receives more keys than before."""
+
+    def __init__(self, n_total_keys: int, bits_per_key: int, world: int, rank: int, device,
+                 src_page_id: int = 0, group=None):
+        import torch
+        from . import abi
+        from .filters import plan_filters
+        self.world, self.rank, self.group, self.dev = world, rank, group, torch.device(device)
+        self.plan = plan_filters(abi.BLOOM, [n_total_keys], bits_per_key, src_page_ids=[src_page_id])
+        seg = self.plan.segs[0]
+        self.n_blocks = int(seg["n_blocks"])
+        self.payload_bytes = int(seg["payload_bytes"])
+        T, q = hash_shard_tiles(self.n_blocks, world)
+        if T < world:
+            raise abi.TkvAmqError(abi.INVALID_ARGUMENT, f"a {T}-tile filter cannot be sharded "
+                                  f"over {world} ranks (each needs >= 1 tile of 1024 blocks)")
+        self.tile_begin, self.tile_end = min(T, rank * q), min(T, (rank + 1) * q)
+        self.slice_bytes = q * BLOOM_TILE_BLOCKS * 64
+        # the payload layout of tkv_amq_build (64-byte header, then the blocks), padded so every
+        # rank's range is a slice of slice_bytes
+        self.out = torch.zeros(64 + world * self.slice_bytes, dtype=torch.uint8, device=self.dev)
+        self.gathered = torch.empty(world * self.slice_bytes, dtype=torch.uint8, device=self.dev)
+        self.d_seg = self.plan.device_segs(self.dev)
+        self.counts = torch.zeros(world, dtype=torch.int32, device=self.dev)
+        self._bufs = {}
+
+    def _buf(self, name, nbytes):
+        import torch
+        b = self._bufs.get(name)
+        if b is None or b.numel() < nbytes:
+            b = torch.empty(max(nbytes, 16), dtype=torch.uint8, device=self.dev)
+            self._bufs[name] = b
+        return b
+
+    def route(self, keys):
+        """keys [n, 16] uint8 on the device -> (routed [n, 16], send counts per rank, int64)."""
+        import torch
+        from . import abi
+        from .filters import _ptr, _stream_handle
+        L = abi.lib()
+        n = keys.shape[0]
+        routed = self._buf("routed", 16 * n)[:16 * n].view(n, 16)
+        ws = self._buf("route_ws", int(L.tkv_amq_bloom_route_ws_bytes(n, self.world)))
+        abi.check(L.tkv_amq_bloom_route(_ptr(keys), n, _ptr(self.d_seg), self.n_blocks, self.world,
+                                        _ptr(routed), _ptr(self.counts), _ptr(ws), ws.numel(),
+                                        _stream_handle()), "tkv_amq_bloom_route")
+        return routed, self.counts.to(dtype=torch.int64)
+
+    def exchange(self, routed, send_counts):
+        """All-to-all of the routed keys: returns the [m, 16] keys this rank owns."""
+        import torch
+        import torch.distributed as dist
+        gloo = dist.get_backend(self.group) != "nccl"
+        sc = send_counts.cpu() if gloo else send_counts
+        rc = torch.empty_like(sc)
+        dist.all_to_all_single(rc, sc, group=self.group)
+        send = [int(x) * 16 for x in sc.tolist()]
+        recv = [int(x) * 16 for x in rc.tolist()]
+        m = sum(recv) // 16
+        out = self._buf("recv", 16 * m)[:16 * m]
+        src = routed.reshape(-1)
+        if gloo:  # CPU rehearsal: stage through host memory
+            host = torch.empty(16 * m, dtype=torch.uint8)
+            dist.all_to_all_single(host, src.cpu(), recv, send, group=self.group)
+            out.copy_(host)
+        else:
+            dist.all_to_all_single(out, src, recv, send, group=self.group)
+        return out.view(m, 16)
+
+    def build_range(self, owned):
+        """This rank's tile range of the filter from the keys it owns (into self.out)."""
+        from . import abi
+        from .filters import _ptr, _stream_handle
+        L = abi.lib()
+        m = owned.shape[0]
+        ws = self._buf("build_ws", int(L.tkv_amq_bloom_build_range_ws_bytes(m, self.tile_begin,
+                                                                             self.tile_end)))
+        abi.check(L.tkv_amq_bloom_build_range(_ptr(owned), m, _ptr(self.d_seg), self.n_blocks,
+                                              self.tile_begin, self.tile_end, _ptr(self.out),
+                                              _ptr(ws), ws.numel(), _stream_handle()),
+                  "tkv_amq_bloom_build_range")
+
+    def local_build(self, keys):
+        """route + exchange + range build: after it, this rank's byte range of the bitmap is final."""
+        if self.world == 1:
+            self.build_range(keys)
+            return
+        routed, sc = self.route(keys)
+        self.build_range(self.exchange(routed, sc))
+
+    def allgather(self):
+        """Every rank's bitmap range -> the whole filter payload (header + bitmap) on every rank."""
+        import torch
+        if self.world == 1:
+            return self.out[:self.payload_bytes]
+        r0 = 64 + self.rank * self.slice_bytes
+        allgather_filters(self.out[r0:r0 + self.slice_bytes], self.gathered, self.group)
+        return torch.cat([self.out[:64], self.gathered[:self.payload_bytes - 64]])
+
+    def build(self, keys):
+        self.local_build(keys)
+        return self.allgather()
