@@ -44,10 +44,17 @@ def _build_range(amq, torch, keys, plan, t0, t1, out):
                                               _ptr(ws), ws.numel(), _stream_handle()), "build_range")
 
 
-@pytest.mark.parametrize("n_keys,bpk,n_parts", [(3_000_000, 12, 3), (1_500_001, 10, 8), (700_000, 12, 1)])
-def test_route_and_range_build_equal_monolithic(oracle, amq, torch, n_keys, bpk, n_parts):
+@pytest.mark.parametrize("n_keys,bpk,n_parts,dup", [(3_000_000, 12, 3, 0), (1_500_001, 10, 8, 0),
+                                                   (700_000, 12, 1, 0), (2_000_000, 12, 4, 600_000),
+                                                   (400_000, 16, 2, 0)])
+def test_route_and_range_build_equal_monolithic(oracle, amq, torch, n_keys, bpk, n_parts, dup):
+    """dup: that many copies of one key (its tile's regions overflow: the record path's
+    overflow lists, applied with tile0 > 0 on most ranks); bpk 16: k = 11 > 8, the ranges
+    partition the 16-byte keys themselves and hash them per tile."""
     from turtle_kv_amd.dist import hash_shard_tiles
     keys = amq.gen_keys16(11, 0, n_keys)
+    if dup:
+        keys[n_keys - dup:] = keys[n_keys // 3]
     plan = amq.plan_filters(0, [n_keys], bpk)
     nb = int(plan.segs[0]["n_blocks"])
     assert 64 * nb > 64 * 1024, "must take the tiled monolithic build"

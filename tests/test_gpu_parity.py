@@ -380,9 +380,10 @@ def test_vqf_hash_matches_xxhash(amq, torch):
 @pytest.mark.parametrize("n,bpk,seed", [(120000, 10, 8), (3000000, 10, 9), (1500000, 12, 10),
                                          (400000, 5, 11), (10000, 64, 12)])
 def test_bloom_monolithic_partitioned(oracle, amq, torch, n, bpk, seed):
-    """One filter larger than the LDS image budget (64 KiB): tiled build over keys partitioned
-    by tile (bloom_part_keys / bloom_tile_build), byte-identical to the oracle.  Covers a
-    ragged last tile, k = 7 / 8 / generic, and 58 tiles over 733 partition workgroups."""
+    """One filter larger than the LDS image budget (64 KiB): the hash-once record path
+    (bloom_rec_partition / bloom_rec_tile), byte-identical to the oracle.  Covers a ragged last
+    tile, k = 7 / 8 / generic <= 8 (12-byte bit records) and k = 32 (the keys themselves are
+    partitioned and hashed per tile), and 58 tiles over 92 partition workgroups."""
     keys = oracle.gen_keys16(seed, 0, n)
     ref = oracle_per_segment(oracle, 0, keys, [n], bpk)
     plan, out = gpu_build(amq, torch, 0, torch.from_numpy(keys).cuda(), [n], bpk)
@@ -392,7 +393,8 @@ def test_bloom_monolithic_partitioned(oracle, amq, torch, n, bpk, seed):
 
 
 def test_bloom_monolithic_duplicate_keys(oracle, amq, torch):
-    """Every key identical (one tile receives the whole batch) and a few distinct ones."""
+    """Every key identical (one tile receives the whole batch: its regions overflow and the
+    overflow lists are applied with device atomics) and a few distinct ones."""
     n = 200000
     keys = np.repeat(oracle.gen_keys16(13, 0, 1), n, axis=0)
     keys[::50000] = oracle.gen_keys16(14, 0, len(keys[::50000]))
@@ -401,17 +403,19 @@ def test_bloom_monolithic_duplicate_keys(oracle, amq, torch):
     assert_same(plan, out, ref)
 
 
-def test_bloom_monolithic_unstaged_matches_atomic_path(amq, torch):
-    """A filter of more tiles than the LDS staging holds (2060 > 2048) takes the unstaged
-    scatter; its bytes must equal the device-atomic path's for the same keys (planned as a
-    two-leaf batch, which routes the big leaf through bloom_global_set)."""
-    n = 108_000_000
+@pytest.mark.parametrize("n,bpk", [(108_000_000, 10), (30_000_000, 64)])
+def test_bloom_monolithic_large_matches_atomic_path(amq, torch, n, bpk):
+    """Full-size monolithic filters against the device-atomic path for the same keys (planned
+    as a two-leaf batch, which routes the big leaf through bloom_global_set): 108M keys at 10
+    bits/key (2,060 tiles, the record path) and 30M keys at 64 bits/key (3,663 tiles, beyond
+    the record path's 3,584: the count / scatter / hash-in-tile path)."""
     keys = amq.KeyBatch.fixed(amq.gen_keys16(16, 0, n + 1))
-    mono = amq.plan_filters(0, [n], 10)
-    assert -(-mono.max_seg_blocks // 1024) > 2048
+    mono = amq.plan_filters(0, [n], bpk)
+    tiles = -(-mono.max_seg_blocks // 1024)
+    assert (tiles > 3584) == (bpk == 64)
     kb = amq.KeyBatch.fixed(keys.data[:n])
     a = amq.build_all_filters(mono, kb)
-    two = amq.plan_filters(0, [n, 1], 10)
+    two = amq.plan_filters(0, [n, 1], bpk)
     assert two.workspace_bytes == 0
     b = amq.build_all_filters(two, keys)
     pa = int(mono.segs[0]["payload_bytes"])

@@ -6,9 +6,11 @@
 //                        lane rounds shared), bits set in an LDS image of the whole filter with
 //                        ds_or_b32, image written out with 16-byte coalesced stores.  Other key
 //                        shapes: 24-byte lanes, or XxhShort for any key under 32 bytes.
-//   bloom_part_* / bloom_tile_build
-//                        one filter larger than LDS: keys partitioned by 64 KiB tile (count,
-//                        scans, LDS-staged scatter), then each tile built in LDS.
+//   bloom_rec_*          one filter larger than LDS (the monolithic variant): each key hashed
+//                        once into a 12-byte bit record, records counting-sorted by 64 KiB
+//                        tile in LDS and appended to per-(tile, workgroup) regions, then each
+//                        tile built in LDS from its records (bloom_part_* / bloom_tile_build:
+//                        the count / scatter / hash-in-tile fallback for larger filters).
 //   vqf_decide           one wave per segment replays the reference's insert order exactly
 //                        (power-of-two-choice decisions depend only on per-block counts, kept
 //                        in LDS); per 64-key chunk every conflict-free lane decides in the same
@@ -480,29 +482,13 @@ __global__ __launch_bounds__(256) void bloom_global_set(const uint8_t* __restric
 // ---------------------------------------------------------------------------------------
 constexpr uint32_t kBloomTileBlocks = 1024;     // 64 KiB LDS image per tile
 constexpr uint32_t kBloomPartMaxTiles = 32768;  // LDS histogram / cursors <= 128 KiB
-constexpr uint32_t kBloomPartMaxWgs = 1024;     // unstaged scatter (256 / 512 / 128 slower)
+constexpr uint32_t kBloomPartMaxWgs = 1024;     // scatter workgroups (256 / 512 / 128 slower)
+constexpr uint32_t kRouteMaxParts = 2048;       // tkv_amq_bloom_route
 constexpr uint32_t kBloomTileThreads = 1024;    // 2 workgroups per CU (512: 6% slower)
-// Staged scatter (filters of <= kStageMaxTiles tiles): one 1024-thread workgroup per CU
-// stages kStageKeys keys per tile in LDS and writes each full bucket as one aligned 64-byte
-// piece.  Every (workgroup, tile) run is padded to a multiple of kStageKeys with copies of
-// one of its keys, which set the same bits again.
-constexpr uint32_t kStageKeys = 4;
-constexpr uint32_t kStageThreads = 1024;
-constexpr uint32_t kStageMaxWgs = 256;
-constexpr uint32_t kStageMaxTiles = 2048;  // 2048 x (64 + 8) B = 144 KiB of LDS
-constexpr uint32_t kStageRound = 2;        // keys staged per thread per round
-
-__host__ __device__ constexpr inline uint32_t bloom_stage_lds_bytes(uint32_t n_tiles)
-{
-  return n_tiles * (16 * kStageKeys + 8);
-}
-
 struct BloomPartGeom {
   uint32_t P;         // partition workgroups
   uint32_t n_tiles;
   uint32_t per;       // keys per partition workgroup
-  uint32_t threads;   // threads per partition workgroup
-  bool staged;
   uint64_t h_words;   // P * n_tiles
   uint64_t part_off;  // byte offset of the partitioned keys in the workspace
   uint64_t bytes;     // workspace bytes
@@ -512,17 +498,13 @@ __host__ __device__ inline BloomPartGeom bloom_part_geom(uint64_t n_keys, uint64
 {
   BloomPartGeom g;
   g.n_tiles = (uint32_t)((nb + kBloomTileBlocks - 1) / kBloomTileBlocks);
-  g.staged = g.n_tiles <= kStageMaxTiles;
-  const uint64_t chunk = g.staged ? 16384 : 4096, cap = g.staged ? kStageMaxWgs : kBloomPartMaxWgs;
-  const uint64_t p = (n_keys + chunk - 1) / chunk;
-  g.P = (uint32_t)(p < 1 ? 1 : (p > cap ? cap : p));
-  g.threads = g.staged ? kStageThreads : 256;
+  const uint64_t p = (n_keys + 4095) / 4096;
+  g.P = (uint32_t)(p < 1 ? 1 : (p > kBloomPartMaxWgs ? kBloomPartMaxWgs : p));
   g.per = (uint32_t)((n_keys + g.P - 1) / g.P);
   g.h_words = (uint64_t)g.P * g.n_tiles;
   // [H: P x n_tiles u32][tile totals: n_tiles u32][bucket bases: n_tiles + 1 u32][keys]
   g.part_off = (4 * (g.h_words + 2ull * g.n_tiles + 1) + 255) & ~255ull;
-  const uint64_t pad = g.staged ? (uint64_t)(kStageKeys - 1) * g.h_words : 0;
-  g.bytes = g.part_off + 16 * (n_keys + pad);
+  g.bytes = g.part_off + 16 * n_keys;
   return g;
 }
 
@@ -607,101 +589,6 @@ __global__ __launch_bounds__(NT) void bloom_part_keys(const uint4* __restrict__ 
   }
 }
 
-// The staged scatter pass.  Keys arrive one per thread per round (prefetched kU rounds
-// ahead); each takes a slot of its tile's LDS bucket, and the thread that takes the last slot
-// writes the full bucket to the tile's next aligned 64-byte piece of this workgroup's run.
-// Keys that find their bucket full retry after the flush (a uniform loop: every thread
-// reaches every barrier).  The runs start at the padded offsets of bloom_part_scan_cols.
-__global__ __launch_bounds__(kStageThreads) void bloom_part_scatter_staged(
-    const uint4* __restrict__ keys, const tkv_amq_segment* __restrict__ segs,
-    uint32_t* __restrict__ ws, uint32_t n_tiles, uint32_t per, uint64_t part_off, uint32_t n_cap,
-    PartWindow pw)
-{
-  extern __shared__ __attribute__((aligned(16))) uint8_t s_stage[];
-  uint4* stage = reinterpret_cast<uint4*>(s_stage);                       // [tile][kStageKeys]
-  uint32_t* fill = reinterpret_cast<uint32_t*>(s_stage + 16 * kStageKeys * n_tiles);
-  uint32_t* cur = fill + n_tiles;  // next 64-byte piece of the tile's run (key index)
-  const tkv_amq_segment sg = segs[0];
-  const uint32_t tid = threadIdx.x, w = blockIdx.x;
-  const uint32_t* H = ws + (uint64_t)w * n_tiles;
-  const uint32_t* base = ws + (uint64_t)gridDim.x * n_tiles + n_tiles;
-  for (uint32_t t = tid; t < n_tiles; t += kStageThreads) {
-    fill[t] = 0;
-    cur[t] = base[t] + H[t];
-  }
-  __syncthreads();
-  const uint32_t n = pw.local ? n_cap : min(sg.n_keys, n_cap), nb = sg.n_blocks;
-  const uint32_t b = min(n, w * per), e = min(n, b + per);
-  const uint4* kp = keys + (pw.local ? 0 : sg.key_begin);
-  uint4* part = reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(ws) + part_off);
-  // each round, every thread stages kR keys (prefetched one round ahead)
-  constexpr uint32_t kR = kStageRound;
-  constexpr uint32_t kRound = kR * kStageThreads;
-  uint4 ring[kR];
-#pragma unroll
-  for (uint32_t u = 0; u < kR; ++u) {
-    const uint32_t i = b + u * kStageThreads + tid;
-    ring[u] = i < e ? load_nt16(kp + i) : make_uint4(0, 0, 0, 0);
-  }
-  for (uint32_t c0 = b; c0 < e; c0 += kRound) {
-    uint4 kv[kR];
-    uint32_t t[kR];
-    bool pend[kR];
-#pragma unroll
-    for (uint32_t u = 0; u < kR; ++u) {
-      const uint32_t i = c0 + u * kStageThreads + tid;
-      kv[u] = ring[u];
-      if (i + kRound < e) ring[u] = load_nt16(kp + i + kRound);
-      t[u] = i < e ? part_tile(kv[u], nb, pw, n_tiles) : ~0u;
-      pend[u] = t[u] != ~0u;
-      if (!pend[u]) t[u] = 0;
-    }
-    for (;;) {
-      uint32_t slot[kR];
-#pragma unroll
-      for (uint32_t u = 0; u < kR; ++u) {
-        slot[u] = ~0u;
-        if (pend[u]) {
-          slot[u] = atomicAdd(fill + t[u], 1u);
-          if (slot[u] < kStageKeys) {
-            stage[t[u] * kStageKeys + slot[u]] = kv[u];
-            pend[u] = false;
-          }
-        }
-      }
-      __syncthreads();
-#pragma unroll
-      for (uint32_t u = 0; u < kR; ++u) {
-        if (slot[u] == kStageKeys - 1) {
-          // this key filled the bucket: write it out, reopen it (keys that found it full
-          // incremented fill past kStageKeys before the barrier and retry below)
-          const uint32_t pos = cur[t[u]];
-          cur[t[u]] = pos + kStageKeys;
-#pragma unroll
-          for (uint32_t q = 0; q < kStageKeys; ++q)
-            part[pos + q] = stage[t[u] * kStageKeys + q];
-          fill[t[u]] = 0;
-        }
-      }
-      bool any = false;
-#pragma unroll
-      for (uint32_t u = 0; u < kR; ++u) any |= pend[u];
-      if (!__syncthreads_or(any)) break;
-    }
-  }
-  __syncthreads();
-  // partly filled buckets: pad with the bucket's first key
-  for (uint32_t t = tid; t < n_tiles; t += kStageThreads) {
-    const uint32_t c = fill[t];
-    if (c != 0) {
-      const uint32_t pos = cur[t];
-      const uint4 k0 = stage[t * kStageKeys];
-#pragma unroll
-      for (uint32_t q = 0; q < kStageKeys; ++q) part[pos + q] = q < c ? stage[t * kStageKeys + q] : k0;
-    }
-  }
-}
-
 // exclusive scan of 256 per-thread values in a 256-thread block; returns this thread's prefix
 // and sets *total
 __device__ inline uint32_t block_exclusive_scan256(uint32_t v, uint32_t* s, uint32_t* total)
@@ -722,9 +609,8 @@ __device__ inline uint32_t block_exclusive_scan256(uint32_t v, uint32_t* s, uint
 }
 
 // One workgroup per tile: H[w][t] <- sum of H[w'][t] over w' < w; totals[t] <- column sum.
-// pad4: the staged scatter's runs, rounded up to whole staging buckets
 __global__ __launch_bounds__(256) void bloom_part_scan_cols(uint32_t* __restrict__ ws, uint32_t P,
-                                                            uint32_t n_tiles, uint32_t pad4)
+                                                            uint32_t n_tiles)
 {
   __shared__ uint32_t s[256];
   const uint32_t t = blockIdx.x, tid = threadIdx.x;
@@ -735,7 +621,6 @@ __global__ __launch_bounds__(256) void bloom_part_scan_cols(uint32_t* __restrict
   for (uint32_t r = 0; r < R; ++r) {
     const uint32_t w = tid * R + r;
     v[r] = w < P ? ws[(uint64_t)w * n_tiles + t] : 0u;
-    if (pad4) v[r] = (v[r] + kStageKeys - 1) & ~(kStageKeys - 1);
     sum += v[r];
   }
   uint32_t total;
@@ -798,6 +683,460 @@ __global__ __launch_bounds__(NT) void bloom_tile_build(
   uint4* dst = reinterpret_cast<uint4*>(payload + kBloomHeader + 64ull * first);
   const uint4* src = reinterpret_cast<const uint4*>(s_bits);
   for (uint32_t q = tid; q < tb * 4; q += NT) dst[q] = src[q];
+}
+
+// ---------------------------------------------------------------------------------------
+// Monolithic Bloom, hash-once record path (filters of <= kRecMaxTiles tiles).  The k hashes
+// of a key are computed once, where the key is read, and what a tile needs of them travels
+// instead of the key:
+//   bloom_rec_partition  one 1024-thread workgroup per CU over a contiguous key range, in
+//                        batches: every key is hashed into a 12-byte bit record (block in
+//                        tile, k <= 8 bit indices, tile id); the batch is counting-sorted by
+//                        tile in LDS and each tile's run is appended to this workgroup's
+//                        region of that tile.  No count pass, no global atomics: regions
+//                        have a fixed capacity (mean + 6 sigma of a uniform hash), and
+//                        records beyond it go to the workgroup's overflow list.
+//   bloom_rec_tile       one workgroup per tile: every workgroup's region of the tile
+//                        through ds_or into the 64 KiB LDS image, then 16-byte stores.
+//   bloom_rec_overflow   the overflow lists (empty unless the keys are not spread by the
+//                        hash, e.g. duplicates) with device-scope atomicOr into the filter.
+// With k > 8 the records are the 16-byte keys themselves (batches of 4096) and the tile
+// kernel hashes them.  The bits set do not depend on which kernel or workgroup sets them,
+// so the filter is byte-identical to the leaf kernel's and the oracle's.
+// Record (k <= 8): w0 = blk | b0 << 10 | b1 << 19 | tile[0:3] << 28,
+//                  w1 = b2 | b3 << 9 | b4 << 18 | tile[4:8] << 27,
+//                  w2 = b5 | b6 << 9 | b7 << 18 | tile[9:13] << 27   (b_j = b_0 for j >= k)
+// ---------------------------------------------------------------------------------------
+constexpr uint32_t kRecThreads = 1024;
+constexpr uint32_t kRecBatchBits = 8192;  // keys per batch, 12-byte records (3 LDS planes)
+constexpr uint32_t kRecBatchKeys = 4096;  // keys per batch, 16-byte keys (4 planes + tile ids)
+constexpr uint32_t kRecMaxTiles = 3584;
+constexpr uint32_t kRecMaxWgs = 256;
+constexpr uint32_t kRecPlaneBytes = 12 * kRecBatchBits;  // = 20 * kRecBatchKeys + 16 KiB
+constexpr uint32_t kRecTileThreads = 1024;
+static_assert(20 * kRecBatchKeys <= kRecPlaneBytes, "LDS planes");
+
+__host__ __device__ constexpr inline uint32_t bloom_rec_lds_bytes(uint32_t n_tiles)
+{
+  return kRecPlaneBytes + 16 * n_tiles + 4 * (kRecThreads / 64 + 1);
+}
+static_assert(kRecPlaneBytes + 16 * kRecMaxTiles + 4 * 17 <= 160 * 1024, "one workgroup per CU");
+
+struct BloomRecGeom {
+  uint32_t P;        // partition workgroups
+  uint32_t n_tiles;
+  uint32_t per;      // keys per partition workgroup
+  uint32_t cap;      // records per (tile, workgroup) region
+  uint64_t counts_off;   // u32 [n_tiles][P]: records in each region
+  uint64_t ovf_n_off;    // u32 [P]: records in each workgroup's overflow list
+  uint64_t regions_off;  // region (t, w) at regions_off + (t * P + w) * cap * 16
+  uint64_t ovf_off;      // workgroup w's overflow list at ovf_off + w * per * 16
+  uint64_t bytes;
+};
+
+// regions sized for 16-byte records (the device picks 12 or 16 by k; the host does not know k)
+inline BloomRecGeom bloom_rec_geom(uint64_t n_keys, uint64_t nb)
+{
+  BloomRecGeom g;
+  g.n_tiles = (uint32_t)((nb + kBloomTileBlocks - 1) / kBloomTileBlocks);
+  const uint64_t p = (n_keys + 32767) / 32768;
+  g.P = (uint32_t)(p < 1 ? 1 : (p > kRecMaxWgs ? kRecMaxWgs : p));
+  g.per = (uint32_t)((n_keys + g.P - 1) / g.P);
+  const double e = (double)g.per / g.n_tiles;
+  g.cap = ((uint32_t)(e + 6.0 * sqrt(e) + 16.0) + 7) & ~7u;
+  const uint64_t regions = (uint64_t)g.n_tiles * g.P;
+  g.counts_off = 256;
+  g.ovf_n_off = g.counts_off + 4 * regions;
+  g.regions_off = (g.ovf_n_off + 4ull * g.P + 255) & ~255ull;
+  g.ovf_off = g.regions_off + 16ull * regions * g.cap;
+  g.bytes = g.ovf_off + 16ull * g.P * g.per;
+  return g;
+}
+
+// Workgroup barrier for LDS hazards only: this wave's LDS operations are complete, its global
+// loads and stores stay in flight (__syncthreads() also drains vmcnt, stores included).
+__device__ inline void lds_barrier()
+{
+  // (the memory clobber keeps the compiler from moving LDS accesses across it)
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// Per-batch tile bookkeeping of bloom_rec_partition (n <= 4 * kRecThreads tiles; thread i owns
+// tiles 4i..4i+3): cursor[t] += prev[t] (the previous batch's run lengths), prev[t] = 0 (the
+// next batch's histogram), start[t] = exclusive scan of cur[t].  Returns the batch's record
+// count.  Two LDS barriers inside.
+__device__ inline uint32_t rec_scan(const uint32_t* cur, uint32_t* prev, uint32_t* start,
+                                    uint32_t* cursor, uint32_t n, uint32_t* wsum)
+{
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  uint32_t x[4], s = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < 4; ++j) {
+    const uint32_t i = 4 * tid + j;
+    x[j] = 0;
+    if (i < n) {
+      x[j] = cur[i];
+      cursor[i] += prev[i];
+      prev[i] = 0;
+    }
+    s += x[j];
+  }
+  uint32_t inc = s;  // inclusive scan over the wave
+#pragma unroll
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(inc, d, 64);
+    if (lane >= d) inc += y;
+  }
+  if (lane == 63) wsum[wave] = inc;
+  lds_barrier();
+  uint32_t before = 0, total = 0;
+#pragma unroll
+  for (uint32_t q = 0; q < kRecThreads / 64; ++q) {
+    const uint32_t t = wsum[q];
+    before += q < wave ? t : 0u;
+    total += t;
+  }
+  uint32_t run = before + inc - s;
+#pragma unroll
+  for (uint32_t j = 0; j < 4; ++j) {
+    const uint32_t i = 4 * tid + j;
+    if (i < n) start[i] = run;
+    run += x[j];
+  }
+  lds_barrier();  // start / cursor complete; wsum is reused by the next call
+  return total;
+}
+
+__device__ inline void rec_pack(uint32_t blk, uint32_t tile, const uint32_t (&b)[8], uint32_t& w0,
+                                uint32_t& w1, uint32_t& w2)
+{
+  w0 = blk | b[0] << 10 | b[1] << 19 | (tile & 15u) << 28;
+  w1 = b[2] | b[3] << 9 | b[4] << 18 | ((tile >> 4) & 31u) << 27;
+  w2 = b[5] | b[6] << 9 | b[7] << 18 | ((tile >> 9) & 31u) << 27;
+}
+
+__device__ inline uint32_t rec_tile(uint32_t w0, uint32_t w1, uint32_t w2)
+{
+  return (w0 >> 28) | ((w1 >> 27) << 4) | ((w2 >> 27) << 9);
+}
+
+// one key of the record path: local tile (~0 outside the window), block in tile, bit record
+template <int K>
+__device__ inline uint32_t rec_hash(const uint4& kv, uint32_t nb, uint32_t k, uint32_t tile0,
+                                    uint32_t n_tiles, uint32_t& w0, uint32_t& w1, uint32_t& w2)
+{
+  const Xxh16 x((uint64_t)kv.x | ((uint64_t)kv.y << 32), (uint64_t)kv.z | ((uint64_t)kv.w << 32));
+  const uint64_t h0 = x.finish(c_bloom.rhinit16[0]);
+  const uint32_t blk = (uint32_t)__umul64hi(h0, (uint64_t)nb);
+  const uint32_t t = blk / kBloomTileBlocks - tile0;  // wraps below the window
+  uint32_t b[8];
+  b[0] = (uint32_t)h0 & 511u;
+#pragma unroll
+  for (uint32_t j = 1; j < 8; ++j) {
+    if (K != 0 ? j < (uint32_t)K : j < k) b[j] = x.finish_lo9(c_bloom.rhinit16[j]) & 511u;
+    else b[j] = b[0];
+  }
+  rec_pack(blk & (kBloomTileBlocks - 1), t, b, w0, w1, w2);
+  return t < n_tiles ? t : ~0u;
+}
+
+// 16-byte keys (k > 8): the record is the key; only its tile is computed here
+__device__ inline uint32_t rec_key_tile(const uint4& kv, uint32_t nb, uint32_t tile0, uint32_t n_tiles)
+{
+  const uint32_t t = bloom_tile_of(kv, nb) - tile0;
+  return t < n_tiles ? t : ~0u;
+}
+
+struct RecArgs {
+  const uint4* keys;  // the window's keys [0, n) (from_seg: the segment's keys, n capped by it)
+  uint32_t n;
+  uint32_t tile0;     // global tile of local tile 0
+  uint32_t from_seg;
+  uint8_t* ws;
+  BloomRecGeom g;
+};
+
+// batches of B keys, U = B / kRecThreads per thread; RAW: 16-byte keys instead of bit records.
+// Per batch: hash (the next batch's keys are then loaded, in flight until its hash), LDS
+// barrier, scan (two), place into the planes, LDS barrier, write out.  The histogram is
+// double-buffered, so no barrier is needed after the write-out: the next batch's hash touches
+// only the other histogram, and its scan comes after a barrier.
+template <int K, bool RAW>
+__device__ void bloom_rec_partition_body(const tkv_amq_segment& sg, const RecArgs& a, uint32_t* lds)
+{
+  constexpr uint32_t B = RAW ? kRecBatchKeys : kRecBatchBits;
+  constexpr uint32_t U = B / kRecThreads;
+  constexpr uint32_t RB = RAW ? 16 : 12;  // record bytes
+  const uint32_t tid = threadIdx.x, w = blockIdx.x, P = a.g.P, T = a.g.n_tiles, cap = a.g.cap;
+  const uint32_t nb = sg.n_blocks, k = sg.hash_count;
+  uint32_t* pl[5];
+#pragma unroll
+  for (uint32_t j = 0; j < 5; ++j) pl[j] = lds + j * B;  // planes (RAW: 4 key words + tile)
+  uint32_t* hist2 = lds + kRecPlaneBytes / 4;  // two histograms
+  uint32_t* start = hist2 + 2 * T;
+  uint32_t* cursor = start + T;
+  uint32_t* wsum = cursor + T;  // 16 wave sums + the overflow count
+  uint32_t* ovf_n = wsum + kRecThreads / 64;
+  for (uint32_t t = tid; t < T; t += kRecThreads) {
+    hist2[t] = 0;
+    hist2[T + t] = 0;
+    cursor[t] = 0;
+  }
+  if (tid == 0) *ovf_n = 0;
+  __syncthreads();
+  const uint32_t n = a.from_seg ? min(a.n, sg.n_keys) : a.n;
+  const uint4* keys = a.keys + (a.from_seg ? sg.key_begin : 0);
+  const uint32_t kb = min(n, w * a.g.per), ke = min(n, kb + a.g.per);
+  uint8_t* regions = a.ws + a.g.regions_off;
+  uint8_t* ovf = a.ws + a.g.ovf_off + (uint64_t)w * a.g.per * 16;
+  // Loads are clamped, not skipped, and every lane stores once per record slot (lanes with
+  // nothing to write hit a sink in the workspace header): a fixed count of memory operations
+  // per batch, so the compiler's wait for a key load never also waits for the stores.
+  uint8_t* const sink = a.ws;
+  const uint32_t last_key = ke > 0 ? ke - 1 : 0;
+  uint4 kv[U];
+#pragma unroll
+  for (uint32_t u = 0; u < U; ++u) kv[u] = load_nt16(keys + min(kb + u * kRecThreads + tid, last_key));
+  uint32_t parity = 0;
+  for (uint32_t b0 = kb; b0 < ke; b0 += B, parity ^= 1) {
+    uint32_t* hist = hist2 + parity * T;
+    uint32_t* prev = hist2 + (parity ^ 1) * T;
+    // per key: its record and its rank in the tile's run (~0: no record); the tile of a bit
+    // record is in the record (fewer live registers while the next batch loads)
+    uint32_t tl[RAW ? U : 1], rk[U], r0[U], r1[U], r2[U], r3[RAW ? U : 1];
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u) {
+      const uint32_t i = b0 + u * kRecThreads + tid;
+      uint32_t t;
+      if constexpr (RAW) {
+        t = tl[u] = i < ke ? rec_key_tile(kv[u], nb, a.tile0, T) : ~0u;
+        r0[u] = kv[u].x;
+        r1[u] = kv[u].y;
+        r2[u] = kv[u].z;
+        r3[u] = kv[u].w;
+      } else {
+        t = i < ke ? rec_hash<K>(kv[u], nb, k, a.tile0, T, r0[u], r1[u], r2[u]) : ~0u;
+      }
+      if (i >= ke) t = ~0u;  // a clamped load past the range
+      rk[u] = t != ~0u ? atomicAdd(hist + t, 1u) : ~0u;
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u)  // the next batch's keys
+      kv[u] = load_nt16(keys + min(b0 + B + u * kRecThreads + tid, last_key));
+    lds_barrier();
+    const uint32_t total = rec_scan(hist, prev, start, cursor, T, wsum);
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u) {
+      if (rk[u] == ~0u) continue;
+      uint32_t t;
+      if constexpr (RAW) t = tl[u];
+      else t = rec_tile(r0[u], r1[u], r2[u]);
+      const uint32_t pos = start[t] + rk[u];
+      pl[0][pos] = r0[u];
+      pl[1][pos] = r1[u];
+      pl[2][pos] = r2[u];
+      if constexpr (RAW) {
+        pl[3][pos] = r3[u];
+        pl[4][pos] = tl[u];
+      }
+    }
+    lds_barrier();
+    // each tile's run goes to the end of this workgroup's region of the tile
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u) {
+      const uint32_t j0 = u * kRecThreads + tid;
+      const bool v = j0 < total;
+      const uint32_t j = v ? j0 : 0u;
+      const uint32_t x0 = pl[0][j], x1 = pl[1][j], x2 = pl[2][j];
+      uint32_t x3 = 0, t;
+      if constexpr (RAW) {
+        x3 = pl[3][j];
+        t = pl[4][j];
+      } else {
+        t = rec_tile(x0, x1, x2);
+      }
+      t = v ? t : 0u;
+      const uint32_t c = cursor[t] + (j - start[t]);
+      uint8_t* dst = sink;
+      if (v) {
+        if (c < cap) dst = regions + ((uint64_t)t * P + w) * cap * 16 + (uint64_t)c * RB;
+        else dst = ovf + 16ull * atomicAdd(ovf_n, 1u);  // LDS atomic, this workgroup's list
+      }
+      uint32_t* d = reinterpret_cast<uint32_t*>(dst);
+      if constexpr (RAW) {
+        *reinterpret_cast<uint4*>(d) = make_uint4(x0, x1, x2, x3);
+      } else {
+        d[0] = x0;
+        d[1] = x1;
+        d[2] = x2;
+      }
+    }
+  }
+  __syncthreads();
+  // the last batch's run lengths (its histogram is the one the loop's last scan read)
+  const uint32_t* last = hist2 + (parity ^ 1) * T;
+  uint32_t* counts = reinterpret_cast<uint32_t*>(a.ws + a.g.counts_off);
+  for (uint32_t t = tid; t < T; t += kRecThreads)
+    counts[(uint64_t)t * P + w] = min(cursor[t] + last[t], cap);
+  if (tid == 0) reinterpret_cast<uint32_t*>(a.ws + a.g.ovf_n_off)[w] = *ovf_n;
+}
+
+__global__ __launch_bounds__(kRecThreads) void bloom_rec_partition(const tkv_amq_segment* __restrict__ segs,
+                                                                   RecArgs a)
+{
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_rec[];
+  const tkv_amq_segment sg = segs[0];
+  const uint32_t k = sg.hash_count;
+  if (k == 0) return;
+  if (k == 7) bloom_rec_partition_body<7, false>(sg, a, s_rec);
+  else if (k == 8) bloom_rec_partition_body<8, false>(sg, a, s_rec);
+  else if (k < 8) bloom_rec_partition_body<0, false>(sg, a, s_rec);
+  else bloom_rec_partition_body<0, true>(sg, a, s_rec);
+}
+
+template <int K>
+__device__ inline void rec_insert(uint32_t* img, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t k)
+{
+  uint32_t* blk = img + 16 * (w0 & (kBloomTileBlocks - 1));
+  const uint32_t b[8] = {w0 >> 10, w0 >> 19, w1, w1 >> 9, w1 >> 18, w2, w2 >> 9, w2 >> 18};
+#pragma unroll
+  for (uint32_t j = 0; j < 8; ++j)
+    if (K != 0 ? j < (uint32_t)K : j < k) lds_set_bit(blk, b[j]);
+}
+
+// one workgroup per local tile t: region (t, w) of every partition workgroup w.  Each wave
+// walks its regions (w = wave, wave + 16, ...) in pieces of 64 * V records, V per lane, and
+// loads the next piece before it inserts the current one (two register sets, unrolled by two:
+// no copy of an in-flight load), so every wave has one piece in flight at all times.
+template <int K, bool RAW>
+__device__ void bloom_rec_tile_body(const tkv_amq_segment& sg, const RecArgs& a, uint32_t* img,
+                                    uint32_t t)
+{
+  constexpr uint32_t RB = RAW ? 16 : 12, NW = kRecTileThreads / 64, V = 4, PIECE = 64 * V;
+  // wave-uniform in an SGPR: region counts are scalar loads (lgkmcnt), so waiting for one
+  // never waits for the record loads in flight
+  const uint32_t lane = threadIdx.x & 63u, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t P = a.g.P, cap = a.g.cap;
+  const uint32_t k = sg.hash_count, nb = sg.n_blocks, first = (a.tile0 + t) * kBloomTileBlocks;
+  const uint32_t* counts = reinterpret_cast<const uint32_t*>(a.ws + a.g.counts_off) + (uint64_t)t * P;
+  const uint8_t* regions = a.ws + a.g.regions_off + (uint64_t)t * P * cap * 16;
+  struct Piece {
+    uint32_t w, i0, c;  // region, first record, records in the region
+    uint32_t x[V][4];
+  };
+  auto count = [&](uint32_t w) { return w < P ? counts[w] : 0u; };
+  auto load = [&](Piece& q) {
+    const uint8_t* reg = q.w < P ? regions + (uint64_t)q.w * cap * 16 : a.ws;
+    const uint32_t lastr = q.c ? q.c - 1 : 0u;
+#pragma unroll
+    for (uint32_t v = 0; v < V; ++v) {
+      const uint32_t* p = reinterpret_cast<const uint32_t*>(reg + (uint64_t)min(q.i0 + v * 64 + lane, lastr) * RB);
+      if constexpr (RAW) {
+        const uint4 e = *reinterpret_cast<const uint4*>(p);
+        q.x[v][0] = e.x; q.x[v][1] = e.y; q.x[v][2] = e.z; q.x[v][3] = e.w;
+      } else {
+        q.x[v][0] = p[0]; q.x[v][1] = p[1]; q.x[v][2] = p[2]; q.x[v][3] = 0;
+      }
+    }
+  };
+  // the piece after `q`: the next PIECE records of its region, else the wave's next region
+  auto advance = [&](const Piece& q, Piece& n) {
+    if (q.i0 + PIECE < q.c) {
+      n.w = q.w;
+      n.i0 = q.i0 + PIECE;
+      n.c = q.c;
+    } else {
+      n.w = q.w + NW;
+      n.i0 = 0;
+      n.c = count(n.w);
+    }
+    load(n);
+  };
+  auto insert = [&](const Piece& q) {
+#pragma unroll
+    for (uint32_t v = 0; v < V; ++v) {
+      if (q.i0 + v * 64 + lane >= q.c) continue;
+      if constexpr (RAW) bloom_insert16<0>(img, nb, k, make_uint4(q.x[v][0], q.x[v][1], q.x[v][2], q.x[v][3]), first);
+      else rec_insert<K>(img, q.x[v][0], q.x[v][1], q.x[v][2], k);
+    }
+  };
+  Piece A, B;
+  A.w = wave;
+  A.i0 = 0;
+  A.c = count(A.w);
+  load(A);
+  while (A.w < P) {
+    advance(A, B);
+    insert(A);
+    if (B.w >= P) break;
+    advance(B, A);
+    insert(B);
+  }
+}
+
+__global__ __launch_bounds__(kRecTileThreads) void bloom_rec_tile(const tkv_amq_segment* __restrict__ segs,
+                                                                  RecArgs a, uint8_t* __restrict__ out,
+                                                                  uint32_t hdr_always)
+{
+  extern __shared__ uint32_t s_img[];
+  const tkv_amq_segment sg = segs[0];
+  const uint32_t t = blockIdx.x, tid = threadIdx.x, k = sg.hash_count;
+  if (k == 0) return;
+  const uint32_t first = (a.tile0 + t) * kBloomTileBlocks;
+  const uint32_t tb = min(kBloomTileBlocks, sg.n_blocks - first);
+  for (uint32_t w = tid; w < tb * 16; w += kRecTileThreads) s_img[w] = 0;
+  __syncthreads();
+  if (k == 7) bloom_rec_tile_body<7, false>(sg, a, s_img, t);
+  else if (k == 8) bloom_rec_tile_body<8, false>(sg, a, s_img, t);
+  else if (k < 8) bloom_rec_tile_body<0, false>(sg, a, s_img, t);
+  else bloom_rec_tile_body<0, true>(sg, a, s_img, t);
+  __syncthreads();
+  uint8_t* payload = out + sg.out_offset;
+  const bool hdr = t == 0 && (a.tile0 == 0 || hdr_always);
+  if (hdr && tid < 4) write_bloom_header(payload, sg, tid);
+  else if (hdr && tid < 8) write_page_header(out, sg, kLayoutBloom, tid - 4);
+  uint4* dst = reinterpret_cast<uint4*>(payload + kBloomHeader + 64ull * first);
+  const uint4* src = reinterpret_cast<const uint4*>(s_img);
+  for (uint32_t q = tid; q < tb * 4; q += kRecTileThreads) dst[q] = src[q];
+}
+
+// one workgroup per partition workgroup's overflow list; device-scope atomics into the filter
+// (runs after bloom_rec_tile has stored every tile)
+__global__ __launch_bounds__(256) void bloom_rec_overflow(const tkv_amq_segment* __restrict__ segs,
+                                                          RecArgs a, uint8_t* __restrict__ out)
+{
+  const tkv_amq_segment sg = segs[0];
+  const uint32_t k = sg.hash_count, w = blockIdx.x;
+  if (k == 0) return;
+  const uint32_t n = reinterpret_cast<const uint32_t*>(a.ws + a.g.ovf_n_off)[w];
+  const uint8_t* list = a.ws + a.g.ovf_off + (uint64_t)w * a.g.per * 16;
+  uint32_t* words = reinterpret_cast<uint32_t*>(out + sg.out_offset + kBloomHeader);
+  for (uint32_t i = threadIdx.x; i < n; i += 256) {
+    const uint4 q = *reinterpret_cast<const uint4*>(list + 16ull * i);
+    uint32_t* blk;
+    uint32_t b[8];
+    uint32_t kk = k;
+    if (k <= 8) {
+      const uint32_t tile = rec_tile(q.x, q.y, q.z);
+      blk = words + 16ull * ((uint64_t)(a.tile0 + tile) * kBloomTileBlocks + (q.x & (kBloomTileBlocks - 1)));
+      b[0] = q.x >> 10; b[1] = q.x >> 19; b[2] = q.y; b[3] = q.y >> 9;
+      b[4] = q.y >> 18; b[5] = q.z; b[6] = q.z >> 9; b[7] = q.z >> 18;
+    } else {
+      const Xxh16 x((uint64_t)q.x | ((uint64_t)q.y << 32), (uint64_t)q.z | ((uint64_t)q.w << 32));
+      const uint64_t h0 = x.finish(c_bloom.rhinit16[0]);
+      blk = words + 16 * (uint64_t)__umul64hi(h0, (uint64_t)sg.n_blocks);
+      atomicOr(blk + ((h0 & 511u) >> 5), 1u << (h0 & 31u));
+      for (uint32_t j = 1; j < k; ++j) {
+        const uint32_t bj = x.finish_lo9(c_bloom.rhinit16[j]) & 511u;
+        atomicOr(blk + (bj >> 5), 1u << (bj & 31u));
+      }
+      kk = 0;
+    }
+    for (uint32_t j = 0; j < kk; ++j) {
+      const uint32_t bj = b[j] & 511u;
+      atomicOr(blk + (bj >> 5), 1u << (bj & 31u));
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -2596,9 +2935,6 @@ inline void set_part_attributes()
                               hipFuncAttributeMaxDynamicSharedMemorySize, cap);
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&bloom_part_keys<1, 256>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, cap);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&bloom_part_scatter_staged),
-                              hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)bloom_stage_lds_bytes(kStageMaxTiles));
   });
 }
 
@@ -2609,25 +2945,41 @@ inline void launch_partitioned_build(const BloomPartGeom& pg, hipStream_t s, con
                                      const PartWindow& pw, uint8_t* d_out)
 {
   const size_t hl = 4ull * pg.n_tiles;
-  if (pg.staged)
-    hipLaunchKernelGGL((bloom_part_keys<0, kStageThreads>), dim3(pg.P), dim3(kStageThreads), hl, s,
-                       k4, d_segs, w, pg.n_tiles, pg.per, pg.part_off, nk, pw);
-  else
-    hipLaunchKernelGGL((bloom_part_keys<0, 256>), dim3(pg.P), dim3(256), hl, s, k4, d_segs, w,
-                       pg.n_tiles, pg.per, pg.part_off, nk, pw);
-  hipLaunchKernelGGL(bloom_part_scan_cols, dim3(pg.n_tiles), dim3(256), 0, s, w, pg.P, pg.n_tiles,
-                     (uint32_t)pg.staged);
+  hipLaunchKernelGGL((bloom_part_keys<0, 256>), dim3(pg.P), dim3(256), hl, s, k4, d_segs, w,
+                     pg.n_tiles, pg.per, pg.part_off, nk, pw);
+  hipLaunchKernelGGL(bloom_part_scan_cols, dim3(pg.n_tiles), dim3(256), 0, s, w, pg.P, pg.n_tiles);
   hipLaunchKernelGGL(bloom_part_scan_tiles, dim3(1), dim3(256), 0, s, w, pg.P, pg.n_tiles);
-  if (pg.staged)
-    hipLaunchKernelGGL(bloom_part_scatter_staged, dim3(pg.P), dim3(kStageThreads),
-                       bloom_stage_lds_bytes(pg.n_tiles), s, k4, d_segs, w, pg.n_tiles, pg.per,
-                       pg.part_off, nk, pw);
-  else
-    hipLaunchKernelGGL((bloom_part_keys<1, 256>), dim3(pg.P), dim3(256), hl, s, k4, d_segs, w,
-                       pg.n_tiles, pg.per, pg.part_off, nk, pw);
+  hipLaunchKernelGGL((bloom_part_keys<1, 256>), dim3(pg.P), dim3(256), hl, s, k4, d_segs, w,
+                     pg.n_tiles, pg.per, pg.part_off, nk, pw);
   hipLaunchKernelGGL(bloom_tile_build<kBloomTileThreads>, dim3(pg.n_tiles), dim3(kBloomTileThreads),
                      64ull * kBloomTileBlocks, s, d_segs, w, pg.P, pg.n_tiles, pg.part_off, d_out,
                      pw);
+}
+
+// the hash-once record path takes a monolithic filter of <= kRecMaxTiles tiles
+inline bool bloom_rec_eligible(uint64_t n_blocks, uint64_t n_keys)
+{
+  return div_up(n_blocks, kBloomTileBlocks) <= kRecMaxTiles && n_keys <= 0xffffffffull;
+}
+
+// partition -> tiles -> overflow over keys [0, n) (from_seg: the segment's own keys) into
+// tiles [tile0, tile0 + g.n_tiles)
+inline void launch_rec_build(const BloomRecGeom& g, hipStream_t s, const uint4* keys, uint32_t n,
+                             uint32_t tile0, uint32_t from_seg, uint32_t hdr_always,
+                             const tkv_amq_segment* d_segs, uint8_t* ws, uint8_t* d_out)
+{
+  static std::once_flag lds_attr[kMaxDevices];
+  once_per_device(lds_attr, [] {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&bloom_rec_partition),
+                              hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)bloom_rec_lds_bytes(kRecMaxTiles));
+  });
+  const RecArgs a{keys, n, tile0, from_seg, ws, g};
+  hipLaunchKernelGGL(bloom_rec_partition, dim3(g.P), dim3(kRecThreads), bloom_rec_lds_bytes(g.n_tiles),
+                     s, d_segs, a);
+  hipLaunchKernelGGL(bloom_rec_tile, dim3(g.n_tiles), dim3(kRecTileThreads), 64ull * kBloomTileBlocks,
+                     s, d_segs, a, d_out, hdr_always);
+  hipLaunchKernelGGL(bloom_rec_overflow, dim3(g.P), dim3(256), 0, s, d_segs, a, d_out);
 }
 
 // Hash-range sharding (BASELINE config 5): T = ceil(n_blocks / tile) tiles, q = ceil(T / parts)
@@ -2643,10 +2995,8 @@ inline BloomPartGeom bloom_route_geom(uint64_t n_keys, uint32_t n_parts)
 {
   BloomPartGeom g;
   g.n_tiles = n_parts;
-  g.staged = false;
   const uint64_t p = (n_keys + 4095) / 4096;
   g.P = (uint32_t)(p < 1 ? 1 : (p > kBloomPartMaxWgs ? kBloomPartMaxWgs : p));
-  g.threads = 256;
   g.per = (uint32_t)((n_keys + g.P - 1) / g.P);
   g.h_words = (uint64_t)g.P * n_parts;
   g.part_off = (4 * (g.h_words + 2ull * n_parts + 1) + 255) & ~255ull;
@@ -2852,7 +3202,9 @@ int tkv_amq_plan(int kind, const uint64_t* counts, const uint64_t* src_ids, uint
     if (kind == TKV_AMQ_VQF && bpk != 0)
       *ws_bytes = vqf_temp_offset(n_segs) + kVqfTempStride * block_base + 8 * key_begin + 64;
     if (kind == TKV_AMQ_BLOOM && bloom_partitioned(n_segs, max_blocks, key_begin))
-      *ws_bytes = bloom_part_geom(key_begin, max_blocks).bytes;  // 16-byte keys
+      *ws_bytes = bloom_rec_eligible(max_blocks, key_begin)  // 16-byte keys
+                      ? bloom_rec_geom(key_begin, max_blocks).bytes
+                      : bloom_part_geom(key_begin, max_blocks).bytes;
     else if (kind == TKV_AMQ_BLOOM)
       *ws_bytes = bloom_split_ws_bytes(n_segs, bloom_split_parts(n_segs, key_begin, max_blocks),
                                        max_blocks);
@@ -2940,8 +3292,13 @@ int tkv_amq_build(int kind, const uint8_t* keys, const uint64_t* offs, uint32_t 
       return hipGetLastError() == hipSuccess ? TKV_AMQ_OK : TKV_AMQ_INTERNAL;
     }
     const BloomPartGeom pg = bloom_part_geom(n_keys, max_blocks);
-    if (bloom_partitioned(n_segs, max_blocks, n_keys) && mode == kKey16 && d_ws &&
-        ws_bytes >= pg.bytes) {
+    const bool mono = bloom_partitioned(n_segs, max_blocks, n_keys) && mode == kKey16 && d_ws;
+    if (mono && bloom_rec_eligible(max_blocks, n_keys) &&
+        ws_bytes >= bloom_rec_geom(n_keys, max_blocks).bytes) {
+      // one monolithic filter: hash once into bit records partitioned by tile, build the tiles
+      launch_rec_build(bloom_rec_geom(n_keys, max_blocks), s, reinterpret_cast<const uint4*>(keys),
+                       (uint32_t)n_keys, 0u, 1u, 0u, d_segs, static_cast<uint8_t*>(d_ws), d_out);
+    } else if (mono && ws_bytes >= pg.bytes) {
       // one monolithic filter: partition the keys by tile, build every tile in LDS
       set_part_attributes();
       launch_partitioned_build(pg, s, reinterpret_cast<const uint4*>(keys), d_segs,
@@ -3031,7 +3388,7 @@ int tkv_amq_build(int kind, const uint8_t* keys, const uint64_t* offs, uint32_t 
 
 uint64_t tkv_amq_bloom_route_ws_bytes(uint64_t n_keys, uint32_t n_parts)
 {
-  if (n_parts == 0 || n_parts > kStageMaxTiles) return 0;
+  if (n_parts == 0 || n_parts > kRouteMaxParts) return 0;
   return bloom_route_geom(n_keys, n_parts).bytes;
 }
 
@@ -3040,7 +3397,7 @@ int tkv_amq_bloom_route(const uint8_t* d_keys16, uint64_t n_keys, const tkv_amq_
                         uint32_t* d_part_counts, void* d_ws, uint64_t ws_bytes, void* stream)
 {
   if (tkv_amq_device_count() == 0) return TKV_AMQ_UNAVAILABLE;
-  if (n_parts == 0 || n_parts > kStageMaxTiles || n_blocks == 0 || !d_seg || !d_part_counts ||
+  if (n_parts == 0 || n_parts > kRouteMaxParts || n_blocks == 0 || !d_seg || !d_part_counts ||
       n_keys > 0xffffffffull)
     return TKV_AMQ_INVALID_ARGUMENT;
   if (n_keys && (!d_keys16 || !d_routed16 || (reinterpret_cast<uintptr_t>(d_keys16) & 15) ||
@@ -3058,7 +3415,7 @@ int tkv_amq_bloom_route(const uint8_t* d_keys16, uint64_t n_keys, const tkv_amq_
   const uint32_t nk = (uint32_t)n_keys;
   hipLaunchKernelGGL((bloom_part_keys<0, 256>), dim3(g.P), dim3(256), hl, s, k4, d_seg, w, n_parts,
                      g.per, g.part_off, nk, pw);
-  hipLaunchKernelGGL(bloom_part_scan_cols, dim3(n_parts), dim3(256), 0, s, w, g.P, n_parts, 0u);
+  hipLaunchKernelGGL(bloom_part_scan_cols, dim3(n_parts), dim3(256), 0, s, w, g.P, n_parts);
   hipLaunchKernelGGL(bloom_part_scan_tiles, dim3(1), dim3(256), 0, s, w, g.P, n_parts);
   hipLaunchKernelGGL((bloom_part_keys<1, 256>), dim3(g.P), dim3(256), hl, s, k4, d_seg, w, n_parts,
                      g.per, g.part_off, nk, pw);
@@ -3072,7 +3429,8 @@ int tkv_amq_bloom_route(const uint8_t* d_keys16, uint64_t n_keys, const tkv_amq_
 uint64_t tkv_amq_bloom_build_range_ws_bytes(uint64_t n_keys, uint32_t tile_begin, uint32_t tile_end)
 {
   if (tile_end <= tile_begin || tile_end - tile_begin > kBloomPartMaxTiles) return 0;
-  return bloom_part_geom(n_keys, (uint64_t)(tile_end - tile_begin) * kBloomTileBlocks).bytes;
+  const uint64_t nb = (uint64_t)(tile_end - tile_begin) * kBloomTileBlocks;
+  return bloom_rec_eligible(nb, n_keys) ? bloom_rec_geom(n_keys, nb).bytes : bloom_part_geom(n_keys, nb).bytes;
 }
 
 int tkv_amq_bloom_build_range(const uint8_t* d_keys16, uint64_t n_keys, const tkv_amq_segment* d_seg,
@@ -3087,7 +3445,16 @@ int tkv_amq_bloom_build_range(const uint8_t* d_keys16, uint64_t n_keys, const tk
   if (n_keys && (!d_keys16 || (reinterpret_cast<uintptr_t>(d_keys16) & 15)))
     return TKV_AMQ_INVALID_ARGUMENT;
   if (tile_begin == tile_end) return TKV_AMQ_OK;
-  const BloomPartGeom pg = bloom_part_geom(n_keys, (uint64_t)(tile_end - tile_begin) * kBloomTileBlocks);
+  const uint64_t nb = (uint64_t)(tile_end - tile_begin) * kBloomTileBlocks;
+  if (d_ws && bloom_rec_eligible(nb, n_keys)) {
+    const BloomRecGeom g = bloom_rec_geom(n_keys, nb);
+    if (ws_bytes >= g.bytes) {
+      launch_rec_build(g, as_stream(stream), reinterpret_cast<const uint4*>(d_keys16), (uint32_t)n_keys,
+                       tile_begin, 0u, 1u, d_seg, static_cast<uint8_t*>(d_ws), d_out);
+      return hipGetLastError() == hipSuccess ? TKV_AMQ_OK : TKV_AMQ_INTERNAL;
+    }
+  }
+  const BloomPartGeom pg = bloom_part_geom(n_keys, nb);
   if (!d_ws || ws_bytes < pg.bytes) return TKV_AMQ_INVALID_ARGUMENT;
   set_part_attributes();
   const PartWindow pw{tile_begin, 1u, 1u, 1u, nullptr};
