@@ -150,8 +150,9 @@ __device__ inline uint32_t davalanche_lo9(uint64_t h)
   h ^= dshr<29>(h);
   const uint32_t yl = lo32(h), yh = hi32(h);
   constexpr uint32_t cl = (uint32_t)kP3, ch = (uint32_t)(kP3 >> 32);
-  const uint32_t h3_hi = mad_u24(cl, yh, mad_u24(ch, yl, __umulhi(yl, cl)));
-  return mul_u24(cl, yl) ^ h3_hi;
+  const uint64_t p = (uint64_t)yl * cl;  // both words in one v_mad_u64_u32
+  const uint32_t h3_hi = mad_u24(cl, yh, mad_u24(ch, yl, hi32(p)));
+  return lo32(p) ^ h3_hi;
 }
 
 // 16-byte key, seed-independent part precomputed once per key.  Rotation distributes over
