@@ -8,10 +8,11 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("kind,bpk,cap", [(0, 10, 0), (1, 12, 32704)])
-def test_build_and_probe_replay_in_graph(oracle, amq, kind, bpk, cap):
+@pytest.mark.parametrize("kind,bpk,cap,counts", [(0, 10, 0, [16384] * 3 + [999, 0, 5]),
+                                                (1, 12, 32704, [16384] * 3 + [999, 0, 5]),
+                                                (0, 10, 0, [300_000])])   # monolithic: record path
+def test_build_and_probe_replay_in_graph(oracle, amq, kind, bpk, cap, counts):
     import torch
-    counts = [16384] * 3 + [999, 0, 5]
     keys = oracle.gen_keys16(91, 0, sum(counts))
     if kind == 1:
         oracle.sort_segments(keys, np.concatenate([[0], np.cumsum(counts)]).astype(np.uint64))
