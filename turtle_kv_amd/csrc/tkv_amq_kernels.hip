@@ -2341,26 +2341,11 @@ __device__ void vqf_place_fused_sort(const tkv_amq_segment& sg, uint32_t seg_ind
         run += incl >> 24;
       }
     }
-    // pass 2a: each entry's slot in insertion order (ds_add_rtn on its bucket counter).  The
-    // atomics are issued back to back: no store whose address depends on a returned slot
-    // sits between them (that ordering made every atomic wait for the previous one).
-    uint32_t slots[NB][(C::kSlots + 3) / 4];  // 4 slot bytes per dword
-#pragma unroll
-    for (uint32_t i = 0; i < C::kSlots; ++i) {
-#pragma unroll
-      for (int j = 0; j < NB; ++j) {
-        const uint32_t e = reinterpret_cast<const E*>(ent[j])[i];
-        const bool on = live[j] && i < c[j];
-        const uint32_t o = on ? e >> T : 0u;
-        const uint32_t old = atomicAdd(reg[j] + (o >> 2), on ? 1u << (8 * (o & 3)) : 0u);
-        const uint32_t slot = (old >> (8 * (o & 3))) & 0xffu;
-        if (i % 4 == 0) slots[j][i / 4] = slot;
-        else slots[j][i / 4] |= slot << (8 * (i % 4));
-      }
-      // groups of kGroup: bounded live ranges (registers set the workgroups per CU)
-      if (i % kGroup == kGroup - 1) __builtin_amdgcn_sched_barrier(0);
-    }
-    // pass 2b: metadata zero at slot + offset; tag bytes into the image
+    // pass 2: each entry's slot in insertion order (ds_add_rtn on its bucket counter), then
+    // its metadata zero at slot + offset and its tag byte in the image.  Groups of kGroup
+    // slots: the group's atomics are issued back to back (a store whose address depends on
+    // a returned slot between them made every atomic wait for the previous one), then the
+    // group's slots are consumed while the next group's atomics queue behind its stores.
     uint64_t md_lo[NB], md_hi[NB];
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
@@ -2368,28 +2353,45 @@ __device__ void vqf_place_fused_sort(const tkv_amq_segment& sg, uint32_t seg_ind
       md_hi[j] = T == 8 ? ~0ull : 0ull;
     }
 #pragma unroll
-    for (uint32_t i = 0; i < C::kSlots; ++i) {
+    for (uint32_t g = 0; g < C::kSlots; g += kGroup) {
+      uint32_t old[NB][kGroup];
 #pragma unroll
-      for (int j = 0; j < NB; ++j) {
-        const uint32_t e = reinterpret_cast<const E*>(ent[j])[i];
-        const bool on = live[j] && i < c[j];
-        const uint32_t o = on ? e >> T : 0u, tag = e & ((1u << T) - 1);
-        const uint32_t slot = (slots[j][i / 4] >> (8 * (i % 4))) & 0xffu;
-        const uint32_t z = slot + o;
-        const uint64_t clr = on ? 1ull << (z & 63) : 0ull;
-        if (z < 64) md_lo[j] &= ~clr;
-        else md_hi[j] &= ~clr;
-        // dead slots store into the region's count word (no longer read)
-        uint8_t* r8 = reinterpret_cast<uint8_t*>(reg[j]);
-        const uint32_t byte = on ? 4 * kTagDword + slot * (T / 8) : 4 * kFusedCountWord;
-        if constexpr (T == 8) {
-          r8[byte] = (uint8_t)tag;
-        } else {
-          const uint16_t t16 = (uint16_t)tag;
-          __builtin_memcpy(r8 + byte, &t16, 2);
+      for (uint32_t u = 0; u < kGroup && g + u < C::kSlots; ++u) {
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+          const uint32_t i = g + u;
+          const uint32_t e = reinterpret_cast<const E*>(ent[j])[i];
+          const bool on = live[j] && i < c[j];
+          const uint32_t o = on ? e >> T : 0u;
+          old[j][u] = atomicAdd(reg[j] + (o >> 2), on ? 1u << (8 * (o & 3)) : 0u);
         }
       }
-      if (i % kGroup == kGroup - 1) __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (uint32_t u = 0; u < kGroup && g + u < C::kSlots; ++u) {
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+          const uint32_t i = g + u;
+          const uint32_t e = reinterpret_cast<const E*>(ent[j])[i];
+          const bool on = live[j] && i < c[j];
+          const uint32_t o = on ? e >> T : 0u, tag = e & ((1u << T) - 1);
+          const uint32_t slot = (old[j][u] >> (8 * (o & 3))) & 0xffu;
+          const uint32_t z = slot + o;
+          const uint64_t clr = on ? 1ull << (z & 63) : 0ull;
+          if (z < 64) md_lo[j] &= ~clr;
+          else md_hi[j] &= ~clr;
+          // dead slots store into the region's count word (no longer read)
+          uint8_t* r8 = reinterpret_cast<uint8_t*>(reg[j]);
+          const uint32_t byte = on ? 4 * kTagDword + slot * (T / 8) : 4 * kFusedCountWord;
+          if constexpr (T == 8) {
+            r8[byte] = (uint8_t)tag;
+          } else {
+            const uint16_t t16 = (uint16_t)tag;
+            __builtin_memcpy(r8 + byte, &t16, 2);
+          }
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
     }
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
@@ -2431,7 +2433,7 @@ __device__ void vqf_place_fused_body(const tkv_amq_segment& sg, uint32_t seg_ind
   for (uint32_t b = tid; b < nb; b += kFusedThreads) lds[b * kFusedRegionWords + kFusedCountWord] = 0;
   __syncthreads();
   const uint32_t gb0 = (uint32_t)sg.block_base;
-  constexpr uint32_t kU = 8;  // 16-byte loads in flight per thread: 32 KB per workgroup
+  constexpr uint32_t kU = 16;  // 16-byte loads in flight per thread: 64 KB per workgroup
   auto put_entry = [&](uint32_t blk, uint32_t rank, uint32_t e) {
     uint32_t* r = lds + blk * kFusedRegionWords;
     if constexpr (T == 8) reinterpret_cast<uint16_t*>(r)[rank] = (uint16_t)e;
