@@ -2351,6 +2351,10 @@ __device__ void vqf_place_fused_sort(const tkv_amq_segment& sg, uint32_t seg_ind
     for (int j = 0; j < NB; ++j) {
       md_lo[j] = ~0ull;
       md_hi[j] = T == 8 ? ~0ull : 0ull;
+      // the per-slot offsets and masks of pass 1 are recomputed below, not kept live across
+      // the prefix scan (48 slots' worth of them set the register count)
+#pragma unroll
+      for (uint32_t w = 0; w < kEntWords; ++w) asm volatile("" : "+v"(ent[j][w]));
     }
 #pragma unroll
     for (uint32_t g = 0; g < C::kSlots; g += kGroup) {
