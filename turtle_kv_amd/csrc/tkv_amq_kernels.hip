@@ -2256,9 +2256,12 @@ __host__ __device__ inline uint32_t vqf_fused_lds_bytes(uint32_t max_nb)
   return vqf_fused_img_bytes(max_nb);
 }
 
-// Phase 2: one thread per block (NB > 1: NB blocks per thread interleaved; NB = 2 doubled the
-// registers to 450 and ran slower).  Measured: phase 2 is bound by its LDS operations
-// (3 per slot, random bucket words, so bank conflicts), not by their latency.
+// Phase 2: one thread per block (NB > 1: NB blocks per thread interleaved; NB = 2 takes 173
+// VGPRs, two workgroups per CU, and ran 9% slower: 0.760 vs 0.699 ms at 100M keys).  At 72
+// VGPRs the LDS image sets three workgroups per CU.  Measured and not kept: a word-major image
+// (dword w of block b at w * 480 + b, so the 32 threads of a bank group never conflict
+// whatever bucket word they pick): 0.752 vs 0.730 ms -- bank conflicts (~59% of the LDS
+// cycles, PMC) do not set this kernel's time.
 template <int T, int NB>
 __device__ void vqf_place_fused_sort(const tkv_amq_segment& sg, uint32_t seg_index,
                                      VqfWorkspace ws, uint8_t* __restrict__ out, uint32_t* lds)
@@ -2329,9 +2332,11 @@ __device__ void vqf_place_fused_sort(const tkv_amq_segment& sg, uint32_t seg_ind
         atomicAdd(reg[j] + (o >> 2), on ? 1u << (8 * (o & 3)) : 0u);
       }
     }
-    // exclusive prefix over buckets: inclusive-in-dword = v * 0x01010101
+    // exclusive prefix over buckets: inclusive-in-dword = v * 0x01010101 (a dead j aliases
+    // the thread's first block, whose counters must be scanned once)
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
+      if (!live[j]) continue;
       uint32_t run = 0;
 #pragma unroll
       for (uint32_t w = 0; w < kCntWords; ++w) {
