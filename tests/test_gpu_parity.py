@@ -278,8 +278,10 @@ def test_vqf_decide_paths(oracle, amq, torch, n_leaves, shape):
     """Batches of up to 768 leaves take vqf_decide_ring (producer waves locate and match
     each 64-key chunk, one decider wave replays the insertion order), larger ones vqf_decide
     (one wave per leaf).  8- and 16-bit tags (12 / 22 bits per key), leaves of <= 512 and
-    > 512 blocks (the producers' 9- and 11-bit matches; a 30000-key leaf), fused and unfused
-    place, ragged leaves, every key shape, sampled against the oracle."""
+    > 512 blocks (the producers' 9- and 11-bit matches, vqf_decide's LDS lane-mask table past
+    512 blocks; a 30000-key leaf of ~740 blocks, placed in LDS), 4- and 8-byte key records,
+    ragged leaves, every key shape, sampled against the oracle.  (The unfused place and the
+    ballot matches: test_vqf_leaf_beyond_ring_blocks.)"""
     rng = np.random.default_rng(1000 + n_leaves)
     counts = [int(c) for c in rng.integers(0, 3000, n_leaves)]
     counts[0], counts[1], counts[2], counts[-1] = 0, 16384, 30000, 1

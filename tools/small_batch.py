@@ -22,14 +22,19 @@ def main():
     ap.add_argument("--bpk", type=int, default=0)
     ap.add_argument("--leaves", default="1,8,64,256,512,1024")
     ap.add_argument("--reps", type=int, default=50)
+    ap.add_argument("--leaf-keys", type=int, default=16384)
+    ap.add_argument("--cap", type=int, default=0,
+                    help="VQF payload capacity (default: the TreeOptions filter page at --bpk)")
     ap.add_argument("--no-ws", action="store_true",
                     help="call the ABI without a workspace (Bloom: the unsplit paths)")
     a = ap.parse_args()
     bpk = a.bpk or (10 if a.kind == 0 else 12)
-    cap = amq.TreeOptions(a.kind).set_filter_bits_per_key(bpk).filter_page_payload_size() if a.kind else 0
+    cap = a.cap or (amq.TreeOptions(a.kind).set_filter_bits_per_key(bpk).filter_page_payload_size()
+                    if a.kind else 0)
+    S = a.leaf_keys
     for L in [int(x) for x in a.leaves.split(",")]:
-        counts = [16384] * L
-        keys = amq.gen_keys16(42, 0, 16384 * L)
+        counts = [S] * L
+        keys = amq.gen_keys16(42, 0, S * L)
         if a.kind == 1:
             keys = sort_segments_device(torch, keys, counts)
         kb = amq.KeyBatch.fixed(keys)
@@ -57,8 +62,8 @@ def main():
             e1.record()
         torch.cuda.synchronize()
         ms = float(np.median([e0.elapsed_time(e1) for e0, e1 in ev]))
-        print(f"kind {a.kind} leaves {L:5d} keys {16384 * L:9d} median {ms * 1e3:8.1f} us "
-              f"{16384 * L / ms / 1e3:9.1f} Mkeys/s ws {plan.workspace_bytes}", flush=True)
+        print(f"kind {a.kind} leaves {L:5d} keys {S * L:9d} median {ms * 1e3:8.1f} us "
+              f"{S * L / ms / 1e3:9.1f} Mkeys/s ws {plan.workspace_bytes}", flush=True)
 
 
 if __name__ == "__main__":

@@ -1375,7 +1375,8 @@ struct Vqf<16> {
 
 constexpr uint32_t kVqfTempStride = 128;  // workspace bytes per block (>= slots * entry)
 constexpr uint32_t kVqfMaxLdsBlocks = 16384;
-constexpr uint32_t kVqfMatchLdsBlocks = 512;  // vqf_decide's LDS lane-mask table (8 B/block)
+constexpr uint32_t kVqfMatchLdsBlocks = 2048;  // vqf_decide's LDS lane-mask table (8 B/block)
+constexpr uint32_t kChipCUs = 256;             // MI355X (gfx950): 8 XCDs x 32 CUs
 
 // workspace: [status u32 x8][record sink u64 x4][nelts u32 x n_segs][pad to 256]
 //            [128-byte record per block]
@@ -1498,7 +1499,8 @@ __device__ inline void vqf_locate_alt(const VqfLoc& l, uint64_t R, uint64_t magi
 // kLdsMatch: the four lane-match masks come from an LDS table of 64-bit lane masks, one per
 // block (each lane ORs its bit into its block's entry, then reads the entries it needs,
 // then clears): a handful of LDS operations instead of ~7 VALU per block-id bit.  Needs
-// 8 B of LDS per block, so it is used for leaves of <= kVqfMatchLdsBlocks blocks.
+// 8 B of LDS per block, so it is used for leaves of <= kVqfMatchLdsBlocks blocks, and only
+// when the table does not cost waves per CU (tkv_amq_build).
 // kCompact (T = 8, <= 512 blocks, fused place): 4-byte key records
 //   block << 21 | rank << 15 | (bucket offset << 8 | tag), or ~0 for a key not inserted
 template <int T, int MODE, int NBITS, bool kLdsMatch, bool kCompact>
@@ -1733,7 +1735,6 @@ __device__ inline void vqf_decide_dispatch(const uint8_t* keys, const uint64_t* 
 {
   // kVqfMaxLdsBlocks = 16384 -> at most 14 block-id bits
   if (sg.n_blocks <= 512) {
-    static_assert(kVqfMatchLdsBlocks == 512, "");
     if (T == 8 && compact_ok) {
       if (match_lds) vqf_decide_body<T, MODE, 9, true, T == 8>(keys, offs, stride, sg, seg_index, ws, recs, cnt, compact_ok);
       else vqf_decide_body<T, MODE, 9, false, T == 8>(keys, offs, stride, sg, seg_index, ws, recs, cnt, compact_ok);
@@ -1741,6 +1742,8 @@ __device__ inline void vqf_decide_dispatch(const uint8_t* keys, const uint64_t* 
       if (match_lds) vqf_decide_body<T, MODE, 9, true, false>(keys, offs, stride, sg, seg_index, ws, recs, cnt, compact_ok);
       else vqf_decide_body<T, MODE, 9, false, false>(keys, offs, stride, sg, seg_index, ws, recs, cnt, compact_ok);
     }
+  } else if (match_lds) {
+    vqf_decide_body<T, MODE, 14, true, false>(keys, offs, stride, sg, seg_index, ws, recs, cnt, compact_ok);
   } else {
     vqf_decide_body<T, MODE, 14, false, false>(keys, offs, stride, sg, seg_index, ws, recs, cnt, compact_ok);
   }
@@ -2162,7 +2165,12 @@ __device__ void vqf_place_body(const tkv_amq_segment& sg, uint32_t seg_index, Vq
       cnt[w] = (incl - v) + run * 0x01010101u;
       run += incl >> 24;
     }
-    // pass 2: slot of each entry in insertion order; metadata zero at slot + offset
+    // pass 2: slot of each entry in insertion order; metadata zero at slot + offset.  Pass 1's
+    // per-slot offsets and masks are recomputed, not kept live across the scan (as in
+    // vqf_place_fused_sort: that kept the kernel at ~230 VGPRs)
+#pragma unroll
+    for (uint32_t q = 0; q < kRecWords; ++q)
+      asm volatile("" : "+v"(rv[q].x), "+v"(rv[q].y), "+v"(rv[q].z), "+v"(rv[q].w));
     uint64_t md_lo = ~0ull, md_hi = T == 8 ? ~0ull : 0ull;
     // (branch-free as in pass 1; slots are distinct, so each tag is a plain byte/short store,
     // dead slots store into the image's pad dword)
@@ -2242,7 +2250,7 @@ __global__ __launch_bounds__(kPlaceThreads) void vqf_place(const tkv_amq_segment
 // 53 KB of LDS (registers, ~234 VGPRs, still hold the kernel to two workgroups per CU; forcing
 // three spilled and ran 29% slower).
 constexpr uint32_t kFusedThreads = 256;
-constexpr uint32_t kFusedLdsBudget = 80 * 1024;
+constexpr uint32_t kFusedLdsBudget = 160 * 1024;  // a leaf of up to 1,241 blocks (one workgroup per CU at the top)
 constexpr uint32_t kFusedRegionWords = 33;
 constexpr uint32_t kFusedCountWord = 32;
 
@@ -3346,7 +3354,13 @@ int tkv_amq_build(int kind, const uint8_t* keys, const uint64_t* offs, uint32_t 
     return TKV_AMQ_INVALID_ARGUMENT;
   if (hipMemsetAsync(d_ws, 0, 64, s) != hipSuccess) return TKV_AMQ_INTERNAL;
   // LDS: u32 block counts (+ the u64 lane-mask table when every leaf is small enough)
-  const int match_lds = max_blocks <= kVqfMatchLdsBlocks;
+  // The lane-mask table costs 8 B of LDS per block in every decide wave: used when it does not
+  // cut the waves per CU below the batch's own leaves per CU (vqf_decide: one wave per leaf;
+  // the ring kernel's LDS is larger than the table anyway)
+  const uint64_t leaves_per_cu = (n_segs + kChipCUs - 1) / kChipCUs;
+  const int match_lds = max_blocks <= kVqfMatchLdsBlocks &&
+                        (n_segs <= kVqfRingMaxSegs ||
+                         12ull * max_blocks * (leaves_per_cu < 24 ? leaves_per_cu : 24) <= 160 * 1024);
   const uint32_t fused_lds = vqf_fused_lds_bytes(max_blocks);
   const bool fused = fused_lds <= kFusedLdsBudget;  // compact records are read only there
   const int flags = match_lds | (fused ? 2 : 0);
