@@ -425,6 +425,35 @@ def test_bloom_monolithic_large_matches_atomic_path(amq, torch, n, bpk):
     assert torch.equal(a[:pa], b[:pa])
 
 
+@pytest.mark.parametrize("shape", ["k16", "k24", "var"])
+def test_bloom_big_leaves_in_lds(oracle, amq, torch, shape):
+    """Batches of >= 64 leaves build leaf images of up to 160 KB in LDS (1024-thread
+    workgroups above 32 KB; TurtleKV leaves of small items reach ~80K keys): a 100000-key leaf
+    (125 KB at 10 bits/key, 150 KB at 12) and a 40000-key one among small leaves; at 14 bits/key
+    the 100000-key leaf (175 KB) sends the batch to the device-atomic path."""
+    rng = np.random.default_rng(77)
+    counts = [int(c) for c in rng.integers(0, 2000, 70)]
+    counts[5], counts[40], counts[69] = 100000, 40000, 0
+    n = sum(counts)
+    offs = None
+    if shape == "k16":
+        keys, stride = oracle.gen_keys16(21, 0, n), 16
+    elif shape == "k24":
+        keys, stride = rng.integers(0, 256, (n, 24), dtype=np.uint8), 24
+    else:
+        lens = rng.integers(4, 40, n)
+        keys, stride = rng.integers(0, 256, int(lens.sum()), dtype=np.uint8), 0
+        offs = np.zeros(n + 1, np.int64)
+        offs[1:] = np.cumsum(lens)
+    for bpk in (10, 12, 14):
+        ref = oracle_per_segment(oracle, 0, keys, counts, bpk, stride=stride,
+                                 offsets=None if offs is None else offs.astype(np.uint64))
+        plan, out = gpu_build(amq, torch, 0, torch.from_numpy(keys).cuda(), counts, bpk,
+                              offsets_t=None if offs is None else torch.from_numpy(offs).cuda())
+        assert (plan.max_seg_blocks * 64 > 160 * 1024) == (bpk == 14)
+        assert_same(plan, out, ref)
+
+
 def test_bloom_oversize_leaf_in_batch_global_path(oracle, amq, torch):
     """A multi-leaf batch holding a leaf beyond the LDS budget takes the device-atomic path."""
     counts = [120000, 500, 16384]

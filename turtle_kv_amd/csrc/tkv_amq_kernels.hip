@@ -2837,6 +2837,13 @@ using namespace tkv;
 namespace {
 
 constexpr uint32_t kBloomLdsBudget = 64 * 1024;
+// Batches of >= kBloomSpreadSegs leaves build every leaf image in LDS up to the whole CU's
+// LDS (a 160 KB image: 1.3M bits, ~130K keys at 10 bits/key; TurtleKV leaves of small items
+// reach ~80K keys).  Images above kBloomWideLds take 1024-thread workgroups (fewer than five
+// 256-thread workgroups would fit a CU).  The split, monolithic and device-atomic paths keep
+// the 64 KiB budget.
+constexpr uint32_t kBloomLeafLdsBudget = 160 * 1024;
+constexpr uint32_t kBloomWideLds = 32 * 1024;
 // The LDS build runs one workgroup per leaf, so a batch of a few leaves (the per-leaf call
 // site, or a small LeafBatcher batch) keeps a few CUs busy for the whole leaf.  Below this many
 // leaves the keys are spread over n_keys/256 workgroups that set bits with device atomics.
@@ -3302,9 +3309,20 @@ int tkv_amq_build(int kind, const uint8_t* keys, const uint64_t* offs, uint32_t 
                          parts, chunks, w, img, d_out);
       return hipGetLastError() == hipSuccess ? TKV_AMQ_OK : TKV_AMQ_INTERNAL;
     }
-    if (lds <= kBloomLdsBudget && n_segs >= kBloomSpreadSegs) {
+    if (lds <= kBloomLeafLdsBudget && n_segs >= kBloomSpreadSegs) {
       const int bmode = build_key_mode(keys, offs, stride);
-      if (n_segs < kBloomWideSegs)
+      if (lds > kBloomLdsBudget) {
+        static std::once_flag big_attr[kMaxDevices];
+        once_per_device(big_attr, [] {
+          for (const void* f : {reinterpret_cast<const void*>(&bloom_build_lds<kKey16, 1024>),
+                                reinterpret_cast<const void*>(&bloom_build_lds<kKey24, 1024>),
+                                reinterpret_cast<const void*>(&bloom_build_lds<kKeyFixed, 1024>),
+                                reinterpret_cast<const void*>(&bloom_build_lds<kKeyVar, 1024>)})
+            (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)kBloomLeafLdsBudget);
+        });
+      }
+      if (n_segs < kBloomWideSegs || lds > kBloomWideLds)
         launch_bloom_lds<1024>(bmode, mode, n_segs, lds, s, keys, offs, stride, d_segs, d_out);
       else
         launch_bloom_lds<256>(bmode, mode, n_segs, lds, s, keys, offs, stride, d_segs, d_out);
