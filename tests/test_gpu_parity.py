@@ -189,11 +189,13 @@ def test_bloom_leaf_kernel_widths(oracle, amq, torch, n_leaves, shape):
         assert segment_bytes(plan, out, s) == ref.tobytes(), f"leaf {s}"
 
 
-@pytest.mark.parametrize("counts", [[16384], [16384, 9000, 1, 0, 52000], [3000] * 200])
+@pytest.mark.parametrize("counts", [[16384], [16384, 9000, 1, 0, 52000], [3000] * 200,
+                                    [100000], [120000, 700, 0, 5]])
 def test_bloom_split_matches_unsplit(oracle, amq, torch, counts):
     """The split build (workspace given) and the one-workgroup / atomic builds (no workspace)
     write the same bytes; the split one also equals the oracle (a 52K-key leaf: a 64 KiB
-    image, the largest the LDS paths take)."""
+    image; 100K- and 120K-key leaves: 125 and 150 KB images, up to the 160 KB the split parts
+    take in LDS)."""
     keys = oracle.gen_keys16(9, 0, sum(counts))
     kt = torch.from_numpy(keys).cuda()
     plan = amq.plan_filters(0, counts, 10)
@@ -379,17 +381,17 @@ def test_vqf_hash_matches_xxhash(amq, torch):
     assert [int(x) for x in h16] == [xxhash.xxh64_intdigest(k.tobytes(), VQF_SEED) for k in k16]
 
 
-@pytest.mark.parametrize("n,bpk,seed", [(120000, 10, 8), (3000000, 10, 9), (1500000, 12, 10),
-                                         (400000, 5, 11), (10000, 64, 12)])
+@pytest.mark.parametrize("n,bpk,seed", [(200000, 10, 8), (3000000, 10, 9), (1500000, 12, 10),
+                                         (400000, 5, 11), (30000, 64, 12)])
 def test_bloom_monolithic_partitioned(oracle, amq, torch, n, bpk, seed):
-    """One filter larger than the LDS image budget (64 KiB): the hash-once record path
+    """One filter larger than the LDS image budget (160 KB): the hash-once record path
     (bloom_rec_partition / bloom_rec_tile), byte-identical to the oracle.  Covers a ragged last
     tile, k = 7 / 8 / generic <= 8 (12-byte bit records) and k = 32 (the keys themselves are
     partitioned and hashed per tile), and 58 tiles over 92 partition workgroups."""
     keys = oracle.gen_keys16(seed, 0, n)
     ref = oracle_per_segment(oracle, 0, keys, [n], bpk)
     plan, out = gpu_build(amq, torch, 0, torch.from_numpy(keys).cuda(), [n], bpk)
-    assert plan.max_seg_blocks * 64 > 64 * 1024
+    assert plan.max_seg_blocks * 64 > 160 * 1024
     assert plan.workspace_bytes >= 16 * n  # the partitioned path's workspace
     assert_same(plan, out, ref)
 
@@ -455,8 +457,9 @@ def test_bloom_big_leaves_in_lds(oracle, amq, torch, shape):
 
 
 def test_bloom_oversize_leaf_in_batch_global_path(oracle, amq, torch):
-    """A multi-leaf batch holding a leaf beyond the LDS budget takes the device-atomic path."""
-    counts = [120000, 500, 16384]
+    """A multi-leaf batch holding a leaf beyond the LDS budget (a 175 KB image) takes the
+    device-atomic path."""
+    counts = [140000, 500, 16384]
     keys = oracle.gen_keys16(15, 0, sum(counts))
     ref = oracle_per_segment(oracle, 0, keys, counts, 10)
     plan, out = gpu_build(amq, torch, 0, torch.from_numpy(keys).cuda(), counts, 10)

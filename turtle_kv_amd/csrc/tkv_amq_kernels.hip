@@ -2836,12 +2836,13 @@ using namespace tkv;
 
 namespace {
 
-constexpr uint32_t kBloomLdsBudget = 64 * 1024;
-// Batches of >= kBloomSpreadSegs leaves build every leaf image in LDS up to the whole CU's
-// LDS (a 160 KB image: 1.3M bits, ~130K keys at 10 bits/key; TurtleKV leaves of small items
-// reach ~80K keys).  Images above kBloomWideLds take 1024-thread workgroups (fewer than five
-// 256-thread workgroups would fit a CU).  The split, monolithic and device-atomic paths keep
-// the 64 KiB budget.
+constexpr uint32_t kBloomLdsBudget = 64 * 1024;  // dynamic LDS a launch gets without the attribute
+// Leaf images are built in LDS up to the whole CU's LDS (a 160 KB image: 1.3M bits, ~130K
+// keys at 10 bits/key; TurtleKV leaves of small items reach ~80K keys): one workgroup per
+// leaf from kBloomSpreadSegs leaves, the split build below kBloomSplitSegs.  Images above
+// kBloomWideLds take 1024-thread workgroups (fewer than five 256-thread workgroups would fit
+// a CU).  A single larger filter takes the tiled monolithic build (64 KiB tiles); anything
+// else beyond kBloomLeafLdsBudget, device atomics.
 constexpr uint32_t kBloomLeafLdsBudget = 160 * 1024;
 constexpr uint32_t kBloomWideLds = 32 * 1024;
 // The LDS build runs one workgroup per leaf, so a batch of a few leaves (the per-leaf call
@@ -2861,7 +2862,7 @@ constexpr uint32_t kBloomWideSegs = 2048;
 // parts per leaf for a batch of n_segs leaves holding n_keys keys (1: no split)
 inline uint32_t bloom_split_parts(uint32_t n_segs, uint64_t n_keys, uint64_t max_blocks)
 {
-  if (n_segs == 0 || n_segs >= kBloomSplitSegs || 64 * max_blocks > kBloomLdsBudget) return 1;
+  if (n_segs == 0 || n_segs >= kBloomSplitSegs || 64 * max_blocks > kBloomLeafLdsBudget) return 1;
   uint64_t p = (kSplitTargetWgs + n_segs - 1) / n_segs;
   const uint64_t per_leaf = n_keys / n_segs;
   const uint64_t by_keys = per_leaf / kSplitMinKeys;
@@ -3034,7 +3035,7 @@ inline BloomPartGeom bloom_route_geom(uint64_t n_keys, uint32_t n_parts)
 // (it needs a workspace of bloom_part_geom(n_keys, n_blocks).bytes and 16-byte keys)
 inline bool bloom_partitioned(uint32_t n_segs, uint64_t max_blocks, uint64_t n_keys)
 {
-  return n_segs == 1 && 64 * max_blocks > kBloomLdsBudget && n_keys <= 0xffffffffull &&
+  return n_segs == 1 && 64 * max_blocks > kBloomLeafLdsBudget && n_keys <= 0xffffffffull &&
          div_up(max_blocks, kBloomTileBlocks) <= kBloomPartMaxTiles;
 }
 
@@ -3278,7 +3279,7 @@ int tkv_amq_build(int kind, const uint8_t* keys, const uint64_t* offs, uint32_t 
       // a small batch: each leaf's keys over `parts` workgroups, then their images ORed
       static std::once_flag split_attr[kMaxDevices];
       once_per_device(split_attr, [] {
-        const int cap = (int)kBloomLdsBudget;
+        const int cap = (int)kBloomLeafLdsBudget;
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&bloom_build_split<kKey16>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, cap);
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&bloom_build_split<kKey24>),
