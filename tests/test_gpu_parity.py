@@ -318,13 +318,15 @@ def test_vqf_decide_paths(oracle, amq, torch, n_leaves, shape):
             assert segment_bytes(plan, out, s) == ref[:p.payload_used].tobytes(), f"bpk {bpk} leaf {s}"
 
 
+@pytest.mark.parametrize("big", [100000, 260000])
 @pytest.mark.parametrize("n_leaves", [4, 800])
-def test_vqf_leaf_beyond_ring_blocks(oracle, amq, torch, n_leaves):
+def test_vqf_leaf_beyond_ring_blocks(oracle, amq, torch, n_leaves, big):
     """A 100000-key leaf in 1 MiB pages has 2451 blocks: more than the ring kernel's count
     table holds, so its wave 0 runs vqf_decide_body (block-id ballots, no LDS match table);
-    in a batch of 800 leaves vqf_decide does the same.  Unfused place (the image is too big
-    for LDS)."""
-    counts = [100000, 500, 0, 16384] + [300] * (n_leaves - 4)
+    in a batch of 800 leaves vqf_decide does the same.  Its LDS place is split over two
+    workgroups per leaf; a 260000-key leaf (6373 blocks, beyond four) takes the unfused
+    scatter + place."""
+    counts = [big, 500, 0, 16384] + [300] * (n_leaves - 4)
     keys = oracle.gen_keys16(6, 0, sum(counts))
     plan, out = gpu_build(amq, torch, 1, torch.from_numpy(keys).cuda(), counts, 12, cap=1 << 20)
     assert plan.segs["n_blocks"][0] > 2048

@@ -2235,7 +2235,8 @@ __global__ __launch_bounds__(kPlaceThreads) void vqf_place(const tkv_amq_segment
   else if (sg.tag_bits == 16) vqf_place_body<16>(sg, blockIdx.x, ws, out, s_cnt, s_img);
 }
 
-// Fused scatter + place for leaves whose block records fit in LDS (one workgroup per leaf):
+// Fused scatter + place for leaves whose block records fit in LDS (one workgroup per leaf, or
+// up to kFusedMaxParts per leaf for a leaf of more than 1,241 blocks):
 // the leaf's placement records stream in coalesced, each entry lands at [block][rank] of an
 // LDS image (no partial-line global writes), then the per-block counting sort runs on it.
 //
@@ -2250,7 +2251,8 @@ __global__ __launch_bounds__(kPlaceThreads) void vqf_place(const tkv_amq_segment
 // 53 KB of LDS (registers, ~234 VGPRs, still hold the kernel to two workgroups per CU; forcing
 // three spilled and ran 29% slower).
 constexpr uint32_t kFusedThreads = 256;
-constexpr uint32_t kFusedLdsBudget = 160 * 1024;  // a leaf of up to 1,241 blocks (one workgroup per CU at the top)
+constexpr uint32_t kFusedLdsBudget = 160 * 1024;  // 1,241 blocks per workgroup (one per CU at the top)
+constexpr uint32_t kFusedMaxParts = 4;            // workgroups per leaf: leaves up to 4,964 blocks
 constexpr uint32_t kFusedRegionWords = 33;
 constexpr uint32_t kFusedCountWord = 32;
 
@@ -2272,7 +2274,8 @@ __host__ __device__ inline uint32_t vqf_fused_lds_bytes(uint32_t max_nb)
 // cycles, PMC) do not set this kernel's time.
 template <int T, int NB>
 __device__ void vqf_place_fused_sort(const tkv_amq_segment& sg, uint32_t seg_index,
-                                     VqfWorkspace ws, uint8_t* __restrict__ out, uint32_t* lds)
+                                     VqfWorkspace ws, uint8_t* __restrict__ out, uint32_t* lds,
+                                     uint32_t lo, uint32_t nbl)
 {
   using C = Vqf<T>;
   using E = typename C::Entry;
@@ -2287,7 +2290,7 @@ __device__ void vqf_place_fused_sort(const tkv_amq_segment& sg, uint32_t seg_ind
   const uint32_t nb = sg.n_blocks;
   uint8_t* payload = out + sg.out_offset;
 
-  if (tid < 5) {
+  if (lo == 0 && tid < 5) {
     // PackedVqfFilter header (vqf_filter_page_view.hpp:79-94) + vqf_metadata
     uint64_t w0, w1;
     switch (tid) {
@@ -2301,12 +2304,13 @@ __device__ void vqf_place_fused_sort(const tkv_amq_segment& sg, uint32_t seg_ind
     v.x = w0;
     v.y = w1;
     reinterpret_cast<ulonglong2*>(payload)[tid] = v;
-  } else if (tid < 9) {
+  } else if (lo == 0 && tid < 9) {
     write_page_header(out, sg, kLayoutVqf, tid - 5);
   }
-  uint4* dst_blocks = reinterpret_cast<uint4*>(payload + kVqfHeader + kVqfMetadata);
+  // this workgroup's blocks: LDS region b - lo, output block b
+  uint4* dst_blocks = reinterpret_cast<uint4*>(payload + kVqfHeader + kVqfMetadata) + 4ull * lo;
 
-  for (uint32_t b0 = tid; b0 < nb; b0 += NB * kFusedThreads) {
+  for (uint32_t b0 = tid; b0 < nbl; b0 += NB * kFusedThreads) {
     uint32_t* reg[NB];
     uint32_t c[NB];
     bool live[NB];
@@ -2314,7 +2318,7 @@ __device__ void vqf_place_fused_sort(const tkv_amq_segment& sg, uint32_t seg_ind
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
       const uint32_t b = b0 + j * kFusedThreads;
-      live[j] = b < nb;
+      live[j] = b < nbl;
       reg[j] = lds + (live[j] ? b : b0) * kFusedRegionWords;
       c[j] = live[j] ? reg[j][kFusedCountWord] : 0u;
 #pragma unroll
@@ -2440,14 +2444,17 @@ __device__ void vqf_place_fused_sort(const tkv_amq_segment& sg, uint32_t seg_ind
   }
 }
 
+// Blocks [lo, lo + nbl) of the leaf (a leaf whose LDS image exceeds the budget is placed by
+// several workgroups, each reading all of the leaf's records and keeping its blocks' ones).
 template <int T>
 __device__ void vqf_place_fused_body(const tkv_amq_segment& sg, uint32_t seg_index,
                                      VqfWorkspace ws, const uint64_t* __restrict__ recs,
-                                     uint8_t* __restrict__ out, uint32_t* lds)
+                                     uint8_t* __restrict__ out, uint32_t* lds, uint32_t lo,
+                                     uint32_t nbl)
 {
   const uint32_t tid = threadIdx.x;
   const uint32_t nb = sg.n_blocks, n = sg.n_keys;
-  for (uint32_t b = tid; b < nb; b += kFusedThreads) lds[b * kFusedRegionWords + kFusedCountWord] = 0;
+  for (uint32_t b = tid; b < nbl; b += kFusedThreads) lds[b * kFusedRegionWords + kFusedCountWord] = 0;
   __syncthreads();
   const uint32_t gb0 = (uint32_t)sg.block_base;
   constexpr uint32_t kU = 16;  // 16-byte loads in flight per thread: 64 KB per workgroup
@@ -2458,7 +2465,8 @@ __device__ void vqf_place_fused_body(const tkv_amq_segment& sg, uint32_t seg_ind
     atomicAdd(r + kFusedCountWord, 1u);
   };
   if (T == 8 && nb <= 512) {
-    // compact 4-byte records (vqf_decide kCompact), four per load
+    // compact 4-byte records (vqf_decide kCompact), four per load (such a leaf has one
+    // workgroup: lo = 0, nbl = nb)
     const uint32_t* r32 = reinterpret_cast<const uint32_t*>(recs + sg.key_begin);
     const uint32_t skip = (uint32_t)((reinterpret_cast<uintptr_t>(r32) & 15) >> 2);  // 0 or 2
     const uint4* r4 = reinterpret_cast<const uint4*>(r32 - skip);
@@ -2490,8 +2498,9 @@ __device__ void vqf_place_fused_body(const tkv_amq_segment& sg, uint32_t seg_ind
     const uint32_t n_pairs = (lo_skip + n + 1) / 2;
     auto put = [&](uint64_t v, uint32_t k) {
       const uint32_t hi = (uint32_t)(v >> 32);
-      if (k >= lo_skip && k < lo_skip + n && hi != 0xffffffffu)
-        put_entry((hi >> 6) - gb0, hi & 63u, (uint32_t)v & 0x7fffffffu);
+      const uint32_t blk = (hi >> 6) - gb0 - lo;  // (a key not inserted: hi = ~0, out of range)
+      if (k >= lo_skip && k < lo_skip + n && hi != 0xffffffffu && blk < nbl)
+        put_entry(blk, hi & 63u, (uint32_t)v & 0x7fffffffu);
     };
     for (uint32_t p0 = 0; p0 < n_pairs; p0 += kFusedThreads * kU) {
       uint4 v[kU];
@@ -2509,21 +2518,27 @@ __device__ void vqf_place_fused_body(const tkv_amq_segment& sg, uint32_t seg_ind
     }
   }
   __syncthreads();
-  vqf_place_fused_sort<T, 1>(sg, seg_index, ws, out, lds);
+  vqf_place_fused_sort<T, 1>(sg, seg_index, ws, out, lds, lo, nbl);
 }
 
+// grid: n_segs * parts workgroups; workgroup (s, p) places blocks [p * span, (p + 1) * span)
+// of leaf s (parts = 1 unless a leaf's image exceeds kFusedLdsBudget)
 __global__ __launch_bounds__(kFusedThreads) void vqf_place_fused(const tkv_amq_segment* __restrict__ segs,
                                                                  void* ws_base, uint64_t ws_bytes,
                                                                  uint32_t n_segs,
-                                                                 uint8_t* __restrict__ out)
+                                                                 uint8_t* __restrict__ out,
+                                                                 uint32_t parts, uint32_t span)
 {
   extern __shared__ __attribute__((aligned(16))) uint32_t s_lds[];
-  const tkv_amq_segment sg = segs[blockIdx.x];
+  const uint32_t seg = blockIdx.x / parts, lo = (blockIdx.x - seg * parts) * span;
+  const tkv_amq_segment sg = segs[seg];
+  if (lo >= sg.n_blocks && lo != 0) return;
+  const uint32_t nbl = sg.n_blocks - lo < span ? sg.n_blocks - lo : span;
   const VqfWorkspace ws = vqf_workspace(ws_base, n_segs);
   if (!vqf_ws_ok(segs, n_segs, ws_bytes, ws)) return;
   const uint64_t* recs = vqf_records(ws, segs, n_segs);
-  if (sg.tag_bits == 8) vqf_place_fused_body<8>(sg, blockIdx.x, ws, recs, out, s_lds);
-  else if (sg.tag_bits == 16) vqf_place_fused_body<16>(sg, blockIdx.x, ws, recs, out, s_lds);
+  if (sg.tag_bits == 8) vqf_place_fused_body<8>(sg, seg, ws, recs, out, s_lds, lo, nbl);
+  else if (sg.tag_bits == 16) vqf_place_fused_body<16>(sg, seg, ws, recs, out, s_lds, lo, nbl);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -3380,8 +3395,12 @@ int tkv_amq_build(int kind, const uint8_t* keys, const uint64_t* offs, uint32_t 
   const int match_lds = max_blocks <= kVqfMatchLdsBlocks &&
                         (n_segs <= kVqfRingMaxSegs ||
                          12ull * max_blocks * (leaves_per_cu < 24 ? leaves_per_cu : 24) <= 160 * 1024);
-  const uint32_t fused_lds = vqf_fused_lds_bytes(max_blocks);
-  const bool fused = fused_lds <= kFusedLdsBudget;  // compact records are read only there
+  // a leaf whose LDS image exceeds the budget is placed by up to kFusedMaxParts workgroups
+  const uint32_t place_parts =
+      (uint32_t)div_up(max_blocks, kFusedLdsBudget / (4 * kFusedRegionWords));
+  const uint32_t place_span = (uint32_t)div_up(max_blocks, place_parts);
+  const uint32_t fused_lds = vqf_fused_lds_bytes(place_span);
+  const bool fused = place_parts <= kFusedMaxParts;  // compact records are read only there
   const int flags = match_lds | (fused ? 2 : 0);
   const size_t lds = 4ull * ((max_blocks + 1) & ~1u) + (match_lds ? 8ull * max_blocks : 0);
   if (n_segs <= kVqfRingMaxSegs) {
@@ -3418,8 +3437,8 @@ int tkv_amq_build(int kind, const uint8_t* keys, const uint64_t* offs, uint32_t 
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&vqf_place_fused),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)kFusedLdsBudget);
     });
-    hipLaunchKernelGGL(vqf_place_fused, dim3(n_segs), dim3(kFusedThreads), fused_lds, s, d_segs,
-                       d_ws, ws_bytes, n_segs, d_out);
+    hipLaunchKernelGGL(vqf_place_fused, dim3(n_segs * place_parts), dim3(kFusedThreads), fused_lds,
+                       s, d_segs, d_ws, ws_bytes, n_segs, d_out, place_parts, place_span);
   } else {
     if (n_keys)
       hipLaunchKernelGGL(vqf_scatter, dim3((uint32_t)div_up(n_keys, 256)), dim3(256), 0, s,
