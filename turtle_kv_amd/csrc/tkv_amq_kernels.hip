@@ -1376,7 +1376,6 @@ struct Vqf<16> {
 constexpr uint32_t kVqfTempStride = 128;  // workspace bytes per block (>= slots * entry)
 constexpr uint32_t kVqfMaxLdsBlocks = 16384;
 constexpr uint32_t kVqfMatchLdsBlocks = 2048;  // vqf_decide's LDS lane-mask table (8 B/block)
-constexpr uint32_t kChipCUs = 256;             // MI355X (gfx950): 8 XCDs x 32 CUs
 
 // workspace: [status u32 x8][record sink u64 x4][nelts u32 x n_segs][pad to 256]
 //            [128-byte record per block]
@@ -1499,8 +1498,7 @@ __device__ inline void vqf_locate_alt(const VqfLoc& l, uint64_t R, uint64_t magi
 // kLdsMatch: the four lane-match masks come from an LDS table of 64-bit lane masks, one per
 // block (each lane ORs its bit into its block's entry, then reads the entries it needs,
 // then clears): a handful of LDS operations instead of ~7 VALU per block-id bit.  Needs
-// 8 B of LDS per block, so it is used for leaves of <= kVqfMatchLdsBlocks blocks, and only
-// when the table does not cost waves per CU (tkv_amq_build).
+// 8 B of LDS per block, so it is used for leaves of <= kVqfMatchLdsBlocks blocks.
 // kCompact (T = 8, <= 512 blocks, fused place): 4-byte key records
 //   block << 21 | rank << 15 | (bucket offset << 8 | tag), or ~0 for a key not inserted
 template <int T, int MODE, int NBITS, bool kLdsMatch, bool kCompact>
@@ -3388,13 +3386,10 @@ int tkv_amq_build(int kind, const uint8_t* keys, const uint64_t* offs, uint32_t 
     return TKV_AMQ_INVALID_ARGUMENT;
   if (hipMemsetAsync(d_ws, 0, 64, s) != hipSuccess) return TKV_AMQ_INTERNAL;
   // LDS: u32 block counts (+ the u64 lane-mask table when every leaf is small enough)
-  // The lane-mask table costs 8 B of LDS per block in every decide wave: used when it does not
-  // cut the waves per CU below the batch's own leaves per CU (vqf_decide: one wave per leaf;
-  // the ring kernel's LDS is larger than the table anyway)
-  const uint64_t leaves_per_cu = (n_segs + kChipCUs - 1) / kChipCUs;
-  const int match_lds = max_blocks <= kVqfMatchLdsBlocks &&
-                        (n_segs <= kVqfRingMaxSegs ||
-                         12ull * max_blocks * (leaves_per_cu < 24 ? leaves_per_cu : 24) <= 160 * 1024);
+  // The lane-mask table costs 8 B of LDS per block in every decide wave, and wins even where
+  // it costs waves per CU: 6,104 leaves of 804 blocks 2.49 -> 2.14 ms (16 instead of 24 waves
+  // per CU), 2,048 of 1,961 blocks 3.03 -> 2.52 ms, against block-id ballots
+  const int match_lds = max_blocks <= kVqfMatchLdsBlocks;
   // a leaf whose LDS image exceeds the budget is placed by up to kFusedMaxParts workgroups
   const uint32_t place_parts =
       (uint32_t)div_up(max_blocks, kFusedLdsBudget / (4 * kFusedRegionWords));
