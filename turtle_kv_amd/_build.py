@@ -2,6 +2,7 @@
 this file so it travels to the GPU box with the repo snapshot."""
 from __future__ import annotations
 
+import hashlib
 import os
 import subprocess
 
@@ -17,18 +18,33 @@ FLAGS = ["-O3", "--offload-arch=gfx950", "-std=c++17", "-shared", "-fPIC",
          "-Wall", "-Wno-unused-function", "-I" + os.path.join(ROOT, "include")]
 
 
+STAMP = LIB + ".src"  # sha256 of the sources and flags the library was built from
+
+
+def source_digest() -> str:
+    h = hashlib.sha256(" ".join([HIPCC, *FLAGS]).encode())
+    for d in DEPS:
+        with open(d, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()
+
+
 def stale() -> bool:
-    if not os.path.exists(LIB):
+    """By content, not mtime: a checkout that restores an older source must rebuild."""
+    if not (os.path.exists(LIB) and os.path.exists(STAMP)):
         return True
-    t = os.path.getmtime(LIB)
-    return any(os.path.getmtime(d) > t for d in DEPS)
+    with open(STAMP) as f:
+        return f.read().strip() != source_digest()
 
 
 def build(force: bool = False) -> str:
     if force or stale():
         tmp = LIB + ".tmp"
+        digest = source_digest()
         subprocess.run([HIPCC, *FLAGS, "-o", tmp, *SOURCES], check=True)
         os.replace(tmp, LIB)
+        with open(STAMP, "w") as f:
+            f.write(digest + "\n")
     return LIB
 
 
