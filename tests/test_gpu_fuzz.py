@@ -73,3 +73,55 @@ def test_random_batches_match_oracle(oracle, amq, torch, case):
         seg = plan.segs[s]
         got = o[int(seg["out_offset"]):int(seg["out_offset"]) + int(seg["payload_bytes"])].tobytes()
         assert got == ref, f"case {case}: kind {kind} bpk {bpk} cap {cap} shape {shape} leaf {s} of {n_leaves}"
+
+
+@pytest.mark.parametrize("case", range(10))
+def test_random_big_leaf_batches_match_oracle(oracle, amq, torch, case):
+    """Batches holding one or two large leaves (TurtleKV leaves of small items, filter pages of
+    64 KiB-1 MiB): Bloom images around the 160 KB LDS budget (split, one-workgroup and
+    device-atomic paths), VQF leaves around 512 / 1,241 / 2,048 / 4,964 blocks (compact and
+    8-byte records, one or several place workgroups per leaf, the unfused place, the LDS
+    lane-mask table and the ballots).  The large leaves are always among those checked."""
+    rng = np.random.default_rng(9100 + case)
+    kind = case % 2
+    n_leaves = [1, 5, 64, 300, 800][(case // 2) % 5]
+    shape = [16, 0, 24][case % 3]
+    if kind == 0:
+        bpk = int(rng.choice([10, 12]))
+        cap = 0
+        big = [int(rng.choice([60000, 100000, 140000])) for _ in range(2)]
+    else:
+        bpk = int(rng.choice([12, 22]))
+        cap = int(rng.choice([65472, 130944, 262080, 1048512]))
+        big = [int(rng.choice([30000, 80000, 200000])) for _ in range(2)]
+    counts = [int(c) for c in rng.integers(0, 800, n_leaves)]
+    where = sorted({0, n_leaves - 1})
+    for i, w in enumerate(where):
+        counts[w] = big[i]
+    n = sum(counts)
+    keys, offs, stride = make_keys(rng, shape, n)
+    plan = amq.plan_filters(kind, counts, bpk, payload_capacity=cap)
+    kt = torch.from_numpy(keys).cuda()
+    kb = amq.KeyBatch.fixed(kt) if offs is None else amq.KeyBatch.variable(kt, torch.from_numpy(offs).cuda())
+    out = amq.build_all_filters(plan, kb)
+    torch.cuda.synchronize()
+    o = out.cpu().numpy()
+    sb = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
+    sample = sorted({*where, *rng.choice(n_leaves, size=min(n_leaves, 6), replace=False).tolist()})
+    for s in sample:
+        b, c = int(sb[s]), counts[s]
+        if offs is None:
+            kp, o_s = keys[b:], None
+        else:
+            kp, o_s = keys[int(offs[b]):], (offs[b:b + c + 1] - offs[b]).astype(np.uint64)
+        if kind == 0:
+            st, ref = oracle.bloom_build(kp, c, bpk, src_page_id=s, offsets=o_s, stride=stride)
+            ref = ref.tobytes()
+        else:
+            st, ref, p = oracle.vqf_build(kp, c, bpk, cap, src_page_id=s, offsets=o_s, stride=stride)
+            ref = ref[:p.payload_used].tobytes()
+        assert st == 0
+        seg = plan.segs[s]
+        got = o[int(seg["out_offset"]):int(seg["out_offset"]) + int(seg["payload_bytes"])].tobytes()
+        assert got == ref, (f"case {case}: kind {kind} bpk {bpk} cap {cap} shape {shape} leaf {s} "
+                            f"of {n_leaves} ({c} keys, {int(seg['n_blocks'])} blocks)")

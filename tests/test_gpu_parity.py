@@ -320,19 +320,21 @@ def test_vqf_decide_paths(oracle, amq, torch, n_leaves, shape):
 
 @pytest.mark.parametrize("big", [100000, 260000])
 @pytest.mark.parametrize("n_leaves", [4, 800])
-def test_vqf_leaf_beyond_ring_blocks(oracle, amq, torch, n_leaves, big):
+@pytest.mark.parametrize("bpk", [12, 22])
+def test_vqf_leaf_beyond_ring_blocks(oracle, amq, torch, n_leaves, big, bpk):
     """A 100000-key leaf in 1 MiB pages has 2451 blocks: more than the ring kernel's count
     table holds, so its wave 0 runs vqf_decide_body (block-id ballots, no LDS match table);
     in a batch of 800 leaves vqf_decide does the same.  Its LDS place is split over two
     workgroups per leaf; a 260000-key leaf (6373 blocks, beyond four) takes the unfused
-    scatter + place."""
+    scatter + place.  At 22 bits/key: 16-bit tags, 4365 / 11349 blocks."""
     counts = [big, 500, 0, 16384] + [300] * (n_leaves - 4)
     keys = oracle.gen_keys16(6, 0, sum(counts))
-    plan, out = gpu_build(amq, torch, 1, torch.from_numpy(keys).cuda(), counts, 12, cap=1 << 20)
-    assert plan.segs["n_blocks"][0] > 2048
+    plan, out = gpu_build(amq, torch, 1, torch.from_numpy(keys).cuda(), counts, bpk, cap=1 << 20)
+    assert plan.segs["n_blocks"][0] > 2048 and plan.segs["hash_val_shift"][0] == 0
+    assert (plan.segs["n_blocks"][0] > 4964) == (big == 260000)
     sb = seg_bounds(counts)
     for s in sorted({0, 1, 2, 3, n_leaves - 1}):
-        st, ref, p = oracle.vqf_build(keys[int(sb[s]):], counts[s], 12, 1 << 20, src_page_id=s)
+        st, ref, p = oracle.vqf_build(keys[int(sb[s]):], counts[s], bpk, 1 << 20, src_page_id=s)
         assert st == 0
         assert segment_bytes(plan, out, s) == ref[:p.payload_used].tobytes(), f"leaf {s}"
 
