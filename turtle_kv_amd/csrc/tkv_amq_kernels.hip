@@ -2248,7 +2248,6 @@ __global__ __launch_bounds__(kPlaceThreads) void vqf_place(const tkv_amq_segment
 // kTagDword; the metadata stays in registers.  No per-thread scratch: a 402-block leaf takes
 // 53 KB of LDS (registers, ~234 VGPRs, still hold the kernel to two workgroups per CU; forcing
 // three spilled and ran 29% slower).
-constexpr uint32_t kFusedThreads = 256;
 constexpr uint32_t kFusedLdsBudget = 160 * 1024;  // 1,241 blocks per workgroup (one per CU at the top)
 constexpr uint32_t kFusedMaxParts = 4;            // workgroups per leaf: leaves up to 4,964 blocks
 constexpr uint32_t kFusedRegionWords = 33;
@@ -2270,7 +2269,7 @@ __host__ __device__ inline uint32_t vqf_fused_lds_bytes(uint32_t max_nb)
 // (dword w of block b at w * 480 + b, so the 32 threads of a bank group never conflict
 // whatever bucket word they pick): 0.752 vs 0.730 ms -- bank conflicts (~59% of the LDS
 // cycles, PMC) do not set this kernel's time.
-template <int T, int NB>
+template <int T, int NB, uint32_t NT>
 __device__ void vqf_place_fused_sort(const tkv_amq_segment& sg, uint32_t seg_index,
                                      VqfWorkspace ws, uint8_t* __restrict__ out, uint32_t* lds,
                                      uint32_t lo, uint32_t nbl)
@@ -2308,14 +2307,14 @@ __device__ void vqf_place_fused_sort(const tkv_amq_segment& sg, uint32_t seg_ind
   // this workgroup's blocks: LDS region b - lo, output block b
   uint4* dst_blocks = reinterpret_cast<uint4*>(payload + kVqfHeader + kVqfMetadata) + 4ull * lo;
 
-  for (uint32_t b0 = tid; b0 < nbl; b0 += NB * kFusedThreads) {
+  for (uint32_t b0 = tid; b0 < nbl; b0 += NB * NT) {
     uint32_t* reg[NB];
     uint32_t c[NB];
     bool live[NB];
     uint32_t ent[NB][kEntWords];
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
-      const uint32_t b = b0 + j * kFusedThreads;
+      const uint32_t b = b0 + j * NT;
       live[j] = b < nbl;
       reg[j] = lds + (live[j] ? b : b0) * kFusedRegionWords;
       c[j] = live[j] ? reg[j][kFusedCountWord] : 0u;
@@ -2420,7 +2419,7 @@ __device__ void vqf_place_fused_sort(const tkv_amq_segment& sg, uint32_t seg_ind
         else md_lo[j] &= ~(1ull << 63);
       }
       const uint32_t* tg = reg[j] + kTagDword;
-      uint4* dst = dst_blocks + (uint64_t)(b0 + j * kFusedThreads) * 4;
+      uint4* dst = dst_blocks + (uint64_t)(b0 + j * NT) * 4;
       uint4 v0;
       v0.x = (uint32_t)md_lo[j];
       v0.y = (uint32_t)(md_lo[j] >> 32);
@@ -2444,7 +2443,7 @@ __device__ void vqf_place_fused_sort(const tkv_amq_segment& sg, uint32_t seg_ind
 
 // Blocks [lo, lo + nbl) of the leaf (a leaf whose LDS image exceeds the budget is placed by
 // several workgroups, each reading all of the leaf's records and keeping its blocks' ones).
-template <int T>
+template <int T, uint32_t NT>
 __device__ void vqf_place_fused_body(const tkv_amq_segment& sg, uint32_t seg_index,
                                      VqfWorkspace ws, const uint64_t* __restrict__ recs,
                                      uint8_t* __restrict__ out, uint32_t* lds, uint32_t lo,
@@ -2452,7 +2451,7 @@ __device__ void vqf_place_fused_body(const tkv_amq_segment& sg, uint32_t seg_ind
 {
   const uint32_t tid = threadIdx.x;
   const uint32_t nb = sg.n_blocks, n = sg.n_keys;
-  for (uint32_t b = tid; b < nbl; b += kFusedThreads) lds[b * kFusedRegionWords + kFusedCountWord] = 0;
+  for (uint32_t b = tid; b < nbl; b += NT) lds[b * kFusedRegionWords + kFusedCountWord] = 0;
   __syncthreads();
   const uint32_t gb0 = (uint32_t)sg.block_base;
   constexpr uint32_t kU = 16;  // 16-byte loads in flight per thread: 64 KB per workgroup
@@ -2472,16 +2471,16 @@ __device__ void vqf_place_fused_body(const tkv_amq_segment& sg, uint32_t seg_ind
     auto put = [&](uint32_t v, uint32_t k) {
       if (k >= skip && k < skip + n && v != 0xffffffffu) put_entry(v >> 21, (v >> 15) & 63u, v & 0x7fffu);
     };
-    for (uint32_t q0 = 0; q0 < n_quads; q0 += kFusedThreads * kU) {
+    for (uint32_t q0 = 0; q0 < n_quads; q0 += NT * kU) {
       uint4 v[kU];
 #pragma unroll
       for (uint32_t u = 0; u < kU; ++u) {
-        const uint32_t q = q0 + u * kFusedThreads + tid;
+        const uint32_t q = q0 + u * NT + tid;
         v[u] = q < n_quads ? load_nt16(r4 + q) : make_uint4(~0u, ~0u, ~0u, ~0u);
       }
 #pragma unroll
       for (uint32_t u = 0; u < kU; ++u) {
-        const uint32_t k = 4 * (q0 + u * kFusedThreads + tid);
+        const uint32_t k = 4 * (q0 + u * NT + tid);
         put(v[u].x, k);
         put(v[u].y, k + 1);
         put(v[u].z, k + 2);
@@ -2500,28 +2499,29 @@ __device__ void vqf_place_fused_body(const tkv_amq_segment& sg, uint32_t seg_ind
       if (k >= lo_skip && k < lo_skip + n && hi != 0xffffffffu && blk < nbl)
         put_entry(blk, hi & 63u, (uint32_t)v & 0x7fffffffu);
     };
-    for (uint32_t p0 = 0; p0 < n_pairs; p0 += kFusedThreads * kU) {
+    for (uint32_t p0 = 0; p0 < n_pairs; p0 += NT * kU) {
       uint4 v[kU];
 #pragma unroll
       for (uint32_t u = 0; u < kU; ++u) {
-        const uint32_t p = p0 + u * kFusedThreads + tid;
+        const uint32_t p = p0 + u * NT + tid;
         v[u] = p < n_pairs ? load_nt16(r2 + p) : make_uint4(0, ~0u, 0, ~0u);
       }
 #pragma unroll
       for (uint32_t u = 0; u < kU; ++u) {
-        const uint32_t k = 2 * (p0 + u * kFusedThreads + tid);
+        const uint32_t k = 2 * (p0 + u * NT + tid);
         put((uint64_t)v[u].x | ((uint64_t)v[u].y << 32), k);
         put((uint64_t)v[u].z | ((uint64_t)v[u].w << 32), k + 1);
       }
     }
   }
   __syncthreads();
-  vqf_place_fused_sort<T, 1>(sg, seg_index, ws, out, lds, lo, nbl);
+  vqf_place_fused_sort<T, 1, NT>(sg, seg_index, ws, out, lds, lo, nbl);
 }
 
 // grid: n_segs * parts workgroups; workgroup (s, p) places blocks [p * span, (p + 1) * span)
 // of leaf s (parts = 1 unless a leaf's image exceeds kFusedLdsBudget)
-__global__ __launch_bounds__(kFusedThreads) void vqf_place_fused(const tkv_amq_segment* __restrict__ segs,
+template <uint32_t NT>
+__global__ __launch_bounds__(NT) void vqf_place_fused(const tkv_amq_segment* __restrict__ segs,
                                                                  void* ws_base, uint64_t ws_bytes,
                                                                  uint32_t n_segs,
                                                                  uint8_t* __restrict__ out,
@@ -2535,8 +2535,8 @@ __global__ __launch_bounds__(kFusedThreads) void vqf_place_fused(const tkv_amq_s
   const VqfWorkspace ws = vqf_workspace(ws_base, n_segs);
   if (!vqf_ws_ok(segs, n_segs, ws_bytes, ws)) return;
   const uint64_t* recs = vqf_records(ws, segs, n_segs);
-  if (sg.tag_bits == 8) vqf_place_fused_body<8>(sg, seg, ws, recs, out, s_lds, lo, nbl);
-  else if (sg.tag_bits == 16) vqf_place_fused_body<16>(sg, seg, ws, recs, out, s_lds, lo, nbl);
+  if (sg.tag_bits == 8) vqf_place_fused_body<8, NT>(sg, seg, ws, recs, out, s_lds, lo, nbl);
+  else if (sg.tag_bits == 16) vqf_place_fused_body<16, NT>(sg, seg, ws, recs, out, s_lds, lo, nbl);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -3429,11 +3429,20 @@ int tkv_amq_build(int kind, const uint8_t* keys, const uint64_t* offs, uint32_t 
   if (fused) {
     static std::once_flag lds_attr[kMaxDevices];
     once_per_device(lds_attr, [] {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&vqf_place_fused),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kFusedLdsBudget);
+      for (const void* f : {reinterpret_cast<const void*>(&vqf_place_fused<256>),
+                            reinterpret_cast<const void*>(&vqf_place_fused<512>)})
+        (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kFusedLdsBudget);
     });
-    hipLaunchKernelGGL(vqf_place_fused, dim3(n_segs * place_parts), dim3(kFusedThreads), fused_lds,
-                       s, d_segs, d_ws, ws_bytes, n_segs, d_out, place_parts, place_span);
+    // 512 threads for a batch that does not fill the chip (the ring-decide sizes) or leaves of
+    // more than 512 blocks: lone leaf 98 -> 95 us, 2,048 x 80K keys 2.51 -> 2.30 ms; 256 for a
+    // full batch of small leaves (0.709 vs 0.697 ms at 100M keys)
+    const dim3 pg(n_segs * place_parts);
+    if (n_segs <= kVqfRingMaxSegs || max_blocks > 512)
+      hipLaunchKernelGGL(vqf_place_fused<512>, pg, dim3(512), fused_lds, s, d_segs, d_ws, ws_bytes,
+                         n_segs, d_out, place_parts, place_span);
+    else
+      hipLaunchKernelGGL(vqf_place_fused<256>, pg, dim3(256), fused_lds, s, d_segs, d_ws, ws_bytes,
+                         n_segs, d_out, place_parts, place_span);
   } else {
     if (n_keys)
       hipLaunchKernelGGL(vqf_scatter, dim3((uint32_t)div_up(n_keys, 256)), dim3(256), 0, s,
