@@ -23,6 +23,10 @@ def main():
     ap.add_argument("--leaves", default="1,8,64,256,512,1024")
     ap.add_argument("--reps", type=int, default=50)
     ap.add_argument("--leaf-keys", type=int, default=16384)
+    ap.add_argument("--key-bytes", type=int, default=16,
+                    help="16 (splitmix keys, sorted per leaf for VQF), 24 (random 24-byte keys) or "
+                         "0 (variable length, 8-31 bytes through an offsets array); the last two "
+                         "in generation order")
     ap.add_argument("--cap", type=int, default=0,
                     help="VQF payload capacity (default: the TreeOptions filter page at --bpk)")
     ap.add_argument("--no-ws", action="store_true",
@@ -34,10 +38,25 @@ def main():
     S = a.leaf_keys
     for L in [int(x) for x in a.leaves.split(",")]:
         counts = [S] * L
-        keys = amq.gen_keys16(42, 0, S * L)
-        if a.kind == 1:
-            keys = sort_segments_device(torch, keys, counts)
-        kb = amq.KeyBatch.fixed(keys)
+        if a.key_bytes == 16:
+            keys = amq.gen_keys16(42, 0, S * L)
+            if a.kind == 1:
+                keys = sort_segments_device(torch, keys, counts)
+            kb = amq.KeyBatch.fixed(keys)
+        elif a.key_bytes == 0:
+            g = torch.Generator(device="cuda")
+            g.manual_seed(42)
+            lens = torch.randint(8, 32, (S * L,), dtype=torch.int64, device="cuda", generator=g)
+            offs = torch.zeros(S * L + 1, dtype=torch.int64, device="cuda")
+            torch.cumsum(lens, 0, out=offs[1:])
+            blob = torch.randint(0, 256, (int(offs[-1].item()),), dtype=torch.uint8, device="cuda",
+                                 generator=g)
+            kb = amq.KeyBatch.variable(blob, offs)
+        else:
+            g = torch.Generator(device="cuda")
+            g.manual_seed(42)
+            kb = amq.KeyBatch.fixed(torch.randint(0, 256, (S * L, a.key_bytes), dtype=torch.uint8,
+                                                  device="cuda", generator=g))
         plan = amq.plan_filters(a.kind, counts, bpk, payload_capacity=cap)
         out = torch.empty(plan.total_out_bytes, dtype=torch.uint8, device="cuda")
         ws = torch.empty(max(plan.workspace_bytes, 1), dtype=torch.uint8, device="cuda")
@@ -62,7 +81,7 @@ def main():
             e1.record()
         torch.cuda.synchronize()
         ms = float(np.median([e0.elapsed_time(e1) for e0, e1 in ev]))
-        print(f"kind {a.kind} leaves {L:5d} keys {S * L:9d} median {ms * 1e3:8.1f} us "
+        print(f"kind {a.kind} kb {a.key_bytes:2d} leaves {L:5d} keys {S * L:9d} median {ms * 1e3:8.1f} us "
               f"{S * L / ms / 1e3:9.1f} Mkeys/s ws {plan.workspace_bytes}", flush=True)
 
 

@@ -1779,7 +1779,7 @@ __global__ __launch_bounds__(64) void vqf_decide(const uint8_t* __restrict__ key
 // chunk + 1); the decider frees a slot once its words are in registers.  LDS operations of
 // a CU take effect in issue order per wave, so a decider that sees the ready word written
 // after the slot's words reads those words.  ~70 KB of LDS: two workgroups per CU.
-// A leaf with more than kRingMaxBlocks blocks runs vqf_decide_body in wave 0.
+// A batch with a leaf of more than kRingMaxBlocks blocks takes vqf_decide instead.
 // Same decisions, same key records as vqf_decide (test_gpu_parity: small and large batches).
 constexpr uint32_t kRingThreads = 512;
 constexpr uint32_t kRingProducers = kRingThreads / 64 - 1;
@@ -1790,8 +1790,8 @@ constexpr uint32_t kRingMaxBlocks = 2048;
 constexpr uint32_t kRingLdsBytes = kRingSlots * kRingSlotWords * 8 + 4 * kRingSlots + 8 +
                                    4 * kRingMaxBlocks;
 constexpr uint32_t kVqfRingMaxSegs = 768;
+constexpr uint32_t kVqfRingMaxSegsOther = 4096;  // keys other than 16 bytes (tkv_amq_build)
 static_assert(kRingLdsBytes <= 160 * 1024 / 3, "three workgroups per CU");
-// (a batch with a leaf beyond kRingMaxBlocks is launched with the LDS vqf_decide_body needs)
 
 // Ring hand-off words: relaxed workgroup-scope atomics, so they stay LDS operations (a
 // volatile access through a generic pointer is compiled as a system-coherent flat access).
@@ -1881,6 +1881,12 @@ __device__ void vqf_ring_produce(const uint8_t* __restrict__ keys, const uint64_
   };
   if (w >= n_chunks) return;
   uint4 kv0 = make_uint4(0, 0, 0, 0), kv1 = kv0, kv2 = kv0;
+  if constexpr (MODE != kKey16) {
+    // other key shapes are read where they are hashed: no buffers to rotate, and one copy of
+    // the (long) hash code keeps the kernel at three workgroups per CU
+    for (uint32_t q = w; q < n_chunks; q += kStep) produce(q, kv0);
+    return;
+  }
   load(w, kv0);
   load(w + kStep, kv1);
   load(w + 2 * kStep, kv2);
@@ -2046,15 +2052,8 @@ __global__ __launch_bounds__(kRingThreads) void vqf_decide_ring(
   const VqfWorkspace ws = vqf_workspace(ws_base, n_segs);
   if (!vqf_ws_ok(segs, n_segs, ws_bytes, ws)) return;
   uint64_t* recs = vqf_records(ws, segs, n_segs);
-  const uint32_t nb = sg.n_blocks;
-  if (nb > kRingMaxBlocks) {
-    if (threadIdx.x >= 64) return;
-    if (sg.tag_bits == 8)
-      vqf_decide_dispatch<8, MODE>(keys, offs, stride, sg, blockIdx.x, ws, recs, s_ring, match_lds, compact_ok);
-    else if (sg.tag_bits == 16)
-      vqf_decide_dispatch<16, MODE>(keys, offs, stride, sg, blockIdx.x, ws, recs, s_ring, match_lds, compact_ok);
-    return;
-  }
+  const uint32_t nb = sg.n_blocks;  // <= kRingMaxBlocks (tkv_amq_build)
+  (void)match_lds;
   // compact records exactly where vqf_decide_dispatch writes them
   if (sg.tag_bits == 8) {
     if (nb <= 512 && compact_ok)
@@ -3398,7 +3397,15 @@ int tkv_amq_build(int kind, const uint8_t* keys, const uint64_t* offs, uint32_t 
   const bool fused = place_parts <= kFusedMaxParts;  // compact records are read only there
   const int flags = match_lds | (fused ? 2 : 0);
   const size_t lds = 4ull * ((max_blocks + 1) & ~1u) + (match_lds ? 8ull * max_blocks : 0);
-  if (n_segs <= kVqfRingMaxSegs) {
+  // the ring kernel for small batches of leaves its count table holds (a batch with a larger
+  // leaf takes vqf_decide: the one-wave body inside the ring kernel set its registers, and so
+  // its workgroups per CU, for every batch).  Keys other than 16 bytes are read where they are
+  // hashed, which puts their load latency on vqf_decide's serial chain: the ring kernel, whose
+  // producers hash off the chain, stays faster up to ~4,096 leaves for them (1,024 leaves of
+  // 24-byte keys 0.47 -> 0.29 ms, variable-length 0.66 -> 0.38 ms; at 6,104 leaves vqf_decide
+  // wins, 1.25 vs 1.45 ms)
+  if (n_segs <= (mode == kKey16 ? kVqfRingMaxSegs : kVqfRingMaxSegsOther) &&
+      max_blocks <= kRingMaxBlocks) {
     static std::once_flag ring_attr[kMaxDevices];
     once_per_device(ring_attr, [] {
       for (const void* f : {reinterpret_cast<const void*>(&vqf_decide_ring<kKey16>),
