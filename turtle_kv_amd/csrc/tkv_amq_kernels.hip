@@ -1437,14 +1437,43 @@ __device__ inline uint32_t& vqf_count(VqfWorkspace ws, uint64_t block)
   return *reinterpret_cast<uint32_t*>(ws.temp + block * kVqfTempStride + kVqfCountByte);
 }
 
+// A key the VQF kernels load one or two chunks ahead of hashing it (16- and 24-byte keys;
+// other shapes are read where they are hashed)
+template <int MODE>
+struct VqfKeyBuf {
+  uint4 v;
+};
+template <>
+struct VqfKeyBuf<kKey24> {
+  uint64_t w[3];
+};
+template <int MODE>
+constexpr bool kVqfPrefetch = MODE == kKey16 || MODE == kKey24;
+
+template <int MODE>
+__device__ inline void vqf_load_key(const uint8_t* __restrict__ keys, uint64_t gi, VqfKeyBuf<MODE>& kb)
+{
+  if constexpr (MODE == kKey16) {
+    kb.v = reinterpret_cast<const uint4*>(keys)[gi];
+  } else if constexpr (MODE == kKey24) {
+    const uint64_t* p = reinterpret_cast<const uint64_t*>(keys) + 3 * gi;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) kb.w[i] = p[i];
+  }
+}
+
 template <int MODE>
 __device__ inline uint64_t vqf_key_hash(const uint8_t* __restrict__ keys,
                                         const uint64_t* __restrict__ offs, uint32_t stride,
-                                        uint64_t gi, const uint4& kv)
+                                        uint64_t gi, const VqfKeyBuf<MODE>& kb)
 {
   if constexpr (MODE == kKey16) {
+    const uint4 kv = kb.v;
     const Xxh16 x((uint64_t)kv.x | ((uint64_t)kv.y << 32), (uint64_t)kv.z | ((uint64_t)kv.w << 32));
     return x.finish(xxh16_rhinit(kVqfHashSeed));
+  } else if constexpr (MODE == kKey24) {
+    const XxhFixed<24> x(kb.w);
+    return x.finish(xxh_fixed_rc<24>(kVqfHashSeed));
   } else {
     return hash_key<MODE>(keys, offs, stride, gi, kVqfHashSeed);
   }
@@ -1516,7 +1545,7 @@ __device__ void vqf_decide_body(const uint8_t* __restrict__ keys, const uint64_t
   const uint64_t lt = lanemask_lt();
   using Rec = typename std::conditional<kCompact, uint32_t, uint64_t>::type;
   Rec* rec = reinterpret_cast<Rec*>(recs + sg.key_begin);
-  const uint4* kp = reinterpret_cast<const uint4*>(keys) + sg.key_begin;
+  using KB = VqfKeyBuf<MODE>;
 
   unsigned long long* mt = reinterpret_cast<unsigned long long*>(cnt + ((nb + 1) & ~1u));
   for (uint32_t b = lane; b < nb; b += 64) {
@@ -1547,17 +1576,17 @@ __device__ void vqf_decide_body(const uint8_t* __restrict__ keys, const uint64_t
   Rec* const sink = reinterpret_cast<Rec*>(ws.sink);
   Rec* pend_ptr = sink;
   Rec pend_val = 0;
-  auto step = [&](uint32_t base, VqfLoc& cur, const uint4& kv_hash, uint4& kv_load) {
+  auto step = [&](uint32_t base, VqfLoc& cur, const KB& kv_hash, KB& kv_load) {
     const VqfLoc L = cur;
     // primary block counts before this chunk (every lane reads: an invalid lane's block is 0)
     const uint32_t cnt_p = cnt[L.pb];
     const uint32_t inext = base + 64 + lane;
     const bool vnext = inext < n;
     uint64_t hn;
-    if constexpr (MODE == kKey16) {
+    if constexpr (kVqfPrefetch<MODE>) {
       // branch-free (clamped index, select on the result): straight-line code lets the
       // compiler count vmcnt exactly instead of draining every outstanding access
-      kv_load = kp[min(inext + 64, n - 1)];
+      vqf_load_key<MODE>(keys, sg.key_begin + min(inext + 64, n - 1), kv_load);
       *pend_ptr = pend_val;
       const uint64_t hh = vqf_key_hash<MODE>(keys, offs, stride, 0, kv_hash);
       hn = vnext ? hh : 0;
@@ -1695,11 +1724,11 @@ __device__ void vqf_decide_body(const uint8_t* __restrict__ keys, const uint64_t
     atomicAdd(cnt + chosen, L.kept ? 1u : 0u);
   };
 
-  uint4 kv0 = {0, 0, 0, 0}, kvA = {0, 0, 0, 0}, kvB = {0, 0, 0, 0};
-  if constexpr (MODE == kKey16) {
+  KB kv0{}, kvA{}, kvB{};
+  if constexpr (kVqfPrefetch<MODE>) {
     if (n > 0) {
-      kv0 = kp[min(lane, n - 1)];
-      kvA = kp[min(lane + 64, n - 1)];
+      vqf_load_key<MODE>(keys, sg.key_begin + min(lane, n - 1), kv0);
+      vqf_load_key<MODE>(keys, sg.key_begin + min(lane + 64, n - 1), kvA);
     }
   }
   VqfLoc cur = vqf_locate<T>(lane < n ? vqf_key_hash<MODE>(keys, offs, stride, sg.key_begin + lane, kv0) : 0,
@@ -1824,14 +1853,14 @@ __device__ void vqf_ring_produce(const uint8_t* __restrict__ keys, const uint64_
   const uint64_t R = (uint64_t)nb * C::kBuckets;
   const uint64_t magic = sg.mod_magic;
   const uint64_t mask = ~0ull << sg.hash_val_shift;  // filter_builder.hpp:187
-  const uint4* kp = reinterpret_cast<const uint4*>(keys) + sg.key_begin;
+  using KB = VqfKeyBuf<MODE>;
   // a producer's next three chunks of keys are in flight (one chunk's load latency is longer
   // than the time to produce it); the loop is unrolled by three so the buffers rotate
   constexpr uint32_t kDepth = 3, kStep = kRingProducers;
-  auto load = [&](uint32_t q, uint4& kv) {  // clamped, not skipped: a fixed count in flight
-    if constexpr (MODE == kKey16) kv = kp[min(q * 64 + lane, n - 1)];
+  auto load = [&](uint32_t q, KB& kv) {  // clamped, not skipped: a fixed count in flight
+    if constexpr (kVqfPrefetch<MODE>) vqf_load_key<MODE>(keys, sg.key_begin + min(q * 64 + lane, n - 1), kv);
   };
-  auto produce = [&](uint32_t q, uint4& kv) {
+  auto produce = [&](uint32_t q, KB& kv) {
     const uint32_t i = q * 64 + lane;
     const bool valid = i < n;
     const uint64_t h = valid ? vqf_key_hash<MODE>(keys, offs, stride, sg.key_begin + i, kv) : 0;
@@ -1880,8 +1909,8 @@ __device__ void vqf_ring_produce(const uint8_t* __restrict__ keys, const uint64_
     if (lane == 0) lds_store_relaxed(ready + q % kRingSlots, q + 1);
   };
   if (w >= n_chunks) return;
-  uint4 kv0 = make_uint4(0, 0, 0, 0), kv1 = kv0, kv2 = kv0;
-  if constexpr (MODE != kKey16) {
+  KB kv0{}, kv1{}, kv2{};
+  if constexpr (!kVqfPrefetch<MODE>) {
     // other key shapes are read where they are hashed: no buffers to rotate, and one copy of
     // the (long) hash code keeps the kernel at three workgroups per CU
     for (uint32_t q = w; q < n_chunks; q += kStep) produce(q, kv0);
@@ -3404,19 +3433,27 @@ int tkv_amq_build(int kind, const uint8_t* keys, const uint64_t* offs, uint32_t 
   // producers hash off the chain, stays faster up to ~4,096 leaves for them (1,024 leaves of
   // 24-byte keys 0.47 -> 0.29 ms, variable-length 0.66 -> 0.38 ms; at 6,104 leaves vqf_decide
   // wins, 1.25 vs 1.45 ms)
-  if (n_segs <= (mode == kKey16 ? kVqfRingMaxSegs : kVqfRingMaxSegsOther) &&
+  // 24-byte keys (TurtleKV's default key size hint), 8-byte aligned, are loaded ahead of
+  // their hash like 16-byte ones
+  const int vmode = build_key_mode(keys, offs, stride);
+  const bool prefetched = vmode == kKey16 || vmode == kKey24;
+  if (n_segs <= (prefetched ? kVqfRingMaxSegs : kVqfRingMaxSegsOther) &&
       max_blocks <= kRingMaxBlocks) {
     static std::once_flag ring_attr[kMaxDevices];
     once_per_device(ring_attr, [] {
       for (const void* f : {reinterpret_cast<const void*>(&vqf_decide_ring<kKey16>),
+                            reinterpret_cast<const void*>(&vqf_decide_ring<kKey24>),
                             reinterpret_cast<const void*>(&vqf_decide_ring<kKeyFixed>),
                             reinterpret_cast<const void*>(&vqf_decide_ring<kKeyVar>)})
         (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     });
     const dim3 g(n_segs), b(kRingThreads);
     const size_t rl = lds > kRingLdsBytes ? lds : kRingLdsBytes;
-    if (mode == kKey16)
+    if (vmode == kKey16)
       hipLaunchKernelGGL(vqf_decide_ring<kKey16>, g, b, rl, s, keys, offs, stride, d_segs, d_ws,
+                         ws_bytes, n_segs, flags);
+    else if (vmode == kKey24)
+      hipLaunchKernelGGL(vqf_decide_ring<kKey24>, g, b, rl, s, keys, offs, stride, d_segs, d_ws,
                          ws_bytes, n_segs, flags);
     else if (mode == kKeyFixed)
       hipLaunchKernelGGL(vqf_decide_ring<kKeyFixed>, g, b, rl, s, keys, offs, stride, d_segs, d_ws,
@@ -3424,8 +3461,11 @@ int tkv_amq_build(int kind, const uint8_t* keys, const uint64_t* offs, uint32_t 
     else
       hipLaunchKernelGGL(vqf_decide_ring<kKeyVar>, g, b, rl, s, keys, offs, stride, d_segs, d_ws,
                          ws_bytes, n_segs, flags);
-  } else if (mode == kKey16)
+  } else if (vmode == kKey16)
     hipLaunchKernelGGL(vqf_decide<kKey16>, dim3(n_segs), dim3(64), lds, s, keys, offs, stride,
+                       d_segs, d_ws, ws_bytes, n_segs, flags);
+  else if (vmode == kKey24)
+    hipLaunchKernelGGL(vqf_decide<kKey24>, dim3(n_segs), dim3(64), lds, s, keys, offs, stride,
                        d_segs, d_ws, ws_bytes, n_segs, flags);
   else if (mode == kKeyFixed)
     hipLaunchKernelGGL(vqf_decide<kKeyFixed>, dim3(n_segs), dim3(64), lds, s, keys, offs, stride,
