@@ -2,8 +2,8 @@
 16-byte keys @ 10 bits/key, bit-exact).
 
   python bench.py [--gpus N] [--steps K] [--warmup W]
-                  [--workload bloom10|bloom12|vqf12|probe10|probe_vqf12|bloom10k24|bloom10var|
-                              bloom10mono|bloom12hash] [--total-keys T]
+                  [--workload bloom10|bloom12|vqf12|probe10|probe_vqf12|bloom10k24|vqf12k24|
+                              bloom10var|bloom10mono|bloom12hash] [--total-keys T]
 
 One step = one pass of the hot path over one batch: build every leaf filter of
 `--keys-per-gpu` (default 100M, BASELINE config 2) 16-byte keys held in HBM, S = 16,384 keys
@@ -51,6 +51,7 @@ WORKLOADS = {
     "probe10": (0, 10, "Bloom @10 probe, 50% hits"),
     "probe_vqf12": (1, 12, "VQF @12 probe, 50% hits"),
     "bloom10k24": (0, 10, "Bloom @10 bits/key, 24-byte keys (TurtleKV default key size)"),
+    "vqf12k24": (1, 12, "VQF @12 bits/key, 24-byte keys (TurtleKV default key size) in generation order"),
     "bloom10mono": (0, 10, "Bloom @10 bits/key, one monolithic filter per GPU"),
     "bloom10var": (0, 10, "Bloom @10 bits/key, variable-length keys (8-31 B)"),
     "bloom12hash": (0, 12, "Bloom @12 bits/key, one filter over all GPUs' keys, hash-range sharded"),
@@ -61,7 +62,7 @@ HASH_SHARDED = {"bloom12hash"}
 # workloads whose one filter spans every key of the GPU (the monolithic
 # single-filter Bloom variant)
 MONOLITHIC = {"bloom10mono"}
-KEY_BYTES = {"bloom10k24": 24, "bloom10var": 0}  # 0: variable length (offsets)
+KEY_BYTES = {"bloom10k24": 24, "vqf12k24": 24, "bloom10var": 0}  # 0: variable length (offsets)
 SWEEP_LEAVES = (64, 256, 1024)                   # + the whole batch
 
 
@@ -295,8 +296,10 @@ def main():
         g = torch.Generator(device=dev)
         g.manual_seed(42 + rank)
         keys = torch.randint(0, 256, (n, key_bytes), dtype=torch.uint8, device=dev, generator=g)
-    if kind == 1:
+    if kind == 1 and key_bytes == 16:
         # VQF inserts in leaf key order: sort each leaf's keys (memcmp order) on the device
+        # (other key shapes are inserted in generation order: the same work, and the oracle
+        # check below inserts them in the same order)
         keys = sort_segments_device(torch, keys, counts)
     kb = amq.KeyBatch.variable(keys, offsets) if offsets is not None else amq.KeyBatch.fixed(keys)
     # zeroed once: the build never writes past a leaf's payload, so the slack bytes of every

@@ -20,6 +20,7 @@ if has bench; then
   timeout -k 10 300 python bench.py --workload probe_vqf12 > $O/bench_probe_vqf12.log 2>&1 || exit 6
   timeout -k 10 300 python bench.py --workload bloom12 --no-e2e > $O/bench_bloom12.log 2>&1 || exit 7
   timeout -k 10 300 python bench.py --workload bloom10k24 > $O/bench_bloom10k24.log 2>&1 || exit 8
+  timeout -k 10 300 python bench.py --workload vqf12k24 > $O/bench_vqf12k24.log 2>&1 || exit 8
   timeout -k 10 300 python bench.py --workload bloom12 --total-keys 1000000000 --steps 10 --no-e2e > $O/bench_bloom12_1B.log 2>&1 || exit 9
   timeout -k 10 300 python bench.py --workload bloom10mono > $O/bench_bloom10mono.log 2>&1 || exit 10
   timeout -k 10 300 python bench.py --workload bloom10var --no-e2e > $O/bench_bloom10var.log 2>&1 || exit 10
