@@ -115,6 +115,9 @@ def _free_port():
 def launch_ranks(n: int) -> int:
     """One child process per rank, as torch.distributed.run would start them; rank 0's
     stdout carries the JSON line.  Returns the first non-zero exit code, else 0."""
+    # build the library once here (hipcc only, no GPU), not in N ranks at once
+    from turtle_kv_amd import _build
+    _build.build()
     port = _free_port()
     procs = []
     for r in range(n):
@@ -246,7 +249,10 @@ def main():
     local = local % max(1, n_dev)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    # a process group whenever ranks exist: N > 1, or one rank under a launcher
+    # (torch.distributed.run --nproc-per-node 1: the RCCL code path at world size 1)
+    pg = world > 1 or "LOCAL_RANK" in os.environ
+    if pg:
         if args.backend == "nccl":
             # the communicator is bound to this rank's device (RCCL over xGMI)
             dist.init_process_group("nccl", device_id=dev)
@@ -254,7 +260,7 @@ def main():
             dist.init_process_group(args.backend)
     kind, bpk, label = WORKLOADS[args.workload]
     if args.workload in HASH_SHARDED:
-        return bench_hash_sharded(args, torch, dist, amq, world, rank, dev, bpk, label)
+        return bench_hash_sharded(args, torch, dist, amq, world, rank, dev, bpk, label, pg)
     # the VQF payload capacity is the default TreeOptions' filter page at this bits/key
     # (tree/tree_options.hpp:177-220): 32 KiB pages, 32,704 payload bytes at 12 bits/key
     cap = (amq.TreeOptions(kind).set_filter_bits_per_key(bpk).filter_page_payload_size()
@@ -307,7 +313,7 @@ def main():
     out = torch.zeros(plan.total_out_bytes, dtype=torch.uint8, device=dev)
     ws = torch.empty(max(plan.workspace_bytes, 1), dtype=torch.uint8, device=dev)
     gathered = (torch.empty(plan.total_out_bytes * world, dtype=torch.uint8, device=dev)
-                if world > 1 else None)
+                if pg else None)
 
     probe = args.workload.startswith("probe")
     if probe:
@@ -323,7 +329,7 @@ def main():
             amq.probe_filters(plan, out, qb, qseg, out=res)
         else:
             amq.build_all_filters(plan, kb, out=out, workspace=ws, check=False)
-        if args.allgather and world > 1:
+        if args.allgather and pg:
             tdist.allgather_filters(out, gathered)
 
     # clock ramp (untimed): a 1 ms step from an idle GPU runs ~15% below the steady clock
@@ -344,7 +350,8 @@ def main():
 
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(args.steps)]
-    if world > 1:
+    coll_dev = dev if args.backend == "nccl" else "cpu"
+    if pg:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -353,14 +360,11 @@ def main():
         step()
         ev[i][1].record(stream)
     torch.cuda.synchronize()
-    if world > 1:
+    if pg:
         dist.barrier()
     wall = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([wall], dtype=torch.float64,
-                         device=dev if args.backend == "nccl" else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        wall = float(t.item())
+    if pg:
+        wall = reduce_max(torch, dist, wall, coll_dev)
     kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
 
     units = 2 * total_keys if probe else total_keys
@@ -380,9 +384,8 @@ def main():
             verified = verify_sample(torch, kind, bpk, cap, plan, keys, offsets, out, key_bytes,
                                      shard, rank, leaf_keys)
             ok = verified["ok"]
-        if world > 1:
-            flag = torch.tensor([1 if ok else 0], dtype=torch.int32,
-                                device=dev if args.backend == "nccl" else "cpu")
+        if pg:
+            flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=coll_dev)
             dist.all_reduce(flag, op=dist.ReduceOp.MIN)
             ok = bool(flag.item())
             if verified is not None:
@@ -407,16 +410,7 @@ def main():
     achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
     prof = load_profile(args.workload)
     traffic = prof.get("hbm_bytes_per_launch")
-    valu_roof = None
-    if prof.get("valu_instr_per_key") and not probe:
-        # the bound this kernel actually sits on: integer VALU issue
-        wave_instr = prof["valu_instr_per_key"] * n / 64
-        ach = wave_instr / (kernel_ms * 1e-3) / 1e9
-        peak = prof.get("valu_peak_ginstr_s_at_2.4GHz", 614.4)
-        valu_roof = {"achieved": round(ach, 1), "peak": peak, "unit": "G wave64-VALU-instr/s",
-                     "frac": round(ach / peak, 4), "instr_per_key": prof["valu_instr_per_key"],
-                     "note": "PMC SQ_INSTS_VALU per key (profiles/traffic_*.json); peak = "
-                             "1024 SIMDs x 2.4 GHz / 4 cycles (tools/ubench_valu.hip)"}
+    valu_roof = valu_roofline(prof, n, kernel_ms) if not probe else None
 
     fabric_roof = None
     if probe and prof.get("TCC_EA0_RDREQ_per_launch"):
@@ -432,7 +426,7 @@ def main():
 
     allgather_ms = None
     gather_ok = None
-    if world > 1:
+    if pg:
         if not args.allgather:
             torch.cuda.synchronize()
             dist.barrier()
@@ -440,7 +434,7 @@ def main():
             for _ in range(3):
                 tdist.allgather_filters(out, gathered)
             torch.cuda.synchronize()
-            allgather_ms = (time.perf_counter() - g0) / 3 * 1e3
+            allgather_ms = reduce_max(torch, dist, (time.perf_counter() - g0) / 3 * 1e3, coll_dev)
         else:
             tdist.allgather_filters(out, gathered)
         if rank == 0 and not args.no_verify and not probe:
@@ -452,21 +446,31 @@ def main():
             args.workload not in MONOLITHIC and len(counts) > SWEEP_LEAVES[0]:
         sweep = batch_sweep(torch, amq, kind, bpk, cap, counts, kb, ws, plan, kernel_ms)
 
+    # the north star's host leg on EVERY rank at once: each GPU's pages go back to host page
+    # memory over its own PCIe link (tree/tree_serialize_context.cpp:62-115); the aggregate is
+    # all ranks' keys over the slowest rank's time
     e2e = None
-    if (rank == 0 and world == 1 and not args.no_e2e and not probe and key_bytes == 16
-            and n <= 200_000_000 and args.workload not in MONOLITHIC):
-        e2e = end_to_end(torch, amq, kind, bpk, cap, counts, keys)
+    if (not args.no_e2e and not probe and key_bytes == 16 and n <= 200_000_000
+            and args.workload not in MONOLITHIC):
+        sync = (lambda: dist.barrier()) if pg else (lambda: None)
+        red = (lambda x: reduce_max(torch, dist, x, coll_dev)) if pg else (lambda x: x)
+        e2e = end_to_end(torch, amq, kind, bpk, cap, counts, keys, sync=sync, reduce_max=red,
+                         total_keys=total_keys, world=world)
 
-    if world > 1:
+    if pg:
         dist.barrier()
     if rank != 0:
         dist.destroy_process_group()
         return
+    if pg:
+        # every other rank has left its last collective: the CPU baseline below runs on a host
+        # whose other ranks are gone (no rank spinning in a barrier beside it)
+        dist.destroy_process_group()
 
     base = None
     cores, _ = host_cpu_share()
     threads = args.cpu_threads or cores
-    if world == 1 and not args.no_cpu_baseline:
+    if not args.no_cpu_baseline:
         if probe:
             base = probe_check.get("cpu_baseline") if probe_check else None
         elif key_bytes == 16:
@@ -476,6 +480,9 @@ def main():
             base = cpu_baseline(kind, bpk, cap, keys[:nk_host].cpu().numpy(),
                                 counts[:lim] if n > 100_000_000 else counts,
                                 threads, leaf_keys)
+            if world > 1:
+                base["note"] = (f"rank 0's keys (the same leaves every rank builds), timed on rank "
+                                f"0's host after the other {world - 1} ranks exited")
 
     kdesc = f"{key_bytes}B" if key_bytes else "8-31B (mean %.1f B)" % (keys.numel() / max(n, 1))
     line = {
@@ -501,7 +508,7 @@ def main():
                    "filter": "bloom-blocked512" if kind == 0 else "vqf",
                    "payload_capacity": cap or None,
                    "parallelism": f"leaf-sharded x{world}",
-                   "backend": args.backend if world > 1 else None},
+                   "backend": args.backend if pg else None},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "kernel_ms": round(kernel_ms, 4),
@@ -517,6 +524,7 @@ def main():
         line["fabric_roofline"] = fabric_roof
     if allgather_ms is not None:
         line["allgather_ms"] = round(allgather_ms, 3)
+        line["allgather_bytes_in_per_gpu"] = (world - 1) * plan.total_out_bytes
         line["build_plus_allgather_mkeys_s"] = round(units / ((ms_per_step + allgather_ms) * 1e-3) / 1e6, 2)
     if gather_ok is not None:
         line["gather_verified"] = gather_ok
@@ -531,14 +539,36 @@ def main():
             line["probe"].update({k: v for k, v in probe_check.items() if k != "cpu_baseline"})
             line["verified"] = probe_check["results_equal_oracle"]
     print(json.dumps(line), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+
+
+def reduce_max(torch, dist, x, device):
+    """max over ranks of one float (a tensor on the rank's device for RCCL, host for gloo)"""
+    t = torch.tensor([float(x)], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def valu_roofline(prof, n_keys, kernel_ms):
+    """The bound a build kernel actually sits on: integer VALU issue,
+    from the PMC counters of profiles/traffic_<workload>.json."""
+    if not prof.get("valu_instr_per_key"):
+        return None
+    wave_instr = prof["valu_instr_per_key"] * n_keys / 64
+    ach = wave_instr / (kernel_ms * 1e-3) / 1e9
+    peak = prof.get("valu_peak_ginstr_s", prof.get("valu_peak_ginstr_s_at_2.4GHz", 614.4))
+    r = {"achieved": round(ach, 1), "peak": peak, "unit": "G wave64-VALU-instr/s",
+         "frac": round(ach / peak, 4), "instr_per_key": prof["valu_instr_per_key"],
+         "note": prof.get("valu_peak_note", "PMC SQ_INSTS_VALU per key (profiles/traffic_*.json); "
+                                            "peak = 1024 SIMDs x 2.4 GHz / 4 cycles")}
+    if prof.get("valu_busy_frac") is not None:
+        r["valu_busy_frac_pmc"] = prof["valu_busy_frac"]
+    return r
 
 
 # ---------------------------------------------------------------------------------------
 # hash-range sharded monolithic Bloom (BASELINE config 5 read literally)
 # ---------------------------------------------------------------------------------------
-def bench_hash_sharded(args, torch, dist, amq, world, rank, dev, bpk, label):
+def bench_hash_sharded(args, torch, dist, amq, world, rank, dev, bpk, label, pg=False):
     """One Bloom filter over every rank's keys; rank r owns a contiguous byte range of its
     bitmap.  A step = route (tkv_amq_bloom_route) + all-to-all of the keys (RCCL) + the rank's
     range build (tkv_amq_bloom_build_range); the all-gather of the ranges is timed separately
@@ -553,7 +583,7 @@ def bench_hash_sharded(args, torch, dist, amq, world, rank, dev, bpk, label):
 
     def step():
         hs.local_build(keys)
-        if args.allgather and world > 1:
+        if args.allgather and pg:
             hs.allgather()
 
     ramp0 = time.perf_counter()
@@ -565,25 +595,24 @@ def bench_hash_sharded(args, torch, dist, amq, world, rank, dev, bpk, label):
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    if world > 1:
+    coll_dev = dev if args.backend == "nccl" else "cpu"
+    if pg:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
     torch.cuda.synchronize()
-    if world > 1:
+    if pg:
         dist.barrier()
     wall = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([wall], dtype=torch.float64, device=dev if args.backend == "nccl" else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        wall = float(t.item())
+    if pg:
+        wall = reduce_max(torch, dist, wall, coll_dev)
 
     # untimed breakdown of one step on this rank (HIP events on the current stream)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
     ev[0].record()
-    if world > 1:
+    if pg:
         routed, sc = hs.route(keys)
         ev[1].record()
         owned = hs.exchange(routed, sc)
@@ -598,13 +627,13 @@ def bench_hash_sharded(args, torch, dist, amq, world, rank, dev, bpk, label):
     n_owned = int(owned.shape[0])
 
     allgather_ms = None
-    if world > 1:
+    if pg:
         dist.barrier()
         g0 = time.perf_counter()
         for _ in range(3):
             hs.allgather()
         torch.cuda.synchronize()
-        allgather_ms = (time.perf_counter() - g0) / 3 * 1e3
+        allgather_ms = reduce_max(torch, dist, (time.perf_counter() - g0) / 3 * 1e3, coll_dev)
     filt = hs.allgather()
     torch.cuda.synchronize()
 
@@ -621,20 +650,25 @@ def bench_hash_sharded(args, torch, dist, amq, world, rank, dev, bpk, label):
             st, oref = O.bloom_build(O.gen_keys16(42, 0, total), total, bpk, src_page_id=0)
             check["equal_to_oracle"] = st == 0 and oref.tobytes() == filt.cpu().numpy().tobytes()
         check["ok"] = all(v for k, v in check.items())
-    if world > 1:
+    if pg:
         flag = torch.tensor([1 if (check is None or check["ok"]) else 0], dtype=torch.int32,
-                            device=dev if args.backend == "nccl" else "cpu")
+                            device=coll_dev)
         dist.all_reduce(flag, op=dist.ReduceOp.MIN)
         ok = bool(flag.item())
     else:
         ok = check is None or check["ok"]
     if not ok:
         raise SystemExit(f"bench.py: hash-sharded filter differs: {check}")
-    if world > 1:
+    if pg:
         dist.barrier()
     if rank != 0:
         dist.destroy_process_group()
         return
+    if pg:
+        dist.destroy_process_group()
+    base = None
+    if not args.no_cpu_baseline:
+        base = cpu_baseline_monolithic(bpk, min(total, 20_000_000))
     ms_per_step = wall / args.steps * 1e3
     value = total * args.steps / wall / 1e6
     alg = n_local * 16 + (int(hs.payload_bytes) - 64) // world  # keys in, this rank's bitmap out
@@ -649,13 +683,13 @@ def bench_hash_sharded(args, torch, dist, amq, world, rank, dev, bpk, label):
                    "keys_per_gpu": n_local, "total_keys": total, "key_bytes": 16,
                    "bits_per_key": bpk, "filter": "bloom-blocked512, monolithic",
                    "parallelism": f"hash-range-sharded x{world}",
-                   "backend": args.backend if world > 1 else None},
+                   "backend": args.backend if pg else None},
         "roofline": {"bound": "hbm", "achieved": round(alg / (ms_per_step * 1e-3) / 1e9, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(alg / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                      "traffic": None, "kernel_ms": round(build_ms, 4), "alg_bytes_per_launch": alg,
                      "note": "whole step on rank 0 (route + all-to-all + range build)"},
-        "cpu_baseline": None,
+        "cpu_baseline": base,
         "step_breakdown_rank0_ms": {"route": round(route_ms, 4), "all_to_all": round(a2a_ms, 4),
                                     "range_build": round(build_ms, 4), "keys_owned": n_owned},
         "verified": check["ok"] if check else None, "verify": check,
@@ -664,8 +698,23 @@ def bench_hash_sharded(args, torch, dist, amq, world, rank, dev, bpk, label):
         line["allgather_ms"] = round(allgather_ms, 3)
         line["build_plus_allgather_mkeys_s"] = round(total / ((ms_per_step + allgather_ms) * 1e-3) / 1e6, 2)
     print(json.dumps(line), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+
+
+def cpu_baseline_monolithic(bpk, n):
+    """One Bloom filter over n keys on one host thread: the reference builds each filter on
+    one thread (filter_builder.hpp:127, WorkerPool::null_pool()), so a single filter gets one
+    core whatever the host has."""
+    O, native, portable = _oracle_libs()
+    keys = O.gen_keys16(42, 0, n)
+    L = native or portable
+    t0 = time.perf_counter()
+    st, _ = O.bloom_build(keys, n, bpk, src_page_id=0, L=L)
+    dt = time.perf_counter() - t0
+    assert st == 0, st
+    return {"value": round(n / dt / 1e6, 2), "unit": "Mkeys/s", "cores": 1, "kind": "port",
+            "sample": f"one {n}-key Bloom filter @{bpk} bits/key, C oracle "
+                      f"({'-O3 -march=native -mbmi2 -mavx2' if native else '-O3 -march=x86-64-v3'}),"
+                      f" 1 thread (one filter per thread, as the reference), {dt:.2f} s wall"}
 
 
 # ---------------------------------------------------------------------------------------
@@ -899,40 +948,49 @@ def make_probe_queries(torch, amq, n, counts, dev, key_begin):
     return q, qs, is_hit
 
 
-def end_to_end(torch, amq, kind, bpk, cap, counts, keys, iters=3):
+def end_to_end(torch, amq, kind, bpk, cap, counts, keys, iters=3, sync=lambda: None,
+               reduce_max=lambda x: x, total_keys=None, world=1):
     """Keys from pinned host memory -> H2D -> build -> D2H into pinned host pages, through
-    turtle_kv_amd.filters.build_filters_from_host (chunked, three streams, overlapped)."""
+    turtle_kv_amd.filters.HostFilterPipeline (chunked, three streams, overlapped).  With
+    several ranks every rank runs its own leg at the same time (`sync` lines them up); the
+    rate is all ranks' keys over the slowest rank's time (`reduce_max`)."""
+    n = keys.shape[0]
+    total_keys = total_keys or n
     h_keys = torch.empty(keys.shape, dtype=torch.uint8, pin_memory=True)
     h_keys.copy_(keys)
     pipe = amq.filters.HostFilterPipeline(kind, counts, bpk, payload_capacity=cap)
     h_out = pipe.run(h_keys)
     torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for _ in range(iters):
         pipe.run(h_keys, h_out)
-    dt = (time.perf_counter() - t0) / iters
-    gbs = (keys.numel() + h_out.numel()) / dt / 1e9
-    res = {"mkeys_s": round(keys.shape[0] / dt / 1e6, 2), "ms_per_batch": round(dt * 1e3, 3),
-           "pcie_gb_s": round(gbs, 1),
+    dt_rank = (time.perf_counter() - t0) / iters
+    dt = reduce_max(dt_rank)
+    gbs = (keys.numel() + h_out.numel()) / dt_rank / 1e9
+    res = {"mkeys_s": round(total_keys / dt / 1e6, 2), "ms_per_batch": round(dt * 1e3, 3),
+           "pcie_gb_s_rank0": round(gbs, 1), "ranks": world,
            "note": "pinned host keys -> H2D -> build -> D2H filter pages; 8M-key chunks "
-                   "pipelined on three streams (HostFilterPipeline)"}
+                   "pipelined on three streams (HostFilterPipeline)"
+                   + ("; every rank at once over its own PCIe link, all ranks' keys / slowest rank"
+                      if world > 1 else "")}
     # the reference's input form: keys viewed inside edit records (EditView), gathered on the
     # host chunk by chunk (tkv_amq_stage_keys) ahead of each chunk's H2D copy
-    n = keys.shape[0]
     rec = np.empty((n, 32), dtype=np.uint8)          # [16-byte key | 16-byte value] per edit
     rec[:, :16] = h_keys.numpy()
     views = amq.key_views(rec, np.arange(n, dtype=np.uint64) * 32, 16)
     h_out2 = pipe.run_views(views)
     assert torch.equal(h_out2, h_out), "staged-from-views pages differ"
     torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for _ in range(iters):
         pipe.run_views(views, h_out2)
-    dt = (time.perf_counter() - t0) / iters
-    res["from_key_views"] = {"mkeys_s": round(n / dt / 1e6, 2), "ms_per_batch": round(dt * 1e3, 3),
+    dt = reduce_max((time.perf_counter() - t0) / iters)
+    res["from_key_views"] = {"mkeys_s": round(total_keys / dt / 1e6, 2), "ms_per_batch": round(dt * 1e3, 3),
                              "note": "keys viewed in 32-byte edit records, gathered by "
-                                     "tkv_amq_stage_keys (16 host threads) chunk by chunk, "
-                                     "overlapping the previous chunk's copies and build"}
+                                     "tkv_amq_stage_keys (16 host threads per rank) chunk by "
+                                     "chunk, overlapping the previous chunk's copies and build"}
     del rec, views
     return res
 

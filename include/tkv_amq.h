@@ -197,7 +197,9 @@ int tkv_amq_bloom_route(const uint8_t* d_keys16, uint64_t n_keys, const tkv_amq_
  * [tile_begin, tile_end) of the filter from the keys this rank received (all of whose tiles
  * must fall in the range; others are ignored) into d_out at the segment's out_offset, exactly
  * where tkv_amq_build puts them, and writes the filter header too.  Bytes of other tiles are
- * not touched, so the ranks' ranges are disjoint and one all-gather of them is the filter. */
+ * not touched, so the ranks' ranges are disjoint and one all-gather of them is the filter.
+ * An empty range (tile_begin == tile_end: a rank past the last tile when ceil(T/q) < ranks)
+ * writes the header only.  Keys are 16 bytes (route and range build alike). */
 uint64_t tkv_amq_bloom_build_range_ws_bytes(uint64_t n_keys, uint32_t tile_begin, uint32_t tile_end);
 int tkv_amq_bloom_build_range(const uint8_t* d_keys16, uint64_t n_keys, const tkv_amq_segment* d_seg,
                               uint32_t n_blocks, uint32_t tile_begin, uint32_t tile_end,

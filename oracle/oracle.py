@@ -134,10 +134,12 @@ def sort_segments(keys: np.ndarray, seg_begin: np.ndarray, n_threads: int = 8) -
     lib().tkvo_sort_keys16_segments(_p(keys), _p(seg_begin), len(seg_begin) - 1, n_threads)
 
 
-def bloom_build(keys, n: int, bpk: int, src_page_id: int = 0, offsets=None, stride: int = 16):
-    cap = lib().tkvo_bloom_payload_size(n, bpk)
+def bloom_build(keys, n: int, bpk: int, src_page_id: int = 0, offsets=None, stride: int = 16,
+                L=None):
+    L = L or lib()
+    cap = L.tkvo_bloom_payload_size(n, bpk)
     out = np.zeros(cap, dtype=np.uint8)
-    st = lib().tkvo_bloom_build_payload(_p(keys), _p(offsets), stride, n, bpk, src_page_id,
+    st = L.tkvo_bloom_build_payload(_p(keys), _p(offsets), stride, n, bpk, src_page_id,
                                        _p(out), cap)
     return st, out
 

@@ -92,14 +92,24 @@ def test_shard_ranges_cover_all_leaves():
 
 def test_hash_shard_tiles_cover_the_filter():
     """Hash-range sharding (config 5 read literally): the ranks' tile ranges are contiguous,
-    disjoint and cover every tile; a filter with fewer tiles than ranks is refused."""
+    disjoint and cover every tile.  With ceil(T/q) < ranks the last ranks own an empty range
+    (T = 17 over 8 ranks: q = 3, ranks 6 and 7; 3 tiles over 8 ranks: ranks 3-7): they are
+    accepted, and their range build writes the header only (GPU test
+    test_gpu_hash_shard.py::test_empty_ranges_write_the_header)."""
     from turtle_kv_amd import abi
     from turtle_kv_amd.dist import HashShardedBloom, hash_shard_tiles
-    for nb, world in [(1, 1), (1024, 1), (1025, 2), (93750, 8), (2_343_750, 8), (29297, 8)]:
+    for nb, world in [(1, 1), (1024, 1), (1025, 2), (93750, 8), (2_343_750, 8), (29297, 8),
+                      (17 * 1024, 8), (3000, 8)]:
         T, q = hash_shard_tiles(nb, world)
         assert T == -(-nb // 1024)
         ranges = [(min(T, r * q), min(T, (r + 1) * q)) for r in range(world)]
         assert ranges[0][0] == 0 and ranges[-1][1] == T
         assert all(a[1] == b[0] for a, b in zip(ranges, ranges[1:]))
+    T, q = hash_shard_tiles(17 * 1024, 8)
+    assert (T, q) == (17, 3)
+    empty = [r for r in range(8) if min(T, r * q) == min(T, (r + 1) * q)]
+    assert empty == [6, 7]
+    hs = HashShardedBloom(100_000, 12, 8, 5, "cpu")   # 3 tiles over 8 ranks: rank 5 owns none
+    assert hs.tile_begin == hs.tile_end == 3
     with pytest.raises(abi.TkvAmqError):
-        HashShardedBloom(100_000, 12, 8, 0, "cpu")   # 3 tiles over 8 ranks
+        hs.route(torch.zeros((10, 24), dtype=torch.uint8))   # 16-byte keys only

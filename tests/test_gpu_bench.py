@@ -106,3 +106,55 @@ def test_bench_single_gpu_line():
     assert [row["leaves"] for row in d["batch_sweep"]] == [64, 184]   # sizes below the batch
     b = d["cpu_baseline"]
     assert b["cores"] >= 1 and "host" in b and b["value"] > 0
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_gloo_host_legs():
+    """N > 1 lines carry the north star's host figures: every rank runs its own end-to-end
+    leg (its pages back to host page memory over its own link) at the same time, and rank 0
+    times the CPU baseline after the other ranks have left."""
+    r = run_bench("--gpus", "2", "--backend", "gloo", "--keys-per-gpu", "2000000",
+                  "--steps", "3", "--warmup", "1", "--ramp-ms", "0", "--cpu-threads", "4")
+    assert r.returncode == 0, r.stderr[-4000:]
+    d = last_json(r)
+    assert d["n_gpus"] == 2 and d["verified"] is True and d["gather_verified"] is True
+    e = d["e2e_pcie_inclusive"]
+    assert e["ranks"] == 2 and e["mkeys_s"] > 0 and e["from_key_views"]["mkeys_s"] > 0
+    b = d["cpu_baseline"]
+    assert b and b["value"] > 0 and b["cores"] >= 1 and "rank 0" in b["note"]
+    assert d["allgather_bytes_in_per_gpu"] > 0
+
+
+def run_launched(*args, timeout=400):
+    """bench.py under torch.distributed.run with one rank: the process-group code paths
+    (RCCL init bound to the device, device all-reduces, the all-gather) at world size 1."""
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    e = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        e.pop(k, None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+           "--gpus", "1", *args]
+    return subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=e, cwd=ROOT)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("workload", ["bloom10", "bloom12hash"])
+def test_bench_nccl_world1(workload):
+    """The RCCL path before any 8-GPU run: init_process_group("nccl", device_id=...), the
+    float64 / int32 all-reduces on the device, all_gather_into_tensor of the filter array, and
+    (bloom12hash) the device all_to_all_single of the routed keys."""
+    r = run_launched("--workload", workload, "--keys-per-gpu", "2000000", *SMALL)
+    assert r.returncode == 0, r.stderr[-4000:]
+    d = last_json(r)
+    assert d["n_gpus"] == 1 and d["config"]["backend"] == "nccl" and d["verified"] is True
+    assert d["allgather_ms"] > 0
+    if workload == "bloom10":
+        assert d["gather_verified"] is True
+    else:
+        assert d["verify"]["equal_to_one_gpu_build"] and d["verify"]["equal_to_oracle"]
+        assert d["step_breakdown_rank0_ms"]["keys_owned"] == 2_000_000

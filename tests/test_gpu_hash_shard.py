@@ -113,3 +113,32 @@ def test_bench_hash_sharded_one_rank():
     assert r.returncode == 0, r.stderr[-4000:]
     d = last_json(r)
     assert d["n_gpus"] == 1 and d["verified"] is True
+
+
+def test_empty_ranges_write_the_header(amq, torch):
+    """T = 17 tiles over 8 ranks: q = 3, so ranks 6 and 7 own no tile.  They receive no keys
+    from the route, and their range build still writes the whole filter header, so every
+    rank's assembled result (its own header + the gathered ranges) equals the one-GPU build."""
+    from turtle_kv_amd.dist import hash_shard_tiles
+    n, world = 720_000, 8
+    keys = amq.gen_keys16(13, 0, n)
+    plan = amq.plan_filters(0, [n], 12)
+    T, q = hash_shard_tiles(int(plan.segs[0]["n_blocks"]), world)
+    assert (T, q) == (17, 3)
+    whole = amq.build_all_filters(plan, amq.KeyBatch.fixed(keys))
+    routed, counts = _route(amq, torch, keys, plan, world)
+    assert counts[6] == 0 and counts[7] == 0 and counts.sum() == n
+    base = np.concatenate([[0], np.cumsum(counts)])
+    outs = []
+    for r in range(world):
+        out = torch.zeros(plan.total_out_bytes, dtype=torch.uint8, device="cuda")
+        _build_range(amq, torch, routed[int(base[r]):int(base[r + 1])], plan, min(T, r * q),
+                     min(T, (r + 1) * q), out)
+        outs.append(out)
+    torch.cuda.synchronize()
+    for r in range(world):
+        assert torch.equal(outs[r][:64], whole[:64]), f"rank {r}'s header"
+    merged = outs[0].clone()
+    for r in range(1, world):
+        merged |= outs[r]
+    assert torch.equal(merged, whole)

@@ -1,7 +1,13 @@
 """In-tree build of libtkv_amq.so (hipcc, gfx950).  No JIT cache: the .so lives next to
-this file so it travels to the GPU box with the repo snapshot."""
+this file so it travels to the GPU box with the repo snapshot.
+
+Several processes may ask for the library at once (bench.py's rank processes, pytest-xdist
+workers): the stale check, the compile and the stamp run under an exclusive flock, the
+check is repeated once the lock is held, and each process compiles into its own temp file
+before the atomic rename."""
 from __future__ import annotations
 
+import fcntl
 import hashlib
 import os
 import subprocess
@@ -19,6 +25,7 @@ FLAGS = ["-O3", "--offload-arch=gfx950", "-std=c++17", "-shared", "-fPIC",
 
 
 STAMP = LIB + ".src"  # sha256 of the sources and flags the library was built from
+LOCK = LIB + ".lock"
 
 
 def source_digest() -> str:
@@ -38,13 +45,24 @@ def stale() -> bool:
 
 
 def build(force: bool = False) -> str:
-    if force or stale():
-        tmp = LIB + ".tmp"
-        digest = source_digest()
-        subprocess.run([HIPCC, *FLAGS, "-o", tmp, *SOURCES], check=True)
-        os.replace(tmp, LIB)
-        with open(STAMP, "w") as f:
-            f.write(digest + "\n")
+    if not force and not stale():
+        return LIB
+    with open(LOCK, "a") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        try:
+            if force or stale():  # another process may have built it while we waited
+                tmp = f"{LIB}.{os.getpid()}.tmp"
+                digest = source_digest()
+                try:
+                    subprocess.run([HIPCC, *FLAGS, "-o", tmp, *SOURCES], check=True)
+                    os.replace(tmp, LIB)
+                finally:
+                    if os.path.exists(tmp):
+                        os.remove(tmp)
+                with open(STAMP, "w") as f:
+                    f.write(digest + "\n")
+        finally:
+            fcntl.flock(lk, fcntl.LOCK_UN)
     return LIB
 
 

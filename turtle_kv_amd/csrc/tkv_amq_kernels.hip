@@ -1100,6 +1100,17 @@ __global__ __launch_bounds__(kRecTileThreads) void bloom_rec_tile(const tkv_amq_
   for (uint32_t q = tid; q < tb * 4; q += kRecTileThreads) dst[q] = src[q];
 }
 
+// the filter header alone (a hash-range shard that owns no tile still returns a whole header)
+__global__ __launch_bounds__(64) void bloom_header_only(const tkv_amq_segment* __restrict__ segs,
+                                                        uint8_t* __restrict__ out)
+{
+  const tkv_amq_segment sg = segs[0];
+  const uint32_t tid = threadIdx.x;
+  if (sg.hash_count == 0) return;
+  if (tid < 4) write_bloom_header(out + sg.out_offset, sg, tid);
+  else if (tid < 8) write_page_header(out, sg, kLayoutBloom, tid - 4);
+}
+
 // one workgroup per partition workgroup's overflow list; device-scope atomics into the filter
 // (runs after bloom_rec_tile has stored every tile)
 __global__ __launch_bounds__(256) void bloom_rec_overflow(const tkv_amq_segment* __restrict__ segs,
@@ -3558,7 +3569,12 @@ int tkv_amq_bloom_build_range(const uint8_t* d_keys16, uint64_t n_keys, const tk
     return TKV_AMQ_INVALID_ARGUMENT;
   if (n_keys && (!d_keys16 || (reinterpret_cast<uintptr_t>(d_keys16) & 15)))
     return TKV_AMQ_INVALID_ARGUMENT;
-  if (tile_begin == tile_end) return TKV_AMQ_OK;
+  if (tile_begin == tile_end) {
+    // a rank past the last tile range (ceil(T / q) < ranks): its part of the result is the
+    // header, which every range build writes
+    hipLaunchKernelGGL(bloom_header_only, dim3(1), dim3(64), 0, as_stream(stream), d_seg, d_out);
+    return hipGetLastError() == hipSuccess ? TKV_AMQ_OK : TKV_AMQ_INTERNAL;
+  }
   const uint64_t nb = (uint64_t)(tile_end - tile_begin) * kBloomTileBlocks;
   if (d_ws && bloom_rec_eligible(nb, n_keys)) {
     const BloomRecGeom g = bloom_rec_geom(n_keys, nb);

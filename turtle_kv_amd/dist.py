@@ -118,9 +118,9 @@ class HashShardedBloom:
         self.n_blocks = int(seg["n_blocks"])
         self.payload_bytes = int(seg["payload_bytes"])
         T, q = hash_shard_tiles(self.n_blocks, world)
-        if T < world:
-            raise abi.TkvAmqError(abi.INVALID_ARGUMENT, f"a {T}-tile filter cannot be sharded "
-                                  f"over {world} ranks (each needs >= 1 tile of 1024 blocks)")
+        # ranks past ceil(T / q) own no tile (e.g. T = 17 over 8 ranks: q = 3, ranks 6 and 7):
+        # they route and exchange keys like the others, and their range build writes only the
+        # filter header
         self.tile_begin, self.tile_end = min(T, rank * q), min(T, (rank + 1) * q)
         self.slice_bytes = q * BLOOM_TILE_BLOCKS * 64
         # the payload layout of tkv_amq_build (64-byte header, then the blocks), padded so every
@@ -145,6 +145,10 @@ class HashShardedBloom:
         from . import abi
         from .filters import _ptr, _stream_handle
         L = abi.lib()
+        if keys.dim() != 2 or keys.shape[1] != 16:
+            # tkv_amq_bloom_route / _build_range hash 16-byte keys only (INTEGRATION.md key shapes)
+            raise abi.TkvAmqError(abi.INVALID_ARGUMENT, "hash-range sharding takes [n, 16] uint8 "
+                                  f"keys (16-byte keys only), got shape {tuple(keys.shape)}")
         n = keys.shape[0]
         routed = self._buf("routed", 16 * n)[:16 * n].view(n, 16)
         ws = self._buf("route_ws", int(L.tkv_amq_bloom_route_ws_bytes(n, self.world)))
@@ -187,18 +191,26 @@ class HashShardedBloom:
                                               _ptr(ws), ws.numel(), _stream_handle()),
                   "tkv_amq_bloom_build_range")
 
+    @property
+    def _collective(self) -> bool:
+        """route + all-to-all + all-gather whenever a process group exists (at world size 1
+        too: that runs the RCCL code path on one GPU); alone, the range build is the filter."""
+        import torch.distributed as dist
+        return self.world > 1 or (dist.is_available() and dist.is_initialized())
+
     def local_build(self, keys):
         """route + exchange + range build: after it, this rank's byte range of the bitmap is final."""
-        if self.world == 1:
+        if not self._collective:
             self.build_range(keys)
             return
         routed, sc = self.route(keys)
         self.build_range(self.exchange(routed, sc))
 
     def allgather(self):
-        """Every rank's bitmap range -> the whole filter payload (header + bitmap) on every rank."""
+        """Every rank's bitmap range -> the whole filter payload (header + bitmap) on every rank.
+        Every rank's range build writes the header (also a rank that owns no tile)."""
         import torch
-        if self.world == 1:
+        if not self._collective:
             return self.out[:self.payload_bytes]
         r0 = 64 + self.rank * self.slice_bytes
         allgather_filters(self.out[r0:r0 + self.slice_bytes], self.gathered, self.group)

@@ -70,6 +70,18 @@ def _stream_handle(stream=None):
     return ctypes.c_void_p(s.cuda_stream)
 
 
+def _hold(stream, *tensors):
+    """Temporaries handed to a kernel launched on `stream` (a torch.cuda.Stream other than the
+    current one): record that stream on them, so the caching allocator does not give their
+    memory to other work before the kernel has read it."""
+    torch = _torch()
+    if stream is None or stream == torch.cuda.current_stream():
+        return
+    for t in tensors:
+        if t is not None and getattr(t, "is_cuda", False):
+            t.record_stream(stream)
+
+
 def _ptr(t) -> ctypes.c_void_p | None:
     if t is None:
         return None
@@ -600,6 +612,8 @@ def probe_filters(plan: FilterPlan, filters, queries: KeyBatch, query_seg, out=N
                                         plan.n_segs, _ptr(queries.data), _ptr(queries.offsets),
                                         queries.stride, queries.n, _ptr(qs), _ptr(out),
                                         ctypes.byref(o), sh)
+        _hold(stream, *_keep)
+    _hold(stream, qs)
     abi.check(st, "tkv_amq_probe")
     return out
 
@@ -634,6 +648,7 @@ def vqf_probe_hashed(plan: FilterPlan, filters, hash_vals, query_seg, out=None, 
                                                     _ptr(qs), _ptr(out), ctypes.byref(o),
                                                     _stream_handle(stream)),
               "tkv_amq_vqf_probe_hashed")
+    _hold(stream, qs, pq, *_keep)
     return out
 
 
@@ -668,6 +683,7 @@ def bloom_probe_hashed(plan: FilterPlan, filters, query_hashes, k_max: int, quer
                                                       _ptr(pq), n, _ptr(qs), _ptr(out),
                                                       ctypes.byref(o), _stream_handle(stream)),
               "tkv_amq_bloom_probe_hashed")
+    _hold(stream, qs, pq, *_keep)
     return out
 
 
