@@ -347,6 +347,26 @@ def test_vqf_leaf_beyond_ring_blocks(oracle, amq, torch, n_leaves, big, bpk):
         assert segment_bytes(plan, out, s) == ref[:p.payload_used].tobytes(), f"leaf {s}"
 
 
+@pytest.mark.parametrize("big,bpk,cap", [(700_000, 12, 4 << 20), (700_000, 22, 4 << 20),
+                                         (7_000_000, 12, 16 << 20)])
+def test_vqf_huge_leaf(oracle, amq, torch, big, bpk, cap):
+    """Leaves past vqf_decide's u32 LDS count table (16,384 blocks), which round 2 refused:
+    a 700K-key leaf (17,157 blocks at 12 bits/key, 30,553 with 16-bit tags at 22) keeps u8
+    counts in LDS; a 7M-key leaf (171,569 blocks) keeps them in the workspace's block records
+    (agent-scope atomics).  Both are placed by the multi-workgroup unfused place, in a batch
+    with small leaves, and must equal the oracle byte for byte."""
+    counts = [big, 500, 0, 16384] if big < 1_000_000 else [big, 3000]
+    keys = oracle.gen_keys16(8, 0, sum(counts))
+    plan, out = gpu_build(amq, torch, 1, torch.from_numpy(keys).cuda(), counts, bpk, cap=cap)
+    nb = int(plan.segs["n_blocks"][0])
+    assert nb > 16384 and (nb > 160 * 1024) == (big > 1_000_000)
+    sb = seg_bounds(counts)
+    for s in range(len(counts)):
+        st, ref, p = oracle.vqf_build(keys[int(sb[s]):], counts[s], bpk, cap, src_page_id=s)
+        assert st == 0
+        assert segment_bytes(plan, out, s) == ref[:p.payload_used].tobytes(), f"leaf {s}"
+
+
 def probe_inputs(oracle, n_keys, counts, n_miss):
     hits = np.arange(n_keys)
     seg_of = np.repeat(np.arange(len(counts)), counts)

@@ -80,12 +80,15 @@ def test_plan_pages_rejects_bad_sizes(amq):
     assert e.value.status == amq.abi.RESOURCE_EXHAUSTED
 
 
-def test_vqf_block_cap(amq):
-    """A VQF leaf above 16,384 blocks (1 MiB of filter; the LDS count table of vqf_decide)
-    is refused with ResourceExhausted at plan time (the reference has no such cap; DESIGN.md
-    section 4 'Caps')."""
-    ok = amq.plan_filters(1, [660000], 12, payload_capacity=4 << 20)
-    assert ok.max_seg_blocks <= 16384
+def test_vqf_large_leaves_plan(amq):
+    """VQF leaves of any size the reference builds are planned: the round-2 cap of 16,384
+    blocks is gone (vqf_decide keeps u8 counts in LDS up to 163,840 blocks and global counts
+    beyond; GPU parity: test_gpu_parity.py::test_vqf_huge_leaf).  Only a filter past 2^24
+    blocks (1 GiB) is refused, with ResourceExhausted."""
+    ok = amq.plan_filters(1, [700000], 12, payload_capacity=4 << 20)
+    assert ok.max_seg_blocks > 16384
+    big = amq.plan_filters(1, [7_000_000], 12, payload_capacity=16 << 20)
+    assert big.max_seg_blocks > 160 * 1024
     with pytest.raises(amq.TkvAmqError) as e:
-        amq.plan_filters(1, [700000], 12, payload_capacity=4 << 20)
+        amq.plan_filters(1, [700_000_000], 12, payload_capacity=2 << 30)
     assert e.value.status == amq.abi.RESOURCE_EXHAUSTED

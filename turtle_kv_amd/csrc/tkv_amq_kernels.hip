@@ -1448,6 +1448,63 @@ __device__ inline uint32_t& vqf_count(VqfWorkspace ws, uint64_t block)
   return *reinterpret_cast<uint32_t*>(ws.temp + block * kVqfTempStride + kVqfCountByte);
 }
 
+// vqf_decide's per-block element counts, by leaf size:
+//   kCntU32     u32 in LDS (leaves of <= kVqfMaxLdsBlocks blocks: the fast path)
+//   kCntU8      u8 in LDS, 4 per dword (<= kVqfU8LdsBlocks blocks, ~10 MB of filter).  A count
+//               passes 255 (and carries into its neighbour) only after its block overflowed
+//               at the 49th insert, which already fails the leaf (Internal, no filter)
+//   kCntGlobal  u32 at byte kVqfCountByte of the leaf's block records in the workspace, with
+//               agent-scope atomics (any larger leaf: one memory round trip per 64-key step)
+enum VqfCountMode : int { kCntU32 = 0, kCntU8 = 1, kCntGlobal = 2 };
+constexpr uint32_t kVqfU8LdsBlocks = 160 * 1024;
+constexpr uint32_t kVqfMaxBlocks = 1u << 24;  // block ids fit the 24-bit ballot match
+
+template <int CNT>
+struct VqfCounts;
+template <>
+struct VqfCounts<kCntU32> {
+  uint32_t* p;
+  __device__ inline uint32_t get(uint32_t b) const { return p[b]; }
+  __device__ inline void add(uint32_t b, uint32_t v) const { atomicAdd(p + b, v); }
+  __device__ inline void clear(uint32_t nb, uint32_t lane) const
+  {
+    for (uint32_t b = lane; b < nb; b += 64) p[b] = 0;
+  }
+};
+template <>
+struct VqfCounts<kCntU8> {
+  uint32_t* p;
+  __device__ inline uint32_t get(uint32_t b) const { return reinterpret_cast<const uint8_t*>(p)[b]; }
+  __device__ inline void add(uint32_t b, uint32_t v) const { atomicAdd(p + (b >> 2), v << (8 * (b & 3))); }
+  __device__ inline void clear(uint32_t nb, uint32_t lane) const
+  {
+    for (uint32_t w = lane; w < (nb + 3) / 4; w += 64) p[w] = 0;
+  }
+};
+template <>
+struct VqfCounts<kCntGlobal> {
+  uint8_t* rec;  // the leaf's first block record
+  __device__ inline uint32_t* at(uint32_t b) const
+  {
+    return reinterpret_cast<uint32_t*>(rec + (uint64_t)b * kVqfTempStride + kVqfCountByte);
+  }
+  __device__ inline uint32_t get(uint32_t b) const
+  {
+    return __hip_atomic_load(at(b), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  // acquire-release: the wave waits for the add before its next step reads the counts
+  __device__ inline void add(uint32_t b, uint32_t v) const
+  {
+    __hip_atomic_fetch_add(at(b), v, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __device__ inline void clear(uint32_t nb, uint32_t lane) const
+  {
+    for (uint32_t b = lane; b < nb; b += 64)
+      __hip_atomic_store(at(b), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  }
+};
+
 // A key the VQF kernels load one or two chunks ahead of hashing it (16- and 24-byte keys;
 // other shapes are read where they are hashed)
 template <int MODE>
@@ -1541,12 +1598,13 @@ __device__ inline void vqf_locate_alt(const VqfLoc& l, uint64_t R, uint64_t magi
 // 8 B of LDS per block, so it is used for leaves of <= kVqfMatchLdsBlocks blocks.
 // kCompact (T = 8, <= 512 blocks, fused place): 4-byte key records
 //   block << 21 | rank << 15 | (bucket offset << 8 | tag), or ~0 for a key not inserted
-template <int T, int MODE, int NBITS, bool kLdsMatch, bool kCompact>
+template <int T, int MODE, int NBITS, bool kLdsMatch, bool kCompact, int CNT = kCntU32>
 __device__ void vqf_decide_body(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs,
                                 uint32_t stride, const tkv_amq_segment& sg, uint32_t seg_index,
-                                VqfWorkspace ws, uint64_t* __restrict__ recs, uint32_t* cnt,
+                                VqfWorkspace ws, uint64_t* __restrict__ recs, uint32_t* s_lds,
                                 bool fused)
 {
+  static_assert(!kLdsMatch || CNT == kCntU32, "the lane-mask table follows u32 counts");
   using C = Vqf<T>;
   const uint32_t lane = threadIdx.x;
   const uint32_t n = sg.n_keys, nb = sg.n_blocks;
@@ -1558,11 +1616,13 @@ __device__ void vqf_decide_body(const uint8_t* __restrict__ keys, const uint64_t
   Rec* rec = reinterpret_cast<Rec*>(recs + sg.key_begin);
   using KB = VqfKeyBuf<MODE>;
 
-  unsigned long long* mt = reinterpret_cast<unsigned long long*>(cnt + ((nb + 1) & ~1u));
-  for (uint32_t b = lane; b < nb; b += 64) {
-    cnt[b] = 0;
-    if constexpr (kLdsMatch) mt[b] = 0;
-  }
+  VqfCounts<CNT> cnt;
+  if constexpr (CNT == kCntGlobal) cnt.rec = ws.temp + sg.block_base * kVqfTempStride;
+  else cnt.p = s_lds;
+  unsigned long long* mt = reinterpret_cast<unsigned long long*>(s_lds + ((nb + 1) & ~1u));
+  cnt.clear(nb, lane);
+  if constexpr (kLdsMatch)
+    for (uint32_t b = lane; b < nb; b += 64) mt[b] = 0;
   // one wave: its LDS operations execute in order, so no workgroup barrier (the body also
   // runs in wave 0 of vqf_decide_ring's workgroup after the other waves have left)
   asm volatile("" ::: "memory");
@@ -1590,7 +1650,7 @@ __device__ void vqf_decide_body(const uint8_t* __restrict__ keys, const uint64_t
   auto step = [&](uint32_t base, VqfLoc& cur, const KB& kv_hash, KB& kv_load) {
     const VqfLoc L = cur;
     // primary block counts before this chunk (every lane reads: an invalid lane's block is 0)
-    const uint32_t cnt_p = cnt[L.pb];
+    const uint32_t cnt_p = cnt.get(L.pb);
     const uint32_t inext = base + 64 + lane;
     const bool vnext = inext < n;
     uint64_t hn;
@@ -1643,7 +1703,7 @@ __device__ void vqf_decide_body(const uint8_t* __restrict__ keys, const uint64_t
     // the alternate block entirely.
     if (__ballot(L.kept && cp >= C::kThreshold) != 0) {
       vqf_locate_alt<T>(L, R, magic, ab, ao);
-      const uint32_t cnt_a = cnt[ab];
+      const uint32_t cnt_a = cnt.get(ab);
       // lanes with pb_j == my ab
       uint32_t mpa_lo = (uint32_t)keptmask, mpa_hi = (uint32_t)(keptmask >> 32);
       if constexpr (kLdsMatch) {
@@ -1732,7 +1792,7 @@ __device__ void vqf_decide_body(const uint8_t* __restrict__ keys, const uint64_t
                                    ? (uint32_t)((sg.block_base + chosen) * 64 + r) : 0xffffffffu;
       pend_val = ((uint64_t)slot_hi << 32) | ((cho << T) | L.tag) | (T == 16 ? 0x80000000u : 0u);
     }
-    atomicAdd(cnt + chosen, L.kept ? 1u : 0u);
+    cnt.add(chosen, L.kept ? 1u : 0u);
   };
 
   KB kv0{}, kvA{}, kvB{};
@@ -1753,9 +1813,9 @@ __device__ void vqf_decide_body(const uint8_t* __restrict__ keys, const uint64_t
   asm volatile("" ::: "memory");
   // the final per-block counts feed only the unfused place path (the fused one recounts in
   // LDS): 4 bytes per 128-byte block record, so skip them when they are not read
-  if (!fused) {
+  if (!fused && CNT != kCntGlobal) {  // (global counts are in the block records already)
     for (uint32_t b = lane; b < nb; b += 64) {
-      const uint32_t c = cnt[b];
+      const uint32_t c = cnt.get(b);
       vqf_count(ws, sg.block_base + b) = c < C::kSlots ? c : C::kSlots;
     }
   }
@@ -1769,8 +1829,17 @@ template <int T, int MODE>
 __device__ inline void vqf_decide_dispatch(const uint8_t* keys, const uint64_t* offs,
                                            uint32_t stride, const tkv_amq_segment& sg,
                                            uint32_t seg_index, VqfWorkspace ws, uint64_t* recs,
-                                           uint32_t* cnt, bool match_lds, bool compact_ok)
+                                           uint32_t* cnt, bool match_lds, bool compact_ok,
+                                           int cnt_mode)
 {
+  if (cnt_mode == kCntU8) {  // <= kVqfU8LdsBlocks -> at most 18 block-id bits
+    vqf_decide_body<T, MODE, 18, false, false, kCntU8>(keys, offs, stride, sg, seg_index, ws, recs, cnt, compact_ok);
+    return;
+  }
+  if (cnt_mode == kCntGlobal) {  // <= kVqfMaxBlocks
+    vqf_decide_body<T, MODE, 24, false, false, kCntGlobal>(keys, offs, stride, sg, seg_index, ws, recs, cnt, compact_ok);
+    return;
+  }
   // kVqfMaxLdsBlocks = 16384 -> at most 14 block-id bits
   if (sg.n_blocks <= 512) {
     if (T == 8 && compact_ok) {
@@ -1795,15 +1864,18 @@ __global__ __launch_bounds__(64) void vqf_decide(const uint8_t* __restrict__ key
                                                  int flags)
 {
   const bool match_lds = flags & 1, compact_ok = flags & 2;
+  const int cnt_mode = (flags >> 2) & 3;
   extern __shared__ __attribute__((aligned(16))) uint32_t s_cnt[];
   const tkv_amq_segment sg = segs[blockIdx.x];
   const VqfWorkspace ws = vqf_workspace(ws_base, n_segs);
   if (!vqf_ws_ok(segs, n_segs, ws_bytes, ws)) return;
   uint64_t* recs = vqf_records(ws, segs, n_segs);
   if (sg.tag_bits == 8)
-    vqf_decide_dispatch<8, MODE>(keys, offs, stride, sg, blockIdx.x, ws, recs, s_cnt, match_lds, compact_ok);
+    vqf_decide_dispatch<8, MODE>(keys, offs, stride, sg, blockIdx.x, ws, recs, s_cnt, match_lds, compact_ok,
+                                 cnt_mode);
   else if (sg.tag_bits == 16)
-    vqf_decide_dispatch<16, MODE>(keys, offs, stride, sg, blockIdx.x, ws, recs, s_cnt, match_lds, compact_ok);
+    vqf_decide_dispatch<16, MODE>(keys, offs, stride, sg, blockIdx.x, ws, recs, s_cnt, match_lds, compact_ok,
+                                  cnt_mode);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -2139,7 +2211,8 @@ constexpr uint32_t kPlaceThreads = 128;
 
 template <int T>
 __device__ void vqf_place_body(const tkv_amq_segment& sg, uint32_t seg_index, VqfWorkspace ws,
-                               uint8_t* __restrict__ out, uint32_t* s_cnt, uint32_t* s_img)
+                               uint8_t* __restrict__ out, uint32_t* s_cnt, uint32_t* s_img,
+                               uint32_t part, uint32_t parts)
 {
   using C = Vqf<T>;
   using E = typename C::Entry;
@@ -2151,7 +2224,7 @@ __device__ void vqf_place_body(const tkv_amq_segment& sg, uint32_t seg_index, Vq
   const uint32_t nb = sg.n_blocks;
   uint8_t* payload = out + sg.out_offset;
 
-  if (tid < 5) {
+  if (part == 0 && tid < 5) {
     // PackedVqfFilter header (vqf_filter_page_view.hpp:79-94) + vqf_metadata
     uint64_t w0, w1;
     switch (tid) {
@@ -2165,7 +2238,7 @@ __device__ void vqf_place_body(const tkv_amq_segment& sg, uint32_t seg_index, Vq
     v.x = w0;
     v.y = w1;
     reinterpret_cast<ulonglong2*>(payload)[tid] = v;
-  } else if (tid < 9) {
+  } else if (part == 0 && tid < 9) {
     write_page_header(out, sg, kLayoutVqf, tid - 5);
   }
 
@@ -2173,7 +2246,7 @@ __device__ void vqf_place_body(const tkv_amq_segment& sg, uint32_t seg_index, Vq
   uint32_t* img = s_img + tid * kImgStride;
   uint4* dst_blocks = reinterpret_cast<uint4*>(payload + kVqfHeader + kVqfMetadata);
 
-  for (uint32_t b = tid; b < nb; b += kPlaceThreads) {
+  for (uint32_t b = part * kPlaceThreads + tid; b < nb; b += parts * kPlaceThreads) {
     const uint8_t* rec = ws.temp + (sg.block_base + b) * kVqfTempStride;
     const uint32_t c = *reinterpret_cast<const uint32_t*>(rec + kVqfCountByte);
     uint4 rv[kRecWords];
@@ -2261,15 +2334,17 @@ __device__ void vqf_place_body(const tkv_amq_segment& sg, uint32_t seg_index, Vq
 
 __global__ __launch_bounds__(kPlaceThreads) void vqf_place(const tkv_amq_segment* __restrict__ segs,
                                                            void* ws_base, uint64_t ws_bytes,
-                                                           uint32_t n_segs, uint8_t* __restrict__ out)
+                                                           uint32_t n_segs, uint8_t* __restrict__ out,
+                                                           uint32_t parts)
 {
   __shared__ uint32_t s_cnt[kPlaceThreads * 21];
   __shared__ uint32_t s_img[kPlaceThreads * 17];
-  const tkv_amq_segment sg = segs[blockIdx.x];
+  const uint32_t seg = blockIdx.x / parts, part = blockIdx.x - seg * parts;
+  const tkv_amq_segment sg = segs[seg];
   const VqfWorkspace ws = vqf_workspace(ws_base, n_segs);
   if (!vqf_ws_ok(segs, n_segs, ws_bytes, ws)) return;
-  if (sg.tag_bits == 8) vqf_place_body<8>(sg, blockIdx.x, ws, out, s_cnt, s_img);
-  else if (sg.tag_bits == 16) vqf_place_body<16>(sg, blockIdx.x, ws, out, s_cnt, s_img);
+  if (sg.tag_bits == 8) vqf_place_body<8>(sg, seg, ws, out, s_cnt, s_img, part, parts);
+  else if (sg.tag_bits == 16) vqf_place_body<16>(sg, seg, ws, out, s_cnt, s_img, part, parts);
 }
 
 // Fused scatter + place for leaves whose block records fit in LDS (one workgroup per leaf, or
@@ -3256,7 +3331,7 @@ int tkv_amq_plan(int kind, const uint64_t* counts, const uint64_t* src_ids, uint
       }
       const uint64_t sl = vqf_slots(t);
       const uint64_t nb = (nslots + sl) / sl;
-      if (nb > kVqfMaxLdsBlocks) return TKV_AMQ_RESOURCE_EXHAUSTED;
+      if (nb > kVqfMaxBlocks) return TKV_AMQ_RESOURCE_EXHAUSTED;
       g.n_blocks = (uint32_t)nb;
       g.tag_bits = (uint8_t)t;
       g.hash_val_shift = (uint8_t)shift;
@@ -3417,7 +3492,7 @@ int tkv_amq_build(int kind, const uint8_t* keys, const uint64_t* offs, uint32_t 
 
   if (kind != TKV_AMQ_VQF) return TKV_AMQ_INVALID_ARGUMENT;
   if (max_blocks == 0) return TKV_AMQ_OK;
-  if (max_blocks > kVqfMaxLdsBlocks) return TKV_AMQ_RESOURCE_EXHAUSTED;
+  if (max_blocks > kVqfMaxBlocks) return TKV_AMQ_RESOURCE_EXHAUSTED;
   if (!d_ws) return TKV_AMQ_INVALID_ARGUMENT;
   // the status word and leaf counts must be writable; the rest is checked on the device
   // against the plan (every leaf with a filter has >= 1 block record, every key one record)
@@ -3435,8 +3510,24 @@ int tkv_amq_build(int kind, const uint8_t* keys, const uint64_t* offs, uint32_t 
   const uint32_t place_span = (uint32_t)div_up(max_blocks, place_parts);
   const uint32_t fused_lds = vqf_fused_lds_bytes(place_span);
   const bool fused = place_parts <= kFusedMaxParts;  // compact records are read only there
-  const int flags = match_lds | (fused ? 2 : 0);
-  const size_t lds = 4ull * ((max_blocks + 1) & ~1u) + (match_lds ? 8ull * max_blocks : 0);
+  // the count table: u32 in LDS up to kVqfMaxLdsBlocks, u8 in LDS up to kVqfU8LdsBlocks, else
+  // in the workspace's block records (VqfCountMode)
+  const int cnt_mode = max_blocks <= kVqfMaxLdsBlocks ? kCntU32
+                       : (max_blocks <= kVqfU8LdsBlocks ? kCntU8 : kCntGlobal);
+  const int flags = match_lds | (fused ? 2 : 0) | (cnt_mode << 2);
+  const size_t lds = cnt_mode == kCntU8 ? (size_t)((max_blocks + 15) & ~15u)
+                     : cnt_mode == kCntGlobal ? 16
+                     : 4ull * ((max_blocks + 1) & ~1u) + (match_lds ? 8ull * max_blocks : 0);
+  if (lds > kBloomLdsBudget) {
+    static std::once_flag big_attr[kMaxDevices];
+    once_per_device(big_attr, [] {
+      for (const void* f : {reinterpret_cast<const void*>(&vqf_decide<kKey16>),
+                            reinterpret_cast<const void*>(&vqf_decide<kKey24>),
+                            reinterpret_cast<const void*>(&vqf_decide<kKeyFixed>),
+                            reinterpret_cast<const void*>(&vqf_decide<kKeyVar>)})
+        (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    });
+  }
   // the ring kernel for small batches of leaves its count table holds (a batch with a larger
   // leaf takes vqf_decide: the one-wave body inside the ring kernel set its registers, and so
   // its workgroups per CU, for every batch).  Keys other than 16 bytes are read where they are
@@ -3505,8 +3596,12 @@ int tkv_amq_build(int kind, const uint8_t* keys, const uint64_t* offs, uint32_t 
     if (n_keys)
       hipLaunchKernelGGL(vqf_scatter, dim3((uint32_t)div_up(n_keys, 256)), dim3(256), 0, s,
                          d_segs, d_ws, ws_bytes, n_segs, n_keys);
-    hipLaunchKernelGGL(vqf_place, dim3(n_segs), dim3(kPlaceThreads), 0, s, d_segs, d_ws, ws_bytes,
-                       n_segs, d_out);
+    // several workgroups per leaf for large leaves (each takes every parts-th group of
+    // kPlaceThreads blocks)
+    const uint32_t parts = (uint32_t)(div_up(max_blocks, 4 * kPlaceThreads) < 256
+                                          ? div_up(max_blocks, 4 * kPlaceThreads) : 256);
+    hipLaunchKernelGGL(vqf_place, dim3(n_segs * parts), dim3(kPlaceThreads), 0, s, d_segs, d_ws,
+                       ws_bytes, n_segs, d_out, parts);
   }
   return hipGetLastError() == hipSuccess ? TKV_AMQ_OK : TKV_AMQ_INTERNAL;
 }
