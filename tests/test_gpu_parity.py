@@ -413,13 +413,14 @@ def test_vqf_hash_matches_xxhash(amq, torch):
     assert [int(x) for x in h16] == [xxhash.xxh64_intdigest(k.tobytes(), VQF_SEED) for k in k16]
 
 
-@pytest.mark.parametrize("n,bpk,seed", [(200000, 10, 8), (3000000, 10, 9), (1500000, 12, 10),
-                                         (400000, 5, 11), (30000, 64, 12)])
+@pytest.mark.parametrize("n,bpk,seed", [(600000, 10, 8), (3000000, 10, 9), (1500000, 12, 10),
+                                         (1100000, 5, 11), (90000, 64, 12)])
 def test_bloom_monolithic_partitioned(oracle, amq, torch, n, bpk, seed):
-    """One filter larger than the LDS image budget (160 KB): the hash-once record path
-    (bloom_rec_partition / bloom_rec_tile), byte-identical to the oracle.  Covers a ragged last
-    tile, k = 7 / 8 / generic <= 8 (12-byte bit records) and k = 32 (the keys themselves are
-    partitioned and hashed per tile), and 58 tiles over 92 partition workgroups."""
+    """One filter of 16-byte keys larger than four LDS windows (640 KB; smaller ones take the
+    window path, tests/test_gpu_window.py): the hash-once record path (bloom_rec_partition /
+    bloom_rec_tile), byte-identical to the oracle.  Covers a ragged last tile, k = 7 / 8 /
+    generic <= 8 (12-byte bit records) and k = 32 (the keys themselves are partitioned and
+    hashed per tile), and 58 tiles over 92 partition workgroups."""
     keys = oracle.gen_keys16(seed, 0, n)
     ref = oracle_per_segment(oracle, 0, keys, [n], bpk)
     plan, out = gpu_build(amq, torch, 0, torch.from_numpy(keys).cuda(), [n], bpk)
@@ -464,7 +465,7 @@ def test_bloom_big_leaves_in_lds(oracle, amq, torch, shape):
     """Batches of >= 64 leaves build leaf images of up to 160 KB in LDS (1024-thread
     workgroups above 32 KB; TurtleKV leaves of small items reach ~80K keys): a 100000-key leaf
     (125 KB at 10 bits/key, 150 KB at 12) and a 40000-key one among small leaves; at 14 bits/key
-    the 100000-key leaf (175 KB) sends the batch to the device-atomic path."""
+    the 100000-key leaf (175 KB) sends the batch to the window path (two windows)."""
     rng = np.random.default_rng(77)
     counts = [int(c) for c in rng.integers(0, 2000, 70)]
     counts[5], counts[40], counts[69] = 100000, 40000, 0
@@ -488,14 +489,16 @@ def test_bloom_big_leaves_in_lds(oracle, amq, torch, shape):
         assert_same(plan, out, ref)
 
 
-def test_bloom_oversize_leaf_in_batch_global_path(oracle, amq, torch):
-    """A multi-leaf batch holding a leaf beyond the LDS budget (a 175 KB image) takes the
-    device-atomic path."""
-    counts = [140000, 500, 16384]
+@pytest.mark.parametrize("big", [140000, 3_000_000])
+def test_bloom_oversize_leaf_in_batch(oracle, amq, torch, big):
+    """A multi-leaf batch holding a leaf beyond the LDS budget: a 175 KB image takes the
+    window path (partial images in the workspace, merged); a 3.75 MB one (24 windows, more
+    than the window path's 16) the device-atomic path, with no workspace."""
+    counts = [big, 500, 16384]
     keys = oracle.gen_keys16(15, 0, sum(counts))
     ref = oracle_per_segment(oracle, 0, keys, counts, 10)
     plan, out = gpu_build(amq, torch, 0, torch.from_numpy(keys).cuda(), counts, 10)
-    assert plan.workspace_bytes == 0
+    assert (plan.workspace_bytes == 0) == (big > 1_000_000)
     assert_same(plan, out, ref)
 
 

@@ -31,6 +31,10 @@ def main():
                     help="VQF payload capacity (default: the TreeOptions filter page at --bpk)")
     ap.add_argument("--no-ws", action="store_true",
                     help="call the ABI without a workspace (Bloom: the unsplit paths)")
+    ap.add_argument("--ws-bytes", type=int, default=-1,
+                    help="call the ABI with exactly this much workspace (Bloom window path: "
+                         "one part per leaf when short of the partial images)")
+
     a = ap.parse_args()
     bpk = a.bpk or (10 if a.kind == 0 else 12)
     cap = a.cap or (amq.TreeOptions(a.kind).set_filter_bits_per_key(bpk).filter_page_payload_size()
@@ -63,8 +67,15 @@ def main():
         lib, F = amq.abi.lib(), amq.filters
         segs = plan.device_segs()
 
+        ws_bytes = a.ws_bytes
+
         def build():
-            if a.no_ws:
+            if ws_bytes >= 0:
+                amq.abi.check(lib.tkv_amq_build(a.kind, F._ptr(kb.data), F._ptr(kb.offsets), kb.stride,
+                                              kb.n, F._ptr(segs), plan.n_segs, plan.max_seg_blocks,
+                                              F._ptr(out), F._ptr(ws) if ws_bytes else None, ws_bytes,
+                                              F._stream_handle()), "build")
+            elif a.no_ws:
                 amq.abi.check(lib.tkv_amq_build(a.kind, F._ptr(kb.data), None, 16, kb.n, F._ptr(segs),
                                               plan.n_segs, plan.max_seg_blocks, F._ptr(out), None, 0,
                                               F._stream_handle()), "build")

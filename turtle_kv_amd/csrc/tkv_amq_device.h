@@ -161,6 +161,7 @@ __device__ inline uint32_t davalanche_lo9(uint64_t h)
 struct Xxh16 {
   uint64_t rk1, k2;
   __device__ inline Xxh16(uint64_t lo, uint64_t hi) : rk1{drotl<27>(dround(0, lo))}, k2{dround(0, hi)} {}
+  __device__ inline Xxh16() : rk1{0}, k2{0} {}  // (a state moved between lanes: set rk1, k2)
   // state before the avalanche
   __device__ inline uint64_t pre(uint64_t rhinit) const
   {
@@ -182,6 +183,7 @@ struct XxhFixed {
   static constexpr int N = L / 8;
   uint64_t rk0;
   uint64_t k[N > 1 ? N - 1 : 1];
+  __device__ inline XxhFixed() : rk0{0}, k{} {}  // (a state moved between lanes)
   __device__ inline explicit XxhFixed(const uint64_t (&lanes)[N])
   {
     rk0 = drotl<27>(dround(0, lanes[0]));
@@ -252,6 +254,19 @@ struct XxhShort {
     const uint32_t nb = n & 3;
 #pragma unroll
     for (uint32_t k = 0; k < 3; ++k) tb[k] = k < nb ? (uint64_t)q[k] * kP5 : 0ull;
+  }
+  // from bytes loaded ahead (VqfKeyBuf<kKeyVar>): the n >> 3 eight-byte lanes, the 4-byte
+  // tail word and the 1..3 tail bytes packed low to high
+  __device__ inline XxhShort(uint32_t n, const uint64_t (&lanes)[3], uint32_t tail4, uint32_t tail_bytes)
+      : len{n}
+  {
+    const uint32_t n8 = n >> 3;
+#pragma unroll
+    for (uint32_t j = 0; j < 3; ++j) r[j] = j < n8 ? dround(0, lanes[j]) : 0ull;
+    t4 = (n & 4) ? (uint64_t)tail4 * kP1 : 0ull;
+    const uint32_t nb = n & 3;
+#pragma unroll
+    for (uint32_t k = 0; k < 3; ++k) tb[k] = k < nb ? (uint64_t)((tail_bytes >> (8 * k)) & 0xffu) * kP5 : 0ull;
   }
   // state before the avalanche; seed_p5 = seed + P5
   __device__ inline uint64_t pre(uint64_t seed_p5) const

@@ -105,6 +105,14 @@ __device__ inline uint64_t hash_key(const uint8_t* keys, const uint64_t* offs, u
   return xxh64_bytes(p, len, seed);
 }
 
+// Workgroup barrier for LDS hazards only: this wave's LDS operations are complete, its global
+// loads and stores stay in flight (__syncthreads() also drains vmcnt, stores included).
+__device__ inline void lds_barrier()
+{
+  // (the memory clobber keeps the compiler from moving LDS accesses across it)
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 // ---------------------------------------------------------------------------------------
 // Bloom build (LDS image per segment)
 // ---------------------------------------------------------------------------------------
@@ -390,6 +398,250 @@ __global__ __launch_bounds__(kMergeThreads) void bloom_split_merge(
     v.w |= o[p].w;
   }
   reinterpret_cast<uint4*>(payload + kBloomHeader)[q] = v;
+}
+
+// ---------------------------------------------------------------------------------------
+// Bloom build, leaves whose image exceeds one CU's LDS, in batches of any size
+// (bloom_build_window).  The image of a leaf of nb blocks is cut into W windows of at most
+// win_blocks blocks (<= kBloomLeafLdsBudget bytes); workgroup (leaf, window, part) streams the
+// keys of its part of the leaf, computes each key's block (h0) and keeps only the keys whose
+// block falls in its window.  Those are packed densely across the wave: each step's in-window
+// lanes are pushed (ds_permute, a full permutation of the 64 lanes) behind the c keys still
+// pending, and whenever 64 are pending the wave computes their other k - 1 hashes and sets
+// their bits.  So only the seed-0 hash is repeated per window (~70 VALU of the ~280 a k = 8
+// key costs); a window never hashes another window's keys.  A key moves as its hash state
+// (16-byte keys: the two lane rounds; 24-byte keys: the three) plus its window block and
+// bit 0; other key shapes move as their index and are re-hashed.  With one part per leaf
+// the window is written straight into the filter; with several, each part writes its
+// windows into a full-size partial image and bloom_split_merge ORs them.
+// ---------------------------------------------------------------------------------------
+constexpr uint32_t kWinThreads = 1024;
+constexpr uint32_t kWinMaxWindows = 16;
+
+template <int MODE>
+struct WinItem {  // any key shape: the key's index in its leaf, then loc
+  static constexpr int N = 2;
+  uint32_t d[N];
+};
+template <>
+struct WinItem<kKey16> {  // Xxh16 state (rk1, k2), then loc
+  static constexpr int N = 5;
+  uint32_t d[N];
+};
+template <>
+struct WinItem<kKey24> {  // XxhFixed<24> state (rk0, k[0], k[1]), then loc
+  static constexpr int N = 7;
+  uint32_t d[N];
+};
+// loc = block in the window (< 4096) | bit index 0 << 12
+
+template <int MODE>
+struct WinKey {};
+template <>
+struct WinKey<kKey16> {
+  uint4 v;
+};
+template <>
+struct WinKey<kKey24> {
+  uint64_t w[3];
+};
+
+template <int MODE>
+__device__ inline void win_load(const uint8_t* __restrict__ keys, uint64_t gi, WinKey<MODE>& kb)
+{
+  if constexpr (MODE == kKey16) {
+    kb.v = load_nt16(keys + 16 * gi);
+  } else if constexpr (MODE == kKey24) {
+    const uint64_t* p = reinterpret_cast<const uint64_t*>(keys) + 3 * gi;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) kb.w[i] = p[i];
+  }
+}
+
+// the key's block in its leaf (from h0) and its item (loc holds bit 0 only)
+template <int MODE>
+__device__ inline uint32_t win_hash(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs,
+                                    uint32_t stride, const tkv_amq_segment& sg, uint32_t i,
+                                    const WinKey<MODE>& kb, WinItem<MODE>& it)
+{
+  uint64_t h0;
+  if constexpr (MODE == kKey16) {
+    const Xxh16 x((uint64_t)kb.v.x | ((uint64_t)kb.v.y << 32), (uint64_t)kb.v.z | ((uint64_t)kb.v.w << 32));
+    h0 = x.finish(c_bloom.rhinit16[0]);
+    it.d[0] = lo32(x.rk1);
+    it.d[1] = hi32(x.rk1);
+    it.d[2] = lo32(x.k2);
+    it.d[3] = hi32(x.k2);
+  } else if constexpr (MODE == kKey24) {
+    const XxhFixed<24> x(kb.w);
+    h0 = x.finish(xxh_fixed_rc<24>(c_bloom.seed[0]));
+    it.d[0] = lo32(x.rk0);
+    it.d[1] = hi32(x.rk0);
+    it.d[2] = lo32(x.k[0]);
+    it.d[3] = hi32(x.k[0]);
+    it.d[4] = lo32(x.k[1]);
+    it.d[5] = hi32(x.k[1]);
+  } else {
+    h0 = hash_key<MODE>(keys, offs, stride, sg.key_begin + i, c_bloom.seed[0]);
+    it.d[0] = i;
+  }
+  it.d[WinItem<MODE>::N - 1] = ((uint32_t)h0 & 511u) << 12;
+  return (uint32_t)__umul64hi(h0, (uint64_t)sg.n_blocks);
+}
+
+// the other k - 1 bits of a packed key, and bit 0
+template <int MODE, int K>
+__device__ inline void win_insert(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs,
+                                  uint32_t stride, const tkv_amq_segment& sg, uint32_t k,
+                                  const WinItem<MODE>& it, uint32_t* s_bits)
+{
+  const uint32_t loc = it.d[WinItem<MODE>::N - 1];
+  uint32_t* blk = s_bits + 16 * (loc & 0xfffu);
+  lds_set_bit(blk, loc >> 12);
+  const uint32_t kk = K != 0 ? (uint32_t)K : k;
+  if constexpr (MODE == kKey16) {
+    Xxh16 x;
+    x.rk1 = mk64(it.d[0], it.d[1]);
+    x.k2 = mk64(it.d[2], it.d[3]);
+    if constexpr (K != 0) {
+#pragma unroll
+      for (uint32_t j = 1; j < (uint32_t)K; ++j) lds_set_bit(blk, x.finish_lo9(c_bloom.rhinit16[j]));
+    } else {
+      for (uint32_t j = 1; j < kk; ++j) lds_set_bit(blk, x.finish_lo9(c_bloom.rhinit16[j]));
+    }
+  } else if constexpr (MODE == kKey24) {
+    XxhFixed<24> x;
+    x.rk0 = mk64(it.d[0], it.d[1]);
+    x.k[0] = mk64(it.d[2], it.d[3]);
+    x.k[1] = mk64(it.d[4], it.d[5]);
+    if constexpr (K != 0) {
+#pragma unroll
+      for (uint32_t j = 1; j < (uint32_t)K; ++j)
+        lds_set_bit(blk, x.finish_lo9(xxh_fixed_rc<24>(c_bloom.seed[j])));
+    } else {
+      for (uint32_t j = 1; j < kk; ++j) lds_set_bit(blk, x.finish_lo9(xxh_fixed_rc<24>(c_bloom.seed[j])));
+    }
+  } else {
+    uint32_t len;
+    const uint8_t* p = key_at<MODE>(keys, offs, stride, sg.key_begin + it.d[0], len);
+    if (len < 32) {
+      const XxhShort x(p, len);
+      for (uint32_t j = 1; j < kk; ++j) lds_set_bit(blk, x.finish_lo9(c_bloom.seed_p5[j]));
+    } else {
+      for (uint32_t j = 1; j < kk; ++j) lds_set_bit(blk, (uint32_t)xxh64_bytes(p, len, c_bloom.seed[j]));
+    }
+  }
+}
+
+__device__ inline uint32_t mbcnt64(uint64_t m)
+{
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// keys [kb, ke) of the leaf, the ones in blocks [wb, wb + wn) into the window image s_bits
+template <int MODE, int K>
+__device__ void bloom_window_keys(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs,
+                                  uint32_t stride, const tkv_amq_segment& sg, uint32_t wb, uint32_t wn,
+                                  uint32_t kb, uint32_t ke, uint32_t* s_bits)
+{
+  constexpr int N = WinItem<MODE>::N;
+  constexpr uint32_t NW = kWinThreads / 64;
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  const uint32_t k = sg.hash_count;
+  if (ke <= kb) return;
+  WinItem<MODE> pend;
+#pragma unroll
+  for (int d = 0; d < N; ++d) pend.d[d] = 0;
+  uint32_t c = 0;  // pending keys, in lanes [0, c)
+  // one 64-key step of this wave; `cur` holds its keys (16 / 24 bytes, loaded a step ahead)
+  auto step = [&](uint32_t base, const WinKey<MODE>& cur) {
+    const uint32_t i = base + lane;
+    WinItem<MODE> it;
+    const uint32_t lb = win_hash<MODE>(keys, offs, stride, sg, min(i, ke - 1), cur, it) - wb;
+    const bool in = i < ke && lb < wn;
+    it.d[N - 1] |= lb & 0xfffu;
+    const uint64_t mask = __ballot(in);
+    const uint32_t m = (uint32_t)__popcll(mask);
+    if (m == 0) return;
+    // a permutation of the lanes: in-window lanes go (in order) behind the pending keys
+    const uint32_t rank = mbcnt64(in ? mask : ~mask) + (in ? 0u : m);
+    const int dest = (int)(((c + rank) & 63u) << 2);
+    WinItem<MODE> pm;
+#pragma unroll
+    for (int d = 0; d < N; ++d) pm.d[d] = (uint32_t)__builtin_amdgcn_ds_permute(dest, (int)it.d[d]);
+    if (c + m >= 64) {
+      WinItem<MODE> full;
+#pragma unroll
+      for (int d = 0; d < N; ++d) full.d[d] = lane < c ? pend.d[d] : pm.d[d];
+      win_insert<MODE, K>(keys, offs, stride, sg, k, full, s_bits);
+      pend = pm;  // the keys that wrapped, in lanes [0, c + m - 64)
+      c = c + m - 64;
+    } else {
+#pragma unroll
+      for (int d = 0; d < N; ++d) pend.d[d] = lane < c ? pend.d[d] : pm.d[d];
+      c += m;
+    }
+  };
+  constexpr bool kPre = MODE == kKey16 || MODE == kKey24;
+  auto load = [&](uint32_t base, WinKey<MODE>& kv) {
+    if constexpr (kPre) win_load<MODE>(keys, sg.key_begin + min(base + lane, ke - 1), kv);
+  };
+  // unrolled by two with the buffers swapping roles (no register copy of a load in flight)
+  WinKey<MODE> A{}, B{};
+  uint32_t base = kb + wave * 64;
+  load(base, A);
+  for (; base < ke; base += 2 * NW * 64) {
+    load(base + NW * 64, B);
+    step(base, A);
+    if (base + NW * 64 >= ke) break;
+    load(base + 2 * NW * 64, A);
+    step(base + NW * 64, B);
+  }
+  if (lane < c) win_insert<MODE, K>(keys, offs, stride, sg, k, pend, s_bits);
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kWinThreads) void bloom_build_window(
+    const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint32_t stride,
+    const tkv_amq_segment* __restrict__ segs, uint32_t n_win, uint32_t win_blocks, uint32_t parts,
+    uint8_t* __restrict__ ws, uint64_t img_stride, uint8_t* __restrict__ out)
+{
+  extern __shared__ uint32_t s_bits[];
+  const uint32_t per_seg = n_win * parts;
+  const uint32_t seg = blockIdx.x / per_seg, r = blockIdx.x - seg * per_seg;
+  const uint32_t w = r / parts, part = r - w * parts;
+  const tkv_amq_segment sg = segs[seg];
+  const uint32_t nb = sg.n_blocks, n = sg.n_keys, k = sg.hash_count;
+  const uint32_t wb = w * win_blocks;
+  if (k == 0 || wb >= nb) return;  // no filter, or a window past this leaf's image
+  const uint32_t wn = min(win_blocks, nb - wb);
+  const uint32_t tid = threadIdx.x;
+  for (uint32_t q = tid; q < wn * 16; q += kWinThreads) s_bits[q] = 0;
+  __syncthreads();
+  const uint32_t chunk = (n + parts - 1) / parts;
+  const uint32_t kb = min(n, part * chunk), ke = min(n, kb + chunk);
+  if (nb <= win_blocks) {  // the whole image in one window: every key (the leaf kernel's loop)
+    bloom_leaf_image<MODE, kWinThreads>(keys, offs, stride, sg, kb, ke, s_bits);
+  } else if (k == 7) {
+    bloom_window_keys<MODE, 7>(keys, offs, stride, sg, wb, wn, kb, ke, s_bits);
+  } else if (k == 8) {
+    bloom_window_keys<MODE, 8>(keys, offs, stride, sg, wb, wn, kb, ke, s_bits);
+  } else {
+    bloom_window_keys<MODE, 0>(keys, offs, stride, sg, wb, wn, kb, ke, s_bits);
+  }
+  __syncthreads();
+  uint8_t* dst8;
+  if (parts == 1) {
+    uint8_t* payload = out + sg.out_offset;
+    if (w == 0 && tid < 4) write_bloom_header(payload, sg, tid);
+    else if (w == 0 && tid < 8) write_page_header(out, sg, kLayoutBloom, tid - 4);
+    dst8 = payload + kBloomHeader + 64ull * wb;
+  } else {
+    dst8 = ws + (uint64_t)(seg * parts + part) * img_stride + 64ull * wb;
+  }
+  uint4* dst = reinterpret_cast<uint4*>(dst8);
+  const uint4* src = reinterpret_cast<const uint4*>(s_bits);
+  for (uint32_t q = tid; q < wn * 4; q += kWinThreads) dst[q] = src[q];
 }
 
 // ---------------------------------------------------------------------------------------
@@ -753,13 +1005,6 @@ inline BloomRecGeom bloom_rec_geom(uint64_t n_keys, uint64_t nb)
   return g;
 }
 
-// Workgroup barrier for LDS hazards only: this wave's LDS operations are complete, its global
-// loads and stores stay in flight (__syncthreads() also drains vmcnt, stores included).
-__device__ inline void lds_barrier()
-{
-  // (the memory clobber keeps the compiler from moving LDS accesses across it)
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-}
 
 // Per-batch tile bookkeeping of bloom_rec_partition (n <= 4 * kRecThreads tiles; thread i owns
 // tiles 4i..4i+3): cursor[t] += prev[t] (the previous batch's run lengths), prev[t] = 0 (the
@@ -1515,8 +1760,51 @@ template <>
 struct VqfKeyBuf<kKey24> {
   uint64_t w[3];
 };
+// Variable-length keys (the reference's KeyView ranges): the bytes of a key under 32 bytes
+// (XxhShort's lanes, 4-byte tail, tail bytes) and the offsets of the key this lane loads
+// next, so a step's byte loads need no offset load of their own: the offsets run one load
+// ahead of the bytes.  Keys of 32 bytes or more are hashed from memory where they are hashed.
+template <>
+struct VqfKeyBuf<kKeyVar> {
+  uint64_t l[3];
+  uint32_t t4, tb, len;
+  uint64_t off;
+  uint64_t noff;
+  uint32_t nlen;
+};
 template <int MODE>
-constexpr bool kVqfPrefetch = MODE == kKey16 || MODE == kKey24;
+constexpr bool kVqfPrefetch = MODE == kKey16 || MODE == kKey24 || MODE == kKeyVar;
+// vqf_decide_ring's producers prefetch 16- and 24-byte keys only (three rotating buffers of
+// variable-length keys would cost the ring kernel its three workgroups per CU)
+template <int MODE>
+constexpr bool kVqfRingPrefetch = MODE == kKey16 || MODE == kKey24;
+
+// the bytes of the key whose offsets `prev` holds, and the offsets of key gi_next.  Every lane
+// issues the same loads (clamped to a safe address when the key is shorter: the offsets
+// array holds >= 16 bytes), so the count in flight is fixed.
+__device__ inline void vqf_load_var(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs,
+                                    uint64_t gi_next, const VqfKeyBuf<kKeyVar>& prev,
+                                    VqfKeyBuf<kKeyVar>& kb)
+{
+  const uint64_t off = prev.noff;
+  const uint32_t len = prev.nlen;
+  const uint8_t* p = keys + off;
+  const uint8_t* safe = reinterpret_cast<const uint8_t*>(offs);
+  const bool sh = len < 32;
+  const uint32_t n8 = len >> 3, nb = len & 3;
+#pragma unroll
+  for (uint32_t j = 0; j < 3; ++j) kb.l[j] = ld64_unaligned(sh && j < n8 ? p + 8 * j : safe);
+  const uint8_t* q = p + 8 * n8;
+  kb.t4 = ld32_unaligned(sh && (len & 4) ? q : safe);
+  q += len & 4;
+  const uint32_t c0 = *(sh && nb > 0 ? q : safe), c1 = *(sh && nb > 1 ? q + 1 : safe),
+                 c2 = *(sh && nb > 2 ? q + 2 : safe);
+  kb.tb = c0 | c1 << 8 | c2 << 16;
+  kb.len = len;
+  kb.off = off;
+  kb.noff = offs[gi_next];
+  kb.nlen = (uint32_t)(offs[gi_next + 1] - kb.noff);
+}
 
 template <int MODE>
 __device__ inline void vqf_load_key(const uint8_t* __restrict__ keys, uint64_t gi, VqfKeyBuf<MODE>& kb)
@@ -1542,6 +1830,9 @@ __device__ inline uint64_t vqf_key_hash(const uint8_t* __restrict__ keys,
   } else if constexpr (MODE == kKey24) {
     const XxhFixed<24> x(kb.w);
     return x.finish(xxh_fixed_rc<24>(kVqfHashSeed));
+  } else if constexpr (MODE == kKeyVar) {
+    if (kb.len < 32) return XxhShort(kb.len, kb.l, kb.t4, kb.tb).finish(kVqfHashSeed + kP5);
+    return xxh64_bytes(keys + kb.off, kb.len, kVqfHashSeed);
   } else {
     return hash_key<MODE>(keys, offs, stride, gi, kVqfHashSeed);
   }
@@ -1657,7 +1948,10 @@ __device__ void vqf_decide_body(const uint8_t* __restrict__ keys, const uint64_t
     if constexpr (kVqfPrefetch<MODE>) {
       // branch-free (clamped index, select on the result): straight-line code lets the
       // compiler count vmcnt exactly instead of draining every outstanding access
-      vqf_load_key<MODE>(keys, sg.key_begin + min(inext + 64, n - 1), kv_load);
+      if constexpr (MODE == kKeyVar)  // bytes of chunk + 2 (offsets in kv_hash), offsets of + 3
+        vqf_load_var(keys, offs, sg.key_begin + min(inext + 128, n - 1), kv_hash, kv_load);
+      else
+        vqf_load_key<MODE>(keys, sg.key_begin + min(inext + 64, n - 1), kv_load);
       *pend_ptr = pend_val;
       const uint64_t hh = vqf_key_hash<MODE>(keys, offs, stride, 0, kv_hash);
       hn = vnext ? hh : 0;
@@ -1798,8 +2092,17 @@ __device__ void vqf_decide_body(const uint8_t* __restrict__ keys, const uint64_t
   KB kv0{}, kvA{}, kvB{};
   if constexpr (kVqfPrefetch<MODE>) {
     if (n > 0) {
-      vqf_load_key<MODE>(keys, sg.key_begin + min(lane, n - 1), kv0);
-      vqf_load_key<MODE>(keys, sg.key_begin + min(lane + 64, n - 1), kvA);
+      if constexpr (MODE == kKeyVar) {
+        KB first{};
+        const uint64_t g0 = sg.key_begin + min(lane, n - 1);
+        first.noff = offs[g0];
+        first.nlen = (uint32_t)(offs[g0 + 1] - first.noff);
+        vqf_load_var(keys, offs, sg.key_begin + min(lane + 64, n - 1), first, kv0);
+        vqf_load_var(keys, offs, sg.key_begin + min(lane + 128, n - 1), kv0, kvA);
+      } else {
+        vqf_load_key<MODE>(keys, sg.key_begin + min(lane, n - 1), kv0);
+        vqf_load_key<MODE>(keys, sg.key_begin + min(lane + 64, n - 1), kvA);
+      }
     }
   }
   VqfLoc cur = vqf_locate<T>(lane < n ? vqf_key_hash<MODE>(keys, offs, stride, sg.key_begin + lane, kv0) : 0,
@@ -1829,17 +2132,8 @@ template <int T, int MODE>
 __device__ inline void vqf_decide_dispatch(const uint8_t* keys, const uint64_t* offs,
                                            uint32_t stride, const tkv_amq_segment& sg,
                                            uint32_t seg_index, VqfWorkspace ws, uint64_t* recs,
-                                           uint32_t* cnt, bool match_lds, bool compact_ok,
-                                           int cnt_mode)
+                                           uint32_t* cnt, bool match_lds, bool compact_ok)
 {
-  if (cnt_mode == kCntU8) {  // <= kVqfU8LdsBlocks -> at most 18 block-id bits
-    vqf_decide_body<T, MODE, 18, false, false, kCntU8>(keys, offs, stride, sg, seg_index, ws, recs, cnt, compact_ok);
-    return;
-  }
-  if (cnt_mode == kCntGlobal) {  // <= kVqfMaxBlocks
-    vqf_decide_body<T, MODE, 24, false, false, kCntGlobal>(keys, offs, stride, sg, seg_index, ws, recs, cnt, compact_ok);
-    return;
-  }
   // kVqfMaxLdsBlocks = 16384 -> at most 14 block-id bits
   if (sg.n_blocks <= 512) {
     if (T == 8 && compact_ok) {
@@ -1864,18 +2158,36 @@ __global__ __launch_bounds__(64) void vqf_decide(const uint8_t* __restrict__ key
                                                  int flags)
 {
   const bool match_lds = flags & 1, compact_ok = flags & 2;
-  const int cnt_mode = (flags >> 2) & 3;
   extern __shared__ __attribute__((aligned(16))) uint32_t s_cnt[];
   const tkv_amq_segment sg = segs[blockIdx.x];
   const VqfWorkspace ws = vqf_workspace(ws_base, n_segs);
   if (!vqf_ws_ok(segs, n_segs, ws_bytes, ws)) return;
   uint64_t* recs = vqf_records(ws, segs, n_segs);
   if (sg.tag_bits == 8)
-    vqf_decide_dispatch<8, MODE>(keys, offs, stride, sg, blockIdx.x, ws, recs, s_cnt, match_lds, compact_ok,
-                                 cnt_mode);
+    vqf_decide_dispatch<8, MODE>(keys, offs, stride, sg, blockIdx.x, ws, recs, s_cnt, match_lds, compact_ok);
   else if (sg.tag_bits == 16)
-    vqf_decide_dispatch<16, MODE>(keys, offs, stride, sg, blockIdx.x, ws, recs, s_cnt, match_lds, compact_ok,
-                                  cnt_mode);
+    vqf_decide_dispatch<16, MODE>(keys, offs, stride, sg, blockIdx.x, ws, recs, s_cnt, match_lds, compact_ok);
+}
+
+// Batches with a leaf past kVqfMaxLdsBlocks (VqfCountMode kCntU8 / kCntGlobal): a kernel of
+// their own, so the wider block-id matches do not raise vqf_decide's registers (and cut its
+// waves per SIMD) for every batch.
+template <int MODE, int CNT>
+__global__ __launch_bounds__(64) void vqf_decide_big(const uint8_t* __restrict__ keys,
+                                                     const uint64_t* __restrict__ offs, uint32_t stride,
+                                                     const tkv_amq_segment* __restrict__ segs,
+                                                     void* ws_base, uint64_t ws_bytes, uint32_t n_segs)
+{
+  constexpr int NBITS = CNT == kCntU8 ? 18 : 24;  // kVqfU8LdsBlocks / kVqfMaxBlocks
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_cnt[];
+  const tkv_amq_segment sg = segs[blockIdx.x];
+  const VqfWorkspace ws = vqf_workspace(ws_base, n_segs);
+  if (!vqf_ws_ok(segs, n_segs, ws_bytes, ws)) return;
+  uint64_t* recs = vqf_records(ws, segs, n_segs);
+  if (sg.tag_bits == 8)
+    vqf_decide_body<8, MODE, NBITS, false, false, CNT>(keys, offs, stride, sg, blockIdx.x, ws, recs, s_cnt, false);
+  else if (sg.tag_bits == 16)
+    vqf_decide_body<16, MODE, NBITS, false, false, CNT>(keys, offs, stride, sg, blockIdx.x, ws, recs, s_cnt, false);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1936,17 +2248,20 @@ __device__ void vqf_ring_produce(const uint8_t* __restrict__ keys, const uint64_
   const uint64_t R = (uint64_t)nb * C::kBuckets;
   const uint64_t magic = sg.mod_magic;
   const uint64_t mask = ~0ull << sg.hash_val_shift;  // filter_builder.hpp:187
-  using KB = VqfKeyBuf<MODE>;
+  // (variable-length keys are read where they are hashed here: kVqfRingPrefetch)
+  using KB = typename std::conditional<kVqfRingPrefetch<MODE>, VqfKeyBuf<MODE>, VqfKeyBuf<kKeyFixed>>::type;
   // a producer's next three chunks of keys are in flight (one chunk's load latency is longer
   // than the time to produce it); the loop is unrolled by three so the buffers rotate
   constexpr uint32_t kDepth = 3, kStep = kRingProducers;
   auto load = [&](uint32_t q, KB& kv) {  // clamped, not skipped: a fixed count in flight
-    if constexpr (kVqfPrefetch<MODE>) vqf_load_key<MODE>(keys, sg.key_begin + min(q * 64 + lane, n - 1), kv);
+    if constexpr (kVqfRingPrefetch<MODE>) vqf_load_key<MODE>(keys, sg.key_begin + min(q * 64 + lane, n - 1), kv);
   };
   auto produce = [&](uint32_t q, KB& kv) {
     const uint32_t i = q * 64 + lane;
     const bool valid = i < n;
-    const uint64_t h = valid ? vqf_key_hash<MODE>(keys, offs, stride, sg.key_begin + i, kv) : 0;
+    uint64_t h = 0;
+    if constexpr (kVqfRingPrefetch<MODE>) h = valid ? vqf_key_hash<MODE>(keys, offs, stride, sg.key_begin + i, kv) : 0;
+    else h = valid ? hash_key<MODE>(keys, offs, stride, sg.key_begin + i, kVqfHashSeed) : 0;
     load(q + kDepth * kStep, kv);
     const VqfLoc l = vqf_locate<T>(h, valid, mask, R, magic);
     uint32_t ab, ao;
@@ -1993,7 +2308,7 @@ __device__ void vqf_ring_produce(const uint8_t* __restrict__ keys, const uint64_
   };
   if (w >= n_chunks) return;
   KB kv0{}, kv1{}, kv2{};
-  if constexpr (!kVqfPrefetch<MODE>) {
+  if constexpr (!kVqfRingPrefetch<MODE>) {
     // other key shapes are read where they are hashed: no buffers to rotate, and one copy of
     // the (long) hash code keeps the kernel at three workgroups per CU
     for (uint32_t q = w; q < n_chunks; q += kStep) produce(q, kv0);
@@ -2963,6 +3278,8 @@ using namespace tkv;
 
 namespace {
 
+inline uint64_t div_up(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
+
 constexpr uint32_t kBloomLdsBudget = 64 * 1024;  // dynamic LDS a launch gets without the attribute
 // Leaf images are built in LDS up to the whole CU's LDS (a 160 KB image: 1.3M bits, ~130K
 // keys at 10 bits/key; TurtleKV leaves of small items reach ~80K keys): one workgroup per
@@ -3001,6 +3318,54 @@ inline uint32_t bloom_split_parts(uint32_t n_segs, uint64_t n_keys, uint64_t max
 inline uint64_t bloom_split_ws_bytes(uint32_t n_segs, uint32_t parts, uint64_t max_blocks)
 {
   return parts < 2 ? 0 : (uint64_t)n_segs * parts * 64 * max_blocks;
+}
+
+// The window path (bloom_build_window): leaves whose image exceeds kBloomLeafLdsBudget, cut
+// into W windows.  A single 16-byte-key filter of more than kWinMonoMax windows takes the tiled
+// monolithic build instead (it hashes each key once, whatever the tile count).
+constexpr uint32_t kWinMonoMax = 4;
+constexpr uint32_t kChipCUs = 256;  // MI355X; plans are made without a device
+
+inline uint32_t bloom_window_count(uint64_t max_blocks)
+{
+  return (uint32_t)div_up(64 * max_blocks, kBloomLeafLdsBudget);
+}
+
+inline uint32_t bloom_window_blocks(uint64_t max_blocks)
+{
+  return (uint32_t)div_up(max_blocks, bloom_window_count(max_blocks));
+}
+
+// Parts per leaf: enough (leaf, window, part) workgroups to fill the chip in whole rounds,
+// at >= kWinMinKeys keys per part; every extra part adds a partial image to write and merge
+inline uint32_t bloom_window_parts(uint32_t n_segs, uint64_t n_keys, uint64_t max_blocks)
+{
+  constexpr uint32_t kWinMinKeys = 4096;
+  if (n_segs == 0) return 1;
+  const uint64_t W = bloom_window_count(max_blocks);
+  const uint64_t per_cu = 64 * bloom_window_blocks(max_blocks) <= kBloomLeafLdsBudget / 2 ? 2 : 1;
+  const uint64_t G = kChipCUs * per_cu;
+  uint64_t max_p = n_keys / n_segs / kWinMinKeys;
+  if (max_p > kSplitMaxParts) max_p = kSplitMaxParts;
+  uint32_t best = 1;
+  double best_cost = 1e30;
+  for (uint64_t p = 1; p <= (max_p < 1 ? 1 : max_p); ++p) {
+    const double rounds = (double)div_up((uint64_t)n_segs * W * p, G);
+    const double cost = rounds / (double)p + (p > 1 ? 0.03 * (double)p : 0.0);
+    if (cost < best_cost - 1e-9) {
+      best_cost = cost;
+      best = (uint32_t)p;
+    }
+  }
+  return best;
+}
+
+// a batch the window path takes (n_keys: the batch's keys; mono16: one filter of 16-byte keys)
+inline bool bloom_window_path(uint32_t n_segs, uint64_t max_blocks, bool mono16)
+{
+  const uint32_t W = bloom_window_count(max_blocks);
+  if (W < 2 || W > kWinMaxWindows) return false;
+  return !(n_segs == 1 && mono16 && W > kWinMonoMax);
 }
 
 template <uint32_t NT>
@@ -3063,7 +3428,6 @@ inline uint32_t probe_grid(uint64_t n, bool ex)
   return (uint32_t)(g < cap ? g : cap);
 }
 
-inline uint64_t div_up(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
 
 // Kernel attributes (dynamic LDS above 64 KiB) are set once per device: a process may drive
 // several GPUs from different threads.
@@ -3355,7 +3719,12 @@ int tkv_amq_plan(int kind, const uint64_t* counts, const uint64_t* src_ids, uint
     *ws_bytes = 0;
     if (kind == TKV_AMQ_VQF && bpk != 0)
       *ws_bytes = vqf_temp_offset(n_segs) + kVqfTempStride * block_base + 8 * key_begin + 64;
-    if (kind == TKV_AMQ_BLOOM && bloom_partitioned(n_segs, max_blocks, key_begin))
+    // (the window path for one 16-byte-key filter above kWinMonoMax windows is not taken: the
+    // monolithic workspace below; any other window batch, its partial images)
+    if (kind == TKV_AMQ_BLOOM && bpk != 0 && bloom_window_path(n_segs, max_blocks, true))
+      *ws_bytes = bloom_split_ws_bytes(n_segs, bloom_window_parts(n_segs, key_begin, max_blocks),
+                                       max_blocks);
+    else if (kind == TKV_AMQ_BLOOM && bloom_partitioned(n_segs, max_blocks, key_begin))
       *ws_bytes = bloom_rec_eligible(max_blocks, key_begin)  // 16-byte keys
                       ? bloom_rec_geom(key_begin, max_blocks).bytes
                       : bloom_part_geom(key_begin, max_blocks).bytes;
@@ -3437,6 +3806,46 @@ int tkv_amq_build(int kind, const uint8_t* keys, const uint64_t* offs, uint32_t 
                          parts, chunks, w, img, d_out);
       return hipGetLastError() == hipSuccess ? TKV_AMQ_OK : TKV_AMQ_INTERNAL;
     }
+    const bool mono16 = bloom_partitioned(n_segs, max_blocks, n_keys) && mode == kKey16 && d_ws;
+    if (bloom_window_path(n_segs, max_blocks, mono16)) {
+      // leaves beyond one CU's LDS: windows of the image, parts of the keys
+      const uint32_t W = bloom_window_count(max_blocks), wblk = bloom_window_blocks(max_blocks);
+      uint32_t wparts = bloom_window_parts(n_segs, n_keys, max_blocks);
+      if (wparts > 1 && (!d_ws || ws_bytes < bloom_split_ws_bytes(n_segs, wparts, max_blocks)))
+        wparts = 1;  // no workspace for partial images: one part per leaf, no merge
+      static std::once_flag win_attr[kMaxDevices];
+      once_per_device(win_attr, [] {
+        for (const void* f : {reinterpret_cast<const void*>(&bloom_build_window<kKey16>),
+                              reinterpret_cast<const void*>(&bloom_build_window<kKey24>),
+                              reinterpret_cast<const void*>(&bloom_build_window<kKeyFixed>),
+                              reinterpret_cast<const void*>(&bloom_build_window<kKeyVar>)})
+          (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)kBloomLeafLdsBudget);
+      });
+      const int bmode = build_key_mode(keys, offs, stride);
+      const dim3 grid(n_segs * W * wparts), block(kWinThreads);
+      const size_t wl = 64ull * wblk;
+      uint8_t* w = static_cast<uint8_t*>(d_ws);
+      const uint64_t img = 64ull * max_blocks;
+      if (bmode == kKey24)
+        hipLaunchKernelGGL(bloom_build_window<kKey24>, grid, block, wl, s, keys, offs, stride, d_segs,
+                           W, wblk, wparts, w, img, d_out);
+      else if (mode == kKey16)
+        hipLaunchKernelGGL(bloom_build_window<kKey16>, grid, block, wl, s, keys, offs, stride, d_segs,
+                           W, wblk, wparts, w, img, d_out);
+      else if (mode == kKeyFixed)
+        hipLaunchKernelGGL(bloom_build_window<kKeyFixed>, grid, block, wl, s, keys, offs, stride, d_segs,
+                           W, wblk, wparts, w, img, d_out);
+      else
+        hipLaunchKernelGGL(bloom_build_window<kKeyVar>, grid, block, wl, s, keys, offs, stride, d_segs,
+                           W, wblk, wparts, w, img, d_out);
+      if (wparts > 1) {
+        const uint32_t chunks = (uint32_t)div_up(4ull * max_blocks, kMergeThreads);
+        hipLaunchKernelGGL(bloom_split_merge, dim3(n_segs * chunks), dim3(kMergeThreads), 0, s, d_segs,
+                           wparts, chunks, w, img, d_out);
+      }
+      return hipGetLastError() == hipSuccess ? TKV_AMQ_OK : TKV_AMQ_INTERNAL;
+    }
     if (lds <= kBloomLeafLdsBudget && n_segs >= kBloomSpreadSegs) {
       const int bmode = build_key_mode(keys, offs, stride);
       if (lds > kBloomLdsBudget) {
@@ -3457,7 +3866,7 @@ int tkv_amq_build(int kind, const uint8_t* keys, const uint64_t* offs, uint32_t 
       return hipGetLastError() == hipSuccess ? TKV_AMQ_OK : TKV_AMQ_INTERNAL;
     }
     const BloomPartGeom pg = bloom_part_geom(n_keys, max_blocks);
-    const bool mono = bloom_partitioned(n_segs, max_blocks, n_keys) && mode == kKey16 && d_ws;
+    const bool mono = mono16;
     if (mono && bloom_rec_eligible(max_blocks, n_keys) &&
         ws_bytes >= bloom_rec_geom(n_keys, max_blocks).bytes) {
       // one monolithic filter: hash once into bit records partitioned by tile, build the tiles
@@ -3514,19 +3923,41 @@ int tkv_amq_build(int kind, const uint8_t* keys, const uint64_t* offs, uint32_t 
   // in the workspace's block records (VqfCountMode)
   const int cnt_mode = max_blocks <= kVqfMaxLdsBlocks ? kCntU32
                        : (max_blocks <= kVqfU8LdsBlocks ? kCntU8 : kCntGlobal);
-  const int flags = match_lds | (fused ? 2 : 0) | (cnt_mode << 2);
+  const int flags = match_lds | (fused ? 2 : 0);
   const size_t lds = cnt_mode == kCntU8 ? (size_t)((max_blocks + 15) & ~15u)
                      : cnt_mode == kCntGlobal ? 16
                      : 4ull * ((max_blocks + 1) & ~1u) + (match_lds ? 8ull * max_blocks : 0);
-  if (lds > kBloomLdsBudget) {
+  const int vmode = build_key_mode(keys, offs, stride);
+  if (cnt_mode != kCntU32) {
+    // a leaf past the u32 count table: vqf_decide_big for the whole batch (fused place is out
+    // of reach for such a leaf, so the records are the 8-byte ones)
     static std::once_flag big_attr[kMaxDevices];
     once_per_device(big_attr, [] {
-      for (const void* f : {reinterpret_cast<const void*>(&vqf_decide<kKey16>),
-                            reinterpret_cast<const void*>(&vqf_decide<kKey24>),
-                            reinterpret_cast<const void*>(&vqf_decide<kKeyFixed>),
-                            reinterpret_cast<const void*>(&vqf_decide<kKeyVar>)})
+      for (const void* f : {reinterpret_cast<const void*>(&vqf_decide_big<kKey16, kCntU8>),
+                            reinterpret_cast<const void*>(&vqf_decide_big<kKey24, kCntU8>),
+                            reinterpret_cast<const void*>(&vqf_decide_big<kKeyFixed, kCntU8>),
+                            reinterpret_cast<const void*>(&vqf_decide_big<kKeyVar, kCntU8>)})
         (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     });
+    const dim3 g(n_segs), b(64);
+#define TKV_DECIDE_BIG(CNT)                                                                         \
+  do {                                                                                              \
+    if (vmode == kKey16)                                                                            \
+      hipLaunchKernelGGL((vqf_decide_big<kKey16, CNT>), g, b, lds, s, keys, offs, stride, d_segs, d_ws, \
+                         ws_bytes, n_segs);                                                         \
+    else if (vmode == kKey24)                                                                       \
+      hipLaunchKernelGGL((vqf_decide_big<kKey24, CNT>), g, b, lds, s, keys, offs, stride, d_segs, d_ws, \
+                         ws_bytes, n_segs);                                                         \
+    else if (mode == kKeyFixed)                                                                     \
+      hipLaunchKernelGGL((vqf_decide_big<kKeyFixed, CNT>), g, b, lds, s, keys, offs, stride, d_segs,    \
+                         d_ws, ws_bytes, n_segs);                                                   \
+    else                                                                                            \
+      hipLaunchKernelGGL((vqf_decide_big<kKeyVar, CNT>), g, b, lds, s, keys, offs, stride, d_segs,      \
+                         d_ws, ws_bytes, n_segs);                                                   \
+  } while (0)
+    if (cnt_mode == kCntU8) TKV_DECIDE_BIG(kCntU8);
+    else TKV_DECIDE_BIG(kCntGlobal);
+#undef TKV_DECIDE_BIG
   }
   // the ring kernel for small batches of leaves its count table holds (a batch with a larger
   // leaf takes vqf_decide: the one-wave body inside the ring kernel set its registers, and so
@@ -3537,10 +3968,11 @@ int tkv_amq_build(int kind, const uint8_t* keys, const uint64_t* offs, uint32_t 
   // wins, 1.25 vs 1.45 ms)
   // 24-byte keys (TurtleKV's default key size hint), 8-byte aligned, are loaded ahead of
   // their hash like 16-byte ones
-  const int vmode = build_key_mode(keys, offs, stride);
   const bool prefetched = vmode == kKey16 || vmode == kKey24;
-  if (n_segs <= (prefetched ? kVqfRingMaxSegs : kVqfRingMaxSegsOther) &&
-      max_blocks <= kRingMaxBlocks) {
+  if (cnt_mode != kCntU32) {
+    // (decided above)
+  } else if (n_segs <= (prefetched ? kVqfRingMaxSegs : kVqfRingMaxSegsOther) &&
+             max_blocks <= kRingMaxBlocks) {
     static std::once_flag ring_attr[kMaxDevices];
     once_per_device(ring_attr, [] {
       for (const void* f : {reinterpret_cast<const void*>(&vqf_decide_ring<kKey16>),
