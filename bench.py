@@ -3,7 +3,8 @@
 
   python bench.py [--gpus N] [--steps K] [--warmup W]
                   [--workload bloom10|bloom12|vqf12|probe10|probe_vqf12|bloom10k24|vqf12k24|
-                              bloom10var|bloom10mono|bloom12hash] [--total-keys T]
+                              bloom10var|vqf12var|bloom12big|bloom10mono|bloom12hash]
+                  [--total-keys T]
 
 One step = one pass of the hot path over one batch: build every leaf filter of
 `--keys-per-gpu` (default 100M, BASELINE config 2) 16-byte keys held in HBM, S = 16,384 keys
@@ -55,6 +56,8 @@ WORKLOADS = {
     "bloom10mono": (0, 10, "Bloom @10 bits/key, one monolithic filter per GPU"),
     "bloom10var": (0, 10, "Bloom @10 bits/key, variable-length keys (8-31 B)"),
     "bloom12hash": (0, 12, "Bloom @12 bits/key, one filter over all GPUs' keys, hash-range sharded"),
+    "vqf12var": (1, 12, "VQF @12 bits/key, variable-length keys (8-31 B) in generation order"),
+    "bloom12big": (0, 12, "Bloom @12 bits/key, 200K-key leaves (images past one CU's LDS: the window path)"),
 }
 # BASELINE config 5 read literally: one monolithic filter whose bitmap byte ranges are owned by
 # the ranks (route -> RCCL all-to-all of the keys -> range build; turtle_kv_amd.dist)
@@ -62,7 +65,8 @@ HASH_SHARDED = {"bloom12hash"}
 # workloads whose one filter spans every key of the GPU (the monolithic
 # single-filter Bloom variant)
 MONOLITHIC = {"bloom10mono"}
-KEY_BYTES = {"bloom10k24": 24, "vqf12k24": 24, "bloom10var": 0}  # 0: variable length (offsets)
+KEY_BYTES = {"bloom10k24": 24, "vqf12k24": 24, "bloom10var": 0, "vqf12var": 0}  # 0: variable length
+LEAF_KEYS = {"bloom12big": 200_000}  # default keys per leaf where it is not SEG_KEYS
 SWEEP_LEAVES = (64, 256, 1024)                   # + the whole batch
 
 
@@ -267,7 +271,7 @@ def main():
            if kind == amq.VQF else 0)
     from turtle_kv_amd import dist as tdist
     strong = args.total_keys is not None
-    leaf_keys = args.leaf_keys or SEG_KEYS
+    leaf_keys = args.leaf_keys or LEAF_KEYS.get(args.workload, SEG_KEYS)
     if args.workload in MONOLITHIC and args.leaf_keys is None:
         leaf_keys = args.total_keys // world if strong else args.keys_per_gpu
     if strong:

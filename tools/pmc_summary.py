@@ -16,11 +16,27 @@ import csv
 import json
 import os
 
-# gfx950 integer VALU issue: one wave64 instruction per ~4 cycles per SIMD, measured by
-# tools/ubench_valu.hip (profiles/r01/ubench_valu.log)
+# gfx950 integer VALU issue, measured by tools/ubench_valu.hip (profiles/r03/ubench_valu.log):
+# v_xor_b32 / v_add_u32 streams, 8 independent chains per wave, 8 waves per SIMD, >= 2 s of
+# back-to-back launches: 578.8-584.5 G wave64-instructions/s at an in-kernel clock of 2.38-2.39
+# GHz, i.e. one wave64 integer instruction per ~4.2 shader cycles per SIMD (v_fma_f32 the same:
+# 583 G/s).  The guide's 2-cycle v_fma_f32 figure (MI355X_MICROARCH.md:473) is not reached by
+# these streams: 1 wave/SIMD 439, 2 waves 531, 4 waves 560, 8 waves 579 G/s.
 SIMDS = 1024
-CYCLES_PER_VALU = 4.0
-CLOCK_GHZ = 2.4
+VALU_PEAK_G = 578.8   # measured, G wave64-instructions/s (the v_xor_b32 row at 8 waves/SIMD)
+VALU_PEAK_NOTE = ("measured integer VALU issue rate: tools/ubench_valu.hip v_xor_b32 at 8 waves/SIMD, "
+                  "in-kernel clock 2.387 GHz (profiles/r03/ubench_valu.log)")
+CUS = 256
+
+
+def kernel_ms(d, kernel):
+    """mean duration of the kernel's dispatches in a counter-collection CSV (ms)"""
+    rows = list(csv.DictReader(open(os.path.join(d, "run_counter_collection.csv"))))
+    seen = {}
+    for r in rows:
+        if any(n in r["Kernel_Name"] for n in kernel.split(",")):
+            seen[r["Dispatch_Id"]] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6
+    return sum(seen.values()) / len(seen) if seen else None
 
 
 def agg(d, kernel):
@@ -47,6 +63,9 @@ def main():
     ap.add_argument("--fetch", required=True)
     ap.add_argument("--write", required=True)
     ap.add_argument("--sq", default=None)
+    ap.add_argument("--valu", default=None,
+                    help="pass with SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_INSTS_VALU "
+                         "GRBM_GUI_ACTIVE (VALUBusy, clock)")
     ap.add_argument("--tcc", default=None,
                     help="pass with TCC_EA0_RDREQ_sum / TCC_HIT_sum / TCC_MISS_sum (probes)")
     ap.add_argument("--ms", type=float, default=None,
@@ -74,8 +93,24 @@ def main():
             "valu_instr_per_key": round(valu * 64 / a.keys, 1),
             "GRBM_GUI_ACTIVE_per_xcd": clk_cycles,
             "valu_cycles_per_wave_instr_per_simd": round(clk_cycles / (valu / SIMDS), 3),
-            "valu_peak_ginstr_s_at_2.4GHz": SIMDS * CLOCK_GHZ / CYCLES_PER_VALU,
         })
+    if a.valu:
+        v = agg(a.valu, a.kernel)
+        ms = kernel_ms(a.valu, a.kernel)
+        clk = v["GRBM_GUI_ACTIVE"] / 8  # rocprofv3 sums GRBM_GUI_ACTIVE over the 8 XCDs
+        res.update({
+            "valu_busy_frac": round(v["SQ_ACTIVE_INST_VALU"] / CUS / clk, 4),
+            "valu_busy_note": "VALUBusy = sum SQ_ACTIVE_INST_VALU (quad-cycles, 4 SIMDs) / CUs / "
+                              "(GRBM_GUI_ACTIVE / 8): the fraction of cycles each SIMD issues VALU",
+            "valu_thread_util": round(v["SQ_THREAD_CYCLES_VALU"] / (v["SQ_ACTIVE_INST_VALU"] * 64), 4),
+            "clock_ghz_effective": round(clk / (ms * 1e-3) / 1e9, 3) if ms else None,
+            "kernel_ms_under_pmc": round(ms, 4) if ms else None,
+        })
+        if "valu_instr_per_key" not in res:
+            res["valu_instr_per_key"] = round(v["SQ_INSTS_VALU"] * 64 / a.keys, 1)
+    if "valu_instr_per_key" in res:
+        res["valu_peak_ginstr_s"] = VALU_PEAK_G
+        res["valu_peak_note"] = VALU_PEAK_NOTE
     if a.tcc:
         t = agg(a.tcc, a.kernel)
         req = t["TCC_EA0_RDREQ_sum"]
@@ -86,7 +121,8 @@ def main():
         })
         if a.ms:
             res["ea_read_requests_g_per_s"] = round(req / (a.ms * 1e-3) / 1e9, 2)
-    res["source"] = f"rocprofv3 --pmc passes: {a.fetch}, {a.write}, {a.sq or '-'}, {a.tcc or '-'}"
+    res["source"] = (f"rocprofv3 --pmc passes: {a.fetch}, {a.write}, {a.sq or '-'}, {a.tcc or '-'}, "
+                     f"{a.valu or '-'}")
     out = a.out or os.path.join("profiles", f"traffic_{a.workload}.json")
     with open(out, "w") as fh:
         json.dump(res, fh, indent=1)

@@ -27,6 +27,9 @@ def main():
                     help="16 (splitmix keys, sorted per leaf for VQF), 24 (random 24-byte keys) or "
                          "0 (variable length, 8-31 bytes through an offsets array); the last two "
                          "in generation order")
+    ap.add_argument("--var-lens", default="8,32",
+                    help="variable-length keys: lengths uniform in [lo, hi) (e.g. 24,25: all 24 bytes "
+                         "through an offsets array, the reference's KeyView form of TurtleKV keys)")
     ap.add_argument("--cap", type=int, default=0,
                     help="VQF payload capacity (default: the TreeOptions filter page at --bpk)")
     ap.add_argument("--no-ws", action="store_true",
@@ -50,7 +53,8 @@ def main():
         elif a.key_bytes == 0:
             g = torch.Generator(device="cuda")
             g.manual_seed(42)
-            lens = torch.randint(8, 32, (S * L,), dtype=torch.int64, device="cuda", generator=g)
+            lo, hi = (int(x) for x in a.var_lens.split(","))
+            lens = torch.randint(lo, hi, (S * L,), dtype=torch.int64, device="cuda", generator=g)
             offs = torch.zeros(S * L + 1, dtype=torch.int64, device="cuda")
             torch.cumsum(lens, 0, out=offs[1:])
             blob = torch.randint(0, 256, (int(offs[-1].item()),), dtype=torch.uint8, device="cuda",

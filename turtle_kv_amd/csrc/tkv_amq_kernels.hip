@@ -304,15 +304,138 @@ __device__ inline void bloom_leaf_image(const uint8_t* __restrict__ keys,
   }
 }
 
-// One workgroup per leaf filter (batches of >= kBloomSplitSegs leaves).
+// Variable-length keys, sorted by length before they are hashed.  XXH64 of a short key runs a
+// different number of lane, 4-byte and byte steps per length, and a wave pays for every step
+// any of its lanes needs (8..31-byte keys in one wave: ~71 VALU per seed instead of ~47 on
+// average).  The Bloom filter does not depend on the order of its keys, so each chunk of
+// kVarChunk(NT) keys is counting-sorted by exact length in LDS, as (offset, length) pairs, and
+// hashed in that order: a wave then holds one or two lengths.  The hash loop runs two keys
+// deep: the next key's bytes (XxhShort's lanes, 4-byte tail, tail bytes) are loaded while the
+// current one is hashed.
+template <uint32_t NT>
+constexpr uint32_t kVarChunk = 4 * NT;
+constexpr uint32_t kVarBins = 64;  // lengths 0..31 and ">= 32" (bin 32); 64 for the scan wave
+template <uint32_t NT>
+constexpr uint32_t kVarAuxWords = 2 * kVarBins + 2 * kVarChunk<NT>;
+
+struct VarKey {  // a key under 32 bytes in registers (a longer one: its address)
+  uint64_t l[3];
+  uint32_t t4, tb, len;
+  const uint8_t* p;
+};
+
+__device__ inline void var_key_load(const uint8_t* p, uint32_t len, const uint8_t* safe, VarKey& k)
+{
+  const bool sh = len < 32;
+  const uint32_t n8 = len >> 3, nb = len & 3;
+#pragma unroll
+  for (uint32_t j = 0; j < 3; ++j) k.l[j] = ld64_unaligned(sh && j < n8 ? p + 8 * j : safe);
+  const uint8_t* q = p + 8 * n8;
+  k.t4 = ld32_unaligned(sh && (len & 4) ? q : safe);
+  q += len & 4;
+  const uint32_t c0 = *(sh && nb > 0 ? q : safe), c1 = *(sh && nb > 1 ? q + 1 : safe),
+                 c2 = *(sh && nb > 2 ? q + 2 : safe);
+  k.tb = c0 | c1 << 8 | c2 << 16;
+  k.len = len;
+  k.p = p;
+}
+
+template <int K>
+__device__ inline void var_key_insert(uint32_t* s_bits, uint32_t nb, uint32_t k, const VarKey& v)
+{
+  if (v.len < 32) {
+    const XxhShort x(v.len, v.l, v.t4, v.tb);
+    const uint64_t h0 = x.finish(c_bloom.seed_p5[0]);
+    uint32_t* blk = s_bits + 16 * (uint32_t)__umul64hi(h0, (uint64_t)nb);
+    lds_set_bit(blk, (uint32_t)h0 & 511u);
+    if constexpr (K != 0) {
+#pragma unroll
+      for (uint32_t j = 1; j < (uint32_t)K; ++j) lds_set_bit(blk, x.finish_lo9(c_bloom.seed_p5[j]));
+    } else {
+      for (uint32_t j = 1; j < k; ++j) lds_set_bit(blk, x.finish_lo9(c_bloom.seed_p5[j]));
+    }
+  } else {
+    bloom_insert_any<K, kKeyVar>(s_bits, nb, k, v.p, v.len);
+  }
+}
+
+template <uint32_t NT, int K>
+__device__ void bloom_var_sorted_image(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs,
+                                       const tkv_amq_segment& sg, uint32_t kb, uint32_t ke,
+                                       uint32_t* s_bits, uint32_t* s_aux)
+{
+  constexpr uint32_t C = kVarChunk<NT>, U = C / NT;
+  uint32_t* bins = s_aux;                        // [kVarBins] counts of this chunk
+  uint32_t* start = s_aux + kVarBins;            // [kVarBins] their exclusive prefix
+  uint2* kl = reinterpret_cast<uint2*>(s_aux + 2 * kVarBins);  // [C] (offset - base, length), sorted
+  const uint32_t tid = threadIdx.x, nb = sg.n_blocks, k = sg.hash_count;
+  const uint64_t* o = offs + sg.key_begin;
+  const uint8_t* safe = reinterpret_cast<const uint8_t*>(offs);  // >= 16 readable bytes
+  for (uint32_t c0 = kb; c0 < ke; c0 += C) {
+    const uint32_t cn = min(C, ke - c0);
+    const uint64_t base = o[c0];
+    if (tid < kVarBins) bins[tid] = 0;
+    __syncthreads();
+    uint32_t bin[U], rank[U], rel[U], len[U];
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u) {
+      const uint32_t j = u * NT + tid;
+      const uint32_t i = c0 + min(j, cn - 1);
+      const uint64_t b = o[i];
+      const uint64_t l = o[i + 1] - b;
+      rel[u] = (uint32_t)(b - base);
+      len[u] = (uint32_t)l;
+      bin[u] = l < 32 ? (uint32_t)l : 32u;
+      rank[u] = j < cn ? atomicAdd(bins + bin[u], 1u) : 0u;
+    }
+    __syncthreads();
+    if (tid < 64) {  // wave 0: exclusive scan of the bins
+      const uint32_t v = bins[tid];
+      uint32_t inc = v;
+#pragma unroll
+      for (uint32_t d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(inc, d, 64);
+        if (tid >= d) inc += y;
+      }
+      start[tid] = inc - v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u) {
+      const uint32_t j = u * NT + tid;
+      if (j < cn) kl[start[bin[u]] + rank[u]] = make_uint2(rel[u], len[u]);
+    }
+    __syncthreads();
+    const uint8_t* kbase = keys + base;
+    VarKey A, B;
+    auto load = [&](uint32_t q, VarKey& v) {
+      const uint2 e = kl[min(q, cn - 1)];
+      var_key_load(kbase + e.x, e.y, safe, v);
+    };
+    load(tid, A);
+    for (uint32_t q = tid; q < cn; q += 2 * NT) {
+      load(q + NT, B);
+      var_key_insert<K>(s_bits, nb, k, A);
+      if (q + NT >= cn) break;
+      load(q + 2 * NT, A);
+      var_key_insert<K>(s_bits, nb, k, B);
+    }
+    __syncthreads();  // (the next chunk rewrites bins and the pairs)
+  }
+}
+
+// One workgroup per leaf filter (batches of >= kBloomSplitSegs leaves).  Variable-length keys
+// (var_sort): the length sort's scratch comes first in the dynamic LDS, then the image.
 template <int MODE, uint32_t NT>
 __global__ __launch_bounds__(NT) void bloom_build_lds(const uint8_t* __restrict__ keys,
                                                        const uint64_t* __restrict__ offs,
                                                        uint32_t stride,
                                                        const tkv_amq_segment* __restrict__ segs,
-                                                       uint8_t* __restrict__ out)
+                                                       uint8_t* __restrict__ out, uint32_t var_sort)
 {
-  extern __shared__ uint32_t s_bits[];
+  extern __shared__ uint32_t s_lds[];
+  const bool sorted = MODE == kKeyVar && var_sort;
+  uint32_t* s_bits = s_lds + (sorted ? kVarAuxWords<NT> : 0u);
   const tkv_amq_segment sg = segs[blockIdx.x];
   const uint32_t n = sg.n_keys, nb = sg.n_blocks, k = sg.hash_count;
   if (k == 0) return;  // bits_per_key == 0: no filter (filter_builder.hpp:115-117)
@@ -321,7 +444,17 @@ __global__ __launch_bounds__(NT) void bloom_build_lds(const uint8_t* __restrict_
 
   for (uint32_t w = tid; w < nwords; w += NT) s_bits[w] = 0;
   __syncthreads();
-  bloom_leaf_image<MODE, NT>(keys, offs, stride, sg, 0, n, s_bits);
+  if constexpr (MODE == kKeyVar) {
+    if (sorted) {
+      if (k == 7) bloom_var_sorted_image<NT, 7>(keys, offs, sg, 0, n, s_bits, s_lds);
+      else if (k == 8) bloom_var_sorted_image<NT, 8>(keys, offs, sg, 0, n, s_bits, s_lds);
+      else bloom_var_sorted_image<NT, 0>(keys, offs, sg, 0, n, s_bits, s_lds);
+    } else {
+      bloom_leaf_image<MODE, NT>(keys, offs, stride, sg, 0, n, s_bits);
+    }
+  } else {
+    bloom_leaf_image<MODE, NT>(keys, offs, stride, sg, 0, n, s_bits);
+  }
   __syncthreads();
 
   uint8_t* payload = out + sg.out_offset;
@@ -3375,13 +3508,18 @@ void launch_bloom_lds(int bmode, int mode, uint32_t n_segs, size_t lds, hipStrea
 {
   const dim3 grid(n_segs), block(NT);
   if (bmode == kKey24)
-    hipLaunchKernelGGL((bloom_build_lds<kKey24, NT>), grid, block, lds, s, keys, offs, stride, d_segs, d_out);
+    hipLaunchKernelGGL((bloom_build_lds<kKey24, NT>), grid, block, lds, s, keys, offs, stride, d_segs, d_out, 0u);
   else if (mode == kKey16)
-    hipLaunchKernelGGL((bloom_build_lds<kKey16, NT>), grid, block, lds, s, keys, offs, stride, d_segs, d_out);
+    hipLaunchKernelGGL((bloom_build_lds<kKey16, NT>), grid, block, lds, s, keys, offs, stride, d_segs, d_out, 0u);
   else if (mode == kKeyFixed)
-    hipLaunchKernelGGL((bloom_build_lds<kKeyFixed, NT>), grid, block, lds, s, keys, offs, stride, d_segs, d_out);
-  else
-    hipLaunchKernelGGL((bloom_build_lds<kKeyVar, NT>), grid, block, lds, s, keys, offs, stride, d_segs, d_out);
+    hipLaunchKernelGGL((bloom_build_lds<kKeyFixed, NT>), grid, block, lds, s, keys, offs, stride, d_segs, d_out, 0u);
+  else {
+    // variable-length keys sorted by length per chunk when the scratch fits beside the image
+    const size_t aux = 4ull * kVarAuxWords<NT>;
+    const uint32_t sort = lds + aux <= kBloomLeafLdsBudget ? 1u : 0u;
+    hipLaunchKernelGGL((bloom_build_lds<kKeyVar, NT>), grid, block, lds + (sort ? aux : 0), s, keys, offs,
+                       stride, d_segs, d_out, sort);
+  }
 }
 
 inline uint32_t vqf_slots(int t) { return t == 8 ? 48u : 28u; }
@@ -3848,7 +3986,8 @@ int tkv_amq_build(int kind, const uint8_t* keys, const uint64_t* offs, uint32_t 
     }
     if (lds <= kBloomLeafLdsBudget && n_segs >= kBloomSpreadSegs) {
       const int bmode = build_key_mode(keys, offs, stride);
-      if (lds > kBloomLdsBudget) {
+      // (variable-length keys add their length-sort scratch: kVarAuxWords)
+      if (lds + (mode == kKeyVar ? 4ull * kVarAuxWords<1024> : 0ull) > kBloomLdsBudget) {
         static std::once_flag big_attr[kMaxDevices];
         once_per_device(big_attr, [] {
           for (const void* f : {reinterpret_cast<const void*>(&bloom_build_lds<kKey16, 1024>),
