@@ -624,7 +624,10 @@ def bench_hash_sharded(args, torch, dist, amq, world, rank, dev, bpk, label, pg=
         ev[1].record()
         owned = keys
     ev[2].record()
-    hs.build_range(owned)
+    if pg:
+        hs.build_owned(owned)  # bit records (k <= 8) or keys, as routed
+    else:
+        hs.build_range(owned)
     ev[3].record()
     torch.cuda.synchronize()
     route_ms, a2a_ms, build_ms = (ev[i].elapsed_time(ev[i + 1]) for i in range(3))

@@ -28,7 +28,7 @@
  *                           TreeOptions::filter_page_size_log2 / expected_items_per_leaf /
  *                           leaf_data_size (tree/tree_options.hpp:177-258, tree_options.cpp:57-60,
  *                           tree/packed_leaf_page.hpp:307-311, core/packed_sizeof_edit.hpp:13-15)
- *   tkv_amq_bloom_route / tkv_amq_bloom_build_range
+ *   tkv_amq_bloom_route / tkv_amq_bloom_build_range (and their _records forms)
  *                           one monolithic Bloom filter sharded by hash range over GPUs
  *                           (BASELINE config 5; the llfs build_bloom_filter_page it replaces is
  *                           called at tree/filter_builder.hpp:126-135)
@@ -205,6 +205,25 @@ int tkv_amq_bloom_build_range(const uint8_t* d_keys16, uint64_t n_keys, const tk
                               uint32_t n_blocks, uint32_t tile_begin, uint32_t tile_end,
                               uint8_t* d_out, void* d_workspace, uint64_t workspace_bytes,
                               void* stream);
+
+/* The same two steps with 12-byte bit records in place of the keys (hash_count <= 8, i.e.
+ * bits_per_key <= 12; InvalidArgument otherwise): tkv_amq_bloom_route_records hashes each key
+ * once and writes its record (block in tile, the k bit indices, the tile relative to its
+ * owner's first tile) into d_recs12 ordered by owner, so the all-to-all carries 12 bytes per key
+ * instead of 16 and the owner does not hash again; tkv_amq_bloom_build_range_records builds the
+ * owner's tiles from the records it received (at most 3,584 tiles per range). */
+uint64_t tkv_amq_bloom_route_records_ws_bytes(uint64_t n_keys, uint32_t n_parts);
+int tkv_amq_bloom_route_records(const uint8_t* d_keys16, uint64_t n_keys, const tkv_amq_segment* d_seg,
+                                uint32_t n_blocks, uint32_t hash_count, uint32_t n_parts,
+                                uint8_t* d_recs12, uint32_t* d_part_counts, void* d_workspace,
+                                uint64_t workspace_bytes, void* stream);
+uint64_t tkv_amq_bloom_build_range_records_ws_bytes(uint64_t n_recs, uint32_t tile_begin,
+                                                    uint32_t tile_end);
+int tkv_amq_bloom_build_range_records(const uint8_t* d_recs12, uint64_t n_recs,
+                                      const tkv_amq_segment* d_seg, uint32_t n_blocks,
+                                      uint32_t hash_count, uint32_t tile_begin, uint32_t tile_end,
+                                      uint8_t* d_out, void* d_workspace, uint64_t workspace_bytes,
+                                      void* stream);
 
 /* Batched probe: query i tests the filter of segment d_query_seg[i].  d_result[i] = 1 if
  * the key may be present, 0 if the filter rejects it (reject_page == kTrue).  A segment index

@@ -142,3 +142,77 @@ def test_empty_ranges_write_the_header(amq, torch):
     for r in range(1, world):
         merged |= outs[r]
     assert torch.equal(merged, whole)
+
+
+def _route_records(amq, torch, keys, plan, n_parts):
+    from turtle_kv_amd.filters import _ptr, _stream_handle
+    L = amq.abi.lib()
+    n = keys.shape[0]
+    seg = plan.segs[0]
+    recs = torch.empty((n, 12), dtype=torch.uint8, device="cuda")
+    counts = torch.zeros(n_parts, dtype=torch.int32, device="cuda")
+    ws = torch.empty(int(L.tkv_amq_bloom_route_records_ws_bytes(n, n_parts)), dtype=torch.uint8,
+                     device="cuda")
+    amq.abi.check(L.tkv_amq_bloom_route_records(_ptr(keys), n, _ptr(plan.device_segs()),
+                                                int(seg["n_blocks"]), int(seg["hash_count"]), n_parts,
+                                                _ptr(recs), _ptr(counts), _ptr(ws), ws.numel(),
+                                                _stream_handle()), "route_records")
+    torch.cuda.synchronize()
+    return recs, counts.cpu().numpy().astype(np.int64)
+
+
+def _build_range_records(amq, torch, recs, plan, t0, t1, out):
+    from turtle_kv_amd.filters import _ptr, _stream_handle
+    L = amq.abi.lib()
+    m = recs.shape[0]
+    seg = plan.segs[0]
+    ws = torch.empty(max(1, int(L.tkv_amq_bloom_build_range_records_ws_bytes(m, t0, t1))),
+                     dtype=torch.uint8, device="cuda")
+    amq.abi.check(L.tkv_amq_bloom_build_range_records(_ptr(recs) if m else None, m,
+                                                      _ptr(plan.device_segs()), int(seg["n_blocks"]),
+                                                      int(seg["hash_count"]), t0, t1, _ptr(out),
+                                                      _ptr(ws), ws.numel(), _stream_handle()),
+                  "build_range_records")
+
+
+@pytest.mark.parametrize("n_keys,bpk,n_parts,dup", [(3_000_000, 12, 3, 0), (1_500_001, 10, 8, 0),
+                                                   (700_000, 12, 1, 0), (2_000_000, 12, 4, 600_000),
+                                                   (720_000, 12, 8, 0), (900_000, 5, 2, 0)])
+def test_route_records_and_range_build_equal_monolithic(oracle, amq, torch, n_keys, bpk, n_parts, dup):
+    """The record form of hash-range sharding (k <= 8): every key hashed once by its sender into
+    a 12-byte bit record with its tile relative to its owner; each owner builds its tiles from
+    the records alone.  Equal to the one-GPU build and the oracle: k = 8, 7 and 3, duplicate
+    keys (one tile's regions overflow), ranks past the last tile (720K keys: 17 tiles over 8)."""
+    from turtle_kv_amd.dist import hash_shard_tiles
+    keys = amq.gen_keys16(21, 0, n_keys)
+    if dup:
+        keys[n_keys - dup:] = keys[n_keys // 3]
+    plan = amq.plan_filters(0, [n_keys], bpk)
+    assert int(plan.segs[0]["hash_count"]) <= 8
+    whole = amq.build_all_filters(plan, amq.KeyBatch.fixed(keys))
+    recs, counts = _route_records(amq, torch, keys, plan, n_parts)
+    assert counts.sum() == n_keys
+    T, q = hash_shard_tiles(int(plan.segs[0]["n_blocks"]), n_parts)
+    out = torch.zeros(plan.total_out_bytes, dtype=torch.uint8, device="cuda")
+    base = np.concatenate([[0], np.cumsum(counts)])
+    for p in range(n_parts):
+        _build_range_records(amq, torch, recs[int(base[p]):int(base[p + 1])], plan, min(T, p * q),
+                             min(T, (p + 1) * q), out)
+    torch.cuda.synchronize()
+    assert torch.equal(out, whole)
+    st, ref = oracle.bloom_build(keys.cpu().numpy(), n_keys, bpk, src_page_id=0)
+    assert st == 0 and out.cpu().numpy().tobytes() == ref.tobytes()
+
+
+def test_route_records_refuse_k_above_8(amq, torch):
+    from turtle_kv_amd.filters import _ptr, _stream_handle
+    L = amq.abi.lib()
+    keys = amq.gen_keys16(22, 0, 1000)
+    plan = amq.plan_filters(0, [1000], 16)     # k = 11
+    ws = torch.empty(int(L.tkv_amq_bloom_route_records_ws_bytes(1000, 2)), dtype=torch.uint8, device="cuda")
+    recs = torch.empty((1000, 12), dtype=torch.uint8, device="cuda")
+    counts = torch.zeros(2, dtype=torch.int32, device="cuda")
+    st = L.tkv_amq_bloom_route_records(_ptr(keys), 1000, _ptr(plan.device_segs()),
+                                       int(plan.segs[0]["n_blocks"]), 11, 2, _ptr(recs), _ptr(counts),
+                                       _ptr(ws), ws.numel(), _stream_handle())
+    assert st == amq.abi.INVALID_ARGUMENT

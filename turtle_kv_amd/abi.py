@@ -86,7 +86,8 @@ EXPORTS = [
     "tkv_amq_filter_page_size_log2", "tkv_amq_plan_pages", "tkv_amq_probe_ex",
     "tkv_amq_vqf_probe_hashed_ex", "tkv_amq_bloom_probe_hashed_ex",
     "tkv_amq_bloom_route_ws_bytes", "tkv_amq_bloom_route", "tkv_amq_bloom_build_range_ws_bytes",
-    "tkv_amq_bloom_build_range",
+    "tkv_amq_bloom_build_range", "tkv_amq_bloom_route_records_ws_bytes", "tkv_amq_bloom_route_records",
+    "tkv_amq_bloom_build_range_records_ws_bytes", "tkv_amq_bloom_build_range_records",
 ]
 
 # tkv_amq_key_view (libstdc++ std::string_view layout)
@@ -173,6 +174,14 @@ def lib(build_if_missing: bool = True):
         L.tkv_amq_bloom_build_range_ws_bytes.argtypes = [u64, u32, u32]
         L.tkv_amq_bloom_build_range.restype = i32
         L.tkv_amq_bloom_build_range.argtypes = [vp, u64, vp, u32, u32, u32, vp, vp, u64, vp]
+        L.tkv_amq_bloom_route_records_ws_bytes.restype = u64
+        L.tkv_amq_bloom_route_records_ws_bytes.argtypes = [u64, u32]
+        L.tkv_amq_bloom_route_records.restype = i32
+        L.tkv_amq_bloom_route_records.argtypes = [vp, u64, vp, u32, u32, u32, vp, vp, vp, u64, vp]
+        L.tkv_amq_bloom_build_range_records_ws_bytes.restype = u64
+        L.tkv_amq_bloom_build_range_records_ws_bytes.argtypes = [u64, u32, u32]
+        L.tkv_amq_bloom_build_range_records.restype = i32
+        L.tkv_amq_bloom_build_range_records.argtypes = [vp, u64, vp, u32, u32, u32, u32, vp, vp, u64, vp]
     _lib = L
     return L
 

@@ -1198,25 +1198,95 @@ __device__ inline uint32_t rec_tile(uint32_t w0, uint32_t w1, uint32_t w2)
   return (w0 >> 28) | ((w1 >> 27) << 4) | ((w2 >> 27) << 9);
 }
 
-// one key of the record path: local tile (~0 outside the window), block in tile, bit record
+// a 16-byte key's block in the filter and its k <= 8 bit indices (b_j = b_0 for j >= k)
 template <int K>
-__device__ inline uint32_t rec_hash(const uint4& kv, uint32_t nb, uint32_t k, uint32_t tile0,
-                                    uint32_t n_tiles, uint32_t& w0, uint32_t& w1, uint32_t& w2)
+__device__ inline uint32_t rec_hash_bits(const uint4& kv, uint32_t nb, uint32_t k, uint32_t (&b)[8])
 {
   const Xxh16 x((uint64_t)kv.x | ((uint64_t)kv.y << 32), (uint64_t)kv.z | ((uint64_t)kv.w << 32));
   const uint64_t h0 = x.finish(c_bloom.rhinit16[0]);
-  const uint32_t blk = (uint32_t)__umul64hi(h0, (uint64_t)nb);
-  const uint32_t t = blk / kBloomTileBlocks - tile0;  // wraps below the window
-  uint32_t b[8];
   b[0] = (uint32_t)h0 & 511u;
 #pragma unroll
   for (uint32_t j = 1; j < 8; ++j) {
     if (K != 0 ? j < (uint32_t)K : j < k) b[j] = x.finish_lo9(c_bloom.rhinit16[j]) & 511u;
     else b[j] = b[0];
   }
+  return (uint32_t)__umul64hi(h0, (uint64_t)nb);
+}
+
+// one key of the record path: local tile (~0 outside the window), block in tile, bit record
+template <int K>
+__device__ inline uint32_t rec_hash(const uint4& kv, uint32_t nb, uint32_t k, uint32_t tile0,
+                                    uint32_t n_tiles, uint32_t& w0, uint32_t& w1, uint32_t& w2)
+{
+  uint32_t b[8];
+  const uint32_t blk = rec_hash_bits<K>(kv, nb, k, b);
+  const uint32_t t = blk / kBloomTileBlocks - tile0;  // wraps below the window
   rec_pack(blk & (kBloomTileBlocks - 1), t, b, w0, w1, w2);
   return t < n_tiles ? t : ~0u;
 }
+
+// tkv_amq_bloom_route_records' scatter pass: the same key ranges and slots as
+// bloom_part_keys<1> (after the same count pass), but each key leaves as its 12-byte bit record
+// (rec_pack) with its tile relative to its owner's first tile (owner = tile / q): k <= 8 only.
+template <uint32_t NT, int K>
+__device__ void bloom_route_recs_body(const uint4* __restrict__ keys, const tkv_amq_segment& sg,
+                                      uint32_t* __restrict__ ws, uint32_t n_parts, uint32_t per,
+                                      uint32_t n_cap, uint32_t q, uint32_t* __restrict__ out,
+                                      uint32_t* s_tile)
+{
+  const uint32_t tid = threadIdx.x, w = blockIdx.x, nb = sg.n_blocks, k = sg.hash_count;
+  const uint32_t n = n_cap;
+  const uint32_t b = min(n, w * per), e = min(n, b + per);
+  constexpr int U = 4;
+  for (uint32_t i0 = b; i0 < e; i0 += NT * U) {
+    uint4 kv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t i = i0 + u * NT + tid;
+      if (i < e) kv[u] = load_nt16(keys + i);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t i = i0 + u * NT + tid;
+      if (i >= e) continue;
+      uint32_t bits[8], r0, r1, r2;
+      // global tile of the key, then its owner and its tile within the owner's range
+      const uint32_t blk = rec_hash_bits<K>(kv[u], nb, k, bits);
+      const uint32_t tg = blk / kBloomTileBlocks;
+      const uint32_t owner = tg / q;
+      if (owner >= n_parts) continue;
+      rec_pack(blk & (kBloomTileBlocks - 1), tg - owner * q, bits, r0, r1, r2);
+      const uint32_t slot = atomicAdd(s_tile + owner, 1u);
+      uint3 v;
+      v.x = r0;
+      v.y = r1;
+      v.z = r2;
+      reinterpret_cast<uint3*>(out)[slot] = v;
+    }
+  }
+}
+
+template <uint32_t NT>
+__global__ __launch_bounds__(NT) void bloom_route_recs(const uint4* __restrict__ keys,
+                                                        const tkv_amq_segment* __restrict__ segs,
+                                                        uint32_t* __restrict__ ws, uint32_t n_parts,
+                                                        uint32_t per, uint32_t n_cap, uint32_t q,
+                                                        uint32_t* __restrict__ out)
+{
+  extern __shared__ uint32_t s_tile[];
+  const tkv_amq_segment sg = segs[0];
+  const uint32_t tid = threadIdx.x, w = blockIdx.x;
+  const uint32_t* H = ws + (uint64_t)w * n_parts;
+  const uint32_t* base = ws + (uint64_t)gridDim.x * n_parts + n_parts;
+  for (uint32_t t = tid; t < n_parts; t += NT) s_tile[t] = base[t] + H[t];
+  __syncthreads();
+  const uint32_t k = sg.hash_count;
+  if (k == 0 || k > 8) return;  // (the ABI refuses k > 8: a record holds 8 bit indices)
+  if (k == 7) bloom_route_recs_body<NT, 7>(keys, sg, ws, n_parts, per, n_cap, q, out, s_tile);
+  else if (k == 8) bloom_route_recs_body<NT, 8>(keys, sg, ws, n_parts, per, n_cap, q, out, s_tile);
+  else bloom_route_recs_body<NT, 0>(keys, sg, ws, n_parts, per, n_cap, q, out, s_tile);
+}
+
 
 // 16-byte keys (k > 8): the record is the key; only its tile is computed here
 __device__ inline uint32_t rec_key_tile(const uint4& kv, uint32_t nb, uint32_t tile0, uint32_t n_tiles)
@@ -1232,6 +1302,8 @@ struct RecArgs {
   uint32_t from_seg;
   uint8_t* ws;
   BloomRecGeom g;
+  const uint32_t* recs;  // instead of keys: 12-byte bit records with local tiles (hash-range
+                         // shards, tkv_amq_bloom_route_records), n of them
 };
 
 // batches of B keys, U = B / kRecThreads per thread; RAW: 16-byte keys instead of bit records.
@@ -1239,9 +1311,17 @@ struct RecArgs {
 // barrier, scan (two), place into the planes, LDS barrier, write out.  The histogram is
 // double-buffered, so no barrier is needed after the write-out: the next batch's hash touches
 // only the other histogram, and its scan comes after a barrier.
-template <int K, bool RAW>
+// one 12-byte record of a.recs (records input: no hashing, the tile is in the record)
+__device__ inline uint4 load_rec12(const uint32_t* recs, uint32_t i)
+{
+  const uint3 r = reinterpret_cast<const uint3*>(recs)[i];
+  return make_uint4(r.x, r.y, r.z, 0u);
+}
+
+template <int K, bool RAW, bool RECIN = false>
 __device__ void bloom_rec_partition_body(const tkv_amq_segment& sg, const RecArgs& a, uint32_t* lds)
 {
+  static_assert(!(RAW && RECIN), "records carry k <= 8 bit indices");
   constexpr uint32_t B = RAW ? kRecBatchKeys : kRecBatchBits;
   constexpr uint32_t U = B / kRecThreads;
   constexpr uint32_t RB = RAW ? 16 : 12;  // record bytes
@@ -1273,8 +1353,12 @@ __device__ void bloom_rec_partition_body(const tkv_amq_segment& sg, const RecArg
   uint8_t* const sink = a.ws;
   const uint32_t last_key = ke > 0 ? ke - 1 : 0;
   uint4 kv[U];
+  auto load_in = [&](uint32_t i) -> uint4 {
+    if constexpr (RECIN) return load_rec12(a.recs, i);
+    else return load_nt16(keys + i);
+  };
 #pragma unroll
-  for (uint32_t u = 0; u < U; ++u) kv[u] = load_nt16(keys + min(kb + u * kRecThreads + tid, last_key));
+  for (uint32_t u = 0; u < U; ++u) kv[u] = load_in(min(kb + u * kRecThreads + tid, last_key));
   uint32_t parity = 0;
   for (uint32_t b0 = kb; b0 < ke; b0 += B, parity ^= 1) {
     uint32_t* hist = hist2 + parity * T;
@@ -1292,6 +1376,12 @@ __device__ void bloom_rec_partition_body(const tkv_amq_segment& sg, const RecArg
         r1[u] = kv[u].y;
         r2[u] = kv[u].z;
         r3[u] = kv[u].w;
+      } else if constexpr (RECIN) {
+        r0[u] = kv[u].x;
+        r1[u] = kv[u].y;
+        r2[u] = kv[u].z;
+        t = rec_tile(r0[u], r1[u], r2[u]);
+        t = t < T ? t : ~0u;
       } else {
         t = i < ke ? rec_hash<K>(kv[u], nb, k, a.tile0, T, r0[u], r1[u], r2[u]) : ~0u;
       }
@@ -1300,7 +1390,7 @@ __device__ void bloom_rec_partition_body(const tkv_amq_segment& sg, const RecArg
     }
 #pragma unroll
     for (uint32_t u = 0; u < U; ++u)  // the next batch's keys
-      kv[u] = load_nt16(keys + min(b0 + B + u * kRecThreads + tid, last_key));
+      kv[u] = load_in(min(b0 + B + u * kRecThreads + tid, last_key));
     lds_barrier();
     const uint32_t total = rec_scan(hist, prev, start, cursor, T, wsum);
 #pragma unroll
@@ -1366,7 +1456,9 @@ __global__ __launch_bounds__(kRecThreads) void bloom_rec_partition(const tkv_amq
   const tkv_amq_segment sg = segs[0];
   const uint32_t k = sg.hash_count;
   if (k == 0) return;
-  if (k == 7) bloom_rec_partition_body<7, false>(sg, a, s_rec);
+  if (a.recs) {
+    if (k <= 8) bloom_rec_partition_body<0, false, true>(sg, a, s_rec);
+  } else if (k == 7) bloom_rec_partition_body<7, false>(sg, a, s_rec);
   else if (k == 8) bloom_rec_partition_body<8, false>(sg, a, s_rec);
   else if (k < 8) bloom_rec_partition_body<0, false>(sg, a, s_rec);
   else bloom_rec_partition_body<0, true>(sg, a, s_rec);
@@ -3622,7 +3714,8 @@ inline bool bloom_rec_eligible(uint64_t n_blocks, uint64_t n_keys)
 // tiles [tile0, tile0 + g.n_tiles)
 inline void launch_rec_build(const BloomRecGeom& g, hipStream_t s, const uint4* keys, uint32_t n,
                              uint32_t tile0, uint32_t from_seg, uint32_t hdr_always,
-                             const tkv_amq_segment* d_segs, uint8_t* ws, uint8_t* d_out)
+                             const tkv_amq_segment* d_segs, uint8_t* ws, uint8_t* d_out,
+                             const uint32_t* recs = nullptr)
 {
   static std::once_flag lds_attr[kMaxDevices];
   once_per_device(lds_attr, [] {
@@ -3630,7 +3723,7 @@ inline void launch_rec_build(const BloomRecGeom& g, hipStream_t s, const uint4* 
                               hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)bloom_rec_lds_bytes(kRecMaxTiles));
   });
-  const RecArgs a{keys, n, tile0, from_seg, ws, g};
+  const RecArgs a{keys, n, tile0, from_seg, ws, g, recs};
   hipLaunchKernelGGL(bloom_rec_partition, dim3(g.P), dim3(kRecThreads), bloom_rec_lds_bytes(g.n_tiles),
                      s, d_segs, a);
   hipLaunchKernelGGL(bloom_rec_tile, dim3(g.n_tiles), dim3(kRecTileThreads), 64ull * kBloomTileBlocks,
@@ -4214,6 +4307,74 @@ int tkv_amq_bloom_route(const uint8_t* d_keys16, uint64_t n_keys, const tkv_amq_
   if (hipMemcpyAsync(d_part_counts, w + g.h_words, 4ull * n_parts, hipMemcpyDeviceToDevice, s) !=
       hipSuccess)
     return TKV_AMQ_INTERNAL;
+  return hipGetLastError() == hipSuccess ? TKV_AMQ_OK : TKV_AMQ_INTERNAL;
+}
+
+uint64_t tkv_amq_bloom_route_records_ws_bytes(uint64_t n_keys, uint32_t n_parts)
+{
+  return tkv_amq_bloom_route_ws_bytes(n_keys, n_parts);
+}
+
+int tkv_amq_bloom_route_records(const uint8_t* d_keys16, uint64_t n_keys, const tkv_amq_segment* d_seg,
+                                uint32_t n_blocks, uint32_t hash_count, uint32_t n_parts,
+                                uint8_t* d_recs12, uint32_t* d_part_counts, void* d_ws, uint64_t ws_bytes,
+                                void* stream)
+{
+  if (tkv_amq_device_count() == 0) return TKV_AMQ_UNAVAILABLE;
+  if (n_parts == 0 || n_parts > kRouteMaxParts || n_blocks == 0 || !d_seg || !d_part_counts ||
+      n_keys > 0xffffffffull || hash_count == 0 || hash_count > 8)
+    return TKV_AMQ_INVALID_ARGUMENT;
+  if (n_keys && (!d_keys16 || !d_recs12 || (reinterpret_cast<uintptr_t>(d_keys16) & 15) ||
+                 (reinterpret_cast<uintptr_t>(d_recs12) & 3)))
+    return TKV_AMQ_INVALID_ARGUMENT;
+  const BloomPartGeom g = bloom_route_geom(n_keys, n_parts);
+  if (!d_ws || ws_bytes < g.bytes) return TKV_AMQ_INVALID_ARGUMENT;
+  const hipStream_t s = as_stream(stream);
+  uint32_t* w = static_cast<uint32_t*>(d_ws);
+  set_part_attributes();
+  const uint32_t q = shard_tiles_per_part(n_blocks, n_parts);
+  const PartWindow pw{0u, q, 1u, 0u, nullptr};
+  const uint4* k4 = reinterpret_cast<const uint4*>(d_keys16);
+  const size_t hl = 4ull * n_parts;
+  const uint32_t nk = (uint32_t)n_keys;
+  hipLaunchKernelGGL((bloom_part_keys<0, 256>), dim3(g.P), dim3(256), hl, s, k4, d_seg, w, n_parts,
+                     g.per, g.part_off, nk, pw);
+  hipLaunchKernelGGL(bloom_part_scan_cols, dim3(n_parts), dim3(256), 0, s, w, g.P, n_parts);
+  hipLaunchKernelGGL(bloom_part_scan_tiles, dim3(1), dim3(256), 0, s, w, g.P, n_parts);
+  hipLaunchKernelGGL(bloom_route_recs<256>, dim3(g.P), dim3(256), hl, s, k4, d_seg, w, n_parts, g.per, nk,
+                     q, reinterpret_cast<uint32_t*>(d_recs12));
+  if (hipMemcpyAsync(d_part_counts, w + g.h_words, 4ull * n_parts, hipMemcpyDeviceToDevice, s) !=
+      hipSuccess)
+    return TKV_AMQ_INTERNAL;
+  return hipGetLastError() == hipSuccess ? TKV_AMQ_OK : TKV_AMQ_INTERNAL;
+}
+
+uint64_t tkv_amq_bloom_build_range_records_ws_bytes(uint64_t n_recs, uint32_t tile_begin, uint32_t tile_end)
+{
+  if (tile_end <= tile_begin || tile_end - tile_begin > kRecMaxTiles || n_recs > 0xffffffffull) return 0;
+  return bloom_rec_geom(n_recs, (uint64_t)(tile_end - tile_begin) * kBloomTileBlocks).bytes;
+}
+
+int tkv_amq_bloom_build_range_records(const uint8_t* d_recs12, uint64_t n_recs, const tkv_amq_segment* d_seg,
+                                      uint32_t n_blocks, uint32_t hash_count, uint32_t tile_begin,
+                                      uint32_t tile_end, uint8_t* d_out, void* d_ws, uint64_t ws_bytes,
+                                      void* stream)
+{
+  if (tkv_amq_device_count() == 0) return TKV_AMQ_UNAVAILABLE;
+  const uint32_t T = (uint32_t)div_up(n_blocks, kBloomTileBlocks);
+  if (!d_seg || !d_out || n_blocks == 0 || tile_begin > tile_end || tile_end > T ||
+      tile_end - tile_begin > kRecMaxTiles || n_recs > 0xffffffffull || hash_count == 0 ||
+      hash_count > 8)
+    return TKV_AMQ_INVALID_ARGUMENT;
+  if (n_recs && (!d_recs12 || (reinterpret_cast<uintptr_t>(d_recs12) & 3))) return TKV_AMQ_INVALID_ARGUMENT;
+  if (tile_begin == tile_end) {
+    hipLaunchKernelGGL(bloom_header_only, dim3(1), dim3(64), 0, as_stream(stream), d_seg, d_out);
+    return hipGetLastError() == hipSuccess ? TKV_AMQ_OK : TKV_AMQ_INTERNAL;
+  }
+  const BloomRecGeom g = bloom_rec_geom(n_recs, (uint64_t)(tile_end - tile_begin) * kBloomTileBlocks);
+  if (!d_ws || ws_bytes < g.bytes) return TKV_AMQ_INVALID_ARGUMENT;
+  launch_rec_build(g, as_stream(stream), nullptr, (uint32_t)n_recs, tile_begin, 0u, 1u, d_seg,
+                   static_cast<uint8_t*>(d_ws), d_out, reinterpret_cast<const uint32_t*>(d_recs12));
   return hipGetLastError() == hipSuccess ? TKV_AMQ_OK : TKV_AMQ_INTERNAL;
 }
 

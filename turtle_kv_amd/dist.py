@@ -88,9 +88,11 @@ def allgather_filters(local, gathered=None, group=None):
 # "1B keys, Bloom @12, hash-range sharded across 8 GPUs, RCCL all-gather").  Unlike the leaf
 # filters above, keys must move: every key's bits fall in the 64-byte block its h0 selects, so
 # a rank can only build its byte range of the bitmap from the keys whose blocks fall there.
-# Steps per build: route (reorder the rank's keys by owning rank, tkv_amq_bloom_route), one
-# all-to-all of the keys (RCCL over xGMI), the rank's tile range built in LDS
-# (tkv_amq_bloom_build_range), then the all-gather of the bitmap ranges.
+# Steps per build: route (reorder the rank's keys by owning rank: tkv_amq_bloom_route_records
+# hashes each key once and ships its 12-byte bit record, k <= 8; tkv_amq_bloom_route ships the
+# 16-byte key otherwise), one all-to-all of them (RCCL over xGMI), the rank's tile range built in
+# LDS (tkv_amq_bloom_build_range_records / _build_range), then the all-gather of the bitmap
+# ranges.
 # ---------------------------------------------------------------------------------------
 BLOOM_TILE_BLOCKS = 1024  # blocks per tile, as tkv_amq_bloom_route / _build_range cut them
 
@@ -130,6 +132,12 @@ class HashShardedBloom:
         self.d_seg = self.plan.device_segs(self.dev)
         self.counts = torch.zeros(world, dtype=torch.int32, device=self.dev)
         self._bufs = {}
+        # k <= 8 (bits_per_key <= 12): 12-byte bit records travel instead of the 16-byte keys,
+        # hashed once by their sender (tkv_amq_bloom_route_records); the owner's range build
+        # reads them without hashing (a range of <= 3,584 tiles: the record path's table)
+        self.hash_count = int(seg["hash_count"])
+        self.records = self.hash_count <= 8 and q <= 3584
+        self.unit = 12 if self.records else 16  # bytes per routed key
 
     def _buf(self, name, nbytes):
         import torch
@@ -150,33 +158,43 @@ class HashShardedBloom:
             raise abi.TkvAmqError(abi.INVALID_ARGUMENT, "hash-range sharding takes [n, 16] uint8 "
                                   f"keys (16-byte keys only), got shape {tuple(keys.shape)}")
         n = keys.shape[0]
-        routed = self._buf("routed", 16 * n)[:16 * n].view(n, 16)
-        ws = self._buf("route_ws", int(L.tkv_amq_bloom_route_ws_bytes(n, self.world)))
-        abi.check(L.tkv_amq_bloom_route(_ptr(keys), n, _ptr(self.d_seg), self.n_blocks, self.world,
-                                        _ptr(routed), _ptr(self.counts), _ptr(ws), ws.numel(),
-                                        _stream_handle()), "tkv_amq_bloom_route")
+        u = self.unit
+        routed = self._buf("routed", u * n)[:u * n].view(n, u)
+        if self.records:
+            ws = self._buf("route_ws", int(L.tkv_amq_bloom_route_records_ws_bytes(n, self.world)))
+            abi.check(L.tkv_amq_bloom_route_records(_ptr(keys), n, _ptr(self.d_seg), self.n_blocks,
+                                                    self.hash_count, self.world, _ptr(routed),
+                                                    _ptr(self.counts), _ptr(ws), ws.numel(),
+                                                    _stream_handle()), "tkv_amq_bloom_route_records")
+        else:
+            ws = self._buf("route_ws", int(L.tkv_amq_bloom_route_ws_bytes(n, self.world)))
+            abi.check(L.tkv_amq_bloom_route(_ptr(keys), n, _ptr(self.d_seg), self.n_blocks, self.world,
+                                            _ptr(routed), _ptr(self.counts), _ptr(ws), ws.numel(),
+                                            _stream_handle()), "tkv_amq_bloom_route")
         return routed, self.counts.to(dtype=torch.int64)
 
     def exchange(self, routed, send_counts):
-        """All-to-all of the routed keys: returns the [m, 16] keys this rank owns."""
+        """All-to-all of the routed units (bit records or keys): returns the [m, unit] units
+        this rank owns."""
         import torch
         import torch.distributed as dist
+        u = self.unit
         gloo = dist.get_backend(self.group) != "nccl"
         sc = send_counts.cpu() if gloo else send_counts
         rc = torch.empty_like(sc)
         dist.all_to_all_single(rc, sc, group=self.group)
-        send = [int(x) * 16 for x in sc.tolist()]
-        recv = [int(x) * 16 for x in rc.tolist()]
-        m = sum(recv) // 16
-        out = self._buf("recv", 16 * m)[:16 * m]
+        send = [int(x) * u for x in sc.tolist()]
+        recv = [int(x) * u for x in rc.tolist()]
+        m = sum(recv) // u
+        out = self._buf("recv", u * m)[:u * m]
         src = routed.reshape(-1)
         if gloo:  # CPU rehearsal: stage through host memory
-            host = torch.empty(16 * m, dtype=torch.uint8)
+            host = torch.empty(u * m, dtype=torch.uint8)
             dist.all_to_all_single(host, src.cpu(), recv, send, group=self.group)
             out.copy_(host)
         else:
             dist.all_to_all_single(out, src, recv, send, group=self.group)
-        return out.view(m, 16)
+        return out.view(m, u)
 
     def build_range(self, owned):
         """This rank's tile range of the filter from the keys it owns (into self.out)."""
@@ -191,6 +209,27 @@ class HashShardedBloom:
                                               _ptr(ws), ws.numel(), _stream_handle()),
                   "tkv_amq_bloom_build_range")
 
+    def build_range_records(self, recs):
+        """This rank's tile range of the filter from the bit records it owns (into self.out)."""
+        from . import abi
+        from .filters import _ptr, _stream_handle
+        L = abi.lib()
+        m = recs.shape[0]
+        ws = self._buf("build_ws", int(L.tkv_amq_bloom_build_range_records_ws_bytes(
+            m, self.tile_begin, self.tile_end)))
+        abi.check(L.tkv_amq_bloom_build_range_records(_ptr(recs), m, _ptr(self.d_seg), self.n_blocks,
+                                                      self.hash_count, self.tile_begin, self.tile_end,
+                                                      _ptr(self.out), _ptr(ws), ws.numel(),
+                                                      _stream_handle()),
+                  "tkv_amq_bloom_build_range_records")
+
+    def build_owned(self, owned):
+        """The range build from what exchange() returned (records or keys)."""
+        if self.records:
+            self.build_range_records(owned)
+        else:
+            self.build_range(owned)
+
     @property
     def _collective(self) -> bool:
         """route + all-to-all + all-gather whenever a process group exists (at world size 1
@@ -204,7 +243,7 @@ class HashShardedBloom:
             self.build_range(keys)
             return
         routed, sc = self.route(keys)
-        self.build_range(self.exchange(routed, sc))
+        self.build_owned(self.exchange(routed, sc))
 
     def allgather(self):
         """Every rank's bitmap range -> the whole filter payload (header + bitmap) on every rank.
