@@ -2551,6 +2551,14 @@ __device__ void vqf_ring_produce(const uint8_t* __restrict__ keys, const uint64_
   }
 }
 
+#ifdef TKV_DIAG_RING
+__device__ uint64_t g_diag[4 * 4096];  // per step of leaf 0: wait, count read, decision, spins
+extern "C" int tkv_amq_diag_read(void* host)
+{
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_diag), sizeof(g_diag)) == hipSuccess ? 0 : 13;
+}
+#endif
+
 template <int T, bool kCompact>
 __device__ void vqf_ring_decide(const tkv_amq_segment& sg, uint32_t seg_index, VqfWorkspace ws,
                                 uint64_t* __restrict__ recs, const uint64_t* ring,
@@ -2587,10 +2595,20 @@ __device__ void vqf_ring_decide(const tkv_amq_segment& sg, uint32_t seg_index, V
     S.ranks = (uint32_t)slot[384 + lane];
   };
   auto step = [&](uint32_t c, Slot& S, Slot& next) {
+#ifdef TKV_DIAG_RING
+    const uint64_t d0 = __builtin_amdgcn_s_memtime();
+    uint32_t spins = 0;
+#endif
     while (S.rdy != c + 1) {
       __builtin_amdgcn_s_sleep(1);
       fetch(c, S);
+#ifdef TKV_DIAG_RING
+      ++spins;
+#endif
     }
+#ifdef TKV_DIAG_RING
+    const uint64_t d1 = __builtin_amdgcn_s_memtime();
+#endif
     const uint64_t wloc = S.loc, Mpp = S.pp, Mpa = S.pa, Map = S.ap, Maa = S.aa;
     const uint64_t conf = S.conf;
     const uint32_t ranks = S.ranks;
@@ -2602,6 +2620,10 @@ __device__ void vqf_ring_decide(const tkv_amq_segment& sg, uint32_t seg_index, V
     const uint32_t ao = (uint32_t)(wloc >> (T + 21)) & 127u;
     const uint32_t ab = (uint32_t)(wloc >> (T + 28)) & 16383u;
     const uint32_t cnt_p = cnt[pb], cnt_a = cnt[ab];
+#ifdef TKV_DIAG_RING
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const uint64_t d2 = __builtin_amdgcn_s_memtime();
+#endif
     // LDS operations complete in issue order: the prefetch goes after the count reads, so
     // waiting for the counts does not wait for it.  Neither the hand-off write nor the
     // prefetch is skipped (every lane writes the same word; the last step re-reads the last
@@ -2635,6 +2657,15 @@ __device__ void vqf_ring_decide(const tkv_amq_segment& sg, uint32_t seg_index, V
         }
       }
     }
+#ifdef TKV_DIAG_RING
+    const uint64_t d3 = __builtin_amdgcn_s_memtime();
+    if (lane == 0 && blockIdx.x == 0 && c < 4096) {
+      g_diag[4 * c] = d1 - d0;
+      g_diag[4 * c + 1] = d2 - d1;
+      g_diag[4 * c + 2] = d3 - d2;
+      g_diag[4 * c + 3] = spins | ((uint64_t)__popcll(altmask) << 32);
+    }
+#endif
     const bool alt = (altmask >> lane) & 1;
     const uint32_t chosen = alt ? ab : pb;
     const uint32_t cho = alt ? ao : po;
