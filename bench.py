@@ -21,9 +21,12 @@ partial leaf, 8 seeded-random ones) with the CPU oracle built from independently
 keys ("verified"); probe workloads compare all 200M answers with the oracle's ("fpr_oracle").
 
 The printed JSON line carries `roofline` (dominant kernel, HIP events on the build stream,
-algorithmic bytes) and `cpu_baseline` (the C oracle -- a restatement of the reference's CPU
-path, -O3 -march=native -mbmi2 -mavx2 on this host -- timed on this host's cores on rank 0,
-N = 1 only).
+algorithmic bytes), `valu_roofline` (the bound the build kernels sit on: PMC VALU instructions
+per key against the measured integer VALU issue rate, profiles/traffic_<workload>.json) and
+`cpu_baseline` (the C oracle -- a restatement of the reference's CPU path, -O3 -march=native
+-mbmi2 -mavx2 on this host -- timed on this host's cores by rank 0 after the other ranks have
+exited).  Every rank also runs the end-to-end leg (pinned host keys in, filter pages back to
+pinned host memory over its own PCIe link) at the same time: `e2e_pcie_inclusive`.
 """
 from __future__ import annotations
 

@@ -69,7 +69,8 @@ def main():
     ap.add_argument("--tcc", default=None,
                     help="pass with TCC_EA0_RDREQ_sum / TCC_HIT_sum / TCC_MISS_sum (probes)")
     ap.add_argument("--ms", type=float, default=None,
-                    help="kernel time per launch (ms), for the request rate of --tcc")
+                    help="step time per launch (ms, the bench's HIP events): the request rate of "
+                         "--tcc and the effective clock of --valu")
     ap.add_argument("--keys", type=int, required=True)
     ap.add_argument("--alg-bytes", type=int, required=True)
     ap.add_argument("--out", default=None)
@@ -96,7 +97,9 @@ def main():
         })
     if a.valu:
         v = agg(a.valu, a.kernel)
-        ms = kernel_ms(a.valu, a.kernel)
+        # the step's time from the bench (HIP events) when given: a dispatch timed under
+        # counter collection runs longer than it does alone
+        ms = a.ms or kernel_ms(a.valu, a.kernel)
         clk = v["GRBM_GUI_ACTIVE"] / 8  # rocprofv3 sums GRBM_GUI_ACTIVE over the 8 XCDs
         res.update({
             "valu_busy_frac": round(v["SQ_ACTIVE_INST_VALU"] / CUS / clk, 4),
@@ -104,7 +107,7 @@ def main():
                               "(GRBM_GUI_ACTIVE / 8): the fraction of cycles each SIMD issues VALU",
             "valu_thread_util": round(v["SQ_THREAD_CYCLES_VALU"] / (v["SQ_ACTIVE_INST_VALU"] * 64), 4),
             "clock_ghz_effective": round(clk / (ms * 1e-3) / 1e9, 3) if ms else None,
-            "kernel_ms_under_pmc": round(ms, 4) if ms else None,
+            "step_ms": round(ms, 4) if ms else None,
         })
         if "valu_instr_per_key" not in res:
             res["valu_instr_per_key"] = round(v["SQ_INSTS_VALU"] * 64 / a.keys, 1)

@@ -17,7 +17,8 @@ KERNELS = {  # kernel-name substrings of one step (pmc_summary sums them)
     "bloom10": "bloom_build_lds", "bloom12": "bloom_build_lds", "bloom10k24": "bloom_build_lds",
     "bloom10var": "bloom_build_lds", "vqf12": "vqf_decide<,vqf_place_fused",
     "vqf12k24": "vqf_decide<,vqf_place_fused", "vqf12var": "vqf_decide<,vqf_place_fused",
-    "bloom10mono": "bloom_rec_", "bloom12big": "bloom_build_window,bloom_split_merge",
+    "bloom10mono": "bloom_rec_partition,bloom_rec_tile,bloom_rec_overflow",
+    "bloom12big": "bloom_build_window,bloom_split_merge",
     "probe10": "bloom_probe", "probe_vqf12": "vqf_probe",
 }
 
@@ -55,7 +56,14 @@ def main():
             if os.path.isdir(src):
                 tgt = os.path.join(dst, f"pmc_{w}_{name}")
                 os.makedirs(tgt, exist_ok=True)
-                shutil.copy(os.path.join(src, "run_counter_collection.csv"), tgt)
+                # only the rows of the step's kernels (the pass also profiles key generation etc.)
+                with open(os.path.join(src, "run_counter_collection.csv")) as fi, \
+                        open(os.path.join(tgt, "run_counter_collection.csv"), "w") as fo:
+                    head = fi.readline()
+                    fo.write(head)
+                    for ln in fi:
+                        if any(k in ln for k in kern.split(",")):
+                            fo.write(ln)
                 passes[name] = tgt
         cmd = [sys.executable, os.path.join(here, "pmc_summary.py"), "--workload", w, "--kernel", kern,
                "--fetch", passes["fetch"], "--write", passes["write"], "--keys", str(units),
@@ -63,8 +71,7 @@ def main():
         for name in ("sq", "valu", "tcc"):
             if name in passes:
                 cmd += [f"--{name}", passes[name]]
-        if "tcc" in passes:
-            cmd += ["--ms", str(line["roofline"]["kernel_ms"])]
+        cmd += ["--ms", str(line["roofline"]["kernel_ms"])]  # the bench's step time (HIP events)
         subprocess.run(cmd, check=True, stdout=subprocess.DEVNULL)
         print(f"{w}: profiles/traffic_{w}.json")
     if a.copy:
