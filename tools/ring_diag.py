@@ -33,22 +33,27 @@ def main():
     torch.cuda.synchronize()
     us = float(np.median([a.elapsed_time(b) for a, b in ev])) * 1e3
     L = amq.abi.lib()
-    buf = np.zeros(4 * 4096, np.uint64)
+    buf = np.zeros(4 * 4096 + 8, np.uint64)
     L.tkv_amq_diag_read.argtypes = [ctypes.c_void_p]
     assert L.tkv_amq_diag_read(buf.ctypes.data) == 0
     steps = (n + 63) // 64
     d = buf[:4 * steps].reshape(steps, 4)
     wait, cntr, dec = d[:, 0].astype(float), d[:, 1].astype(float), d[:, 2].astype(float)
     spins = (d[:, 3] & 0xffffffff).astype(int)
-    alts = (d[:, 3] >> 32).astype(int)
+    alts = (d[:, 3] >> 32).astype(int)  # 1: a lane reached the threshold (the slow path)
     print(f"leaf {n} keys, {steps} steps, build median {us:.1f} us")
     for name, v in (("wait", wait), ("count read", cntr), ("decision", dec)):
         print(f"  {name:10s} mean {v.mean():7.1f}  median {np.median(v):7.1f}  p90 {np.percentile(v, 90):7.1f} cycles")
     alt = alts > 0
-    print(f"  steps with movers {alt.mean():.2f}: decision {dec[alt].mean():.0f} vs {dec[~alt].mean():.0f} cycles")
+    print(f"  slow steps {alt.mean():.2f}: decision {dec[alt].mean():.0f} vs {dec[~alt].mean():.0f} cycles; "
+          f"step total {(wait + cntr + dec)[alt].mean():.0f} vs {(wait + cntr + dec)[~alt].mean():.0f}")
     print(f"  steps that waited for a slot: {(spins > 0).mean():.2f}")
     tot = wait + cntr + dec
     print(f"  sum per step {tot.mean():.0f} cycles = {tot.sum() / 2.4e3:.1f} us at 2.4 GHz")
+    k = buf[4 * 4096:4 * 4096 + 3].astype(np.int64)
+    if k[2] > 0:
+        print(f"  ring_place kernel (leaf 0): decide {(k[1] - k[0]) / 2.4e3:.1f} us, "
+              f"place sort {(k[2] - k[1]) / 2.4e3:.1f} us at 2.4 GHz (s_memtime)")
 
 
 if __name__ == "__main__":

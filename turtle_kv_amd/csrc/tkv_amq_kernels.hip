@@ -29,6 +29,7 @@
 
 #include <mutex>
 #include <type_traits>
+#include <vector>
 
 #include <math.h>
 #include <stdint.h>
@@ -1858,15 +1859,18 @@ constexpr uint32_t kVqfTempStride = 128;  // workspace bytes per block (>= slots
 constexpr uint32_t kVqfMaxLdsBlocks = 16384;
 constexpr uint32_t kVqfMatchLdsBlocks = 2048;  // vqf_decide's LDS lane-mask table (8 B/block)
 
-// workspace: [status u32 x8][record sink u64 x4][nelts u32 x n_segs][pad to 256]
+// workspace: [header u32 x8][record sink u64 x4][nelts u32 x n_segs][pad to 256]
 //            [128-byte record per block]
 //            [u64 placement record per key]
+// header[1] = n_segs of the last build (written by every decide workgroup; read by
+// tkv_amq_build_check); nelts[s] = leaf s's element count | its failure flags (below).  Every
+// build rewrites both for every leaf, so no memset precedes a build.
 // block record = slots x Entry (insertion order) ... u32 final count at byte 124
 // key record (written by vqf_decide in key order, coalesced; scattered by vqf_scatter):
 //   hi 32 = global block * 64 + rank in the block, or ~0 for a key that is not inserted
 //   lo 32 = Entry ((bucket offset << T) | tag), bit 31 set for 32-bit entries (T = 16)
 struct VqfWorkspace {
-  uint32_t* status;
+  uint32_t* hdr;
   uint32_t* nelts;
   uint8_t* temp;
   uint64_t* sink;  // write-only target of vqf_decide's stores for lanes with no record
@@ -1882,7 +1886,7 @@ __host__ __device__ inline VqfWorkspace vqf_workspace(void* base, uint32_t n_seg
 {
   uint8_t* p = static_cast<uint8_t*>(base);
   VqfWorkspace w;
-  w.status = reinterpret_cast<uint32_t*>(p);
+  w.hdr = reinterpret_cast<uint32_t*>(p);
   w.nelts = reinterpret_cast<uint32_t*>(p + 64);
   w.sink = reinterpret_cast<uint64_t*>(p + 32);
   w.temp = p + vqf_temp_offset(n_segs);
@@ -1898,19 +1902,33 @@ __device__ inline uint64_t* vqf_records(VqfWorkspace ws, const tkv_amq_segment* 
 
 // Bytes of workspace the plan's VQF kernels touch (tkv_amq_plan's workspace_bytes minus the
 // tail pad).  Every VQF kernel checks it against the size the caller passed and, if the
-// workspace is too small, records kVqfStatusWorkspace and writes nothing else.
-constexpr uint32_t kVqfStatusOverflow = 1u;   // a block overflowed (vqf_insert failed)
-constexpr uint32_t kVqfStatusWorkspace = 2u;  // workspace smaller than the plan needs
+// workspace is too small, flags its leaf kVqfFlagWorkspace and writes nothing else.
+constexpr uint32_t kVqfFlagOverflow = 1u << 31;   // a block overflowed (vqf_insert failed)
+constexpr uint32_t kVqfFlagWorkspace = 1u << 30;  // workspace smaller than the plan needs
+constexpr uint32_t kVqfNeltsMask = kVqfFlagWorkspace - 1;
 
+// seg: the leaf whose nelts word takes the flag (~0u: none, e.g. a per-key kernel)
 __device__ inline bool vqf_ws_ok(const tkv_amq_segment* segs, uint32_t n_segs, uint64_t ws_bytes,
-                                 VqfWorkspace ws)
+                                 VqfWorkspace ws, uint32_t seg)
 {
   const tkv_amq_segment& last = segs[n_segs - 1];
   const uint64_t need = vqf_temp_offset(n_segs) + kVqfTempStride * (last.block_base + last.n_blocks) +
                         8 * (last.key_begin + last.n_keys);
   if (need <= ws_bytes) return true;
-  if (threadIdx.x == 0) atomicOr(ws.status, kVqfStatusWorkspace);
+  if (threadIdx.x == 0 && seg != ~0u) ws.nelts[seg] = kVqfFlagWorkspace;
   return false;
+}
+
+// the first thing every decide workgroup does: the build's leaf count for tkv_amq_build_check
+// (the header lies inside the part of the workspace the host checks)
+__device__ inline void vqf_mark_build(VqfWorkspace ws, uint32_t n_segs)
+{
+  if (threadIdx.x == 0) ws.hdr[1] = n_segs;
+}
+
+__device__ inline uint32_t vqf_nelts_word(uint32_t nelts, bool fail)
+{
+  return (nelts & kVqfNeltsMask) | (fail ? kVqfFlagOverflow : 0u);
 }
 
 __device__ inline uint32_t& vqf_count(VqfWorkspace ws, uint64_t block)
@@ -2347,10 +2365,7 @@ __device__ void vqf_decide_body(const uint8_t* __restrict__ keys, const uint64_t
       vqf_count(ws, sg.block_base + b) = c < C::kSlots ? c : C::kSlots;
     }
   }
-  if (lane == 0) {
-    ws.nelts[seg_index] = nelts;
-    if (fail) atomicOr(ws.status, kVqfStatusOverflow);
-  }
+  if (lane == 0) ws.nelts[seg_index] = vqf_nelts_word(nelts, fail);
 }
 
 template <int T, int MODE>
@@ -2386,12 +2401,15 @@ __global__ __launch_bounds__(64) void vqf_decide(const uint8_t* __restrict__ key
   extern __shared__ __attribute__((aligned(16))) uint32_t s_cnt[];
   const tkv_amq_segment sg = segs[blockIdx.x];
   const VqfWorkspace ws = vqf_workspace(ws_base, n_segs);
-  if (!vqf_ws_ok(segs, n_segs, ws_bytes, ws)) return;
+  vqf_mark_build(ws, n_segs);
+  if (!vqf_ws_ok(segs, n_segs, ws_bytes, ws, blockIdx.x)) return;
   uint64_t* recs = vqf_records(ws, segs, n_segs);
   if (sg.tag_bits == 8)
     vqf_decide_dispatch<8, MODE>(keys, offs, stride, sg, blockIdx.x, ws, recs, s_cnt, match_lds, compact_ok);
   else if (sg.tag_bits == 16)
     vqf_decide_dispatch<16, MODE>(keys, offs, stride, sg, blockIdx.x, ws, recs, s_cnt, match_lds, compact_ok);
+  else if (threadIdx.x == 0)
+    ws.nelts[blockIdx.x] = 0;  // no filter (bits_per_key 0)
 }
 
 // Batches with a leaf past kVqfMaxLdsBlocks (VqfCountMode kCntU8 / kCntGlobal): a kernel of
@@ -2407,13 +2425,22 @@ __global__ __launch_bounds__(64) void vqf_decide_big(const uint8_t* __restrict__
   extern __shared__ __attribute__((aligned(16))) uint32_t s_cnt[];
   const tkv_amq_segment sg = segs[blockIdx.x];
   const VqfWorkspace ws = vqf_workspace(ws_base, n_segs);
-  if (!vqf_ws_ok(segs, n_segs, ws_bytes, ws)) return;
+  vqf_mark_build(ws, n_segs);
+  if (!vqf_ws_ok(segs, n_segs, ws_bytes, ws, blockIdx.x)) return;
   uint64_t* recs = vqf_records(ws, segs, n_segs);
   if (sg.tag_bits == 8)
     vqf_decide_body<8, MODE, NBITS, false, false, CNT>(keys, offs, stride, sg, blockIdx.x, ws, recs, s_cnt, false);
   else if (sg.tag_bits == 16)
     vqf_decide_body<16, MODE, NBITS, false, false, CNT>(keys, offs, stride, sg, blockIdx.x, ws, recs, s_cnt, false);
+  else if (threadIdx.x == 0)
+    ws.nelts[blockIdx.x] = 0;
 }
+
+// the fused place's LDS image (vqf_place_fused_body; vqf_ring_place writes it from the decider)
+constexpr uint32_t kFusedLdsBudget = 160 * 1024;  // 1,241 blocks per workgroup (one per CU at the top)
+constexpr uint32_t kFusedMaxParts = 4;            // workgroups per leaf: leaves up to 4,964 blocks
+constexpr uint32_t kFusedRegionWords = 33;
+constexpr uint32_t kFusedCountWord = 32;
 
 // ---------------------------------------------------------------------------------------
 // Small batches: vqf_decide_ring.  A lone leaf's decide is a serial chain of 64-key steps, so
@@ -2432,15 +2459,47 @@ __global__ __launch_bounds__(64) void vqf_decide_big(const uint8_t* __restrict__
 // Same decisions, same key records as vqf_decide (test_gpu_parity: small and large batches).
 constexpr uint32_t kRingThreads = 512;
 constexpr uint32_t kRingProducers = kRingThreads / 64 - 1;
-constexpr uint32_t kRingSlots = 12;
-// u64 per lane: location, Mpp, Mpa, Map, Maa, conflict mask, ranks (kRankPP / PA / AP bytes)
-constexpr uint32_t kRingSlotWords = 7 * 64;
+constexpr uint32_t kRingSlots = 10;
+// A slot holds, per lane of its chunk, these u32 words (plane w at [w * 64 + lane]), all the
+// producers can know, so the decider's step is the decision and nothing else:
+enum VqfSlotWord : uint32_t {
+  kSwPb4 = 0,            // 4 x primary block: the byte offset of its count (a key not inserted:
+                         // the dummy block n_blocks, whose count stays 0)
+  kSwAb4 = 1,            // 4 x alternate block (dummy likewise)
+  kSwRanks = 2,          // r_pp | r_pa << 8 | r_ap << 16 | kept << 24 | eligible << 25
+  kSwRecP = 3,           // the key's record with its primary block, rank bits 0 (VqfRecMode)
+  kSwRecA = 4,           // ... with its alternate block
+  kSwMpp = 5,            // lo, hi: earlier kept lanes with my primary as their primary
+  kSwMpa = kSwMpp + 2,   // ... with my alternate as their primary
+  kSwMap = kSwMpa + 2,   // ... with my primary as their alternate
+  kSwMaa = kSwMap + 2,   // ... with my alternate as their alternate
+  kSwConf = kSwMaa + 2,  // union of the four: earlier lanes sharing a block
+  kSwCount = kSwConf + 2
+};
+// r_pp / r_pa / r_ap: popcounts of Mpp / Mpa / Map (0 for a key not inserted); eligible: kept
+// and its two blocks differ (vqf_insert's alternate test)
+constexpr uint32_t kRingSlotU32 = kSwCount * 64;
 constexpr uint32_t kRingMaxBlocks = 2048;
-constexpr uint32_t kRingLdsBytes = kRingSlots * kRingSlotWords * 8 + 4 * kRingSlots + 8 +
-                                   4 * kRingMaxBlocks;
+constexpr uint32_t kRingBaseBytes = kRingSlots * kRingSlotU32 * 4 + 4 * kRingSlots + 8;
+constexpr uint32_t kRingLdsBytes = kRingBaseBytes + 4 * (kRingMaxBlocks + 1);
 constexpr uint32_t kVqfRingMaxSegs = 768;
 constexpr uint32_t kVqfRingMaxSegsOther = 4096;  // keys other than 16 bytes (tkv_amq_build)
 static_assert(kRingLdsBytes <= 160 * 1024 / 3, "three workgroups per CU");
+
+// 64-lane ballot of a bool (HIP's __ballot takes an int, and the int round trip can leave a
+// compare mask materialised as 0/1 in a VGPR and compared again)
+__device__ inline uint64_t bal(bool b)
+{
+  return __builtin_amdgcn_ballot_w64(b);
+}
+
+// per lane: bit `lane` of the wave-uniform mask m ? a : b, as one v_cndmask on the mask's SGPRs
+__device__ inline uint32_t sel_mask(uint64_t m, uint32_t a, uint32_t b)
+{
+  uint32_t r;
+  asm("v_cndmask_b32_e64 %0, %2, %1, %3" : "=v"(r) : "v"(a), "v"(b), "s"(m));
+  return r;
+}
 
 // Ring hand-off words: relaxed workgroup-scope atomics, so they stay LDS operations (a
 // volatile access through a generic pointer is compiled as a system-coherent flat access).
@@ -2453,31 +2512,56 @@ __device__ inline void lds_store_relaxed(uint32_t* p, uint32_t v)
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-// location word: tag | po << T | pb << (T + 7) | ao << (T + 21) | ab << (T + 28) | kept << 63
-template <int T>
-__device__ inline uint64_t vqf_pack_loc(const VqfLoc& l, uint32_t ab, uint32_t ao)
+// Where vqf_ring_decide puts each key's (block, rank, bucket, tag):
+//   kRecWide     8-byte key records in the workspace (vqf_decide_body's form)
+//   kRecCompact  4-byte key records (T = 8, <= 512 blocks)
+//   kRecImage    straight into the leaf's LDS image, entry at [block][rank] (vqf_ring_place:
+//                the place's sort then runs in the same workgroup; no key records at all)
+enum VqfRecMode : int { kRecWide = 0, kRecCompact = 1, kRecImage = 2 };
+
+// kSwRecP / kSwRecA by record mode: compact: block << 21 | bucket << 8 | tag (~0 for a key not
+// inserted: OR-ing the rank keeps it ~0); wide / image: the entry (bucket << T | tag; wide
+// sets bit 31 for 32-bit entries)
+template <int T, int REC>
+__device__ inline uint32_t vqf_ring_rec(bool kept, uint32_t block, uint32_t bucket, uint32_t tag)
 {
-  return (uint64_t)l.tag | ((uint64_t)l.po << T) | ((uint64_t)l.pb << (T + 7)) |
-         ((uint64_t)ao << (T + 21)) | ((uint64_t)ab << (T + 28)) | ((uint64_t)l.kept << 63);
+  if constexpr (REC == kRecCompact) return kept ? (block << 21) | (bucket << 8) | tag : ~0u;
+  else if constexpr (REC == kRecWide) return (bucket << T) | tag | (T == 16 ? 0x80000000u : 0u);
+  else return (bucket << T) | tag;
 }
 
-template <int T, int MODE, int NBITS>
+// kTbl (vqf_ring_place, leaves of <= kRingTblBlocks blocks): the four lane-match masks from two
+// LDS tables of 64-bit lane masks per producer (P[block]: lanes with that primary, A[block]:
+// with that alternate; each lane ORs its bit into P[pb] and A[ab], reads P[pb], P[ab], A[pb],
+// A[ab], clears its two entries): eight LDS operations instead of ~12 VALU per block-id bit,
+// which made the producers, not the decider, set a lone leaf's time.  Six producers (waves 1-3
+// and 5-7): wave 4 idles so the decider has its SIMD to itself (a workgroup's waves are
+// placed on the CU's four SIMDs in turn).  Otherwise seven producers and block-id ballots.
+constexpr uint32_t kRingTblBlocks = 512;
+constexpr uint32_t kRingTblProducers = 6;
+
+template <int T, int MODE, int NBITS, int REC, bool kTbl>
 __device__ void vqf_ring_produce(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs,
-                                 uint32_t stride, const tkv_amq_segment& sg, uint64_t* ring,
-                                 uint32_t* ready, uint32_t* freed)
+                                 uint32_t stride, const tkv_amq_segment& sg, uint32_t* ring,
+                                 uint32_t* ready, uint32_t* freed, uint64_t* tbl)
 {
   using C = Vqf<T>;
-  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x / 64 - 1;
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x / 64;
+  if (kTbl && wave == 4) return;
+  const uint32_t w = kTbl ? (wave < 4 ? wave - 1 : wave - 2) : wave - 1;
   const uint32_t n = sg.n_keys, nb = sg.n_blocks;
   const uint32_t n_chunks = (n + 63) / 64;
   const uint64_t R = (uint64_t)nb * C::kBuckets;
   const uint64_t magic = sg.mod_magic;
   const uint64_t mask = ~0ull << sg.hash_val_shift;  // filter_builder.hpp:187
+  const uint64_t lt = lanemask_lt();
   // (variable-length keys are read where they are hashed here: kVqfRingPrefetch)
   using KB = typename std::conditional<kVqfRingPrefetch<MODE>, VqfKeyBuf<MODE>, VqfKeyBuf<kKeyFixed>>::type;
   // a producer's next three chunks of keys are in flight (one chunk's load latency is longer
   // than the time to produce it); the loop is unrolled by three so the buffers rotate
-  constexpr uint32_t kDepth = 3, kStep = kRingProducers;
+  constexpr uint32_t kDepth = 3, kStep = kTbl ? kRingTblProducers : kRingProducers;
+  uint64_t* const tp = tbl + (kTbl ? w * 2 * (nb + 1) : 0);  // this producer's P, then A
+  uint64_t* const ta = tp + nb + 1;
   auto load = [&](uint32_t q, KB& kv) {  // clamped, not skipped: a fixed count in flight
     if constexpr (kVqfRingPrefetch<MODE>) vqf_load_key<MODE>(keys, sg.key_begin + min(q * 64 + lane, n - 1), kv);
   };
@@ -2494,8 +2578,28 @@ __device__ void vqf_ring_produce(const uint8_t* __restrict__ keys, const uint64_
     const uint64_t keptmask = __ballot(l.kept);
     uint32_t pp_lo = (uint32_t)keptmask, pp_hi = (uint32_t)(keptmask >> 32);
     uint32_t pa_lo = pp_lo, pa_hi = pp_hi, ap_lo = pp_lo, ap_hi = pp_hi, aa_lo = pp_lo, aa_hi = pp_hi;
+    if constexpr (kTbl) {
+      // (LDS operations of a wave complete in order: every lane's OR lands before any read,
+      // every read before any clear; lanes without a key OR 0, so the masks hold kept lanes)
+      const uint64_t mybit = l.kept ? 1ull << lane : 0ull;
+      atomicOr(reinterpret_cast<unsigned long long*>(tp + l.pb), mybit);
+      atomicOr(reinterpret_cast<unsigned long long*>(ta + ab), mybit);
+      asm volatile("" ::: "memory");
+      const uint64_t xpp = tp[l.pb], xpa = tp[ab], xap = ta[l.pb], xaa = ta[ab];
+      asm volatile("" ::: "memory");
+      tp[l.pb] = 0;
+      ta[ab] = 0;
+      pp_lo &= lo32(xpp);
+      pp_hi &= hi32(xpp);
+      pa_lo &= lo32(xpa);
+      pa_hi &= hi32(xpa);
+      ap_lo &= lo32(xap);
+      ap_hi &= hi32(xap);
+      aa_lo &= lo32(xaa);
+      aa_hi &= hi32(xaa);
+    }
 #pragma unroll
-    for (int j = 0; j < NBITS; ++j) {
+    for (int j = 0; j < (kTbl ? 0 : NBITS); ++j) {
       const uint32_t xp = (uint32_t)__builtin_amdgcn_sbfe((int32_t)l.pb, j, 1);  // 0 or ~0
       const uint32_t xa = (uint32_t)__builtin_amdgcn_sbfe((int32_t)ab, j, 1);
       const uint64_t bp = __ballot(xp != 0), ba = __ballot(xa != 0);
@@ -2510,24 +2614,37 @@ __device__ void vqf_ring_produce(const uint8_t* __restrict__ keys, const uint64_
       aa_lo &= ~(bal ^ xa);
       aa_hi &= ~(bah ^ xa);
     }
+    // only earlier lanes matter to a lane (later lanes' moves cannot change its counts)
+    const uint64_t Mpp = mk64(pp_lo, pp_hi) & lt, Mpa = mk64(pa_lo, pa_hi) & lt;
+    const uint64_t Map = mk64(ap_lo, ap_hi) & lt, Maa = mk64(aa_lo, aa_hi) & lt;
+    const uint64_t conf = Mpp | Mpa | Map | Maa;
+    const bool kept = l.kept;
+    const uint32_t ranks = kept ? (uint32_t)__popcll(Mpp) | ((uint32_t)__popcll(Mpa) << 8) |
+                                      ((uint32_t)__popcll(Map) << 16) | (1u << 24) |
+                                      (l.pb != ab ? 1u << 25 : 0u)
+                                : 0u;
+    const uint32_t pb4 = 4 * (kept ? l.pb : nb), ab4 = 4 * (kept ? ab : nb);
+    const uint32_t recP = vqf_ring_rec<T, REC>(kept, l.pb, l.po, l.tag);
+    const uint32_t recA = vqf_ring_rec<T, REC>(kept, ab, ao, l.tag);
     // the slot is free once the decider has taken chunk q - kRingSlots
     while (q >= kRingSlots && lds_load_relaxed(freed) < q - kRingSlots + 1) __builtin_amdgcn_s_sleep(1);
     asm volatile("" ::: "memory");  // no slot write above the wait, none below the publish
-    uint64_t* slot = ring + (q % kRingSlots) * kRingSlotWords;
-    slot[lane] = vqf_pack_loc<T>(l, ab, ao);
-    slot[64 + lane] = ((uint64_t)pp_hi << 32) | pp_lo;
-    slot[128 + lane] = ((uint64_t)pa_hi << 32) | pa_lo;
-    slot[192 + lane] = ((uint64_t)ap_hi << 32) | ap_lo;
-    slot[256 + lane] = ((uint64_t)aa_hi << 32) | aa_lo;
-    // what the decider needs of the masks before any lane moves: earlier lanes sharing a
-    // block, and the counts of earlier lanes with my primary as primary / as alternate and
-    // with my alternate as primary
-    const uint64_t lt = lanemask_lt();
-    slot[320 + lane] = ((((uint64_t)(pp_hi | pa_hi | ap_hi | aa_hi)) << 32) | (pp_lo | pa_lo | ap_lo | aa_lo)) & lt;
-    const uint32_t r_pp = __popcll((((uint64_t)pp_hi << 32) | pp_lo) & lt);
-    const uint32_t r_pa = __popcll((((uint64_t)pa_hi << 32) | pa_lo) & lt);
-    const uint32_t r_ap = __popcll((((uint64_t)ap_hi << 32) | ap_lo) & lt);
-    slot[384 + lane] = r_pp | (r_pa << 8) | (r_ap << 16);
+    uint32_t* slot = ring + (q % kRingSlots) * kRingSlotU32 + lane;
+    slot[64 * kSwPb4] = pb4;
+    slot[64 * kSwAb4] = ab4;
+    slot[64 * kSwRanks] = ranks;
+    slot[64 * kSwRecP] = recP;
+    slot[64 * kSwRecA] = recA;
+    slot[64 * kSwMpp] = lo32(Mpp);
+    slot[64 * (kSwMpp + 1)] = hi32(Mpp);
+    slot[64 * kSwMpa] = lo32(Mpa);
+    slot[64 * (kSwMpa + 1)] = hi32(Mpa);
+    slot[64 * kSwMap] = lo32(Map);
+    slot[64 * (kSwMap + 1)] = hi32(Map);
+    slot[64 * kSwMaa] = lo32(Maa);
+    slot[64 * (kSwMaa + 1)] = hi32(Maa);
+    slot[64 * kSwConf] = lo32(conf);
+    slot[64 * (kSwConf + 1)] = hi32(conf);
     asm volatile("" ::: "memory");
     if (lane == 0) lds_store_relaxed(ready + q % kRingSlots, q + 1);
   };
@@ -2552,49 +2669,71 @@ __device__ void vqf_ring_produce(const uint8_t* __restrict__ keys, const uint64_
 }
 
 #ifdef TKV_DIAG_RING
-__device__ uint64_t g_diag[4 * 4096];  // per step of leaf 0: wait, count read, decision, spins
+// per step of leaf 0: wait, count read, decision, spins | slow << 32; then (g_diag[4 * 4096 +])
+// the kernel's stamps: start, decider done, place sort done
+__device__ uint64_t g_diag[4 * 4096 + 8];
 extern "C" int tkv_amq_diag_read(void* host)
 {
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_diag), sizeof(g_diag)) == hipSuccess ? 0 : 13;
 }
+__device__ inline void diag_stamp(int i)
+{
+  if (blockIdx.x == 0 && threadIdx.x == 0) g_diag[4 * 4096 + i] = __builtin_amdgcn_s_memtime();
+}
+#else
+__device__ inline void diag_stamp(int) {}
 #endif
 
-template <int T, bool kCompact>
+// The decider wave.  Per 64-key step: the two block counts (one LDS round trip; the next
+// slot is read a step ahead), then -- in the steps where no lane's primary has reached the
+// threshold, most of a leaf -- a handful of VALU operations: every key takes its primary at
+// rank cp, its record is recP | cp.  Otherwise the rounds of vqf_decide_body, with every mask
+// at hand.
+template <int T, int REC>
 __device__ void vqf_ring_decide(const tkv_amq_segment& sg, uint32_t seg_index, VqfWorkspace ws,
-                                uint64_t* __restrict__ recs, const uint64_t* ring,
-                                uint32_t* ready, uint32_t* freed, uint32_t* cnt, bool fused)
+                                uint64_t* __restrict__ recs, const uint32_t* ring,
+                                uint32_t* ready, uint32_t* freed, uint32_t* cnt, bool fused,
+                                uint8_t* img8, uint32_t* img_sink, uint32_t* s_nelts)
 {
   using C = Vqf<T>;
+  constexpr bool kCompact = REC == kRecCompact;
   const uint32_t lane = threadIdx.x;
   const uint32_t n = sg.n_keys, nb = sg.n_blocks;
   const uint32_t n_chunks = (n + 63) / 64;
-  const uint64_t lt = lanemask_lt();
   using Rec = typename std::conditional<kCompact, uint32_t, uint64_t>::type;
   Rec* rec = reinterpret_cast<Rec*>(recs + sg.key_begin);
   Rec* const sink = reinterpret_cast<Rec*>(ws.sink);  // see vqf_decide_body
   Rec* pend_ptr = sink;
   Rec pend_val = 0;
-  uint32_t nelts = 0;
+  uint8_t* const cnt8 = reinterpret_cast<uint8_t*>(cnt);
+  // the image sink as an offset from the image (a full block's key writes there)
+  const uint32_t sink_off = (uint32_t)(reinterpret_cast<uint8_t*>(img_sink) - img8);
   // The next chunk's ready word and slot are read one step ahead (they do not depend on the
   // counts), so a step waits for one LDS round trip: the block counts.  Two slot register
   // sets alternate (the loop is unrolled by two), so no step copies the prefetched words.
   struct Slot {
-    uint32_t rdy, ranks;
-    uint64_t loc, pp, pa, ap, aa, conf;
+    uint32_t rdy, pb4, ab4, ranks, recP, recA;
+    uint64_t pp, pa, ap, aa, conf;
   };
   auto fetch = [&](uint32_t c, Slot& S) {
-    const uint64_t* slot = ring + (c % kRingSlots) * kRingSlotWords;
+    const uint32_t* slot = ring + (c % kRingSlots) * kRingSlotU32 + lane;
     S.rdy = lds_load_relaxed(ready + c % kRingSlots);
     asm volatile("" ::: "memory");  // the slot words are read after the ready word
-    S.loc = slot[lane];
-    S.pp = slot[64 + lane];
-    S.pa = slot[128 + lane];
-    S.ap = slot[192 + lane];
-    S.aa = slot[256 + lane];
-    S.conf = slot[320 + lane];
-    S.ranks = (uint32_t)slot[384 + lane];
+    S.pb4 = slot[64 * kSwPb4];
+    S.ab4 = slot[64 * kSwAb4];
+    S.ranks = slot[64 * kSwRanks];
+    S.recP = slot[64 * kSwRecP];
+    S.recA = slot[64 * kSwRecA];
+    S.pp = mk64(slot[64 * kSwMpp], slot[64 * (kSwMpp + 1)]);
+    S.pa = mk64(slot[64 * kSwMpa], slot[64 * (kSwMpa + 1)]);
+    S.ap = mk64(slot[64 * kSwMap], slot[64 * (kSwMap + 1)]);
+    S.aa = mk64(slot[64 * kSwMaa], slot[64 * (kSwMaa + 1)]);
+    S.conf = mk64(slot[64 * kSwConf], slot[64 * (kSwConf + 1)]);
   };
-  auto step = [&](uint32_t c, Slot& S, Slot& next) {
+  // PH: the two copies of the step in the unrolled loop differ by an asm marker, so they are
+  // not merged into one body with the slot registers copied between the sets
+  auto step = [&](uint32_t c, Slot& S, Slot& next, auto PH) {
+    asm volatile("; ring step %0" ::"n"(decltype(PH)::value));
 #ifdef TKV_DIAG_RING
     const uint64_t d0 = __builtin_amdgcn_s_memtime();
     uint32_t spins = 0;
@@ -2609,17 +2748,13 @@ __device__ void vqf_ring_decide(const tkv_amq_segment& sg, uint32_t seg_index, V
 #ifdef TKV_DIAG_RING
     const uint64_t d1 = __builtin_amdgcn_s_memtime();
 #endif
-    const uint64_t wloc = S.loc, Mpp = S.pp, Mpa = S.pa, Map = S.ap, Maa = S.aa;
-    const uint64_t conf = S.conf;
-    const uint32_t ranks = S.ranks;
-    const uint32_t base = c * 64;
-    const bool kept = wloc >> 63;
-    const uint32_t tag = (uint32_t)wloc & ((1u << T) - 1);
-    const uint32_t po = (uint32_t)(wloc >> T) & 127u;
-    const uint32_t pb = (uint32_t)(wloc >> (T + 7)) & 16383u;
-    const uint32_t ao = (uint32_t)(wloc >> (T + 21)) & 127u;
-    const uint32_t ab = (uint32_t)(wloc >> (T + 28)) & 16383u;
-    const uint32_t cnt_p = cnt[pb], cnt_a = cnt[ab];
+#ifdef TKV_EXP_NODECIDE  // experiment: the producers' rate (the decider only frees slots)
+    lds_store_relaxed(freed, c + 1);
+    fetch(min(c + 1, n_chunks - 1), next);
+    return;
+#endif
+    const uint32_t cnt_p = *reinterpret_cast<const uint32_t*>(cnt8 + S.pb4);
+    const uint32_t cnt_a = *reinterpret_cast<const uint32_t*>(cnt8 + S.ab4);
 #ifdef TKV_DIAG_RING
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     const uint64_t d2 = __builtin_amdgcn_s_memtime();
@@ -2631,31 +2766,47 @@ __device__ void vqf_ring_decide(const tkv_amq_segment& sg, uint32_t seg_index, V
     asm volatile("" ::: "memory");
     lds_store_relaxed(freed, c + 1);  // the slot's words are in registers (LDS order)
     fetch(min(c + 1, n_chunks - 1), next);
-    *pend_ptr = pend_val;
-    const uint64_t keptmask = __ballot(kept);
-    nelts += __popcll(keptmask);
-    // the decision logic of vqf_decide_body, with every mask at hand
-    uint32_t cp = kept ? cnt_p + (ranks & 0xffu) : 0u;
-    uint32_t ca = 0;
-    uint64_t altmask = 0;
-    if (__ballot(kept && cp >= C::kThreshold) != 0) {
-      ca = kept ? cnt_a + ((ranks >> 8) & 0xffu) : 0u;
-      uint64_t U = __ballot(kept && pb != ab);
-      uint64_t F = __ballot((cp >= C::kThreshold) & (ca < cp)) & U;
+    if constexpr (REC != kRecImage) *pend_ptr = pend_val;
+    const uint32_t ranks = S.ranks;
+    // count of my primary if every earlier lane of the chunk takes its primary (a key not
+    // inserted: 0, the dummy block's count and no ranks)
+    uint32_t cp = cnt_p + (ranks & 0xffu);
+    uint32_t chosen4 = S.pb4, r = cp, recx = S.recP;
+#ifdef TKV_DIAG_RING
+    uint64_t slow = 0;
+#endif
+#ifdef TKV_EXP_FASTONLY  // experiment: every step takes the fast path (wrong filters; timing only)
+    if (false) {
+#else
+    if (bal(cp >= C::kThreshold) != 0) {
+#endif
+#ifdef TKV_DIAG_RING
+      slow = 1;
+#endif
+      uint32_t ca = cnt_a + ((ranks >> 8) & 0xffu);
+      uint64_t U = bal(ranks >= (2u << 24));  // eligible
+      // (cp >= threshold and ca < cp) as one compare: max(ca, threshold - 1) < cp
+      uint64_t F = bal(max(ca, C::kThreshold - 1) < cp) & U;
+      uint64_t altmask = 0;
       if (F != 0) {
-        U &= __ballot(cp + (ranks >> 16) >= C::kThreshold);
+        // a lane whose primary cannot reach the threshold even if every earlier lane with
+        // its alternate there moved in stays primary: it is decided already
+        U &= bal(cp + ((ranks >> 16) & 0xffu) >= C::kThreshold);
         F &= U;
         while (F != 0) {
-          const uint64_t res = __ballot((conf & U) == 0) & U;
+          const uint64_t res = bal((S.conf & U) == 0) & U;
           const uint64_t A = res & F;
           altmask |= A;
           U &= ~res;
-          const uint64_t Al = A & lt;
-          cp = cp + (uint32_t)__popcll(Map & Al) - (uint32_t)__popcll(Mpp & Al);
-          ca = ca + (uint32_t)__popcll(Maa & Al) - (uint32_t)__popcll(Mpa & Al);
-          F = __ballot((cp >= C::kThreshold) & (ca < cp)) & U;
+          cp = cp + (uint32_t)__popcll(S.ap & A) - (uint32_t)__popcll(S.pp & A);
+          ca = ca + (uint32_t)__popcll(S.aa & A) - (uint32_t)__popcll(S.pa & A);
+          F = bal(max(ca, C::kThreshold - 1) < cp) & U;
         }
       }
+      // (selects on the mask itself: no per-lane bit test)
+      chosen4 = sel_mask(altmask, S.ab4, S.pb4);
+      r = sel_mask(altmask, ca, cp);  // a full block (r >= slots) shows in the final counts
+      recx = sel_mask(altmask, S.recA, S.recP);
     }
 #ifdef TKV_DIAG_RING
     const uint64_t d3 = __builtin_amdgcn_s_memtime();
@@ -2663,64 +2814,89 @@ __device__ void vqf_ring_decide(const tkv_amq_segment& sg, uint32_t seg_index, V
       g_diag[4 * c] = d1 - d0;
       g_diag[4 * c + 1] = d2 - d1;
       g_diag[4 * c + 2] = d3 - d2;
-      g_diag[4 * c + 3] = spins | ((uint64_t)__popcll(altmask) << 32);
+      g_diag[4 * c + 3] = spins | (slow << 32);
     }
 #endif
-    const bool alt = (altmask >> lane) & 1;
-    const uint32_t chosen = alt ? ab : pb;
-    const uint32_t cho = alt ? ao : po;
-    const uint32_t r = alt ? ca : cp;  // a full block (r >= slots) shows in the final counts
-    pend_ptr = base + lane < n ? rec + base + lane : sink;
-    if constexpr (kCompact) {
-      pend_val = (kept && r < C::kSlots) ? (chosen << 21) | (r << 15) | (cho << T) | tag : 0xffffffffu;
+    const uint32_t kept = (ranks >> 24) & 1u;
+    if constexpr (REC == kRecImage) {
+      // entry at [chosen][r] of the image (vqf_place_fused_body's phase 1, done here); a key
+      // not inserted lands in the dummy block's region, a full block's key on the sink word,
+      // so every step issues the same LDS operations
+      constexpr uint32_t kE = sizeof(typename C::Entry);
+      const uint32_t off = r < C::kSlots ? chosen4 * kFusedRegionWords + r * kE : sink_off;
+      uint8_t* dst = img8 + off;
+      if constexpr (T == 8) *reinterpret_cast<uint16_t*>(dst) = (uint16_t)recx;
+      else *reinterpret_cast<uint32_t*>(dst) = recx;
     } else {
-      const uint32_t slot_hi = (kept && r < C::kSlots)
-                                   ? (uint32_t)((sg.block_base + chosen) * 64 + r) : 0xffffffffu;
-      pend_val = ((uint64_t)slot_hi << 32) | ((cho << T) | tag) | (T == 16 ? 0x80000000u : 0u);
+      pend_ptr = c * 64 + lane < n ? rec + c * 64 + lane : sink;
+      if constexpr (kCompact) {
+        pend_val = r < C::kSlots ? recx | (r << 15) : 0xffffffffu;
+      } else {
+        const uint32_t slot_hi = (kept && r < C::kSlots)
+                                     ? (uint32_t)((sg.block_base + chosen4 / 4) * 64 + r) : 0xffffffffu;
+        pend_val = ((uint64_t)slot_hi << 32) | recx;
+      }
     }
-    atomicAdd(cnt + chosen, kept ? 1u : 0u);
+    atomicAdd(reinterpret_cast<uint32_t*>(cnt8 + chosen4), kept);
   };
   Slot A, B;
   if (n_chunks > 0) fetch(0, A);
   for (uint32_t c = 0; c < n_chunks; c += 2) {
-    step(c, A, B);
+    step(c, A, B, std::integral_constant<int, 0>{});
     if (c + 1 >= n_chunks) break;
-    step(c + 1, B, A);
+    step(c + 1, B, A, std::integral_constant<int, 1>{});
   }
-  // a key found its block full (vqf_insert fails) iff that block's final count exceeds slots
-  uint32_t fail = 0;
-  for (uint32_t b = lane; b < nb; b += 64) fail |= cnt[b] > C::kSlots;
-  if (pend_ptr != sink) *pend_ptr = pend_val;
+  // a key found its block full (vqf_insert fails) iff that block's final count exceeds
+  // slots; the element count is the sum of the counts (the dummy block's stays 0)
+  uint32_t fail = 0, nelts = 0;
+  for (uint32_t b = lane; b < nb; b += 64) {
+    const uint32_t cb = cnt[b];
+    fail |= cb > C::kSlots;
+    nelts += cb;
+  }
+  if constexpr (REC != kRecImage) {
+    if (pend_ptr != sink) *pend_ptr = pend_val;
+  }
   asm volatile("" ::: "memory");
-  if (!fused) {  // block counts for the unfused place (as vqf_decide_body)
+  if (REC != kRecImage && !fused) {  // block counts for the unfused place (as vqf_decide_body)
     for (uint32_t b = lane; b < nb; b += 64) {
-      const uint32_t c = cnt[b];
-      vqf_count(ws, sg.block_base + b) = c < C::kSlots ? c : C::kSlots;
+      const uint32_t cb = cnt[b];
+      vqf_count(ws, sg.block_base + b) = cb < C::kSlots ? cb : C::kSlots;
     }
   }
   const bool any_fail = __ballot(fail) != 0;
+  nelts = wave_sum(nelts);
   if (lane == 0) {
-    ws.nelts[seg_index] = nelts;
-    if (any_fail) atomicOr(ws.status, kVqfStatusOverflow);
+    ws.nelts[seg_index] = vqf_nelts_word(nelts, any_fail);
+    if constexpr (REC == kRecImage) *s_nelts = nelts;
   }
 }
 
-template <int T, int MODE, bool kCompact, int NBITS>
+template <int T, int MODE, int REC, int NBITS, bool kTbl = false>
 __device__ void vqf_ring_body(const uint8_t* keys, const uint64_t* offs, uint32_t stride,
                               const tkv_amq_segment& sg, uint32_t seg_index, VqfWorkspace ws,
-                              uint64_t* recs, uint32_t* lds, bool fused)
+                              uint64_t* recs, uint32_t* lds, bool fused, uint32_t cnt_words = 0)
 {
-  uint64_t* ring = reinterpret_cast<uint64_t*>(lds);
-  uint32_t* ready = reinterpret_cast<uint32_t*>(ring + kRingSlots * kRingSlotWords);
+  uint32_t* ring = lds;
+  uint32_t* ready = ring + kRingSlots * kRingSlotU32;
   uint32_t* freed = ready + kRingSlots;
-  uint32_t* cnt = freed + 2;
+  uint32_t* cnt = freed + 2;  // n_blocks + 1 counts: the last is the dummy block's
+  // kRecImage: the image after the count table ((n_blocks + 1) regions: the dummy block's
+  // last), then the sink word and the nelts word
+  uint32_t* img = cnt + cnt_words;
+  uint32_t* img_sink = img + (sg.n_blocks + 1) * kFusedRegionWords;
+  // kTbl: the producers' match tables after the sink and nelts words (8-byte aligned)
+  uint64_t* tbl = reinterpret_cast<uint64_t*>(img_sink + 2 + ((sg.n_blocks + 1) * kFusedRegionWords & 1));
   for (uint32_t i = threadIdx.x; i < kRingSlots + 1; i += kRingThreads) ready[i] = 0;  // + freed
-  for (uint32_t b = threadIdx.x; b < sg.n_blocks; b += kRingThreads) cnt[b] = 0;
+  for (uint32_t b = threadIdx.x; b <= sg.n_blocks; b += kRingThreads) cnt[b] = 0;
+  if constexpr (kTbl)
+    for (uint32_t e = threadIdx.x; e < 2 * kRingTblProducers * (sg.n_blocks + 1); e += kRingThreads) tbl[e] = 0;
   __syncthreads();
   if (threadIdx.x < 64)
-    vqf_ring_decide<T, kCompact>(sg, seg_index, ws, recs, ring, ready, freed, cnt, fused);
+    vqf_ring_decide<T, REC>(sg, seg_index, ws, recs, ring, ready, freed, cnt, fused,
+                            reinterpret_cast<uint8_t*>(img), img_sink, img_sink + 1);
   else
-    vqf_ring_produce<T, MODE, NBITS>(keys, offs, stride, sg, ring, ready, freed);
+    vqf_ring_produce<T, MODE, NBITS, REC, kTbl>(keys, offs, stride, sg, ring, ready, freed, tbl);
 }
 
 template <int MODE>
@@ -2729,27 +2905,29 @@ __global__ __launch_bounds__(kRingThreads) void vqf_decide_ring(
     const tkv_amq_segment* __restrict__ segs, void* ws_base, uint64_t ws_bytes, uint32_t n_segs,
     int flags)
 {
-  const bool match_lds = flags & 1, compact_ok = flags & 2;
+  const bool compact_ok = flags & 2;
   extern __shared__ __attribute__((aligned(16))) uint32_t s_ring[];
   const tkv_amq_segment sg = segs[blockIdx.x];
   const VqfWorkspace ws = vqf_workspace(ws_base, n_segs);
-  if (!vqf_ws_ok(segs, n_segs, ws_bytes, ws)) return;
+  vqf_mark_build(ws, n_segs);
+  if (!vqf_ws_ok(segs, n_segs, ws_bytes, ws, blockIdx.x)) return;
   uint64_t* recs = vqf_records(ws, segs, n_segs);
   const uint32_t nb = sg.n_blocks;  // <= kRingMaxBlocks (tkv_amq_build)
-  (void)match_lds;
   // compact records exactly where vqf_decide_dispatch writes them
   if (sg.tag_bits == 8) {
     if (nb <= 512 && compact_ok)
-      vqf_ring_body<8, MODE, true, 9>(keys, offs, stride, sg, blockIdx.x, ws, recs, s_ring, compact_ok);
+      vqf_ring_body<8, MODE, kRecCompact, 9>(keys, offs, stride, sg, blockIdx.x, ws, recs, s_ring, compact_ok);
     else if (nb <= 512)
-      vqf_ring_body<8, MODE, false, 9>(keys, offs, stride, sg, blockIdx.x, ws, recs, s_ring, compact_ok);
+      vqf_ring_body<8, MODE, kRecWide, 9>(keys, offs, stride, sg, blockIdx.x, ws, recs, s_ring, compact_ok);
     else
-      vqf_ring_body<8, MODE, false, 11>(keys, offs, stride, sg, blockIdx.x, ws, recs, s_ring, compact_ok);
+      vqf_ring_body<8, MODE, kRecWide, 11>(keys, offs, stride, sg, blockIdx.x, ws, recs, s_ring, compact_ok);
   } else if (sg.tag_bits == 16) {
     if (nb <= 512)
-      vqf_ring_body<16, MODE, false, 9>(keys, offs, stride, sg, blockIdx.x, ws, recs, s_ring, compact_ok);
+      vqf_ring_body<16, MODE, kRecWide, 9>(keys, offs, stride, sg, blockIdx.x, ws, recs, s_ring, compact_ok);
     else
-      vqf_ring_body<16, MODE, false, 11>(keys, offs, stride, sg, blockIdx.x, ws, recs, s_ring, compact_ok);
+      vqf_ring_body<16, MODE, kRecWide, 11>(keys, offs, stride, sg, blockIdx.x, ws, recs, s_ring, compact_ok);
+  } else if (threadIdx.x == 0) {
+    ws.nelts[blockIdx.x] = 0;
   }
 }
 
@@ -2762,7 +2940,7 @@ __global__ __launch_bounds__(256) void vqf_scatter(const tkv_amq_segment* __rest
   const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   const tkv_amq_segment& last = segs[n_segs - 1];
   const VqfWorkspace ws = vqf_workspace(ws_base, n_segs);
-  if (!vqf_ws_ok(segs, n_segs, ws_bytes, ws)) return;
+  if (!vqf_ws_ok(segs, n_segs, ws_bytes, ws, ~0u)) return;
   if (i >= n_keys || i >= last.key_begin + last.n_keys) return;
   const uint64_t r = __builtin_nontemporal_load(vqf_records(ws, segs, n_segs) + i);
   const uint32_t hi = (uint32_t)(r >> 32), lo = (uint32_t)r;
@@ -2803,7 +2981,7 @@ __device__ void vqf_place_body(const tkv_amq_segment& sg, uint32_t seg_index, Vq
       case 1: w0 = kVqfHashSeed; w1 = ~0ull << sg.hash_val_shift; break;
       case 2: w0 = 64ull * nb; w1 = T; break;
       case 3: w0 = (uint64_t)nb * C::kBuckets << T; w1 = nb; break;
-      default: w0 = ws.nelts[seg_index]; w1 = (uint64_t)nb * C::kSlots; break;
+      default: w0 = ws.nelts[seg_index] & kVqfNeltsMask; w1 = (uint64_t)nb * C::kSlots; break;
     }
     ulonglong2 v;
     v.x = w0;
@@ -2913,7 +3091,7 @@ __global__ __launch_bounds__(kPlaceThreads) void vqf_place(const tkv_amq_segment
   const uint32_t seg = blockIdx.x / parts, part = blockIdx.x - seg * parts;
   const tkv_amq_segment sg = segs[seg];
   const VqfWorkspace ws = vqf_workspace(ws_base, n_segs);
-  if (!vqf_ws_ok(segs, n_segs, ws_bytes, ws)) return;
+  if (!vqf_ws_ok(segs, n_segs, ws_bytes, ws, seg)) return;
   if (sg.tag_bits == 8) vqf_place_body<8>(sg, seg, ws, out, s_cnt, s_img, part, parts);
   else if (sg.tag_bits == 16) vqf_place_body<16>(sg, seg, ws, out, s_cnt, s_img, part, parts);
 }
@@ -2933,10 +3111,7 @@ __global__ __launch_bounds__(kPlaceThreads) void vqf_place(const tkv_amq_segment
 // kTagDword; the metadata stays in registers.  No per-thread scratch: a 402-block leaf takes
 // 53 KB of LDS (registers, ~234 VGPRs, still hold the kernel to two workgroups per CU; forcing
 // three spilled and ran 29% slower).
-constexpr uint32_t kFusedLdsBudget = 160 * 1024;  // 1,241 blocks per workgroup (one per CU at the top)
-constexpr uint32_t kFusedMaxParts = 4;            // workgroups per leaf: leaves up to 4,964 blocks
-constexpr uint32_t kFusedRegionWords = 33;
-constexpr uint32_t kFusedCountWord = 32;
+// (kFusedLdsBudget, kFusedMaxParts, kFusedRegionWords, kFusedCountWord: above vqf_decide_ring)
 
 __host__ __device__ inline uint32_t vqf_fused_img_bytes(uint32_t nb)
 {
@@ -2955,8 +3130,8 @@ __host__ __device__ inline uint32_t vqf_fused_lds_bytes(uint32_t max_nb)
 // whatever bucket word they pick): 0.752 vs 0.730 ms -- bank conflicts (~59% of the LDS
 // cycles, PMC) do not set this kernel's time.
 template <int T, int NB, uint32_t NT>
-__device__ void vqf_place_fused_sort(const tkv_amq_segment& sg, uint32_t seg_index,
-                                     VqfWorkspace ws, uint8_t* __restrict__ out, uint32_t* lds,
+__device__ void vqf_place_fused_sort(const tkv_amq_segment& sg, uint32_t nelts,
+                                     uint8_t* __restrict__ out, uint32_t* lds,
                                      uint32_t lo, uint32_t nbl)
 {
   using C = Vqf<T>;
@@ -2980,7 +3155,7 @@ __device__ void vqf_place_fused_sort(const tkv_amq_segment& sg, uint32_t seg_ind
       case 1: w0 = kVqfHashSeed; w1 = ~0ull << sg.hash_val_shift; break;
       case 2: w0 = 64ull * nb; w1 = T; break;
       case 3: w0 = (uint64_t)nb * C::kBuckets << T; w1 = nb; break;
-      default: w0 = ws.nelts[seg_index]; w1 = (uint64_t)nb * C::kSlots; break;
+      default: w0 = nelts; w1 = (uint64_t)nb * C::kSlots; break;
     }
     ulonglong2 v;
     v.x = w0;
@@ -3200,7 +3375,7 @@ __device__ void vqf_place_fused_body(const tkv_amq_segment& sg, uint32_t seg_ind
     }
   }
   __syncthreads();
-  vqf_place_fused_sort<T, 1, NT>(sg, seg_index, ws, out, lds, lo, nbl);
+  vqf_place_fused_sort<T, 1, NT>(sg, lo == 0 ? ws.nelts[seg_index] & kVqfNeltsMask : 0u, out, lds, lo, nbl);
 }
 
 // grid: n_segs * parts workgroups; workgroup (s, p) places blocks [p * span, (p + 1) * span)
@@ -3218,10 +3393,90 @@ __global__ __launch_bounds__(NT) void vqf_place_fused(const tkv_amq_segment* __r
   if (lo >= sg.n_blocks && lo != 0) return;
   const uint32_t nbl = sg.n_blocks - lo < span ? sg.n_blocks - lo : span;
   const VqfWorkspace ws = vqf_workspace(ws_base, n_segs);
-  if (!vqf_ws_ok(segs, n_segs, ws_bytes, ws)) return;
+  if (!vqf_ws_ok(segs, n_segs, ws_bytes, ws, seg)) return;
   const uint64_t* recs = vqf_records(ws, segs, n_segs);
   if (sg.tag_bits == 8) vqf_place_fused_body<8, NT>(sg, seg, ws, recs, out, s_lds, lo, nbl);
   else if (sg.tag_bits == 16) vqf_place_fused_body<16, NT>(sg, seg, ws, recs, out, s_lds, lo, nbl);
+}
+
+// ---------------------------------------------------------------------------------------
+// vqf_ring_place: vqf_decide_ring and vqf_place_fused in one workgroup per leaf, for batches
+// that do not fill the chip with one workgroup per CU (<= kRingPlaceMaxSegs leaves) of leaves
+// whose LDS image fits beside the ring (<= kRingPlaceMaxBlocks blocks).  The decider writes
+// each key's entry straight to [block][rank] of the leaf's LDS image (the rank is the block's
+// count at the key's insertion), so no key record goes through HBM; once the decider is done,
+// all eight waves run the place's per-block counting sort on the image and write the filter.
+// One kernel instead of two (and no records written and read back): the small-batch latency.
+// LDS: ring | ready/freed | counts [cnt_words] | image [nb x 33 dwords] | sink | nelts.
+// ---------------------------------------------------------------------------------------
+constexpr uint32_t kRingPlaceMaxSegs = 256;
+__host__ __device__ inline uint32_t ring_place_cnt_words(uint32_t max_nb)
+{
+  return (max_nb + 1 + 3) & ~3u;  // + the dummy block
+}
+
+__host__ __device__ constexpr inline uint32_t ring_place_lds_bytes(uint32_t max_nb)
+{
+  return kRingBaseBytes + 4 * ((max_nb + 4) & ~3u) + 4 * kFusedRegionWords * (max_nb + 1) + 16 +
+         (max_nb <= kRingTblBlocks ? 16 * kRingTblProducers * (max_nb + 1) : 0);
+}
+
+constexpr uint32_t kRingPlaceMaxBlocks =
+    ((160 * 1024 - kRingBaseBytes - 16 - 4 * kFusedRegionWords - 16) / (4 * kFusedRegionWords + 4)) & ~3u;
+static_assert(ring_place_lds_bytes(kRingPlaceMaxBlocks) <= 160 * 1024, "vqf_ring_place LDS");
+static_assert(ring_place_lds_bytes(kRingTblBlocks) <= 160 * 1024, "vqf_ring_place match tables");
+
+template <int T, int MODE, int NBITS>
+__device__ void vqf_ring_place_body(const uint8_t* keys, const uint64_t* offs, uint32_t stride,
+                                    const tkv_amq_segment& sg, uint32_t seg_index, VqfWorkspace ws,
+                                    uint8_t* out, uint32_t* lds, uint32_t cnt_words, bool tbl)
+{
+  using C = Vqf<T>;
+  diag_stamp(0);
+  if (NBITS == 9 && tbl)  // (the batch's leaves are <= kRingTblBlocks blocks: the host sized the tables)
+    vqf_ring_body<T, MODE, kRecImage, NBITS, true>(keys, offs, stride, sg, seg_index, ws, nullptr, lds,
+                                                   true, cnt_words);
+  else
+    vqf_ring_body<T, MODE, kRecImage, NBITS, false>(keys, offs, stride, sg, seg_index, ws, nullptr, lds,
+                                                    true, cnt_words);
+  const uint32_t nb = sg.n_blocks;
+  uint32_t* cnt = reinterpret_cast<uint32_t*>(lds) + kRingBaseBytes / 4;
+  uint32_t* img = cnt + cnt_words;
+  __syncthreads();  // the decider is done (its LDS writes are visible to the workgroup)
+  // the sort reads each block's count from its region (a full block keeps its slots)
+  for (uint32_t b = threadIdx.x; b < nb; b += kRingThreads) {
+    const uint32_t c = cnt[b];
+    img[b * kFusedRegionWords + kFusedCountWord] = c < C::kSlots ? c : C::kSlots;
+  }
+  const uint32_t nelts = img[(nb + 1) * kFusedRegionWords + 1];
+  __syncthreads();
+  diag_stamp(1);
+  vqf_place_fused_sort<T, 1, kRingThreads>(sg, nelts, out, img, 0, nb);
+  __syncthreads();
+  diag_stamp(2);
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kRingThreads) void vqf_ring_place(
+    const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint32_t stride,
+    const tkv_amq_segment* __restrict__ segs, void* ws_base, uint64_t ws_bytes, uint32_t n_segs,
+    uint8_t* __restrict__ out, uint32_t cnt_words, uint32_t tbl)
+{
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_ring[];
+  const tkv_amq_segment sg = segs[blockIdx.x];
+  const VqfWorkspace ws = vqf_workspace(ws_base, n_segs);
+  vqf_mark_build(ws, n_segs);
+  if (!vqf_ws_ok(segs, n_segs, ws_bytes, ws, blockIdx.x)) return;
+  const uint32_t nb = sg.n_blocks;  // <= kRingPlaceMaxBlocks (tkv_amq_build)
+  if (sg.tag_bits == 8) {
+    if (nb <= 512) vqf_ring_place_body<8, MODE, 9>(keys, offs, stride, sg, blockIdx.x, ws, out, s_ring, cnt_words, tbl != 0);
+    else vqf_ring_place_body<8, MODE, 10>(keys, offs, stride, sg, blockIdx.x, ws, out, s_ring, cnt_words, tbl != 0);
+  } else if (sg.tag_bits == 16) {
+    if (nb <= 512) vqf_ring_place_body<16, MODE, 9>(keys, offs, stride, sg, blockIdx.x, ws, out, s_ring, cnt_words, tbl != 0);
+    else vqf_ring_place_body<16, MODE, 10>(keys, offs, stride, sg, blockIdx.x, ws, out, s_ring, cnt_words, tbl != 0);
+  } else if (threadIdx.x == 0) {
+    ws.nelts[blockIdx.x] = 0;
+  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -4163,14 +4418,20 @@ int tkv_amq_build(int kind, const uint8_t* keys, const uint64_t* offs, uint32_t 
   }
 
   if (kind != TKV_AMQ_VQF) return TKV_AMQ_INVALID_ARGUMENT;
-  if (max_blocks == 0) return TKV_AMQ_OK;
+  if (max_blocks == 0) {
+    // no kernel runs: a later tkv_amq_build_check must not read an earlier build's flags
+    if (d_ws && ws_bytes >= 64 && hipMemsetAsync(static_cast<uint8_t*>(d_ws) + 4, 0, 4, s) != hipSuccess)
+      return TKV_AMQ_INTERNAL;
+    return TKV_AMQ_OK;
+  }
   if (max_blocks > kVqfMaxBlocks) return TKV_AMQ_RESOURCE_EXHAUSTED;
   if (!d_ws) return TKV_AMQ_INVALID_ARGUMENT;
   // the status word and leaf counts must be writable; the rest is checked on the device
   // against the plan (every leaf with a filter has >= 1 block record, every key one record)
   if (ws_bytes < vqf_temp_offset(n_segs) + kVqfTempStride * (uint64_t)max_blocks + 8 * n_keys)
     return TKV_AMQ_INVALID_ARGUMENT;
-  if (hipMemsetAsync(d_ws, 0, 64, s) != hipSuccess) return TKV_AMQ_INTERNAL;
+  // (no memset: every decide workgroup writes the header's leaf count and its leaf's nelts
+  // word, flags included, so tkv_amq_build_check reads only this build's results)
   // LDS: u32 block counts (+ the u64 lane-mask table when every leaf is small enough)
   // The lane-mask table costs 8 B of LDS per block in every decide wave, and wins even where
   // it costs waves per CU: 6,104 leaves of 804 blocks 2.49 -> 2.14 ms (16 instead of 24 waves
@@ -4232,6 +4493,34 @@ int tkv_amq_build(int kind, const uint8_t* keys, const uint64_t* offs, uint32_t 
   // 24-byte keys (TurtleKV's default key size hint), 8-byte aligned, are loaded ahead of
   // their hash like 16-byte ones
   const bool prefetched = vmode == kKey16 || vmode == kKey24;
+  if (cnt_mode == kCntU32 && n_segs <= kRingPlaceMaxSegs && max_blocks <= kRingPlaceMaxBlocks) {
+    // decide and place in one workgroup per leaf (vqf_ring_place): no key records, one launch
+    static std::once_flag rp_attr[kMaxDevices];
+    once_per_device(rp_attr, [] {
+      for (const void* f : {reinterpret_cast<const void*>(&vqf_ring_place<kKey16>),
+                            reinterpret_cast<const void*>(&vqf_ring_place<kKey24>),
+                            reinterpret_cast<const void*>(&vqf_ring_place<kKeyFixed>),
+                            reinterpret_cast<const void*>(&vqf_ring_place<kKeyVar>)})
+        (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    });
+    const dim3 g(n_segs), b(kRingThreads);
+    const uint32_t cw = ring_place_cnt_words(max_blocks);
+    const size_t rl = ring_place_lds_bytes(max_blocks);
+    const uint32_t tbl = max_blocks <= kRingTblBlocks;  // (ring_place_lds_bytes sized them)
+    if (vmode == kKey16)
+      hipLaunchKernelGGL(vqf_ring_place<kKey16>, g, b, rl, s, keys, offs, stride, d_segs, d_ws,
+                         ws_bytes, n_segs, d_out, cw, tbl);
+    else if (vmode == kKey24)
+      hipLaunchKernelGGL(vqf_ring_place<kKey24>, g, b, rl, s, keys, offs, stride, d_segs, d_ws,
+                         ws_bytes, n_segs, d_out, cw, tbl);
+    else if (mode == kKeyFixed)
+      hipLaunchKernelGGL(vqf_ring_place<kKeyFixed>, g, b, rl, s, keys, offs, stride, d_segs, d_ws,
+                         ws_bytes, n_segs, d_out, cw, tbl);
+    else
+      hipLaunchKernelGGL(vqf_ring_place<kKeyVar>, g, b, rl, s, keys, offs, stride, d_segs, d_ws,
+                         ws_bytes, n_segs, d_out, cw, tbl);
+    return hipGetLastError() == hipSuccess ? TKV_AMQ_OK : TKV_AMQ_INTERNAL;
+  }
   if (cnt_mode != kCntU32) {
     // (decided above)
   } else if (n_segs <= (prefetched ? kVqfRingMaxSegs : kVqfRingMaxSegsOther) &&
@@ -4457,10 +4746,20 @@ int tkv_amq_build_check(int kind, const void* d_ws, uint64_t ws_bytes, void* str
   const hipStream_t s = as_stream(stream);
   if (hipStreamSynchronize(s) != hipSuccess) return TKV_AMQ_INTERNAL;
   if (kind != TKV_AMQ_VQF || !d_ws || ws_bytes < 64) return TKV_AMQ_OK;
-  uint32_t status = 0;
-  if (hipMemcpy(&status, d_ws, 4, hipMemcpyDeviceToHost) != hipSuccess) return TKV_AMQ_INTERNAL;
-  if (status & kVqfStatusWorkspace) return TKV_AMQ_INVALID_ARGUMENT;
-  return status ? TKV_AMQ_INTERNAL : TKV_AMQ_OK;
+  // the last build's leaf count, then every leaf's flags (VqfWorkspace)
+  uint32_t hdr[2] = {0, 0};
+  if (hipMemcpy(hdr, d_ws, 8, hipMemcpyDeviceToHost) != hipSuccess) return TKV_AMQ_INTERNAL;
+  const uint64_t n_segs = hdr[1];
+  if (n_segs == 0) return TKV_AMQ_OK;
+  if (64 + 4 * n_segs > ws_bytes) return TKV_AMQ_INVALID_ARGUMENT;
+  std::vector<uint32_t> nelts(n_segs);
+  if (hipMemcpy(nelts.data(), static_cast<const uint8_t*>(d_ws) + 64, 4 * n_segs,
+                hipMemcpyDeviceToHost) != hipSuccess)
+    return TKV_AMQ_INTERNAL;
+  uint32_t flags = 0;
+  for (const uint32_t w : nelts) flags |= w;
+  if (flags & kVqfFlagWorkspace) return TKV_AMQ_INVALID_ARGUMENT;
+  return (flags & kVqfFlagOverflow) ? TKV_AMQ_INTERNAL : TKV_AMQ_OK;
 }
 
 int tkv_amq_probe(int kind, const uint8_t* d_filters, const tkv_amq_segment* d_segs,

@@ -933,6 +933,13 @@ class HostFilterPipeline:
     def new_host_output(self):
         return _torch().empty(self.plan.total_out_bytes, dtype=_torch().uint8, pin_memory=True)
 
+    def _fold_flags(self, slot: int, chunk) -> None:
+        """Add the chunk's failed-leaf count (the flag bits 30/31 of each leaf's nelts word in
+        the VQF workspace, tkv_amq_build_check's source) to self.fail, on the device."""
+        b0, b1 = chunk
+        w = self.d_ws[slot][64:64 + 4 * (b1 - b0)].view(_torch().int32)
+        self.fail.add_(((w >> 30) != 0).sum(dtype=_torch().int32))
+
     def run_views(self, views, host_out=None, view_stride: int = 16, n_threads: int = 16,
                   check: bool = True):
         """Keys given as tkv_amq_key_view records (the EditView key range; KEY_VIEW_DTYPE
@@ -1000,8 +1007,8 @@ class HostFilterPipeline:
                 self.s_run.wait_event(ev_in[c])
                 if c >= 2:
                     self.s_run.wait_event(ev_out[c - 2])      # slot's output copied out
-                    if self.kind == VQF:                      # fold chunk c-2's failure word
-                        self.fail.add_(self.d_ws[slot][:4].view(torch.int32))
+                    if self.kind == VQF:                      # fold chunk c-2's failure flags
+                        self._fold_flags(slot, self.chunks[c - 2])
                 build_all_filters(self.plans[c], KeyBatch.fixed(self.d_keys[slot][:k1 - k0]),
                                   out=self.d_out[slot], workspace=self.d_ws[slot],
                                   stream=self.s_run, check=False)
@@ -1014,7 +1021,7 @@ class HostFilterPipeline:
         if self.kind == VQF:
             with torch.cuda.stream(self.s_run):
                 for c in range(max(0, n - 2), n):
-                    self.fail.add_(self.d_ws[c & 1][:4].view(torch.int32))
+                    self._fold_flags(c & 1, self.chunks[c])
         self.s_out.synchronize()
         if check and self.kind == VQF:
             self.s_run.synchronize()
