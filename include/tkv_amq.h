@@ -165,14 +165,22 @@ int tkv_amq_plan_pages(int kind, const uint64_t* seg_key_counts, const uint64_t*
  *  d_workspace  device workspace (workspace_bytes, 16-byte aligned)
  * Asynchronous on `stream`.  VQF insert failures (the reference BATT_CHECKs,
  * filter_builder.hpp:211) are recorded in the workspace; read them with
- * tkv_amq_build_check after the stream completes. */
+ * tkv_amq_build_check after the stream completes.  VQF workspace header (written by every
+ * build, so no clearing is needed between builds): bytes [4, 8) = the build's n_segs; bytes
+ * [64 + 4*s, 68 + 4*s) = leaf s's element count, with TKV_AMQ_VQF_FLAG_OVERFLOW set if one of
+ * its inserts failed and TKV_AMQ_VQF_FLAG_WORKSPACE if the workspace was short (a caller may
+ * copy these words back with its own results instead of calling tkv_amq_build_check). */
+#define TKV_AMQ_VQF_NELTS_OFFSET 64u
+#define TKV_AMQ_VQF_FLAG_OVERFLOW 0x80000000u
+#define TKV_AMQ_VQF_FLAG_WORKSPACE 0x40000000u
 int tkv_amq_build(int kind, const uint8_t* keys, const uint64_t* key_offsets,
                   uint32_t key_stride, uint64_t n_keys, const tkv_amq_segment* d_segs,
                   uint32_t n_segs, uint32_t max_seg_blocks, uint8_t* d_out,
                   void* d_workspace, uint64_t workspace_bytes, void* stream);
 
-/* Synchronises `stream`; returns TKV_AMQ_OK or TKV_AMQ_INTERNAL (a VQF block overflowed).
- * Bloom builds cannot fail on the device. */
+/* Synchronises `stream`; returns TKV_AMQ_OK, TKV_AMQ_INTERNAL (a VQF block overflowed) or
+ * TKV_AMQ_INVALID_ARGUMENT (the workspace was smaller than the plan).  Bloom builds cannot
+ * fail on the device. */
 int tkv_amq_build_check(int kind, const void* d_workspace, uint64_t workspace_bytes,
                         void* stream);
 

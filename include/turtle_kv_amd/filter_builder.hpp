@@ -470,11 +470,15 @@ inline Status build_one(FilterKind kind, usize bpk, u64 leaf_page_id,
   if (st != TKV_AMQ_OK) return Status::from(st, "tkv_amq_build");
   if (hipMemcpyAsync(h_payload, sc.d_out.get(), used, hipMemcpyDeviceToHost, s) != hipSuccess)
     return Status::from(TKV_AMQ_INTERNAL, "hipMemcpyAsync payload");
-  if ((kind == FilterKind::kQuotient && ws_bytes >= 4 &&
-       hipMemcpyAsync(h_status, sc.d_ws.get(), 4, hipMemcpyDeviceToHost, s) != hipSuccess) ||
+  // (the leaf's nelts word: its failure flags, tkv_amq.h)
+  if ((kind == FilterKind::kQuotient && ws_bytes >= TKV_AMQ_VQF_NELTS_OFFSET + 4 &&
+       hipMemcpyAsync(h_status, sc.d_ws.get<u8>() + TKV_AMQ_VQF_NELTS_OFFSET, 4, hipMemcpyDeviceToHost,
+                      s) != hipSuccess) ||
       hipStreamSynchronize(s) != hipSuccess)
     return Status::from(TKV_AMQ_INTERNAL, "hipStreamSynchronize");
-  if (*h_status != 0) return Status::from(TKV_AMQ_INTERNAL, "vqf_insert (filter_builder.hpp:211)");
+  if (*h_status & TKV_AMQ_VQF_FLAG_WORKSPACE) return Status::from(TKV_AMQ_INVALID_ARGUMENT, "workspace");
+  if (*h_status & TKV_AMQ_VQF_FLAG_OVERFLOW)
+    return Status::from(TKV_AMQ_INTERNAL, "vqf_insert (filter_builder.hpp:211)");
   page_payload.assign(page_payload_bytes ? page_payload_bytes : used, 0);
   std::memcpy(page_payload.data(), h_payload, used);
   return OkStatus();
@@ -815,7 +819,8 @@ class LeafBatcher
                           segs.data(), &total_out, &ws_bytes, &max_blocks);
     if (st != TKV_AMQ_OK) return Status::from(st, "tkv_amq_plan");
     const usize seg_bytes = n_segs * sizeof(tkv_amq_segment);
-    const usize io_bytes = seg_bytes + 64 + total_out;
+    const usize flag_bytes = (4 * n_segs + 63) / 64 * 64;  // the leaves' nelts words (VQF)
+    const usize io_bytes = seg_bytes + flag_bytes + total_out;
     if (!detail::LeafScratch::grow_pinned(b.h_io, b.h_io_cap, io_bytes <= b.h_io_cap ? io_bytes : io_bytes + io_bytes / 2))
       return Status::from(TKV_AMQ_RESOURCE_EXHAUSTED, "hipHostMalloc");
     const u64 n = b.n, bytes = b.bytes;
@@ -823,9 +828,9 @@ class LeafBatcher
         !reserve_device(b.d_out, total_out))
       return Status::from(TKV_AMQ_RESOURCE_EXHAUSTED, "hipMalloc");
     std::memcpy(b.h_io, segs.data(), seg_bytes);
-    u32* h_status = reinterpret_cast<u32*>(b.h_io + seg_bytes);
-    *h_status = 0;
-    u8* h_out = b.h_io + seg_bytes + 64;
+    u32* h_flags = reinterpret_cast<u32*>(b.h_io + seg_bytes);
+    std::memset(h_flags, 0, 4 * n_segs);
+    u8* h_out = b.h_io + seg_bytes + flag_bytes;
     if (b.stride == 0) b.h_offs[n] = bytes;
     hipStream_t s = b.stream;
     if ((bytes && hipMemcpyAsync(b.d_keys.get(), b.h_keys, bytes, hipMemcpyHostToDevice, s) != hipSuccess) ||
@@ -837,11 +842,16 @@ class LeafBatcher
                        b.d_ws.get(), ws_bytes, s);
     if (st != TKV_AMQ_OK) return Status::from(st, "tkv_amq_build");
     if (hipMemcpyAsync(h_out, b.d_out.get(), total_out, hipMemcpyDeviceToHost, s) != hipSuccess ||
-        (b.kind == FilterKind::kQuotient && ws_bytes >= 4 &&
-         hipMemcpyAsync(h_status, b.d_ws.get(), 4, hipMemcpyDeviceToHost, s) != hipSuccess) ||
+        (b.kind == FilterKind::kQuotient && ws_bytes >= TKV_AMQ_VQF_NELTS_OFFSET + 4 * n_segs &&
+         hipMemcpyAsync(h_flags, b.d_ws.get<u8>() + TKV_AMQ_VQF_NELTS_OFFSET, 4 * n_segs,
+                        hipMemcpyDeviceToHost, s) != hipSuccess) ||
         hipStreamSynchronize(s) != hipSuccess)
       return Status::from(TKV_AMQ_INTERNAL, "hipMemcpyAsync pages");
-    if (*h_status != 0) return Status::from(TKV_AMQ_INTERNAL, "vqf_insert (filter_builder.hpp:211)");
+    u32 flags = 0;
+    for (usize i = 0; i < n_segs; ++i) flags |= h_flags[i];
+    if (flags & TKV_AMQ_VQF_FLAG_WORKSPACE) return Status::from(TKV_AMQ_INVALID_ARGUMENT, "workspace");
+    if (flags & TKV_AMQ_VQF_FLAG_OVERFLOW)
+      return Status::from(TKV_AMQ_INTERNAL, "vqf_insert (filter_builder.hpp:211)");
     for (usize i = 0; i < n_segs; ++i) {
       b.reqs[i]->page = h_out + segs[i].out_offset;
       b.reqs[i]->page_bytes = segs[i].payload_bytes;

@@ -1887,7 +1887,7 @@ __host__ __device__ inline VqfWorkspace vqf_workspace(void* base, uint32_t n_seg
   uint8_t* p = static_cast<uint8_t*>(base);
   VqfWorkspace w;
   w.hdr = reinterpret_cast<uint32_t*>(p);
-  w.nelts = reinterpret_cast<uint32_t*>(p + 64);
+  w.nelts = reinterpret_cast<uint32_t*>(p + TKV_AMQ_VQF_NELTS_OFFSET);
   w.sink = reinterpret_cast<uint64_t*>(p + 32);
   w.temp = p + vqf_temp_offset(n_segs);
   return w;
@@ -1903,8 +1903,9 @@ __device__ inline uint64_t* vqf_records(VqfWorkspace ws, const tkv_amq_segment* 
 // Bytes of workspace the plan's VQF kernels touch (tkv_amq_plan's workspace_bytes minus the
 // tail pad).  Every VQF kernel checks it against the size the caller passed and, if the
 // workspace is too small, flags its leaf kVqfFlagWorkspace and writes nothing else.
-constexpr uint32_t kVqfFlagOverflow = 1u << 31;   // a block overflowed (vqf_insert failed)
-constexpr uint32_t kVqfFlagWorkspace = 1u << 30;  // workspace smaller than the plan needs
+constexpr uint32_t kVqfFlagOverflow = TKV_AMQ_VQF_FLAG_OVERFLOW;    // a block overflowed (vqf_insert failed)
+constexpr uint32_t kVqfFlagWorkspace = TKV_AMQ_VQF_FLAG_WORKSPACE;  // workspace smaller than the plan needs
+static_assert(kVqfFlagOverflow == 1u << 31 && kVqfFlagWorkspace == 1u << 30, "");
 constexpr uint32_t kVqfNeltsMask = kVqfFlagWorkspace - 1;
 
 // seg: the leaf whose nelts word takes the flag (~0u: none, e.g. a per-key kernel)
