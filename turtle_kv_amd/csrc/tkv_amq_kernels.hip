@@ -319,33 +319,119 @@ constexpr uint32_t kVarBins = 64;  // lengths 0..31 and ">= 32" (bin 32); 64 for
 template <uint32_t NT>
 constexpr uint32_t kVarAuxWords = 2 * kVarBins + 2 * kVarChunk<NT>;
 
-struct VarKey {  // a key under 32 bytes in registers (a longer one: its address)
-  uint64_t l[3];
-  uint32_t t4, tb, len;
-  const uint8_t* p;
+// Short keys through a buffer resource.  A resource covers a range of the key array (a chunk
+// or a leaf) plus the 32 bytes after it, clipped to the array's end; every key under 32 bytes
+// is read as one 32-byte window (two 16-byte loads, the offset relative to the resource, no
+// per-load address arithmetic), the window's start clamped into the resource, so every lane
+// issues the same two loads and none reads past the array.  A clamped window (a key among the
+// array's last 32 bytes) is realigned after the loads arrive.  Bytes past a key are never
+// used.  The 4-byte tail and the tail bytes are then picked out of word n8 = len / 8.
+typedef uint32_t u32x4_b __attribute__((ext_vector_type(4)));
+
+__device__ inline __amdgpu_buffer_rsrc_t byte_rsrc(const uint8_t* base, uint32_t bytes)
+{
+  // word 3 = 0x00020000: DATA_FORMAT 32, as raw buffer loads need on gfx9
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(base), (short)0, (int)bytes, 0x00020000);
+}
+
+struct VarRsrc {
+  __amdgpu_buffer_rsrc_t r;
+  uint64_t base;  // key-array offset of the resource's first byte
+  uint32_t nrec;  // bytes it covers; 0: not usable (fewer than 32 bytes, or a range >= 2 GiB)
 };
 
-__device__ inline void var_key_load(const uint8_t* p, uint32_t len, const uint8_t* safe, VarKey& k)
+// keys [.., ..) whose bytes are [base, end) of an array of key_end bytes
+__device__ inline VarRsrc var_rsrc(const uint8_t* keys, uint64_t base, uint64_t end, uint64_t key_end)
+{
+  const uint64_t want = end - base + 32, avail = key_end - base;
+  const uint64_t n = want < avail ? want : avail;
+  VarRsrc v;
+  v.base = base;
+  v.nrec = (n >= 32 && n < (1ull << 31)) ? (uint32_t)n : 0u;
+  v.r = byte_rsrc(keys + base, v.nrec);
+  return v;
+}
+
+struct KeyWin {  // 32 bytes of a key as loaded: starting d bytes before it when clamped
+  u32x4_b a, b;
+  uint32_t d;
+};
+
+__device__ inline void key_win_load(const VarRsrc& v, uint32_t rel, KeyWin& w)
+{
+  const uint32_t relc = min(rel, v.nrec - 32);
+  w.a = __builtin_amdgcn_raw_buffer_load_b128(v.r, relc, 0, 0);
+  w.b = __builtin_amdgcn_raw_buffer_load_b128(v.r, relc + 16, 0, 0);
+  w.d = rel - relc;
+}
+
+// the window's key as XxhShort's lanes, 4-byte tail word and tail bytes (len < 32)
+__device__ inline void key_win_parts(const KeyWin& w, uint32_t len, uint64_t (&l)[3], uint32_t& t4,
+                                     uint32_t& tb)
+{
+  uint32_t x[8] = {w.a.x, w.a.y, w.a.z, w.a.w, w.b.x, w.b.y, w.b.z, w.b.w};
+  if (w.d != 0) {  // (divergent, rare: shift the window down by d bytes)
+    asm volatile("");  // (a branch, not if-converted into every key's instruction stream)
+    const uint32_t d = w.d;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) x[i] = (d & 16) ? (i + 4 < 8 ? x[i + 4] : 0u) : x[i];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) x[i] = (d & 8) ? (i + 2 < 8 ? x[i + 2] : 0u) : x[i];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) x[i] = (d & 4) ? (i + 1 < 8 ? x[i + 1] : 0u) : x[i];
+    const uint32_t r = d & 3;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) x[i] = __builtin_amdgcn_alignbyte(i + 1 < 8 ? x[i + 1] : 0u, x[i], r);
+  }
+  l[0] = mk64(x[0], x[1]);
+  l[1] = mk64(x[2], x[3]);
+  l[2] = mk64(x[4], x[5]);
+  const uint32_t n8 = len >> 3;
+  const uint32_t tlo = n8 == 0 ? x[0] : n8 == 1 ? x[2] : n8 == 2 ? x[4] : x[6];
+  const uint32_t thi = n8 == 0 ? x[1] : n8 == 1 ? x[3] : n8 == 2 ? x[5] : x[7];
+  t4 = tlo;
+  tb = (len & 4) ? thi : tlo;
+}
+
+// Without a usable resource: the key's full 8-byte lanes, its 4-byte tail and its tail bytes
+// loaded one by one (clamped to `safe`, >= 16 readable bytes, past the key), packed as the
+// window key_win_parts reads (the tail word at word n8).
+__device__ inline void key_win_load_clamped(const uint8_t* p, uint32_t len, const uint8_t* safe, KeyWin& w)
 {
   const bool sh = len < 32;
   const uint32_t n8 = len >> 3, nb = len & 3;
+  uint64_t l[3];
 #pragma unroll
-  for (uint32_t j = 0; j < 3; ++j) k.l[j] = ld64_unaligned(sh && j < n8 ? p + 8 * j : safe);
+  for (uint32_t j = 0; j < 3; ++j) l[j] = ld64_unaligned(sh && j < n8 ? p + 8 * j : safe);
   const uint8_t* q = p + 8 * n8;
-  k.t4 = ld32_unaligned(sh && (len & 4) ? q : safe);
+  const uint32_t t4 = ld32_unaligned(sh && (len & 4) ? q : safe);
   q += len & 4;
   const uint32_t c0 = *(sh && nb > 0 ? q : safe), c1 = *(sh && nb > 1 ? q + 1 : safe),
                  c2 = *(sh && nb > 2 ? q + 2 : safe);
-  k.tb = c0 | c1 << 8 | c2 << 16;
-  k.len = len;
-  k.p = p;
+  const uint32_t tb = c0 | c1 << 8 | c2 << 16;
+  const uint32_t tlo = (len & 4) ? t4 : tb;  // word n8 as key_win_parts reads it
+  w.a = u32x4_b{lo32(l[0]), hi32(l[0]), lo32(l[1]), hi32(l[1])};
+  w.b = u32x4_b{lo32(l[2]), hi32(l[2]), tlo, tb};
+  if (n8 == 0) { w.a.x = tlo; w.a.y = tb; }
+  else if (n8 == 1) { w.a.z = tlo; w.a.w = tb; }
+  else if (n8 == 2) { w.b.x = tlo; w.b.y = tb; }
+  w.d = 0;
 }
+
+struct VarKey {  // a key under 32 bytes as its window (a longer one: its address)
+  KeyWin w;
+  uint32_t len;
+  const uint8_t* p;
+};
 
 template <int K>
 __device__ inline void var_key_insert(uint32_t* s_bits, uint32_t nb, uint32_t k, const VarKey& v)
 {
   if (v.len < 32) {
-    const XxhShort x(v.len, v.l, v.t4, v.tb);
+    uint64_t l[3];
+    uint32_t t4, tb;
+    key_win_parts(v.w, v.len, l, t4, tb);
+    const XxhShort x(v.len, l, t4, tb);
     const uint64_t h0 = x.finish(c_bloom.seed_p5[0]);
     uint32_t* blk = s_bits + 16 * (uint32_t)__umul64hi(h0, (uint64_t)nb);
     lds_set_bit(blk, (uint32_t)h0 & 511u);
@@ -360,10 +446,11 @@ __device__ inline void var_key_insert(uint32_t* s_bits, uint32_t nb, uint32_t k,
   }
 }
 
+// key_end: offset one past the key array's last byte (offs[batch keys])
 template <uint32_t NT, int K>
 __device__ void bloom_var_sorted_image(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs,
                                        const tkv_amq_segment& sg, uint32_t kb, uint32_t ke,
-                                       uint32_t* s_bits, uint32_t* s_aux)
+                                       uint32_t* s_bits, uint32_t* s_aux, uint64_t key_end)
 {
   constexpr uint32_t C = kVarChunk<NT>, U = C / NT;
   uint32_t* bins = s_aux;                        // [kVarBins] counts of this chunk
@@ -408,10 +495,16 @@ __device__ void bloom_var_sorted_image(const uint8_t* __restrict__ keys, const u
     }
     __syncthreads();
     const uint8_t* kbase = keys + base;
+    // the chunk's bytes through a buffer resource (KeyWin) when they span < 2 GiB (always,
+    // but for keys of megabytes)
+    const VarRsrc vr = var_rsrc(keys, base, o[c0 + cn], key_end);
     VarKey A, B;
     auto load = [&](uint32_t q, VarKey& v) {
       const uint2 e = kl[min(q, cn - 1)];
-      var_key_load(kbase + e.x, e.y, safe, v);
+      if (vr.nrec) key_win_load(vr, e.x, v.w);  // (uniform)
+      else key_win_load_clamped(kbase + e.x, e.y, safe, v.w);
+      v.len = e.y;
+      v.p = kbase + e.x;
     };
     load(tid, A);
     for (uint32_t q = tid; q < cn; q += 2 * NT) {
@@ -447,9 +540,12 @@ __global__ __launch_bounds__(NT) void bloom_build_lds(const uint8_t* __restrict_
   __syncthreads();
   if constexpr (MODE == kKeyVar) {
     if (sorted) {
-      if (k == 7) bloom_var_sorted_image<NT, 7>(keys, offs, sg, 0, n, s_bits, s_lds);
-      else if (k == 8) bloom_var_sorted_image<NT, 8>(keys, offs, sg, 0, n, s_bits, s_lds);
-      else bloom_var_sorted_image<NT, 0>(keys, offs, sg, 0, n, s_bits, s_lds);
+      // (one workgroup per leaf: the batch's last leaf ends the key array)
+      const tkv_amq_segment& last = segs[gridDim.x - 1];
+      const uint64_t key_end = offs[last.key_begin + last.n_keys];
+      if (k == 7) bloom_var_sorted_image<NT, 7>(keys, offs, sg, 0, n, s_bits, s_lds, key_end);
+      else if (k == 8) bloom_var_sorted_image<NT, 8>(keys, offs, sg, 0, n, s_bits, s_lds, key_end);
+      else bloom_var_sorted_image<NT, 0>(keys, offs, sg, 0, n, s_bits, s_lds, key_end);
     } else {
       bloom_leaf_image<MODE, NT>(keys, offs, stride, sg, 0, n, s_bits);
     }
@@ -2010,8 +2106,8 @@ struct VqfKeyBuf<kKey24> {
 // ahead of the bytes.  Keys of 32 bytes or more are hashed from memory where they are hashed.
 template <>
 struct VqfKeyBuf<kKeyVar> {
-  uint64_t l[3];
-  uint32_t t4, tb, len;
+  KeyWin w;  // the key's bytes (a key under 32 bytes)
+  uint32_t len;
   uint64_t off;
   uint64_t noff;
   uint32_t nlen;
@@ -2025,25 +2121,16 @@ constexpr bool kVqfRingPrefetch = MODE == kKey16 || MODE == kKey24;
 
 // the bytes of the key whose offsets `prev` holds, and the offsets of key gi_next.  Every lane
 // issues the same loads (clamped to a safe address when the key is shorter: the offsets
-// array holds >= 16 bytes), so the count in flight is fixed.
+// array holds >= 16 bytes; or the leaf's buffer resource, KeyWin), so the count in flight is
+// fixed.
 __device__ inline void vqf_load_var(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs,
                                     uint64_t gi_next, const VqfKeyBuf<kKeyVar>& prev,
-                                    VqfKeyBuf<kKeyVar>& kb)
+                                    VqfKeyBuf<kKeyVar>& kb, const VarRsrc& vr)
 {
   const uint64_t off = prev.noff;
   const uint32_t len = prev.nlen;
-  const uint8_t* p = keys + off;
-  const uint8_t* safe = reinterpret_cast<const uint8_t*>(offs);
-  const bool sh = len < 32;
-  const uint32_t n8 = len >> 3, nb = len & 3;
-#pragma unroll
-  for (uint32_t j = 0; j < 3; ++j) kb.l[j] = ld64_unaligned(sh && j < n8 ? p + 8 * j : safe);
-  const uint8_t* q = p + 8 * n8;
-  kb.t4 = ld32_unaligned(sh && (len & 4) ? q : safe);
-  q += len & 4;
-  const uint32_t c0 = *(sh && nb > 0 ? q : safe), c1 = *(sh && nb > 1 ? q + 1 : safe),
-                 c2 = *(sh && nb > 2 ? q + 2 : safe);
-  kb.tb = c0 | c1 << 8 | c2 << 16;
+  if (vr.nrec) key_win_load(vr, (uint32_t)(off - vr.base), kb.w);  // (uniform per leaf)
+  else key_win_load_clamped(keys + off, len, reinterpret_cast<const uint8_t*>(offs), kb.w);
   kb.len = len;
   kb.off = off;
   kb.noff = offs[gi_next];
@@ -2075,7 +2162,12 @@ __device__ inline uint64_t vqf_key_hash(const uint8_t* __restrict__ keys,
     const XxhFixed<24> x(kb.w);
     return x.finish(xxh_fixed_rc<24>(kVqfHashSeed));
   } else if constexpr (MODE == kKeyVar) {
-    if (kb.len < 32) return XxhShort(kb.len, kb.l, kb.t4, kb.tb).finish(kVqfHashSeed + kP5);
+    if (kb.len < 32) {
+      uint64_t l[3];
+      uint32_t t4, tb;
+      key_win_parts(kb.w, kb.len, l, t4, tb);
+      return XxhShort(kb.len, l, t4, tb).finish(kVqfHashSeed + kP5);
+    }
     return xxh64_bytes(keys + kb.off, kb.len, kVqfHashSeed);
   } else {
     return hash_key<MODE>(keys, offs, stride, gi, kVqfHashSeed);
@@ -2137,7 +2229,7 @@ template <int T, int MODE, int NBITS, bool kLdsMatch, bool kCompact, int CNT = k
 __device__ void vqf_decide_body(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs,
                                 uint32_t stride, const tkv_amq_segment& sg, uint32_t seg_index,
                                 VqfWorkspace ws, uint64_t* __restrict__ recs, uint32_t* s_lds,
-                                bool fused)
+                                bool fused, uint64_t key_end)
 {
   static_assert(!kLdsMatch || CNT == kCntU32, "the lane-mask table follows u32 counts");
   using C = Vqf<T>;
@@ -2150,6 +2242,10 @@ __device__ void vqf_decide_body(const uint8_t* __restrict__ keys, const uint64_t
   using Rec = typename std::conditional<kCompact, uint32_t, uint64_t>::type;
   Rec* rec = reinterpret_cast<Rec*>(recs + sg.key_begin);
   using KB = VqfKeyBuf<MODE>;
+  // variable-length keys: the leaf's bytes through a buffer resource (KeyWin)
+  VarRsrc vr{};
+  if constexpr (MODE == kKeyVar)
+    if (n > 0) vr = var_rsrc(keys, offs[sg.key_begin], offs[sg.key_begin + n], key_end);
 
   VqfCounts<CNT> cnt;
   if constexpr (CNT == kCntGlobal) cnt.rec = ws.temp + sg.block_base * kVqfTempStride;
@@ -2193,7 +2289,7 @@ __device__ void vqf_decide_body(const uint8_t* __restrict__ keys, const uint64_t
       // branch-free (clamped index, select on the result): straight-line code lets the
       // compiler count vmcnt exactly instead of draining every outstanding access
       if constexpr (MODE == kKeyVar)  // bytes of chunk + 2 (offsets in kv_hash), offsets of + 3
-        vqf_load_var(keys, offs, sg.key_begin + min(inext + 128, n - 1), kv_hash, kv_load);
+        vqf_load_var(keys, offs, sg.key_begin + min(inext + 128, n - 1), kv_hash, kv_load, vr);
       else
         vqf_load_key<MODE>(keys, sg.key_begin + min(inext + 64, n - 1), kv_load);
       *pend_ptr = pend_val;
@@ -2341,8 +2437,8 @@ __device__ void vqf_decide_body(const uint8_t* __restrict__ keys, const uint64_t
         const uint64_t g0 = sg.key_begin + min(lane, n - 1);
         first.noff = offs[g0];
         first.nlen = (uint32_t)(offs[g0 + 1] - first.noff);
-        vqf_load_var(keys, offs, sg.key_begin + min(lane + 64, n - 1), first, kv0);
-        vqf_load_var(keys, offs, sg.key_begin + min(lane + 128, n - 1), kv0, kvA);
+        vqf_load_var(keys, offs, sg.key_begin + min(lane + 64, n - 1), first, kv0, vr);
+        vqf_load_var(keys, offs, sg.key_begin + min(lane + 128, n - 1), kv0, kvA, vr);
       } else {
         vqf_load_key<MODE>(keys, sg.key_begin + min(lane, n - 1), kv0);
         vqf_load_key<MODE>(keys, sg.key_begin + min(lane + 64, n - 1), kvA);
@@ -2369,25 +2465,35 @@ __device__ void vqf_decide_body(const uint8_t* __restrict__ keys, const uint64_t
   if (lane == 0) ws.nelts[seg_index] = vqf_nelts_word(nelts, fail);
 }
 
+// variable-length keys: one past the key array's last byte (the batch's last leaf ends it)
+template <int MODE>
+__device__ inline uint64_t vqf_key_end(const uint64_t* offs, const tkv_amq_segment* segs, uint32_t n_segs)
+{
+  if constexpr (MODE != kKeyVar) return 0;
+  const tkv_amq_segment& last = segs[n_segs - 1];
+  return offs[last.key_begin + last.n_keys];
+}
+
 template <int T, int MODE>
 __device__ inline void vqf_decide_dispatch(const uint8_t* keys, const uint64_t* offs,
                                            uint32_t stride, const tkv_amq_segment& sg,
                                            uint32_t seg_index, VqfWorkspace ws, uint64_t* recs,
-                                           uint32_t* cnt, bool match_lds, bool compact_ok)
+                                           uint32_t* cnt, bool match_lds, bool compact_ok,
+                                           uint64_t key_end)
 {
   // kVqfMaxLdsBlocks = 16384 -> at most 14 block-id bits
   if (sg.n_blocks <= 512) {
     if (T == 8 && compact_ok) {
-      if (match_lds) vqf_decide_body<T, MODE, 9, true, T == 8>(keys, offs, stride, sg, seg_index, ws, recs, cnt, compact_ok);
-      else vqf_decide_body<T, MODE, 9, false, T == 8>(keys, offs, stride, sg, seg_index, ws, recs, cnt, compact_ok);
+      if (match_lds) vqf_decide_body<T, MODE, 9, true, T == 8>(keys, offs, stride, sg, seg_index, ws, recs, cnt, compact_ok, key_end);
+      else vqf_decide_body<T, MODE, 9, false, T == 8>(keys, offs, stride, sg, seg_index, ws, recs, cnt, compact_ok, key_end);
     } else {
-      if (match_lds) vqf_decide_body<T, MODE, 9, true, false>(keys, offs, stride, sg, seg_index, ws, recs, cnt, compact_ok);
-      else vqf_decide_body<T, MODE, 9, false, false>(keys, offs, stride, sg, seg_index, ws, recs, cnt, compact_ok);
+      if (match_lds) vqf_decide_body<T, MODE, 9, true, false>(keys, offs, stride, sg, seg_index, ws, recs, cnt, compact_ok, key_end);
+      else vqf_decide_body<T, MODE, 9, false, false>(keys, offs, stride, sg, seg_index, ws, recs, cnt, compact_ok, key_end);
     }
   } else if (match_lds) {
-    vqf_decide_body<T, MODE, 14, true, false>(keys, offs, stride, sg, seg_index, ws, recs, cnt, compact_ok);
+    vqf_decide_body<T, MODE, 14, true, false>(keys, offs, stride, sg, seg_index, ws, recs, cnt, compact_ok, key_end);
   } else {
-    vqf_decide_body<T, MODE, 14, false, false>(keys, offs, stride, sg, seg_index, ws, recs, cnt, compact_ok);
+    vqf_decide_body<T, MODE, 14, false, false>(keys, offs, stride, sg, seg_index, ws, recs, cnt, compact_ok, key_end);
   }
 }
 
@@ -2405,10 +2511,11 @@ __global__ __launch_bounds__(64) void vqf_decide(const uint8_t* __restrict__ key
   vqf_mark_build(ws, n_segs);
   if (!vqf_ws_ok(segs, n_segs, ws_bytes, ws, blockIdx.x)) return;
   uint64_t* recs = vqf_records(ws, segs, n_segs);
+  const uint64_t key_end = vqf_key_end<MODE>(offs, segs, n_segs);
   if (sg.tag_bits == 8)
-    vqf_decide_dispatch<8, MODE>(keys, offs, stride, sg, blockIdx.x, ws, recs, s_cnt, match_lds, compact_ok);
+    vqf_decide_dispatch<8, MODE>(keys, offs, stride, sg, blockIdx.x, ws, recs, s_cnt, match_lds, compact_ok, key_end);
   else if (sg.tag_bits == 16)
-    vqf_decide_dispatch<16, MODE>(keys, offs, stride, sg, blockIdx.x, ws, recs, s_cnt, match_lds, compact_ok);
+    vqf_decide_dispatch<16, MODE>(keys, offs, stride, sg, blockIdx.x, ws, recs, s_cnt, match_lds, compact_ok, key_end);
   else if (threadIdx.x == 0)
     ws.nelts[blockIdx.x] = 0;  // no filter (bits_per_key 0)
 }
@@ -2429,10 +2536,11 @@ __global__ __launch_bounds__(64) void vqf_decide_big(const uint8_t* __restrict__
   vqf_mark_build(ws, n_segs);
   if (!vqf_ws_ok(segs, n_segs, ws_bytes, ws, blockIdx.x)) return;
   uint64_t* recs = vqf_records(ws, segs, n_segs);
+  const uint64_t key_end = vqf_key_end<MODE>(offs, segs, n_segs);
   if (sg.tag_bits == 8)
-    vqf_decide_body<8, MODE, NBITS, false, false, CNT>(keys, offs, stride, sg, blockIdx.x, ws, recs, s_cnt, false);
+    vqf_decide_body<8, MODE, NBITS, false, false, CNT>(keys, offs, stride, sg, blockIdx.x, ws, recs, s_cnt, false, key_end);
   else if (sg.tag_bits == 16)
-    vqf_decide_body<16, MODE, NBITS, false, false, CNT>(keys, offs, stride, sg, blockIdx.x, ws, recs, s_cnt, false);
+    vqf_decide_body<16, MODE, NBITS, false, false, CNT>(keys, offs, stride, sg, blockIdx.x, ws, recs, s_cnt, false, key_end);
   else if (threadIdx.x == 0)
     ws.nelts[blockIdx.x] = 0;
 }
@@ -2544,7 +2652,7 @@ constexpr uint32_t kRingTblProducers = 6;
 template <int T, int MODE, int NBITS, int REC, bool kTbl>
 __device__ void vqf_ring_produce(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs,
                                  uint32_t stride, const tkv_amq_segment& sg, uint32_t* ring,
-                                 uint32_t* ready, uint32_t* freed, uint64_t* tbl)
+                                 uint32_t* ready, uint32_t* freed, uint64_t* tbl, uint64_t key_end)
 {
   using C = Vqf<T>;
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x / 64;
@@ -2566,12 +2674,36 @@ __device__ void vqf_ring_produce(const uint8_t* __restrict__ keys, const uint64_
   auto load = [&](uint32_t q, KB& kv) {  // clamped, not skipped: a fixed count in flight
     if constexpr (kVqfRingPrefetch<MODE>) vqf_load_key<MODE>(keys, sg.key_begin + min(q * 64 + lane, n - 1), kv);
   };
+  // variable-length keys: the leaf's bytes through a buffer resource (KeyWin)
+  VarRsrc vr{};
+  if constexpr (MODE == kKeyVar)
+    if (n > 0) vr = var_rsrc(keys, offs[sg.key_begin], offs[sg.key_begin + n], key_end);
   auto produce = [&](uint32_t q, KB& kv) {
     const uint32_t i = q * 64 + lane;
     const bool valid = i < n;
     uint64_t h = 0;
-    if constexpr (kVqfRingPrefetch<MODE>) h = valid ? vqf_key_hash<MODE>(keys, offs, stride, sg.key_begin + i, kv) : 0;
-    else h = valid ? hash_key<MODE>(keys, offs, stride, sg.key_begin + i, kVqfHashSeed) : 0;
+    if constexpr (kVqfRingPrefetch<MODE>) {
+      h = valid ? vqf_key_hash<MODE>(keys, offs, stride, sg.key_begin + i, kv) : 0;
+    } else if constexpr (MODE == kKeyVar) {
+      const uint64_t gi = sg.key_begin + min(i, n - 1), o0 = offs[gi];
+      const uint32_t len = (uint32_t)(offs[gi + 1] - o0);
+      if (vr.nrec) {  // (uniform per leaf; every lane loads its window, valid or not)
+        KeyWin kw;
+        key_win_load(vr, (uint32_t)(o0 - vr.base), kw);
+        if (valid && len < 32) {
+          uint64_t l[3];
+          uint32_t t4, tb;
+          key_win_parts(kw, len, l, t4, tb);
+          h = XxhShort(len, l, t4, tb).finish(kVqfHashSeed + kP5);
+        } else if (valid) {
+          h = xxh64_bytes(keys + o0, len, kVqfHashSeed);
+        }
+      } else {
+        h = valid ? hash_key<MODE>(keys, offs, stride, gi, kVqfHashSeed) : 0;
+      }
+    } else {
+      h = valid ? hash_key<MODE>(keys, offs, stride, sg.key_begin + i, kVqfHashSeed) : 0;
+    }
     load(q + kDepth * kStep, kv);
     const VqfLoc l = vqf_locate<T>(h, valid, mask, R, magic);
     uint32_t ab, ao;
@@ -2876,7 +3008,8 @@ __device__ void vqf_ring_decide(const tkv_amq_segment& sg, uint32_t seg_index, V
 template <int T, int MODE, int REC, int NBITS, bool kTbl = false>
 __device__ void vqf_ring_body(const uint8_t* keys, const uint64_t* offs, uint32_t stride,
                               const tkv_amq_segment& sg, uint32_t seg_index, VqfWorkspace ws,
-                              uint64_t* recs, uint32_t* lds, bool fused, uint32_t cnt_words = 0)
+                              uint64_t* recs, uint32_t* lds, bool fused, uint32_t cnt_words,
+                              uint64_t key_end)
 {
   uint32_t* ring = lds;
   uint32_t* ready = ring + kRingSlots * kRingSlotU32;
@@ -2897,7 +3030,7 @@ __device__ void vqf_ring_body(const uint8_t* keys, const uint64_t* offs, uint32_
     vqf_ring_decide<T, REC>(sg, seg_index, ws, recs, ring, ready, freed, cnt, fused,
                             reinterpret_cast<uint8_t*>(img), img_sink, img_sink + 1);
   else
-    vqf_ring_produce<T, MODE, NBITS, REC, kTbl>(keys, offs, stride, sg, ring, ready, freed, tbl);
+    vqf_ring_produce<T, MODE, NBITS, REC, kTbl>(keys, offs, stride, sg, ring, ready, freed, tbl, key_end);
 }
 
 template <int MODE>
@@ -2913,20 +3046,21 @@ __global__ __launch_bounds__(kRingThreads) void vqf_decide_ring(
   vqf_mark_build(ws, n_segs);
   if (!vqf_ws_ok(segs, n_segs, ws_bytes, ws, blockIdx.x)) return;
   uint64_t* recs = vqf_records(ws, segs, n_segs);
+  const uint64_t key_end = vqf_key_end<MODE>(offs, segs, n_segs);
   const uint32_t nb = sg.n_blocks;  // <= kRingMaxBlocks (tkv_amq_build)
   // compact records exactly where vqf_decide_dispatch writes them
   if (sg.tag_bits == 8) {
     if (nb <= 512 && compact_ok)
-      vqf_ring_body<8, MODE, kRecCompact, 9>(keys, offs, stride, sg, blockIdx.x, ws, recs, s_ring, compact_ok);
+      vqf_ring_body<8, MODE, kRecCompact, 9>(keys, offs, stride, sg, blockIdx.x, ws, recs, s_ring, compact_ok, 0, key_end);
     else if (nb <= 512)
-      vqf_ring_body<8, MODE, kRecWide, 9>(keys, offs, stride, sg, blockIdx.x, ws, recs, s_ring, compact_ok);
+      vqf_ring_body<8, MODE, kRecWide, 9>(keys, offs, stride, sg, blockIdx.x, ws, recs, s_ring, compact_ok, 0, key_end);
     else
-      vqf_ring_body<8, MODE, kRecWide, 11>(keys, offs, stride, sg, blockIdx.x, ws, recs, s_ring, compact_ok);
+      vqf_ring_body<8, MODE, kRecWide, 11>(keys, offs, stride, sg, blockIdx.x, ws, recs, s_ring, compact_ok, 0, key_end);
   } else if (sg.tag_bits == 16) {
     if (nb <= 512)
-      vqf_ring_body<16, MODE, kRecWide, 9>(keys, offs, stride, sg, blockIdx.x, ws, recs, s_ring, compact_ok);
+      vqf_ring_body<16, MODE, kRecWide, 9>(keys, offs, stride, sg, blockIdx.x, ws, recs, s_ring, compact_ok, 0, key_end);
     else
-      vqf_ring_body<16, MODE, kRecWide, 11>(keys, offs, stride, sg, blockIdx.x, ws, recs, s_ring, compact_ok);
+      vqf_ring_body<16, MODE, kRecWide, 11>(keys, offs, stride, sg, blockIdx.x, ws, recs, s_ring, compact_ok, 0, key_end);
   } else if (threadIdx.x == 0) {
     ws.nelts[blockIdx.x] = 0;
   }
@@ -3430,16 +3564,17 @@ static_assert(ring_place_lds_bytes(kRingTblBlocks) <= 160 * 1024, "vqf_ring_plac
 template <int T, int MODE, int NBITS>
 __device__ void vqf_ring_place_body(const uint8_t* keys, const uint64_t* offs, uint32_t stride,
                                     const tkv_amq_segment& sg, uint32_t seg_index, VqfWorkspace ws,
-                                    uint8_t* out, uint32_t* lds, uint32_t cnt_words, bool tbl)
+                                    uint8_t* out, uint32_t* lds, uint32_t cnt_words, bool tbl,
+                                    uint64_t key_end)
 {
   using C = Vqf<T>;
   diag_stamp(0);
   if (NBITS == 9 && tbl)  // (the batch's leaves are <= kRingTblBlocks blocks: the host sized the tables)
     vqf_ring_body<T, MODE, kRecImage, NBITS, true>(keys, offs, stride, sg, seg_index, ws, nullptr, lds,
-                                                   true, cnt_words);
+                                                   true, cnt_words, key_end);
   else
     vqf_ring_body<T, MODE, kRecImage, NBITS, false>(keys, offs, stride, sg, seg_index, ws, nullptr, lds,
-                                                    true, cnt_words);
+                                                    true, cnt_words, key_end);
   const uint32_t nb = sg.n_blocks;
   uint32_t* cnt = reinterpret_cast<uint32_t*>(lds) + kRingBaseBytes / 4;
   uint32_t* img = cnt + cnt_words;
@@ -3468,13 +3603,14 @@ __global__ __launch_bounds__(kRingThreads) void vqf_ring_place(
   const VqfWorkspace ws = vqf_workspace(ws_base, n_segs);
   vqf_mark_build(ws, n_segs);
   if (!vqf_ws_ok(segs, n_segs, ws_bytes, ws, blockIdx.x)) return;
+  const uint64_t key_end = vqf_key_end<MODE>(offs, segs, n_segs);
   const uint32_t nb = sg.n_blocks;  // <= kRingPlaceMaxBlocks (tkv_amq_build)
   if (sg.tag_bits == 8) {
-    if (nb <= 512) vqf_ring_place_body<8, MODE, 9>(keys, offs, stride, sg, blockIdx.x, ws, out, s_ring, cnt_words, tbl != 0);
-    else vqf_ring_place_body<8, MODE, 10>(keys, offs, stride, sg, blockIdx.x, ws, out, s_ring, cnt_words, tbl != 0);
+    if (nb <= 512) vqf_ring_place_body<8, MODE, 9>(keys, offs, stride, sg, blockIdx.x, ws, out, s_ring, cnt_words, tbl != 0, key_end);
+    else vqf_ring_place_body<8, MODE, 10>(keys, offs, stride, sg, blockIdx.x, ws, out, s_ring, cnt_words, tbl != 0, key_end);
   } else if (sg.tag_bits == 16) {
-    if (nb <= 512) vqf_ring_place_body<16, MODE, 9>(keys, offs, stride, sg, blockIdx.x, ws, out, s_ring, cnt_words, tbl != 0);
-    else vqf_ring_place_body<16, MODE, 10>(keys, offs, stride, sg, blockIdx.x, ws, out, s_ring, cnt_words, tbl != 0);
+    if (nb <= 512) vqf_ring_place_body<16, MODE, 9>(keys, offs, stride, sg, blockIdx.x, ws, out, s_ring, cnt_words, tbl != 0, key_end);
+    else vqf_ring_place_body<16, MODE, 10>(keys, offs, stride, sg, blockIdx.x, ws, out, s_ring, cnt_words, tbl != 0, key_end);
   } else if (threadIdx.x == 0) {
     ws.nelts[blockIdx.x] = 0;
   }
