@@ -358,6 +358,21 @@ __device__ inline uint64_t lanemask_lt()
   return lane == 0 ? 0ull : (~0ull >> (64 - lane));
 }
 
+// 64-lane ballot of a bool (HIP's __ballot takes an int, and the int round trip can leave a
+// compare mask materialised as 0/1 in a VGPR and compared again)
+__device__ inline uint64_t bal(bool b)
+{
+  return __builtin_amdgcn_ballot_w64(b);
+}
+
+// per lane: bit `lane` of the wave-uniform mask m ? a : b, as one v_cndmask on the mask's SGPRs
+__device__ inline uint32_t sel_mask(uint64_t m, uint32_t a, uint32_t b)
+{
+  uint32_t r;
+  asm("v_cndmask_b32_e64 %0, %2, %1, %3" : "=v"(r) : "v"(a), "v"(b), "s"(m));
+  return r;
+}
+
 // position of the r-th (0-based) set bit of x; x must have > r set bits
 __device__ inline int select64(uint64_t x, int r)
 {

@@ -2335,7 +2335,7 @@ __device__ void vqf_decide_body(const uint8_t* __restrict__ keys, const uint64_t
     // its primary holds >= kThreshold elements, and with all earlier lanes primary it holds
     // cp).  This is most steps of a leaf (blocks fill towards ~0.85 x slots), and they skip
     // the alternate block entirely.
-    if (__ballot(L.kept && cp >= C::kThreshold) != 0) {
+    if (bal(cp >= C::kThreshold) != 0) {  // (cp = 0 for a key not inserted)
       vqf_locate_alt<T>(L, R, magic, ab, ao);
       const uint32_t cnt_a = cnt.get(ab);
       // lanes with pb_j == my ab
@@ -2365,8 +2365,9 @@ __device__ void vqf_decide_body(const uint8_t* __restrict__ keys, const uint64_t
       // with no undecided earlier lane sharing a block is final now: all of them decide in
       // one round and the movers' effects are applied to later lanes with four masked
       // popcounts.
-      uint64_t U = __ballot(L.kept && pb != ab);  // blocks differ (vqf_insert alt test)
-      uint64_t F = __ballot((cp >= C::kThreshold) & (ca < cp)) & U;
+      uint64_t U = bal(L.kept && pb != ab);  // blocks differ (vqf_insert alt test)
+      // (cp >= threshold and ca < cp) as one compare: max(ca, threshold - 1) < cp
+      uint64_t F = bal(max(ca, C::kThreshold - 1) < cp) & U;
       if (F != 0) {
         // lanes whose alternate block is my primary / my alternate
         uint32_t map_lo = (uint32_t)keptmask, map_hi = (uint32_t)(keptmask >> 32);
@@ -2398,25 +2399,24 @@ __device__ void vqf_decide_body(const uint8_t* __restrict__ keys, const uint64_t
         const uint64_t conf = (Mpp | Mpa | Map | Maa) & lt;  // earlier lanes sharing a block
         // a lane whose primary cannot reach the threshold even if every earlier lane with
         // its alternate there moved in stays primary: it is decided already
-        U &= __ballot(cp + (uint32_t)__popcll(Map & lt) >= C::kThreshold);
+        U &= bal(cp + (uint32_t)__popcll(Map & lt) >= C::kThreshold);
         F &= U;
         while (F != 0) {
-          const uint64_t res = __ballot((conf & U) == 0) & U;
+          const uint64_t res = bal((conf & U) == 0) & U;
           const uint64_t A = res & F;
           altmask |= A;
           U &= ~res;
           const uint64_t Al = A & lt;
           cp = cp + (uint32_t)__popcll(Map & Al) - (uint32_t)__popcll(Mpp & Al);
           ca = ca + (uint32_t)__popcll(Maa & Al) - (uint32_t)__popcll(Mpa & Al);
-          F = __ballot((cp >= C::kThreshold) & (ca < cp)) & U;
+          F = bal(max(ca, C::kThreshold - 1) < cp) & U;
         }
       }
     }
-    const bool alt = (altmask >> lane) & 1;
-    const uint32_t chosen = alt ? ab : pb;
-    const uint32_t cho = alt ? ao : L.po;
-    const uint32_t r = alt ? ca : cp;  // count of the chosen block when this key is inserted
-    fail |= (uint32_t)(__ballot(L.kept && r >= C::kSlots) != 0);
+    const uint32_t chosen = sel_mask(altmask, ab, pb);
+    const uint32_t cho = sel_mask(altmask, ao, L.po);
+    const uint32_t r = sel_mask(altmask, ca, cp);  // count of the chosen block when this key is inserted
+    fail |= (uint32_t)(bal(L.kept && r >= C::kSlots) != 0);
     pend_ptr = base + lane < n ? rec + base + lane : sink;
     if constexpr (kCompact) {
       pend_val = (L.kept && r < C::kSlots) ? (chosen << 21) | (r << 15) | (cho << T) | L.tag
@@ -2594,21 +2594,6 @@ constexpr uint32_t kRingLdsBytes = kRingBaseBytes + 4 * (kRingMaxBlocks + 1);
 constexpr uint32_t kVqfRingMaxSegs = 768;
 constexpr uint32_t kVqfRingMaxSegsOther = 4096;  // keys other than 16 bytes (tkv_amq_build)
 static_assert(kRingLdsBytes <= 160 * 1024 / 3, "three workgroups per CU");
-
-// 64-lane ballot of a bool (HIP's __ballot takes an int, and the int round trip can leave a
-// compare mask materialised as 0/1 in a VGPR and compared again)
-__device__ inline uint64_t bal(bool b)
-{
-  return __builtin_amdgcn_ballot_w64(b);
-}
-
-// per lane: bit `lane` of the wave-uniform mask m ? a : b, as one v_cndmask on the mask's SGPRs
-__device__ inline uint32_t sel_mask(uint64_t m, uint32_t a, uint32_t b)
-{
-  uint32_t r;
-  asm("v_cndmask_b32_e64 %0, %2, %1, %3" : "=v"(r) : "v"(a), "v"(b), "s"(m));
-  return r;
-}
 
 // Ring hand-off words: relaxed workgroup-scope atomics, so they stay LDS operations (a
 // volatile access through a generic pointer is compiled as a system-coherent flat access).
