@@ -2589,7 +2589,12 @@ enum VqfSlotWord : uint32_t {
 // and its two blocks differ (vqf_insert's alternate test)
 constexpr uint32_t kRingSlotU32 = kSwCount * 64;
 constexpr uint32_t kRingMaxBlocks = 2048;
-constexpr uint32_t kRingBaseBytes = kRingSlots * kRingSlotU32 * 4 + 4 * kRingSlots + 8;
+// ring | ready[NS] | freed (+1 spare): the count table starts here
+__host__ __device__ constexpr inline uint32_t ring_base_bytes(uint32_t NS)
+{
+  return NS * kRingSlotU32 * 4 + 4 * NS + 8;
+}
+constexpr uint32_t kRingBaseBytes = ring_base_bytes(kRingSlots);
 constexpr uint32_t kRingLdsBytes = kRingBaseBytes + 4 * (kRingMaxBlocks + 1);
 constexpr uint32_t kVqfRingMaxSegs = 768;
 constexpr uint32_t kVqfRingMaxSegsOther = 4096;  // keys other than 16 bytes (tkv_amq_build)
@@ -2634,7 +2639,7 @@ __device__ inline uint32_t vqf_ring_rec(bool kept, uint32_t block, uint32_t buck
 constexpr uint32_t kRingTblBlocks = 512;
 constexpr uint32_t kRingTblProducers = 6;
 
-template <int T, int MODE, int NBITS, int REC, bool kTbl>
+template <int T, int MODE, int NBITS, int REC, bool kTbl, uint32_t NS>
 __device__ void vqf_ring_produce(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs,
                                  uint32_t stride, const tkv_amq_segment& sg, uint32_t* ring,
                                  uint32_t* ready, uint32_t* freed, uint64_t* tbl, uint64_t key_end)
@@ -2744,10 +2749,10 @@ __device__ void vqf_ring_produce(const uint8_t* __restrict__ keys, const uint64_
     const uint32_t pb4 = 4 * (kept ? l.pb : nb), ab4 = 4 * (kept ? ab : nb);
     const uint32_t recP = vqf_ring_rec<T, REC>(kept, l.pb, l.po, l.tag);
     const uint32_t recA = vqf_ring_rec<T, REC>(kept, ab, ao, l.tag);
-    // the slot is free once the decider has taken chunk q - kRingSlots
-    while (q >= kRingSlots && lds_load_relaxed(freed) < q - kRingSlots + 1) __builtin_amdgcn_s_sleep(1);
+    // the slot is free once the decider has taken chunk q - NS
+    while (q >= NS && lds_load_relaxed(freed) < q - NS + 1) __builtin_amdgcn_s_sleep(1);
     asm volatile("" ::: "memory");  // no slot write above the wait, none below the publish
-    uint32_t* slot = ring + (q % kRingSlots) * kRingSlotU32 + lane;
+    uint32_t* slot = ring + (q % NS) * kRingSlotU32 + lane;
     slot[64 * kSwPb4] = pb4;
     slot[64 * kSwAb4] = ab4;
     slot[64 * kSwRanks] = ranks;
@@ -2764,7 +2769,7 @@ __device__ void vqf_ring_produce(const uint8_t* __restrict__ keys, const uint64_
     slot[64 * kSwConf] = lo32(conf);
     slot[64 * (kSwConf + 1)] = hi32(conf);
     asm volatile("" ::: "memory");
-    if (lane == 0) lds_store_relaxed(ready + q % kRingSlots, q + 1);
+    if (lane == 0) lds_store_relaxed(ready + q % NS, q + 1);
   };
   if (w >= n_chunks) return;
   KB kv0{}, kv1{}, kv2{};
@@ -2807,7 +2812,7 @@ __device__ inline void diag_stamp(int) {}
 // threshold, most of a leaf -- a handful of VALU operations: every key takes its primary at
 // rank cp, its record is recP | cp.  Otherwise the rounds of vqf_decide_body, with every mask
 // at hand.
-template <int T, int REC>
+template <int T, int REC, uint32_t NS>
 __device__ void vqf_ring_decide(const tkv_amq_segment& sg, uint32_t seg_index, VqfWorkspace ws,
                                 uint64_t* __restrict__ recs, const uint32_t* ring,
                                 uint32_t* ready, uint32_t* freed, uint32_t* cnt, bool fused,
@@ -2834,8 +2839,8 @@ __device__ void vqf_ring_decide(const tkv_amq_segment& sg, uint32_t seg_index, V
     uint64_t pp, pa, ap, aa, conf;
   };
   auto fetch = [&](uint32_t c, Slot& S) {
-    const uint32_t* slot = ring + (c % kRingSlots) * kRingSlotU32 + lane;
-    S.rdy = lds_load_relaxed(ready + c % kRingSlots);
+    const uint32_t* slot = ring + (c % NS) * kRingSlotU32 + lane;
+    S.rdy = lds_load_relaxed(ready + c % NS);
     asm volatile("" ::: "memory");  // the slot words are read after the ready word
     S.pb4 = slot[64 * kSwPb4];
     S.ab4 = slot[64 * kSwAb4];
@@ -2990,15 +2995,15 @@ __device__ void vqf_ring_decide(const tkv_amq_segment& sg, uint32_t seg_index, V
   }
 }
 
-template <int T, int MODE, int REC, int NBITS, bool kTbl = false>
+template <int T, int MODE, int REC, int NBITS, bool kTbl = false, uint32_t NS = kRingSlots>
 __device__ void vqf_ring_body(const uint8_t* keys, const uint64_t* offs, uint32_t stride,
                               const tkv_amq_segment& sg, uint32_t seg_index, VqfWorkspace ws,
                               uint64_t* recs, uint32_t* lds, bool fused, uint32_t cnt_words,
                               uint64_t key_end)
 {
   uint32_t* ring = lds;
-  uint32_t* ready = ring + kRingSlots * kRingSlotU32;
-  uint32_t* freed = ready + kRingSlots;
+  uint32_t* ready = ring + NS * kRingSlotU32;
+  uint32_t* freed = ready + NS;
   uint32_t* cnt = freed + 2;  // n_blocks + 1 counts: the last is the dummy block's
   // kRecImage: the image after the count table ((n_blocks + 1) regions: the dummy block's
   // last), then the sink word and the nelts word
@@ -3006,16 +3011,16 @@ __device__ void vqf_ring_body(const uint8_t* keys, const uint64_t* offs, uint32_
   uint32_t* img_sink = img + (sg.n_blocks + 1) * kFusedRegionWords;
   // kTbl: the producers' match tables after the sink and nelts words (8-byte aligned)
   uint64_t* tbl = reinterpret_cast<uint64_t*>(img_sink + 2 + ((sg.n_blocks + 1) * kFusedRegionWords & 1));
-  for (uint32_t i = threadIdx.x; i < kRingSlots + 1; i += kRingThreads) ready[i] = 0;  // + freed
+  for (uint32_t i = threadIdx.x; i < NS + 1; i += kRingThreads) ready[i] = 0;  // + freed
   for (uint32_t b = threadIdx.x; b <= sg.n_blocks; b += kRingThreads) cnt[b] = 0;
   if constexpr (kTbl)
     for (uint32_t e = threadIdx.x; e < 2 * kRingTblProducers * (sg.n_blocks + 1); e += kRingThreads) tbl[e] = 0;
   __syncthreads();
   if (threadIdx.x < 64)
-    vqf_ring_decide<T, REC>(sg, seg_index, ws, recs, ring, ready, freed, cnt, fused,
+    vqf_ring_decide<T, REC, NS>(sg, seg_index, ws, recs, ring, ready, freed, cnt, fused,
                             reinterpret_cast<uint8_t*>(img), img_sink, img_sink + 1);
   else
-    vqf_ring_produce<T, MODE, NBITS, REC, kTbl>(keys, offs, stride, sg, ring, ready, freed, tbl, key_end);
+    vqf_ring_produce<T, MODE, NBITS, REC, kTbl, NS>(keys, offs, stride, sg, ring, ready, freed, tbl, key_end);
 }
 
 template <int MODE>
@@ -3535,18 +3540,28 @@ __host__ __device__ inline uint32_t ring_place_cnt_words(uint32_t max_nb)
   return (max_nb + 1 + 3) & ~3u;  // + the dummy block
 }
 
-__host__ __device__ constexpr inline uint32_t ring_place_lds_bytes(uint32_t max_nb)
+__host__ __device__ constexpr inline uint32_t ring_place_lds_bytes(uint32_t max_nb, uint32_t NS = kRingSlots,
+                                                                  bool tbl = true)
 {
-  return kRingBaseBytes + 4 * ((max_nb + 4) & ~3u) + 4 * kFusedRegionWords * (max_nb + 1) + 16 +
-         (max_nb <= kRingTblBlocks ? 16 * kRingTblProducers * (max_nb + 1) : 0);
+  return ring_base_bytes(NS) + 4 * ((max_nb + 4) & ~3u) + 4 * kFusedRegionWords * (max_nb + 1) + 16 +
+         (tbl && max_nb <= kRingTblBlocks ? 16 * kRingTblProducers * (max_nb + 1) : 0);
 }
 
 constexpr uint32_t kRingPlaceMaxBlocks =
     ((160 * 1024 - kRingBaseBytes - 16 - 4 * kFusedRegionWords - 16) / (4 * kFusedRegionWords + 4)) & ~3u;
 static_assert(ring_place_lds_bytes(kRingPlaceMaxBlocks) <= 160 * 1024, "vqf_ring_place LDS");
 static_assert(ring_place_lds_bytes(kRingTblBlocks) <= 160 * 1024, "vqf_ring_place match tables");
+// Batches of kRingPlaceMaxSegs..kRingPlace2MaxSegs leaves: two workgroups per CU, each with a
+// ring of kRingPlace2Slots slots, no match tables, leaves of <= kRingPlace2MaxBlocks blocks
+// (the bench layout's 402-block leaves: one round of 512 leaves instead of the unfused pair)
+constexpr uint32_t kRingPlace2Slots = 6;
+constexpr uint32_t kRingPlace2MaxSegs = 512;
+constexpr uint32_t kRingPlace2MaxBlocks =
+    ((80 * 1024 - ring_base_bytes(kRingPlace2Slots) - 16 - 4 * kFusedRegionWords - 16) / (4 * kFusedRegionWords + 4)) & ~3u;
+static_assert(ring_place_lds_bytes(kRingPlace2MaxBlocks, kRingPlace2Slots, false) <= 80 * 1024,
+              "two vqf_ring_place workgroups per CU");
 
-template <int T, int MODE, int NBITS>
+template <int T, int MODE, int NBITS, uint32_t NS>
 __device__ void vqf_ring_place_body(const uint8_t* keys, const uint64_t* offs, uint32_t stride,
                                     const tkv_amq_segment& sg, uint32_t seg_index, VqfWorkspace ws,
                                     uint8_t* out, uint32_t* lds, uint32_t cnt_words, bool tbl,
@@ -3554,14 +3569,14 @@ __device__ void vqf_ring_place_body(const uint8_t* keys, const uint64_t* offs, u
 {
   using C = Vqf<T>;
   diag_stamp(0);
-  if (NBITS == 9 && tbl)  // (the batch's leaves are <= kRingTblBlocks blocks: the host sized the tables)
-    vqf_ring_body<T, MODE, kRecImage, NBITS, true>(keys, offs, stride, sg, seg_index, ws, nullptr, lds,
+  if (NBITS == 9 && NS == kRingSlots && tbl)  // (leaves <= kRingTblBlocks blocks: the host sized the tables)
+    vqf_ring_body<T, MODE, kRecImage, NBITS, true, NS>(keys, offs, stride, sg, seg_index, ws, nullptr, lds,
                                                    true, cnt_words, key_end);
   else
-    vqf_ring_body<T, MODE, kRecImage, NBITS, false>(keys, offs, stride, sg, seg_index, ws, nullptr, lds,
+    vqf_ring_body<T, MODE, kRecImage, NBITS, false, NS>(keys, offs, stride, sg, seg_index, ws, nullptr, lds,
                                                     true, cnt_words, key_end);
   const uint32_t nb = sg.n_blocks;
-  uint32_t* cnt = reinterpret_cast<uint32_t*>(lds) + kRingBaseBytes / 4;
+  uint32_t* cnt = reinterpret_cast<uint32_t*>(lds) + ring_base_bytes(NS) / 4;
   uint32_t* img = cnt + cnt_words;
   __syncthreads();  // the decider is done (its LDS writes are visible to the workgroup)
   // the sort reads each block's count from its region (a full block keeps its slots)
@@ -3577,7 +3592,7 @@ __device__ void vqf_ring_place_body(const uint8_t* keys, const uint64_t* offs, u
   diag_stamp(2);
 }
 
-template <int MODE>
+template <int MODE, uint32_t NS>
 __global__ __launch_bounds__(kRingThreads) void vqf_ring_place(
     const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint32_t stride,
     const tkv_amq_segment* __restrict__ segs, void* ws_base, uint64_t ws_bytes, uint32_t n_segs,
@@ -3591,11 +3606,11 @@ __global__ __launch_bounds__(kRingThreads) void vqf_ring_place(
   const uint64_t key_end = vqf_key_end<MODE>(offs, segs, n_segs);
   const uint32_t nb = sg.n_blocks;  // <= kRingPlaceMaxBlocks (tkv_amq_build)
   if (sg.tag_bits == 8) {
-    if (nb <= 512) vqf_ring_place_body<8, MODE, 9>(keys, offs, stride, sg, blockIdx.x, ws, out, s_ring, cnt_words, tbl != 0, key_end);
-    else vqf_ring_place_body<8, MODE, 10>(keys, offs, stride, sg, blockIdx.x, ws, out, s_ring, cnt_words, tbl != 0, key_end);
+    if (nb <= 512) vqf_ring_place_body<8, MODE, 9, NS>(keys, offs, stride, sg, blockIdx.x, ws, out, s_ring, cnt_words, tbl != 0, key_end);
+    else vqf_ring_place_body<8, MODE, 10, NS>(keys, offs, stride, sg, blockIdx.x, ws, out, s_ring, cnt_words, tbl != 0, key_end);
   } else if (sg.tag_bits == 16) {
-    if (nb <= 512) vqf_ring_place_body<16, MODE, 9>(keys, offs, stride, sg, blockIdx.x, ws, out, s_ring, cnt_words, tbl != 0, key_end);
-    else vqf_ring_place_body<16, MODE, 10>(keys, offs, stride, sg, blockIdx.x, ws, out, s_ring, cnt_words, tbl != 0, key_end);
+    if (nb <= 512) vqf_ring_place_body<16, MODE, 9, NS>(keys, offs, stride, sg, blockIdx.x, ws, out, s_ring, cnt_words, tbl != 0, key_end);
+    else vqf_ring_place_body<16, MODE, 10, NS>(keys, offs, stride, sg, blockIdx.x, ws, out, s_ring, cnt_words, tbl != 0, key_end);
   } else if (threadIdx.x == 0) {
     ws.nelts[blockIdx.x] = 0;
   }
@@ -4615,32 +4630,45 @@ int tkv_amq_build(int kind, const uint8_t* keys, const uint64_t* offs, uint32_t 
   // 24-byte keys (TurtleKV's default key size hint), 8-byte aligned, are loaded ahead of
   // their hash like 16-byte ones
   const bool prefetched = vmode == kKey16 || vmode == kKey24;
-  if (cnt_mode == kCntU32 && n_segs <= kRingPlaceMaxSegs && max_blocks <= kRingPlaceMaxBlocks) {
-    // decide and place in one workgroup per leaf (vqf_ring_place): no key records, one launch
+  const bool rp1 = n_segs <= kRingPlaceMaxSegs && max_blocks <= kRingPlaceMaxBlocks;
+  const bool rp2 = !rp1 && n_segs <= kRingPlace2MaxSegs && max_blocks <= kRingPlace2MaxBlocks;
+  if (cnt_mode == kCntU32 && (rp1 || rp2)) {
+    // decide and place in one workgroup per leaf (vqf_ring_place): no key records, one launch;
+    // up to 256 leaves one workgroup per CU (ring of kRingSlots, match tables), up to 512 two
     static std::once_flag rp_attr[kMaxDevices];
     once_per_device(rp_attr, [] {
-      for (const void* f : {reinterpret_cast<const void*>(&vqf_ring_place<kKey16>),
-                            reinterpret_cast<const void*>(&vqf_ring_place<kKey24>),
-                            reinterpret_cast<const void*>(&vqf_ring_place<kKeyFixed>),
-                            reinterpret_cast<const void*>(&vqf_ring_place<kKeyVar>)})
+      for (const void* f : {reinterpret_cast<const void*>(&vqf_ring_place<kKey16, kRingSlots>),
+                            reinterpret_cast<const void*>(&vqf_ring_place<kKey24, kRingSlots>),
+                            reinterpret_cast<const void*>(&vqf_ring_place<kKeyFixed, kRingSlots>),
+                            reinterpret_cast<const void*>(&vqf_ring_place<kKeyVar, kRingSlots>),
+                            reinterpret_cast<const void*>(&vqf_ring_place<kKey16, kRingPlace2Slots>),
+                            reinterpret_cast<const void*>(&vqf_ring_place<kKey24, kRingPlace2Slots>),
+                            reinterpret_cast<const void*>(&vqf_ring_place<kKeyFixed, kRingPlace2Slots>),
+                            reinterpret_cast<const void*>(&vqf_ring_place<kKeyVar, kRingPlace2Slots>)})
         (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     });
     const dim3 g(n_segs), b(kRingThreads);
     const uint32_t cw = ring_place_cnt_words(max_blocks);
-    const size_t rl = ring_place_lds_bytes(max_blocks);
-    const uint32_t tbl = max_blocks <= kRingTblBlocks;  // (ring_place_lds_bytes sized them)
-    if (vmode == kKey16)
-      hipLaunchKernelGGL(vqf_ring_place<kKey16>, g, b, rl, s, keys, offs, stride, d_segs, d_ws,
-                         ws_bytes, n_segs, d_out, cw, tbl);
-    else if (vmode == kKey24)
-      hipLaunchKernelGGL(vqf_ring_place<kKey24>, g, b, rl, s, keys, offs, stride, d_segs, d_ws,
-                         ws_bytes, n_segs, d_out, cw, tbl);
-    else if (mode == kKeyFixed)
-      hipLaunchKernelGGL(vqf_ring_place<kKeyFixed>, g, b, rl, s, keys, offs, stride, d_segs, d_ws,
-                         ws_bytes, n_segs, d_out, cw, tbl);
-    else
-      hipLaunchKernelGGL(vqf_ring_place<kKeyVar>, g, b, rl, s, keys, offs, stride, d_segs, d_ws,
-                         ws_bytes, n_segs, d_out, cw, tbl);
+    const uint32_t tbl = rp1 && max_blocks <= kRingTblBlocks;  // (ring_place_lds_bytes sizes them)
+    const size_t rl = rp1 ? ring_place_lds_bytes(max_blocks) : ring_place_lds_bytes(max_blocks, kRingPlace2Slots, false);
+#define TKV_RING_PLACE(NS)                                                                              \
+  do {                                                                                                  \
+    if (vmode == kKey16)                                                                                \
+      hipLaunchKernelGGL((vqf_ring_place<kKey16, NS>), g, b, rl, s, keys, offs, stride, d_segs, d_ws,     \
+                         ws_bytes, n_segs, d_out, cw, tbl);                                             \
+    else if (vmode == kKey24)                                                                           \
+      hipLaunchKernelGGL((vqf_ring_place<kKey24, NS>), g, b, rl, s, keys, offs, stride, d_segs, d_ws,     \
+                         ws_bytes, n_segs, d_out, cw, tbl);                                             \
+    else if (mode == kKeyFixed)                                                                         \
+      hipLaunchKernelGGL((vqf_ring_place<kKeyFixed, NS>), g, b, rl, s, keys, offs, stride, d_segs, d_ws,  \
+                         ws_bytes, n_segs, d_out, cw, tbl);                                             \
+    else                                                                                                \
+      hipLaunchKernelGGL((vqf_ring_place<kKeyVar, NS>), g, b, rl, s, keys, offs, stride, d_segs, d_ws,    \
+                         ws_bytes, n_segs, d_out, cw, tbl);                                             \
+  } while (0)
+    if (rp1) TKV_RING_PLACE(kRingSlots);
+    else TKV_RING_PLACE(kRingPlace2Slots);
+#undef TKV_RING_PLACE
     return hipGetLastError() == hipSuccess ? TKV_AMQ_OK : TKV_AMQ_INTERNAL;
   }
   if (cnt_mode != kCntU32) {
