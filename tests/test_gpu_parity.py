@@ -134,6 +134,34 @@ def test_variable_length_keys(oracle, amq, torch, kind):
     assert_same(plan, out, ref)
 
 
+@pytest.mark.parametrize("kind", [0, 1])
+@pytest.mark.parametrize("tail", ["tiny", "every_length"])
+def test_variable_length_key_windows(oracle, amq, torch, kind, tail):
+    """Short keys are read as 32-byte windows through a buffer resource over their chunk or
+    leaf, the window clamped into the key array: the array's last keys come through a shifted
+    window and are realigned by 1..31 bytes (every length 0..31 ends the array here), and an
+    array of fewer than 32 bytes takes the per-piece loads.  Bloom (64+ leaves: the length-
+    sorted LDS build) and VQF (ring kernels) against the oracle."""
+    rng = np.random.default_rng(23)
+    if tail == "tiny":
+        lens = np.array([0, 1, 2, 3, 4, 5, 6], np.int64)  # 21 bytes in all
+        counts = [len(lens)] + [0] * 63
+    else:
+        body = rng.integers(6, 40, 5000)  # (many duplicates of very short keys would overflow
+                                          # a VQF block, in the oracle too)
+        lens = np.concatenate([body, np.arange(31, -1, -1), np.arange(0, 32)]).astype(np.int64)
+        counts = [int(c) for c in rng.integers(0, 70, 63)]
+        counts.append(len(lens) - sum(counts))
+    blob = rng.integers(0, 256, int(lens.sum()), dtype=np.uint8)
+    offs = np.zeros(len(lens) + 1, np.int64)
+    offs[1:] = np.cumsum(lens)
+    bpk = 10 if kind == 0 else 12
+    ref = oracle_per_segment(oracle, kind, blob, counts, bpk, offsets=offs.astype(np.uint64))
+    plan, out = gpu_build(amq, torch, kind, torch.from_numpy(blob).cuda(), counts, bpk,
+                          offsets_t=torch.from_numpy(offs).cuda())
+    assert_same(plan, out, ref)
+
+
 @pytest.mark.parametrize("big_leaf", [False, True])
 def test_variable_length_keys_many_leaves(oracle, amq, torch, big_leaf):
     """Batches of >= 64 leaves take the per-leaf LDS build, bloom_build_lds<kKeyVar> (fewer
