@@ -355,28 +355,28 @@ def test_vqf_decide_paths(oracle, amq, torch, n_leaves, shape):
 
 
 @pytest.mark.parametrize("n_leaves", [1, 256, 257, 512])
-@pytest.mark.parametrize("edge", ["b402", "tbl", "ring512", "ring884", "plain885"])
+@pytest.mark.parametrize("edge", ["b402", "tbl", "ring512", "ring960", "plain961"])
 @pytest.mark.parametrize("bpk", [12, 22])
 def test_vqf_ring_place_classes(oracle, amq, torch, n_leaves, edge, bpk):
     """Batches of <= 256 leaves whose largest leaf has <= 884 blocks take vqf_ring_place
     (decide and place in one workgroup per leaf, entries straight into the LDS image; <= 512
-    blocks: the producers' LDS match tables), batches of up to 512 leaves of <= 428 blocks two
+    blocks: the producers' LDS match tables), batches of up to 512 leaves of <= 420 blocks two
     such workgroups per CU (b402: the bench layout's 16K-key leaves), others vqf_decide_ring +
-    vqf_place_fused.  The batch's largest leaf sits at each threshold (512 / 513 / 884 / 885
+    vqf_place_fused.  The batch's largest leaf sits at each threshold (512 / 513 / 960 / 961
     blocks in 64 KiB pages), 8- and 16-bit tags; byte-equal to the oracle."""
-    big = {12: {"b402": 16384, "tbl": 20889, "ring512": 20890, "ring884": 36067, "plain885": 36068},
-           22: {"b402": 9000, "tbl": 11729, "ring512": 11730, "ring884": 20251, "plain885": 20252}}[bpk][edge]
+    big = {12: {"b402": 16384, "tbl": 20889, "ring512": 20890, "ring960": 39167, "plain961": 39168},
+           22: {"b402": 9000, "tbl": 11729, "ring512": 11730, "ring960": 21992, "plain961": 21993}}[bpk][edge]
     rng = np.random.default_rng(7 + n_leaves)
     counts = [big] + [int(c) for c in rng.integers(0, 3000, n_leaves - 1)]
     if n_leaves > 2:
         counts[1] = 0
     keys = oracle.gen_keys16(9, 0, sum(counts))
     plan, out = gpu_build(amq, torch, 1, torch.from_numpy(keys).cuda(), counts, bpk, cap=65472)
-    want = {"b402": None, "tbl": 512, "ring512": 513, "ring884": 884, "plain885": 885}[edge]
+    want = {"b402": None, "tbl": 512, "ring512": 513, "ring960": 960, "plain961": 961}[edge]
     if want is not None:
         assert int(plan.segs["n_blocks"].max()) == want
     else:
-        assert int(plan.segs["n_blocks"].max()) <= 428
+        assert int(plan.segs["n_blocks"].max()) <= 420
     sb = seg_bounds(counts)
     for s in sorted({0, n_leaves - 1, *rng.integers(0, n_leaves, 4).tolist()}):
         st, ref, p = oracle.vqf_build(keys[int(sb[s]):], counts[s], bpk, 65472, src_page_id=s)

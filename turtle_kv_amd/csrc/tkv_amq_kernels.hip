@@ -2569,16 +2569,18 @@ constexpr uint32_t kFusedCountWord = 32;
 constexpr uint32_t kRingThreads = 512;
 constexpr uint32_t kRingProducers = kRingThreads / 64 - 1;
 constexpr uint32_t kRingSlots = 10;
+constexpr uint32_t kRingPlaceSlots = 8;  // vqf_ring_place, one workgroup per CU
 // A slot holds, per lane of its chunk, these u32 words (plane w at [w * 64 + lane]), all the
 // producers can know, so the decider's step is the decision and nothing else:
 enum VqfSlotWord : uint32_t {
-  kSwPb4 = 0,            // 4 x primary block: the byte offset of its count (a key not inserted:
-                         // the dummy block n_blocks, whose count stays 0)
-  kSwAb4 = 1,            // 4 x alternate block (dummy likewise)
+  kSwPb4 = 0,            // LDS address of the primary block's count (a key not inserted: the
+                         // dummy block n_blocks, whose count stays 0)
+  kSwAb4 = 1,            // LDS address of the alternate block's count (dummy likewise)
   kSwRanks = 2,          // r_pp | r_pa << 8 | r_ap << 16 | kept << 24 | eligible << 25
   kSwRecP = 3,           // the key's record with its primary block, rank bits 0 (VqfRecMode)
   kSwRecA = 4,           // ... with its alternate block
-  kSwMpp = 5,            // lo, hi: earlier kept lanes with my primary as their primary
+  kSwImgP = 5,           // kRecImage: LDS address of the primary block's image region
+  kSwMpp = 6,            // lo, hi: earlier kept lanes with my primary as their primary
   kSwMpa = kSwMpp + 2,   // ... with my alternate as their primary
   kSwMap = kSwMpa + 2,   // ... with my primary as their alternate
   kSwMaa = kSwMap + 2,   // ... with my alternate as their alternate
@@ -2586,8 +2588,26 @@ enum VqfSlotWord : uint32_t {
   kSwCount = kSwConf + 2
 };
 // r_pp / r_pa / r_ap: popcounts of Mpp / Mpa / Map (0 for a key not inserted); eligible: kept
-// and its two blocks differ (vqf_insert's alternate test)
+// and its two blocks differ (vqf_insert's alternate test).  The decider uses the LDS addresses
+// as they are (ds_read / ds_add with no address arithmetic).
 constexpr uint32_t kRingSlotU32 = kSwCount * 64;
+static_assert(kSwCount == 16, "a 4 KiB slot");
+
+// LDS byte addresses (the low word of a generic pointer to LDS is its LDS address)
+typedef __attribute__((address_space(3))) uint32_t lds_u32_t;
+typedef __attribute__((address_space(3))) uint16_t lds_u16_t;
+__device__ inline uint32_t lds_addr(const void* p)
+{
+  return (uint32_t)reinterpret_cast<uintptr_t>(p);
+}
+__device__ inline uint32_t lds_rd(uint32_t a)
+{
+  return *reinterpret_cast<const lds_u32_t*>((uintptr_t)a);
+}
+__device__ inline void lds_add(uint32_t a, uint32_t v)
+{
+  __atomic_fetch_add(reinterpret_cast<lds_u32_t*>((uintptr_t)a), v, __ATOMIC_RELAXED);
+}
 constexpr uint32_t kRingMaxBlocks = 2048;
 // ring | ready[NS] | freed (+1 spare): the count table starts here
 __host__ __device__ constexpr inline uint32_t ring_base_bytes(uint32_t NS)
@@ -2642,8 +2662,10 @@ constexpr uint32_t kRingTblProducers = 6;
 template <int T, int MODE, int NBITS, int REC, bool kTbl, uint32_t NS>
 __device__ void vqf_ring_produce(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs,
                                  uint32_t stride, const tkv_amq_segment& sg, uint32_t* ring,
-                                 uint32_t* ready, uint32_t* freed, uint64_t* tbl, uint64_t key_end)
+                                 uint32_t* ready, uint32_t* freed, uint64_t* tbl, uint64_t key_end,
+                                 const uint32_t* cnt, const uint32_t* img)
 {
+  const uint32_t cnt_base = lds_addr(cnt), img_base = lds_addr(img);
   using C = Vqf<T>;
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x / 64;
   if (kTbl && wave == 4) return;
@@ -2746,7 +2768,9 @@ __device__ void vqf_ring_produce(const uint8_t* __restrict__ keys, const uint64_
                                       ((uint32_t)__popcll(Map) << 16) | (1u << 24) |
                                       (l.pb != ab ? 1u << 25 : 0u)
                                 : 0u;
-    const uint32_t pb4 = 4 * (kept ? l.pb : nb), ab4 = 4 * (kept ? ab : nb);
+    const uint32_t pbk = kept ? l.pb : nb;
+    const uint32_t pb4 = cnt_base + 4 * pbk, ab4 = cnt_base + 4 * (kept ? ab : nb);
+    const uint32_t imgP = img_base + 4 * kFusedRegionWords * pbk;
     const uint32_t recP = vqf_ring_rec<T, REC>(kept, l.pb, l.po, l.tag);
     const uint32_t recA = vqf_ring_rec<T, REC>(kept, ab, ao, l.tag);
     // the slot is free once the decider has taken chunk q - NS
@@ -2758,6 +2782,7 @@ __device__ void vqf_ring_produce(const uint8_t* __restrict__ keys, const uint64_
     slot[64 * kSwRanks] = ranks;
     slot[64 * kSwRecP] = recP;
     slot[64 * kSwRecA] = recA;
+    slot[64 * kSwImgP] = imgP;
     slot[64 * kSwMpp] = lo32(Mpp);
     slot[64 * (kSwMpp + 1)] = hi32(Mpp);
     slot[64 * kSwMpa] = lo32(Mpa);
@@ -2807,11 +2832,26 @@ __device__ inline void diag_stamp(int i)
 __device__ inline void diag_stamp(int) {}
 #endif
 
-// The decider wave.  Per 64-key step: the two block counts (one LDS round trip; the next
-// slot is read a step ahead), then -- in the steps where no lane's primary has reached the
-// threshold, most of a leaf -- a handful of VALU operations: every key takes its primary at
-// rank cp, its record is recP | cp.  Otherwise the rounds of vqf_decide_body, with every mask
-// at hand.
+// NS steps of the decider's loop with compile-time slot indices (no modulo, no slot address
+// arithmetic): f(c + I, integral_constant<I>) for I = 0.. while c + I < n
+template <uint32_t I, uint32_t NS, typename F>
+__device__ inline bool ring_unroll(F& f, uint32_t c, uint32_t n)
+{
+  if constexpr (I == NS) {
+    return true;
+  } else {
+    if (c + I >= n) return false;
+    f(c + I, std::integral_constant<uint32_t, I>{});
+    return ring_unroll<I + 1, NS>(f, c, n);
+  }
+}
+
+// The decider wave.  Per 64-key step: the two block counts (one LDS round trip at the LDS
+// addresses the producers wrote; the next slot is read a step ahead), then -- in the steps
+// where no lane's primary has reached the threshold, most of a leaf -- a handful of
+// instructions: every key takes its primary at rank cp, its record is recP | cp (kRecImage:
+// its entry lands at imgP + cp).  Otherwise the rounds of vqf_decide_body, with every mask at
+// hand.  The loop is unrolled by the ring's NS slots, so every slot offset is an immediate.
 template <int T, int REC, uint32_t NS>
 __device__ void vqf_ring_decide(const tkv_amq_segment& sg, uint32_t seg_index, VqfWorkspace ws,
                                 uint64_t* __restrict__ recs, const uint32_t* ring,
@@ -2819,7 +2859,9 @@ __device__ void vqf_ring_decide(const tkv_amq_segment& sg, uint32_t seg_index, V
                                 uint8_t* img8, uint32_t* img_sink, uint32_t* s_nelts)
 {
   using C = Vqf<T>;
+  static_assert(NS % 2 == 0, "two slot register sets alternate");
   constexpr bool kCompact = REC == kRecCompact;
+  constexpr uint32_t kE = sizeof(typename C::Entry);
   const uint32_t lane = threadIdx.x;
   const uint32_t n = sg.n_keys, nb = sg.n_blocks;
   const uint32_t n_chunks = (n + 63) / 64;
@@ -2828,42 +2870,42 @@ __device__ void vqf_ring_decide(const tkv_amq_segment& sg, uint32_t seg_index, V
   Rec* const sink = reinterpret_cast<Rec*>(ws.sink);  // see vqf_decide_body
   Rec* pend_ptr = sink;
   Rec pend_val = 0;
-  uint8_t* const cnt8 = reinterpret_cast<uint8_t*>(cnt);
-  // the image sink as an offset from the image (a full block's key writes there)
-  const uint32_t sink_off = (uint32_t)(reinterpret_cast<uint8_t*>(img_sink) - img8);
-  // The next chunk's ready word and slot are read one step ahead (they do not depend on the
-  // counts), so a step waits for one LDS round trip: the block counts.  Two slot register
-  // sets alternate (the loop is unrolled by two), so no step copies the prefetched words.
+  const uint32_t cnt_base = lds_addr(cnt), img_base = lds_addr(img8);
+  const uint32_t sink_addr = lds_addr(img_sink);  // a full block's key writes its entry here
+  // Two slot register sets alternate (even / odd steps), so no step copies the prefetched words.
   struct Slot {
-    uint32_t rdy, pb4, ab4, ranks, recP, recA;
+    uint32_t rdy, pb4, ab4, ranks, recP, recA, imgP;
     uint64_t pp, pa, ap, aa, conf;
   };
-  auto fetch = [&](uint32_t c, Slot& S) {
-    const uint32_t* slot = ring + (c % NS) * kRingSlotU32 + lane;
-    S.rdy = lds_load_relaxed(ready + c % NS);
+  auto fetch = [&](uint32_t q, Slot& S) {  // slot q (compile-time in the unrolled loop)
+    const uint32_t* slot = ring + q * kRingSlotU32 + lane;
+    S.rdy = lds_load_relaxed(ready + q);
     asm volatile("" ::: "memory");  // the slot words are read after the ready word
     S.pb4 = slot[64 * kSwPb4];
     S.ab4 = slot[64 * kSwAb4];
     S.ranks = slot[64 * kSwRanks];
     S.recP = slot[64 * kSwRecP];
     S.recA = slot[64 * kSwRecA];
+    S.imgP = slot[64 * kSwImgP];
     S.pp = mk64(slot[64 * kSwMpp], slot[64 * (kSwMpp + 1)]);
     S.pa = mk64(slot[64 * kSwMpa], slot[64 * (kSwMpa + 1)]);
     S.ap = mk64(slot[64 * kSwMap], slot[64 * (kSwMap + 1)]);
     S.aa = mk64(slot[64 * kSwMaa], slot[64 * (kSwMaa + 1)]);
     S.conf = mk64(slot[64 * kSwConf], slot[64 * (kSwConf + 1)]);
   };
-  // PH: the two copies of the step in the unrolled loop differ by an asm marker, so they are
-  // not merged into one body with the slot registers copied between the sets
-  auto step = [&](uint32_t c, Slot& S, Slot& next, auto PH) {
-    asm volatile("; ring step %0" ::"n"(decltype(PH)::value));
+  Slot A, B;
+  auto step = [&](uint32_t c, auto I) {
+    constexpr uint32_t q = decltype(I)::value;
+    Slot& S = q % 2 == 0 ? A : B;
+    Slot& next = q % 2 == 0 ? B : A;
+    asm volatile("; ring step %0" ::"n"(q));  // (keeps the copies distinct)
 #ifdef TKV_DIAG_RING
     const uint64_t d0 = __builtin_amdgcn_s_memtime();
     uint32_t spins = 0;
 #endif
     while (S.rdy != c + 1) {
       __builtin_amdgcn_s_sleep(1);
-      fetch(c, S);
+      fetch(q, S);
 #ifdef TKV_DIAG_RING
       ++spins;
 #endif
@@ -2873,28 +2915,30 @@ __device__ void vqf_ring_decide(const tkv_amq_segment& sg, uint32_t seg_index, V
 #endif
 #ifdef TKV_EXP_NODECIDE  // experiment: the producers' rate (the decider only frees slots)
     lds_store_relaxed(freed, c + 1);
-    fetch(min(c + 1, n_chunks - 1), next);
+    fetch((q + 1) % NS, next);
     return;
 #endif
-    const uint32_t cnt_p = *reinterpret_cast<const uint32_t*>(cnt8 + S.pb4);
-    const uint32_t cnt_a = *reinterpret_cast<const uint32_t*>(cnt8 + S.ab4);
+    const uint32_t cnt_p = lds_rd(S.pb4);
+    const uint32_t cnt_a = lds_rd(S.ab4);
 #ifdef TKV_DIAG_RING
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     const uint64_t d2 = __builtin_amdgcn_s_memtime();
 #endif
     // LDS operations complete in issue order: the prefetch goes after the count reads, so
     // waiting for the counts does not wait for it.  Neither the hand-off write nor the
-    // prefetch is skipped (every lane writes the same word; the last step re-reads the last
-    // slot), so the compiler's count of LDS operations in flight is exact on every path.
+    // prefetch is skipped (every lane writes the same word; after the last chunk the prefetch
+    // reads a slot no producer writes any more), so the compiler's count of LDS operations in
+    // flight is exact on every path.
     asm volatile("" ::: "memory");
     lds_store_relaxed(freed, c + 1);  // the slot's words are in registers (LDS order)
-    fetch(min(c + 1, n_chunks - 1), next);
+    fetch((q + 1) % NS, next);
     if constexpr (REC != kRecImage) *pend_ptr = pend_val;
     const uint32_t ranks = S.ranks;
     // count of my primary if every earlier lane of the chunk takes its primary (a key not
     // inserted: 0, the dummy block's count and no ranks)
     uint32_t cp = cnt_p + (ranks & 0xffu);
     uint32_t chosen4 = S.pb4, r = cp, recx = S.recP;
+    uint32_t dst = S.imgP + cp * kE;  // kRecImage: cp < threshold < slots on the fast path
 #ifdef TKV_DIAG_RING
     uint64_t slow = 0;
 #endif
@@ -2918,11 +2962,11 @@ __device__ void vqf_ring_decide(const tkv_amq_segment& sg, uint32_t seg_index, V
         F &= U;
         while (F != 0) {
           const uint64_t res = bal((S.conf & U) == 0) & U;
-          const uint64_t A = res & F;
-          altmask |= A;
+          const uint64_t Am = res & F;
+          altmask |= Am;
           U &= ~res;
-          cp = cp + (uint32_t)__popcll(S.ap & A) - (uint32_t)__popcll(S.pp & A);
-          ca = ca + (uint32_t)__popcll(S.aa & A) - (uint32_t)__popcll(S.pa & A);
+          cp = cp + (uint32_t)__popcll(S.ap & Am) - (uint32_t)__popcll(S.pp & Am);
+          ca = ca + (uint32_t)__popcll(S.aa & Am) - (uint32_t)__popcll(S.pa & Am);
           F = bal(max(ca, C::kThreshold - 1) < cp) & U;
         }
       }
@@ -2930,6 +2974,8 @@ __device__ void vqf_ring_decide(const tkv_amq_segment& sg, uint32_t seg_index, V
       chosen4 = sel_mask(altmask, S.ab4, S.pb4);
       r = sel_mask(altmask, ca, cp);  // a full block (r >= slots) shows in the final counts
       recx = sel_mask(altmask, S.recA, S.recP);
+      if constexpr (REC == kRecImage)
+        dst = r < C::kSlots ? img_base + (chosen4 - cnt_base) * kFusedRegionWords + r * kE : sink_addr;
     }
 #ifdef TKV_DIAG_RING
     const uint64_t d3 = __builtin_amdgcn_s_memtime();
@@ -2945,30 +2991,24 @@ __device__ void vqf_ring_decide(const tkv_amq_segment& sg, uint32_t seg_index, V
       // entry at [chosen][r] of the image (vqf_place_fused_body's phase 1, done here); a key
       // not inserted lands in the dummy block's region, a full block's key on the sink word,
       // so every step issues the same LDS operations
-      constexpr uint32_t kE = sizeof(typename C::Entry);
-      const uint32_t off = r < C::kSlots ? chosen4 * kFusedRegionWords + r * kE : sink_off;
-      uint8_t* dst = img8 + off;
-      if constexpr (T == 8) *reinterpret_cast<uint16_t*>(dst) = (uint16_t)recx;
-      else *reinterpret_cast<uint32_t*>(dst) = recx;
+      if constexpr (T == 8) *reinterpret_cast<lds_u16_t*>((uintptr_t)dst) = (uint16_t)recx;
+      else *reinterpret_cast<lds_u32_t*>((uintptr_t)dst) = recx;
     } else {
       pend_ptr = c * 64 + lane < n ? rec + c * 64 + lane : sink;
       if constexpr (kCompact) {
         pend_val = r < C::kSlots ? recx | (r << 15) : 0xffffffffu;
       } else {
         const uint32_t slot_hi = (kept && r < C::kSlots)
-                                     ? (uint32_t)((sg.block_base + chosen4 / 4) * 64 + r) : 0xffffffffu;
+                                     ? (uint32_t)((sg.block_base + (chosen4 - cnt_base) / 4) * 64 + r)
+                                     : 0xffffffffu;
         pend_val = ((uint64_t)slot_hi << 32) | recx;
       }
     }
-    atomicAdd(reinterpret_cast<uint32_t*>(cnt8 + chosen4), kept);
+    lds_add(chosen4, kept);
   };
-  Slot A, B;
   if (n_chunks > 0) fetch(0, A);
-  for (uint32_t c = 0; c < n_chunks; c += 2) {
-    step(c, A, B, std::integral_constant<int, 0>{});
-    if (c + 1 >= n_chunks) break;
-    step(c + 1, B, A, std::integral_constant<int, 1>{});
-  }
+  for (uint32_t c = 0; c < n_chunks; c += NS)
+    if (!ring_unroll<0, NS>(step, c, n_chunks)) break;
   // a key found its block full (vqf_insert fails) iff that block's final count exceeds
   // slots; the element count is the sum of the counts (the dummy block's stays 0)
   uint32_t fail = 0, nelts = 0;
@@ -3020,7 +3060,8 @@ __device__ void vqf_ring_body(const uint8_t* keys, const uint64_t* offs, uint32_
     vqf_ring_decide<T, REC, NS>(sg, seg_index, ws, recs, ring, ready, freed, cnt, fused,
                             reinterpret_cast<uint8_t*>(img), img_sink, img_sink + 1);
   else
-    vqf_ring_produce<T, MODE, NBITS, REC, kTbl, NS>(keys, offs, stride, sg, ring, ready, freed, tbl, key_end);
+    vqf_ring_produce<T, MODE, NBITS, REC, kTbl, NS>(keys, offs, stride, sg, ring, ready, freed, tbl, key_end,
+                                                    cnt, img);
 }
 
 template <int MODE>
@@ -3540,7 +3581,7 @@ __host__ __device__ inline uint32_t ring_place_cnt_words(uint32_t max_nb)
   return (max_nb + 1 + 3) & ~3u;  // + the dummy block
 }
 
-__host__ __device__ constexpr inline uint32_t ring_place_lds_bytes(uint32_t max_nb, uint32_t NS = kRingSlots,
+__host__ __device__ constexpr inline uint32_t ring_place_lds_bytes(uint32_t max_nb, uint32_t NS = kRingPlaceSlots,
                                                                   bool tbl = true)
 {
   return ring_base_bytes(NS) + 4 * ((max_nb + 4) & ~3u) + 4 * kFusedRegionWords * (max_nb + 1) + 16 +
@@ -3548,7 +3589,8 @@ __host__ __device__ constexpr inline uint32_t ring_place_lds_bytes(uint32_t max_
 }
 
 constexpr uint32_t kRingPlaceMaxBlocks =
-    ((160 * 1024 - kRingBaseBytes - 16 - 4 * kFusedRegionWords - 16) / (4 * kFusedRegionWords + 4)) & ~3u;
+    ((160 * 1024 - ring_base_bytes(kRingPlaceSlots) - 16 - 4 * kFusedRegionWords - 16) / (4 * kFusedRegionWords + 4)) & ~3u;
+static_assert(kRingPlaceMaxBlocks == 960, "(DESIGN.md and test_vqf_ring_place_classes quote it)");
 static_assert(ring_place_lds_bytes(kRingPlaceMaxBlocks) <= 160 * 1024, "vqf_ring_place LDS");
 static_assert(ring_place_lds_bytes(kRingTblBlocks) <= 160 * 1024, "vqf_ring_place match tables");
 // Batches of kRingPlaceMaxSegs..kRingPlace2MaxSegs leaves: two workgroups per CU, each with a
@@ -3560,6 +3602,7 @@ constexpr uint32_t kRingPlace2MaxBlocks =
     ((80 * 1024 - ring_base_bytes(kRingPlace2Slots) - 16 - 4 * kFusedRegionWords - 16) / (4 * kFusedRegionWords + 4)) & ~3u;
 static_assert(ring_place_lds_bytes(kRingPlace2MaxBlocks, kRingPlace2Slots, false) <= 80 * 1024,
               "two vqf_ring_place workgroups per CU");
+static_assert(kRingPlace2MaxBlocks == 420, "(DESIGN.md and test_vqf_ring_place_classes quote it)");
 
 template <int T, int MODE, int NBITS, uint32_t NS>
 __device__ void vqf_ring_place_body(const uint8_t* keys, const uint64_t* offs, uint32_t stride,
@@ -3569,7 +3612,7 @@ __device__ void vqf_ring_place_body(const uint8_t* keys, const uint64_t* offs, u
 {
   using C = Vqf<T>;
   diag_stamp(0);
-  if (NBITS == 9 && NS == kRingSlots && tbl)  // (leaves <= kRingTblBlocks blocks: the host sized the tables)
+  if (NBITS == 9 && NS == kRingPlaceSlots && tbl)  // (leaves <= kRingTblBlocks blocks: the host sized the tables)
     vqf_ring_body<T, MODE, kRecImage, NBITS, true, NS>(keys, offs, stride, sg, seg_index, ws, nullptr, lds,
                                                    true, cnt_words, key_end);
   else
@@ -4634,13 +4677,13 @@ int tkv_amq_build(int kind, const uint8_t* keys, const uint64_t* offs, uint32_t 
   const bool rp2 = !rp1 && n_segs <= kRingPlace2MaxSegs && max_blocks <= kRingPlace2MaxBlocks;
   if (cnt_mode == kCntU32 && (rp1 || rp2)) {
     // decide and place in one workgroup per leaf (vqf_ring_place): no key records, one launch;
-    // up to 256 leaves one workgroup per CU (ring of kRingSlots, match tables), up to 512 two
+    // up to 256 leaves one workgroup per CU (ring of kRingPlaceSlots, match tables), up to 512 two
     static std::once_flag rp_attr[kMaxDevices];
     once_per_device(rp_attr, [] {
-      for (const void* f : {reinterpret_cast<const void*>(&vqf_ring_place<kKey16, kRingSlots>),
-                            reinterpret_cast<const void*>(&vqf_ring_place<kKey24, kRingSlots>),
-                            reinterpret_cast<const void*>(&vqf_ring_place<kKeyFixed, kRingSlots>),
-                            reinterpret_cast<const void*>(&vqf_ring_place<kKeyVar, kRingSlots>),
+      for (const void* f : {reinterpret_cast<const void*>(&vqf_ring_place<kKey16, kRingPlaceSlots>),
+                            reinterpret_cast<const void*>(&vqf_ring_place<kKey24, kRingPlaceSlots>),
+                            reinterpret_cast<const void*>(&vqf_ring_place<kKeyFixed, kRingPlaceSlots>),
+                            reinterpret_cast<const void*>(&vqf_ring_place<kKeyVar, kRingPlaceSlots>),
                             reinterpret_cast<const void*>(&vqf_ring_place<kKey16, kRingPlace2Slots>),
                             reinterpret_cast<const void*>(&vqf_ring_place<kKey24, kRingPlace2Slots>),
                             reinterpret_cast<const void*>(&vqf_ring_place<kKeyFixed, kRingPlace2Slots>),
@@ -4666,7 +4709,7 @@ int tkv_amq_build(int kind, const uint8_t* keys, const uint64_t* offs, uint32_t 
       hipLaunchKernelGGL((vqf_ring_place<kKeyVar, NS>), g, b, rl, s, keys, offs, stride, d_segs, d_ws,    \
                          ws_bytes, n_segs, d_out, cw, tbl);                                             \
   } while (0)
-    if (rp1) TKV_RING_PLACE(kRingSlots);
+    if (rp1) TKV_RING_PLACE(kRingPlaceSlots);
     else TKV_RING_PLACE(kRingPlace2Slots);
 #undef TKV_RING_PLACE
     return hipGetLastError() == hipSuccess ? TKV_AMQ_OK : TKV_AMQ_INTERNAL;
