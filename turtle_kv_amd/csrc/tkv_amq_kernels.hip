@@ -2657,7 +2657,7 @@ __device__ inline uint32_t vqf_ring_rec(bool kept, uint32_t block, uint32_t buck
 // and 5-7): wave 4 idles so the decider has its SIMD to itself (a workgroup's waves are
 // placed on the CU's four SIMDs in turn).  Otherwise seven producers and block-id ballots.
 constexpr uint32_t kRingTblBlocks = 512;
-constexpr uint32_t kRingTblProducers = 6;
+constexpr uint32_t kRingTblProducers = 7;
 
 template <int T, int MODE, int NBITS, int REC, bool kTbl, uint32_t NS>
 __device__ void vqf_ring_produce(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs,
@@ -2668,8 +2668,9 @@ __device__ void vqf_ring_produce(const uint8_t* __restrict__ keys, const uint64_
   const uint32_t cnt_base = lds_addr(cnt), img_base = lds_addr(img);
   using C = Vqf<T>;
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x / 64;
-  if (kTbl && wave == 4) return;
-  const uint32_t w = kTbl ? (wave < 4 ? wave - 1 : wave - 2) : wave - 1;
+  // (with six table producers wave 4 idles: the decider's SIMD without a producer)
+  if (kTbl && kRingTblProducers == 6 && wave == 4) return;
+  const uint32_t w = (kTbl && kRingTblProducers == 6) ? (wave < 4 ? wave - 1 : wave - 2) : wave - 1;
   const uint32_t n = sg.n_keys, nb = sg.n_blocks;
   const uint32_t n_chunks = (n + 63) / 64;
   const uint64_t R = (uint64_t)nb * C::kBuckets;
