@@ -2660,7 +2660,7 @@ constexpr uint32_t kRingTblBlocks = 512;
 constexpr uint32_t kRingTblProducers = 7;
 
 template <int T, int MODE, int NBITS, int REC, bool kTbl, uint32_t NS>
-__device__ void vqf_ring_produce(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs,
+__device__ __attribute__((always_inline)) void vqf_ring_produce(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs,
                                  uint32_t stride, const tkv_amq_segment& sg, uint32_t* ring,
                                  uint32_t* ready, uint32_t* freed, uint64_t* tbl, uint64_t key_end,
                                  const uint32_t* cnt, const uint32_t* img)
@@ -2853,8 +2853,10 @@ __device__ inline bool ring_unroll(F& f, uint32_t c, uint32_t n)
 // instructions: every key takes its primary at rank cp, its record is recP | cp (kRecImage:
 // its entry lands at imgP + cp).  Otherwise the rounds of vqf_decide_body, with every mask at
 // hand.  The loop is unrolled by the ring's NS slots, so every slot offset is an immediate.
+// (always inlined: out of line, the unrolled loop of the larger instantiations became a call
+// with a scratch frame -- 768 leaves of variable-length keys 253 -> 384 us)
 template <int T, int REC, uint32_t NS>
-__device__ void vqf_ring_decide(const tkv_amq_segment& sg, uint32_t seg_index, VqfWorkspace ws,
+__device__ __attribute__((always_inline)) void vqf_ring_decide(const tkv_amq_segment& sg, uint32_t seg_index, VqfWorkspace ws,
                                 uint64_t* __restrict__ recs, const uint32_t* ring,
                                 uint32_t* ready, uint32_t* freed, uint32_t* cnt, bool fused,
                                 uint8_t* img8, uint32_t* img_sink, uint32_t* s_nelts)
@@ -3037,7 +3039,7 @@ __device__ void vqf_ring_decide(const tkv_amq_segment& sg, uint32_t seg_index, V
 }
 
 template <int T, int MODE, int REC, int NBITS, bool kTbl = false, uint32_t NS = kRingSlots>
-__device__ void vqf_ring_body(const uint8_t* keys, const uint64_t* offs, uint32_t stride,
+__device__ __attribute__((always_inline)) void vqf_ring_body(const uint8_t* keys, const uint64_t* offs, uint32_t stride,
                               const tkv_amq_segment& sg, uint32_t seg_index, VqfWorkspace ws,
                               uint64_t* recs, uint32_t* lds, bool fused, uint32_t cnt_words,
                               uint64_t key_end)
@@ -3606,7 +3608,7 @@ static_assert(ring_place_lds_bytes(kRingPlace2MaxBlocks, kRingPlace2Slots, false
 static_assert(kRingPlace2MaxBlocks == 420, "(DESIGN.md and test_vqf_ring_place_classes quote it)");
 
 template <int T, int MODE, int NBITS, uint32_t NS>
-__device__ void vqf_ring_place_body(const uint8_t* keys, const uint64_t* offs, uint32_t stride,
+__device__ __attribute__((always_inline)) void vqf_ring_place_body(const uint8_t* keys, const uint64_t* offs, uint32_t stride,
                                     const tkv_amq_segment& sg, uint32_t seg_index, VqfWorkspace ws,
                                     uint8_t* out, uint32_t* lds, uint32_t cnt_words, bool tbl,
                                     uint64_t key_end)
