@@ -225,6 +225,15 @@ int tkv_amq_bloom_route_records(const uint8_t* d_keys16, uint64_t n_keys, const 
                                 uint32_t n_blocks, uint32_t hash_count, uint32_t n_parts,
                                 uint8_t* d_recs12, uint32_t* d_part_counts, void* d_workspace,
                                 uint64_t workspace_bytes, void* stream);
+/* tkv_amq_bloom_route_records_ex: the same with key_bytes 16 or 24 (24-byte keys 8-byte
+ * aligned: TurtleKV's default key size, tree/tree_options.hpp:58); the records, and so the
+ * exchange and tkv_amq_bloom_build_range_records, do not depend on the key size.  Same
+ * workspace as tkv_amq_bloom_route_records_ws_bytes. */
+int tkv_amq_bloom_route_records_ex(const uint8_t* d_keys, uint32_t key_bytes, uint64_t n_keys,
+                                   const tkv_amq_segment* d_seg, uint32_t n_blocks,
+                                   uint32_t hash_count, uint32_t n_parts, uint8_t* d_recs12,
+                                   uint32_t* d_part_counts, void* d_workspace,
+                                   uint64_t workspace_bytes, void* stream);
 uint64_t tkv_amq_bloom_build_range_records_ws_bytes(uint64_t n_recs, uint32_t tile_begin,
                                                     uint32_t tile_end);
 int tkv_amq_bloom_build_range_records(const uint8_t* d_recs12, uint64_t n_recs,

@@ -111,5 +111,9 @@ def test_hash_shard_tiles_cover_the_filter():
     assert empty == [6, 7]
     hs = HashShardedBloom(100_000, 12, 8, 5, "cpu")   # 3 tiles over 8 ranks: rank 5 owns none
     assert hs.tile_begin == hs.tile_end == 3
-    with pytest.raises(abi.TkvAmqError):
-        hs.route(torch.zeros((10, 24), dtype=torch.uint8))   # 16-byte keys only
+    with pytest.raises(abi.TkvAmqError, match="got shape"):
+        hs.route(torch.zeros((10, 20), dtype=torch.uint8))   # 16- or 24-byte keys only
+    hk = HashShardedBloom(100_000, 16, 8, 0, "cpu")         # k = 11: keys travel, 16 bytes only
+    assert not hk.records
+    with pytest.raises(abi.TkvAmqError, match="got shape"):
+        hk.route(torch.zeros((10, 24), dtype=torch.uint8))

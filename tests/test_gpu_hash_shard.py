@@ -204,6 +204,53 @@ def test_route_records_and_range_build_equal_monolithic(oracle, amq, torch, n_ke
     assert st == 0 and out.cpu().numpy().tobytes() == ref.tobytes()
 
 
+@pytest.mark.parametrize("n_keys,bpk,n_parts,dup", [(1_200_000, 12, 3, 0), (900_001, 10, 8, 0),
+                                                   (800_000, 12, 2, 300_000), (500_000, 5, 1, 0)])
+def test_route_records_k24_equal_monolithic(oracle, amq, torch, n_keys, bpk, n_parts, dup):
+    """Hash-range sharding of 24-byte keys (tkv_amq_bloom_route_records_ex): the sender hashes
+    each key once into the same 12-byte records as for 16-byte keys, so the owners' range
+    builds are unchanged.  Equal to the one-GPU build of the same keys and to the oracle."""
+    from turtle_kv_amd.dist import hash_shard_tiles
+    from turtle_kv_amd.filters import _ptr, _stream_handle
+    L = amq.abi.lib()
+    rng = np.random.default_rng(n_keys)
+    kn = rng.integers(0, 256, (n_keys, 24), dtype=np.uint8)
+    if dup:
+        kn[n_keys - dup:] = kn[n_keys // 3]
+    keys = torch.from_numpy(kn).cuda()
+    plan = amq.plan_filters(0, [n_keys], bpk)
+    seg = plan.segs[0]
+    whole = amq.build_all_filters(plan, amq.KeyBatch.fixed(keys))
+    recs = torch.empty((n_keys, 12), dtype=torch.uint8, device="cuda")
+    counts = torch.zeros(n_parts, dtype=torch.int32, device="cuda")
+    ws = torch.empty(int(L.tkv_amq_bloom_route_records_ws_bytes(n_keys, n_parts)), dtype=torch.uint8,
+                     device="cuda")
+    amq.abi.check(L.tkv_amq_bloom_route_records_ex(_ptr(keys), 24, n_keys, _ptr(plan.device_segs()),
+                                                   int(seg["n_blocks"]), int(seg["hash_count"]), n_parts,
+                                                   _ptr(recs), _ptr(counts), _ptr(ws), ws.numel(),
+                                                   _stream_handle()), "route_records_ex")
+    torch.cuda.synchronize()
+    counts = counts.cpu().numpy().astype(np.int64)
+    assert counts.sum() == n_keys
+    T, q = hash_shard_tiles(int(seg["n_blocks"]), n_parts)
+    out = torch.zeros(plan.total_out_bytes, dtype=torch.uint8, device="cuda")
+    base = np.concatenate([[0], np.cumsum(counts)])
+    for p in range(n_parts):
+        _build_range_records(amq, torch, recs[int(base[p]):int(base[p + 1])], plan, min(T, p * q),
+                             min(T, (p + 1) * q), out)
+    torch.cuda.synchronize()
+    assert torch.equal(out, whole)
+    st, ref = oracle.bloom_build(kn, n_keys, bpk, src_page_id=0, stride=24)
+    assert st == 0 and out.cpu().numpy().tobytes() == ref.tobytes()
+    # key sizes other than 16 and 24 are refused
+    counts_t = torch.zeros(n_parts, dtype=torch.int32, device="cuda")
+    st = L.tkv_amq_bloom_route_records_ex(_ptr(keys), 20, n_keys, _ptr(plan.device_segs()),
+                                          int(seg["n_blocks"]), int(seg["hash_count"]), n_parts,
+                                          _ptr(recs), _ptr(counts_t), _ptr(ws), ws.numel(),
+                                          _stream_handle())
+    assert st == amq.abi.INVALID_ARGUMENT
+
+
 def test_route_records_refuse_k_above_8(amq, torch):
     from turtle_kv_amd.filters import _ptr, _stream_handle
     L = amq.abi.lib()

@@ -487,6 +487,25 @@ def test_bloom_monolithic_partitioned(oracle, amq, torch, n, bpk, seed):
     assert_same(plan, out, ref)
 
 
+@pytest.mark.parametrize("n,bpk,dup", [(600000, 10, 0), (1500000, 12, 0), (1100000, 5, 0),
+                                       (400000, 14, 0), (90000, 64, 0), (700000, 10, 200000),
+                                       (450000, 14, 150000)])
+def test_bloom_monolithic_k24(oracle, amq, torch, n, bpk, dup):
+    """One filter of 24-byte keys (TurtleKV's default key size) beyond four windows: the record
+    path's own partition kernel (bloom_rec_partition24) hashes each key once into a 12-byte bit
+    record; k > 8 (14 and 64 bits/key) keeps the first eight bits in the records and
+    bloom_rec_overflow sets the others; duplicates overflow the regions of one tile.
+    Byte-identical to the oracle (round 2: device atomics)."""
+    rng = np.random.default_rng(n + bpk)
+    keys = rng.integers(0, 256, (n, 24), dtype=np.uint8)
+    if dup:
+        keys[n - dup:] = keys[n // 3]
+    ref = oracle_per_segment(oracle, 0, keys, [n], bpk, stride=24)
+    plan, out = gpu_build(amq, torch, 0, torch.from_numpy(keys).cuda(), [n], bpk)
+    assert plan.max_seg_blocks * 64 > 4 * 160 * 1024
+    assert_same(plan, out, ref)
+
+
 def test_bloom_monolithic_duplicate_keys(oracle, amq, torch):
     """Every key identical (one tile receives the whole batch: its regions overflow and the
     overflow lists are applied with device atomics) and a few distinct ones."""

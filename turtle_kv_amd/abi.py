@@ -88,6 +88,7 @@ EXPORTS = [
     "tkv_amq_bloom_route_ws_bytes", "tkv_amq_bloom_route", "tkv_amq_bloom_build_range_ws_bytes",
     "tkv_amq_bloom_build_range", "tkv_amq_bloom_route_records_ws_bytes", "tkv_amq_bloom_route_records",
     "tkv_amq_bloom_build_range_records_ws_bytes", "tkv_amq_bloom_build_range_records",
+    "tkv_amq_bloom_route_records_ex",
 ]
 
 # tkv_amq_key_view (libstdc++ std::string_view layout)
@@ -178,6 +179,8 @@ def lib(build_if_missing: bool = True):
         L.tkv_amq_bloom_route_records_ws_bytes.argtypes = [u64, u32]
         L.tkv_amq_bloom_route_records.restype = i32
         L.tkv_amq_bloom_route_records.argtypes = [vp, u64, vp, u32, u32, u32, vp, vp, vp, u64, vp]
+        L.tkv_amq_bloom_route_records_ex.restype = i32
+        L.tkv_amq_bloom_route_records_ex.argtypes = [vp, u32, u64, vp, u32, u32, u32, vp, vp, vp, u64, vp]
         L.tkv_amq_bloom_build_range_records_ws_bytes.restype = u64
         L.tkv_amq_bloom_build_range_records_ws_bytes.argtypes = [u64, u32, u32]
         L.tkv_amq_bloom_build_range_records.restype = i32

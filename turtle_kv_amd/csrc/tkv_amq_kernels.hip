@@ -997,6 +997,35 @@ __device__ inline uint32_t bloom_tile_of(const uint4& kv, uint32_t nb)
   return (uint32_t)__umul64hi(h0, (uint64_t)nb) / kBloomTileBlocks;
 }
 
+// 24-byte keys (TurtleKV's default key size, 8-byte aligned) where the hash-once paths take
+// them: the record partition of a monolithic filter and the hash-range route's count and
+// record passes.  (16-byte keys stay uint4.)
+struct Key24 {
+  uint64_t w[3];
+};
+
+__device__ inline Key24 load_key24(const uint8_t* keys, uint32_t i)
+{
+  const uint64_t* p = reinterpret_cast<const uint64_t*>(keys) + 3ull * i;
+  return Key24{{__builtin_nontemporal_load(p), __builtin_nontemporal_load(p + 1),
+                __builtin_nontemporal_load(p + 2)}};
+}
+
+__device__ inline uint32_t bloom_tile_of(const Key24& kv, uint32_t nb)
+{
+  const XxhFixed<24> x(kv.w);
+  const uint64_t h0 = x.finish(xxh_fixed_rc<24>(c_bloom.seed[0]));
+  return (uint32_t)__umul64hi(h0, (uint64_t)nb) / kBloomTileBlocks;
+}
+
+// key i of a 16- or 24-byte key array
+template <int KB>
+__device__ inline auto load_rec_key(const uint8_t* keys, uint32_t i)
+{
+  if constexpr (KB == 24) return load_key24(keys, i);
+  else return load_nt16(keys + 16ull * i);
+}
+
 // The window of a partition pass.  The whole monolithic filter: tile0 = 0, div = 1, keys
 // from the segment.  Hash-range sharding (tkv_amq_bloom_route / _build_range): the route
 // partitions a rank's keys by owner (div = tiles per part, output to `out`); a rank's range
@@ -1015,15 +1044,17 @@ __host__ __device__ inline PartWindow whole_filter_window()
 }
 
 // local tile of a key, or ~0 outside the window (below tile0 the subtraction wraps)
-__device__ inline uint32_t part_tile(const uint4& kv, uint32_t nb, const PartWindow& pw,
+template <class KV>
+__device__ inline uint32_t part_tile(const KV& kv, uint32_t nb, const PartWindow& pw,
                                      uint32_t n_tiles)
 {
   const uint32_t t = (bloom_tile_of(kv, nb) - pw.tile0) / pw.div;
   return t < n_tiles ? t : ~0u;
 }
 
-// PASS 0: histogram; PASS 1: scatter.  Both walk the same key range in the same way.
-template <int PASS, uint32_t NT>
+// PASS 0: histogram; PASS 1: scatter.  Both walk the same key range in the same way.  KB = 24:
+// 24-byte keys, the histogram only (tkv_amq_bloom_route_records_ex's count pass)
+template <int PASS, uint32_t NT, int KB = 16>
 __global__ __launch_bounds__(NT) void bloom_part_keys(const uint4* __restrict__ keys,
                                                        const tkv_amq_segment* __restrict__ segs,
                                                        uint32_t* __restrict__ ws, uint32_t n_tiles,
@@ -1040,15 +1071,16 @@ __global__ __launch_bounds__(NT) void bloom_part_keys(const uint4* __restrict__ 
   // n_cap: keys the caller passed (the partition buffer holds that many)
   const uint32_t n = pw.local ? n_cap : min(sg.n_keys, n_cap), nb = sg.n_blocks;
   const uint32_t b = min(n, w * per), e = min(n, b + per);
-  const uint4* kp = keys + (pw.local ? 0 : sg.key_begin);
+  static_assert(KB == 16 || (KB == 24 && PASS == 0), "24-byte keys: the count pass only");
+  const uint8_t* kp = reinterpret_cast<const uint8_t*>(keys) + (uint64_t)KB * (pw.local ? 0 : sg.key_begin);
   uint4* part = pw.out ? pw.out : reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(ws) + part_off);
   constexpr int U = 4;
   for (uint32_t i0 = b; i0 < e; i0 += NT * U) {
-    uint4 kv[U];
+    decltype(load_rec_key<KB>(kp, 0)) kv[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint32_t i = i0 + u * NT + tid;
-      if (i < e) kv[u] = load_nt16(kp + i);
+      if (i < e) kv[u] = load_rec_key<KB>(kp, i);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -1058,7 +1090,7 @@ __global__ __launch_bounds__(NT) void bloom_part_keys(const uint4* __restrict__ 
         if (t == ~0u) continue;
         if constexpr (PASS == 0) {
           atomicAdd(s_tile + t, 1u);
-        } else {
+        } else if constexpr (KB == 16) {
           const uint32_t slot = atomicAdd(s_tile + t, 1u);
           part[slot] = kv[u];
         }
@@ -1310,9 +1342,25 @@ __device__ inline uint32_t rec_hash_bits(const uint4& kv, uint32_t nb, uint32_t 
   return (uint32_t)__umul64hi(h0, (uint64_t)nb);
 }
 
-// one key of the record path: local tile (~0 outside the window), block in tile, bit record
+// a 24-byte key's block and its bit indices (k > 8: the first eight; bloom_rec_overflow sets
+// the others)
 template <int K>
-__device__ inline uint32_t rec_hash(const uint4& kv, uint32_t nb, uint32_t k, uint32_t tile0,
+__device__ inline uint32_t rec_hash_bits(const Key24& kv, uint32_t nb, uint32_t k, uint32_t (&b)[8])
+{
+  const XxhFixed<24> x(kv.w);
+  const uint64_t h0 = x.finish(xxh_fixed_rc<24>(c_bloom.seed[0]));
+  b[0] = (uint32_t)h0 & 511u;
+#pragma unroll
+  for (uint32_t j = 1; j < 8; ++j) {
+    if (K != 0 ? j < (uint32_t)K : j < k) b[j] = x.finish_lo9(xxh_fixed_rc<24>(c_bloom.seed[j])) & 511u;
+    else b[j] = b[0];
+  }
+  return (uint32_t)__umul64hi(h0, (uint64_t)nb);
+}
+
+// one key of the record path: local tile (~0 outside the window), block in tile, bit record
+template <int K, class KV>
+__device__ inline uint32_t rec_hash(const KV& kv, uint32_t nb, uint32_t k, uint32_t tile0,
                                     uint32_t n_tiles, uint32_t& w0, uint32_t& w1, uint32_t& w2)
 {
   uint32_t b[8];
@@ -1325,8 +1373,8 @@ __device__ inline uint32_t rec_hash(const uint4& kv, uint32_t nb, uint32_t k, ui
 // tkv_amq_bloom_route_records' scatter pass: the same key ranges and slots as
 // bloom_part_keys<1> (after the same count pass), but each key leaves as its 12-byte bit record
 // (rec_pack) with its tile relative to its owner's first tile (owner = tile / q): k <= 8 only.
-template <uint32_t NT, int K>
-__device__ void bloom_route_recs_body(const uint4* __restrict__ keys, const tkv_amq_segment& sg,
+template <uint32_t NT, int K, int KB>
+__device__ void bloom_route_recs_body(const uint8_t* __restrict__ keys, const tkv_amq_segment& sg,
                                       uint32_t* __restrict__ ws, uint32_t n_parts, uint32_t per,
                                       uint32_t n_cap, uint32_t q, uint32_t* __restrict__ out,
                                       uint32_t* s_tile)
@@ -1336,11 +1384,11 @@ __device__ void bloom_route_recs_body(const uint4* __restrict__ keys, const tkv_
   const uint32_t b = min(n, w * per), e = min(n, b + per);
   constexpr int U = 4;
   for (uint32_t i0 = b; i0 < e; i0 += NT * U) {
-    uint4 kv[U];
+    decltype(load_rec_key<KB>(keys, 0)) kv[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint32_t i = i0 + u * NT + tid;
-      if (i < e) kv[u] = load_nt16(keys + i);
+      if (i < e) kv[u] = load_rec_key<KB>(keys, i);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -1363,8 +1411,8 @@ __device__ void bloom_route_recs_body(const uint4* __restrict__ keys, const tkv_
   }
 }
 
-template <uint32_t NT>
-__global__ __launch_bounds__(NT) void bloom_route_recs(const uint4* __restrict__ keys,
+template <uint32_t NT, int KB>
+__global__ __launch_bounds__(NT) void bloom_route_recs(const uint8_t* __restrict__ keys,
                                                         const tkv_amq_segment* __restrict__ segs,
                                                         uint32_t* __restrict__ ws, uint32_t n_parts,
                                                         uint32_t per, uint32_t n_cap, uint32_t q,
@@ -1379,9 +1427,9 @@ __global__ __launch_bounds__(NT) void bloom_route_recs(const uint4* __restrict__
   __syncthreads();
   const uint32_t k = sg.hash_count;
   if (k == 0 || k > 8) return;  // (the ABI refuses k > 8: a record holds 8 bit indices)
-  if (k == 7) bloom_route_recs_body<NT, 7>(keys, sg, ws, n_parts, per, n_cap, q, out, s_tile);
-  else if (k == 8) bloom_route_recs_body<NT, 8>(keys, sg, ws, n_parts, per, n_cap, q, out, s_tile);
-  else bloom_route_recs_body<NT, 0>(keys, sg, ws, n_parts, per, n_cap, q, out, s_tile);
+  if (k == 7) bloom_route_recs_body<NT, 7, KB>(keys, sg, ws, n_parts, per, n_cap, q, out, s_tile);
+  else if (k == 8) bloom_route_recs_body<NT, 8, KB>(keys, sg, ws, n_parts, per, n_cap, q, out, s_tile);
+  else bloom_route_recs_body<NT, 0, KB>(keys, sg, ws, n_parts, per, n_cap, q, out, s_tile);
 }
 
 
@@ -1401,6 +1449,8 @@ struct RecArgs {
   BloomRecGeom g;
   const uint32_t* recs;  // instead of keys: 12-byte bit records with local tiles (hash-range
                          // shards, tkv_amq_bloom_route_records), n of them
+  uint32_t kb;           // key bytes, 16 or 24 (24: bit records for any k, the first eight
+                         // bits in the records, the others set by bloom_rec_overflow)
 };
 
 // batches of B keys, U = B / kRecThreads per thread; RAW: 16-byte keys instead of bit records.
@@ -1415,10 +1465,11 @@ __device__ inline uint4 load_rec12(const uint32_t* recs, uint32_t i)
   return make_uint4(r.x, r.y, r.z, 0u);
 }
 
-template <int K, bool RAW, bool RECIN = false>
+template <int K, bool RAW, bool RECIN = false, int KB = 16>
 __device__ void bloom_rec_partition_body(const tkv_amq_segment& sg, const RecArgs& a, uint32_t* lds)
 {
   static_assert(!(RAW && RECIN), "records carry k <= 8 bit indices");
+  static_assert(KB == 16 || (!RAW && !RECIN), "24-byte keys leave as bit records");
   constexpr uint32_t B = RAW ? kRecBatchKeys : kRecBatchBits;
   constexpr uint32_t U = B / kRecThreads;
   constexpr uint32_t RB = RAW ? 16 : 12;  // record bytes
@@ -1440,7 +1491,7 @@ __device__ void bloom_rec_partition_body(const tkv_amq_segment& sg, const RecArg
   if (tid == 0) *ovf_n = 0;
   __syncthreads();
   const uint32_t n = a.from_seg ? min(a.n, sg.n_keys) : a.n;
-  const uint4* keys = a.keys + (a.from_seg ? sg.key_begin : 0);
+  const uint8_t* keys = reinterpret_cast<const uint8_t*>(a.keys) + (uint64_t)KB * (a.from_seg ? sg.key_begin : 0);
   const uint32_t kb = min(n, w * a.g.per), ke = min(n, kb + a.g.per);
   uint8_t* regions = a.ws + a.g.regions_off;
   uint8_t* ovf = a.ws + a.g.ovf_off + (uint64_t)w * a.g.per * 16;
@@ -1449,10 +1500,11 @@ __device__ void bloom_rec_partition_body(const tkv_amq_segment& sg, const RecArg
   // per batch, so the compiler's wait for a key load never also waits for the stores.
   uint8_t* const sink = a.ws;
   const uint32_t last_key = ke > 0 ? ke - 1 : 0;
-  uint4 kv[U];
-  auto load_in = [&](uint32_t i) -> uint4 {
+  using KV = typename std::conditional<KB == 24, Key24, uint4>::type;
+  KV kv[U];
+  auto load_in = [&](uint32_t i) -> KV {
     if constexpr (RECIN) return load_rec12(a.recs, i);
-    else return load_nt16(keys + i);
+    else return load_rec_key<KB>(keys, i);
   };
 #pragma unroll
   for (uint32_t u = 0; u < U; ++u) kv[u] = load_in(min(kb + u * kRecThreads + tid, last_key));
@@ -1561,6 +1613,20 @@ __global__ __launch_bounds__(kRecThreads) void bloom_rec_partition(const tkv_amq
   else bloom_rec_partition_body<0, true>(sg, a, s_rec);
 }
 
+// 24-byte keys (a kernel of its own: their six key words per prefetched key would raise the
+// 16-byte kernel's register count)
+__global__ __launch_bounds__(kRecThreads) void bloom_rec_partition24(const tkv_amq_segment* __restrict__ segs,
+                                                                     RecArgs a)
+{
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_rec[];
+  const tkv_amq_segment sg = segs[0];
+  const uint32_t k = sg.hash_count;
+  if (k == 0) return;
+  if (k == 7) bloom_rec_partition_body<7, false, false, 24>(sg, a, s_rec);
+  else if (k == 8) bloom_rec_partition_body<8, false, false, 24>(sg, a, s_rec);
+  else bloom_rec_partition_body<0, false, false, 24>(sg, a, s_rec);
+}
+
 template <int K>
 __device__ inline void rec_insert(uint32_t* img, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t k)
 {
@@ -1655,7 +1721,7 @@ __global__ __launch_bounds__(kRecTileThreads) void bloom_rec_tile(const tkv_amq_
   __syncthreads();
   if (k == 7) bloom_rec_tile_body<7, false>(sg, a, s_img, t);
   else if (k == 8) bloom_rec_tile_body<8, false>(sg, a, s_img, t);
-  else if (k < 8) bloom_rec_tile_body<0, false>(sg, a, s_img, t);
+  else if (k < 8 || a.kb == 24) bloom_rec_tile_body<0, false>(sg, a, s_img, t);  // (24: 8 bits)
   else bloom_rec_tile_body<0, true>(sg, a, s_img, t);
   __syncthreads();
   uint8_t* payload = out + sg.out_offset;
@@ -1679,7 +1745,8 @@ __global__ __launch_bounds__(64) void bloom_header_only(const tkv_amq_segment* _
 }
 
 // one workgroup per partition workgroup's overflow list; device-scope atomics into the filter
-// (runs after bloom_rec_tile has stored every tile)
+// (runs after bloom_rec_tile has stored every tile).  24-byte keys with k > 8 (bits_per_key
+// >= 13): the bits past the eighth of the workgroup's keys, also with atomics.
 __global__ __launch_bounds__(256) void bloom_rec_overflow(const tkv_amq_segment* __restrict__ segs,
                                                           RecArgs a, uint8_t* __restrict__ out)
 {
@@ -1689,12 +1756,28 @@ __global__ __launch_bounds__(256) void bloom_rec_overflow(const tkv_amq_segment*
   const uint32_t n = reinterpret_cast<const uint32_t*>(a.ws + a.g.ovf_n_off)[w];
   const uint8_t* list = a.ws + a.g.ovf_off + (uint64_t)w * a.g.per * 16;
   uint32_t* words = reinterpret_cast<uint32_t*>(out + sg.out_offset + kBloomHeader);
+  if (a.kb == 24 && k > 8 && !a.recs) {
+    const uint32_t nk = a.from_seg ? min(a.n, sg.n_keys) : a.n;
+    const uint8_t* keys = reinterpret_cast<const uint8_t*>(a.keys) + 24ull * (a.from_seg ? sg.key_begin : 0);
+    const uint32_t kb = min(nk, w * a.g.per), ke = min(nk, kb + a.g.per);
+    for (uint32_t i = kb + threadIdx.x; i < ke; i += 256) {
+      const XxhFixed<24> x(load_key24(keys, i).w);
+      const uint64_t h0 = x.finish(xxh_fixed_rc<24>(c_bloom.seed[0]));
+      const uint32_t blk = (uint32_t)__umul64hi(h0, (uint64_t)sg.n_blocks);
+      if (blk / kBloomTileBlocks - a.tile0 >= a.g.n_tiles) continue;  // (outside the window)
+      uint32_t* bw = words + 16ull * blk;
+      for (uint32_t j = 8; j < k; ++j) {
+        const uint32_t bj = x.finish_lo9(xxh_fixed_rc<24>(c_bloom.seed[j])) & 511u;
+        atomicOr(bw + (bj >> 5), 1u << (bj & 31u));
+      }
+    }
+  }
   for (uint32_t i = threadIdx.x; i < n; i += 256) {
     const uint4 q = *reinterpret_cast<const uint4*>(list + 16ull * i);
     uint32_t* blk;
     uint32_t b[8];
-    uint32_t kk = k;
-    if (k <= 8) {
+    uint32_t kk = k < 8 ? k : 8u;
+    if (k <= 8 || a.kb == 24) {
       const uint32_t tile = rec_tile(q.x, q.y, q.z);
       blk = words + 16ull * ((uint64_t)(a.tile0 + tile) * kBloomTileBlocks + (q.x & (kBloomTileBlocks - 1)));
       b[0] = q.x >> 10; b[1] = q.x >> 19; b[2] = q.y; b[3] = q.y >> 9;
@@ -4184,17 +4267,22 @@ inline bool bloom_rec_eligible(uint64_t n_blocks, uint64_t n_keys)
 inline void launch_rec_build(const BloomRecGeom& g, hipStream_t s, const uint4* keys, uint32_t n,
                              uint32_t tile0, uint32_t from_seg, uint32_t hdr_always,
                              const tkv_amq_segment* d_segs, uint8_t* ws, uint8_t* d_out,
-                             const uint32_t* recs = nullptr)
+                             const uint32_t* recs = nullptr, uint32_t key_bytes = 16)
 {
   static std::once_flag lds_attr[kMaxDevices];
   once_per_device(lds_attr, [] {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&bloom_rec_partition),
-                              hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)bloom_rec_lds_bytes(kRecMaxTiles));
+    for (const void* f : {reinterpret_cast<const void*>(&bloom_rec_partition),
+                          reinterpret_cast<const void*>(&bloom_rec_partition24)})
+      (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)bloom_rec_lds_bytes(kRecMaxTiles));
   });
-  const RecArgs a{keys, n, tile0, from_seg, ws, g, recs};
-  hipLaunchKernelGGL(bloom_rec_partition, dim3(g.P), dim3(kRecThreads), bloom_rec_lds_bytes(g.n_tiles),
-                     s, d_segs, a);
+  const RecArgs a{keys, n, tile0, from_seg, ws, g, recs, key_bytes};
+  if (key_bytes == 24 && !recs)
+    hipLaunchKernelGGL(bloom_rec_partition24, dim3(g.P), dim3(kRecThreads), bloom_rec_lds_bytes(g.n_tiles),
+                       s, d_segs, a);
+  else
+    hipLaunchKernelGGL(bloom_rec_partition, dim3(g.P), dim3(kRecThreads), bloom_rec_lds_bytes(g.n_tiles),
+                       s, d_segs, a);
   hipLaunchKernelGGL(bloom_rec_tile, dim3(g.n_tiles), dim3(kRecTileThreads), 64ull * kBloomTileBlocks,
                      s, d_segs, a, d_out, hdr_always);
   hipLaunchKernelGGL(bloom_rec_overflow, dim3(g.P), dim3(256), 0, s, d_segs, a, d_out);
@@ -4506,8 +4594,14 @@ int tkv_amq_build(int kind, const uint8_t* keys, const uint64_t* offs, uint32_t 
                          parts, chunks, w, img, d_out);
       return hipGetLastError() == hipSuccess ? TKV_AMQ_OK : TKV_AMQ_INTERNAL;
     }
-    const bool mono16 = bloom_partitioned(n_segs, max_blocks, n_keys) && mode == kKey16 && d_ws;
-    if (bloom_window_path(n_segs, max_blocks, mono16)) {
+    // one filter beyond the window path: 16-byte keys take the record path or the key
+    // partition, 24-byte keys the record path (the keys hashed once either way)
+    const int mono_mode = build_key_mode(keys, offs, stride);
+    const bool mono_part = bloom_partitioned(n_segs, max_blocks, n_keys) && d_ws;
+    const bool mono16 = mono_part && mode == kKey16;
+    const bool mono24 = mono_part && mono_mode == kKey24 && bloom_rec_eligible(max_blocks, n_keys) &&
+                        ws_bytes >= bloom_rec_geom(n_keys, max_blocks).bytes;
+    if (bloom_window_path(n_segs, max_blocks, mono16 || mono24)) {
       // leaves beyond one CU's LDS: windows of the image, parts of the keys
       const uint32_t W = bloom_window_count(max_blocks), wblk = bloom_window_blocks(max_blocks);
       uint32_t wparts = bloom_window_parts(n_segs, n_keys, max_blocks);
@@ -4568,7 +4662,10 @@ int tkv_amq_build(int kind, const uint8_t* keys, const uint64_t* offs, uint32_t 
     }
     const BloomPartGeom pg = bloom_part_geom(n_keys, max_blocks);
     const bool mono = mono16;
-    if (mono && bloom_rec_eligible(max_blocks, n_keys) &&
+    if (mono24) {
+      launch_rec_build(bloom_rec_geom(n_keys, max_blocks), s, reinterpret_cast<const uint4*>(keys),
+                       (uint32_t)n_keys, 0u, 1u, 0u, d_segs, static_cast<uint8_t*>(d_ws), d_out, nullptr, 24u);
+    } else if (mono && bloom_rec_eligible(max_blocks, n_keys) &&
         ws_bytes >= bloom_rec_geom(n_keys, max_blocks).bytes) {
       // one monolithic filter: hash once into bit records partitioned by tile, build the tiles
       launch_rec_build(bloom_rec_geom(n_keys, max_blocks), s, reinterpret_cast<const uint4*>(keys),
@@ -4581,7 +4678,8 @@ int tkv_amq_build(int kind, const uint8_t* keys, const uint64_t* offs, uint32_t 
                                d_out);
     } else {
       // fewer than kBloomSpreadSegs leaves, leaves beyond the LDS budget in a multi-leaf batch,
-      // or a monolithic filter whose keys are not 16 bytes: device atomics
+      // or a monolithic filter whose keys are neither 16 nor 24 bytes (or of more than
+      // kRecMaxTiles tiles with 24-byte keys): device atomics
       const dim3 g1(n_segs), b(256);
       hipLaunchKernelGGL(bloom_global_init, g1, b, 0, s, d_segs, d_out);
       const uint32_t g2 = (uint32_t)(div_up(n_keys, 256) < 8192 ? div_up(n_keys, 256) : 8192);
@@ -4836,11 +4934,21 @@ int tkv_amq_bloom_route_records(const uint8_t* d_keys16, uint64_t n_keys, const 
                                 uint8_t* d_recs12, uint32_t* d_part_counts, void* d_ws, uint64_t ws_bytes,
                                 void* stream)
 {
+  return tkv_amq_bloom_route_records_ex(d_keys16, 16, n_keys, d_seg, n_blocks, hash_count, n_parts,
+                                        d_recs12, d_part_counts, d_ws, ws_bytes, stream);
+}
+
+int tkv_amq_bloom_route_records_ex(const uint8_t* d_keys, uint32_t key_bytes, uint64_t n_keys,
+                                   const tkv_amq_segment* d_seg, uint32_t n_blocks, uint32_t hash_count,
+                                   uint32_t n_parts, uint8_t* d_recs12, uint32_t* d_part_counts,
+                                   void* d_ws, uint64_t ws_bytes, void* stream)
+{
   if (tkv_amq_device_count() == 0) return TKV_AMQ_UNAVAILABLE;
   if (n_parts == 0 || n_parts > kRouteMaxParts || n_blocks == 0 || !d_seg || !d_part_counts ||
-      n_keys > 0xffffffffull || hash_count == 0 || hash_count > 8)
+      n_keys > 0xffffffffull || hash_count == 0 || hash_count > 8 || (key_bytes != 16 && key_bytes != 24))
     return TKV_AMQ_INVALID_ARGUMENT;
-  if (n_keys && (!d_keys16 || !d_recs12 || (reinterpret_cast<uintptr_t>(d_keys16) & 15) ||
+  const uintptr_t kalign = key_bytes == 16 ? 15 : 7;
+  if (n_keys && (!d_keys || !d_recs12 || (reinterpret_cast<uintptr_t>(d_keys) & kalign) ||
                  (reinterpret_cast<uintptr_t>(d_recs12) & 3)))
     return TKV_AMQ_INVALID_ARGUMENT;
   const BloomPartGeom g = bloom_route_geom(n_keys, n_parts);
@@ -4850,15 +4958,23 @@ int tkv_amq_bloom_route_records(const uint8_t* d_keys16, uint64_t n_keys, const 
   set_part_attributes();
   const uint32_t q = shard_tiles_per_part(n_blocks, n_parts);
   const PartWindow pw{0u, q, 1u, 0u, nullptr};
-  const uint4* k4 = reinterpret_cast<const uint4*>(d_keys16);
+  const uint4* k4 = reinterpret_cast<const uint4*>(d_keys);
   const size_t hl = 4ull * n_parts;
   const uint32_t nk = (uint32_t)n_keys;
-  hipLaunchKernelGGL((bloom_part_keys<0, 256>), dim3(g.P), dim3(256), hl, s, k4, d_seg, w, n_parts,
-                     g.per, g.part_off, nk, pw);
+  if (key_bytes == 24)
+    hipLaunchKernelGGL((bloom_part_keys<0, 256, 24>), dim3(g.P), dim3(256), hl, s, k4, d_seg, w, n_parts,
+                       g.per, g.part_off, nk, pw);
+  else
+    hipLaunchKernelGGL((bloom_part_keys<0, 256>), dim3(g.P), dim3(256), hl, s, k4, d_seg, w, n_parts,
+                       g.per, g.part_off, nk, pw);
   hipLaunchKernelGGL(bloom_part_scan_cols, dim3(n_parts), dim3(256), 0, s, w, g.P, n_parts);
   hipLaunchKernelGGL(bloom_part_scan_tiles, dim3(1), dim3(256), 0, s, w, g.P, n_parts);
-  hipLaunchKernelGGL(bloom_route_recs<256>, dim3(g.P), dim3(256), hl, s, k4, d_seg, w, n_parts, g.per, nk,
-                     q, reinterpret_cast<uint32_t*>(d_recs12));
+  if (key_bytes == 24)
+    hipLaunchKernelGGL((bloom_route_recs<256, 24>), dim3(g.P), dim3(256), hl, s, d_keys, d_seg, w, n_parts,
+                       g.per, nk, q, reinterpret_cast<uint32_t*>(d_recs12));
+  else
+    hipLaunchKernelGGL((bloom_route_recs<256, 16>), dim3(g.P), dim3(256), hl, s, d_keys, d_seg, w, n_parts,
+                       g.per, nk, q, reinterpret_cast<uint32_t*>(d_recs12));
   if (hipMemcpyAsync(d_part_counts, w + g.h_words, 4ull * n_parts, hipMemcpyDeviceToDevice, s) !=
       hipSuccess)
     return TKV_AMQ_INTERNAL;

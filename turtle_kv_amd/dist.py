@@ -148,24 +148,29 @@ class HashShardedBloom:
         return b
 
     def route(self, keys):
-        """keys [n, 16] uint8 on the device -> (routed [n, 16], send counts per rank, int64)."""
+        """keys [n, 16] (or [n, 24] with bit records) uint8 on the device -> (routed [n, unit],
+        send counts per rank, int64)."""
         import torch
         from . import abi
         from .filters import _ptr, _stream_handle
         L = abi.lib()
-        if keys.dim() != 2 or keys.shape[1] != 16:
-            # tkv_amq_bloom_route / _build_range hash 16-byte keys only (INTEGRATION.md key shapes)
+        kb = keys.shape[1] if keys.dim() == 2 else 0
+        if not (kb == 16 or (kb == 24 and self.records)):
+            # bit records (k <= 8) are routed from 16- or 24-byte keys
+            # (tkv_amq_bloom_route_records_ex); keys themselves (k > 8) travel as 16 bytes only
+            # (tkv_amq_bloom_route / _build_range; INTEGRATION.md key shapes)
             raise abi.TkvAmqError(abi.INVALID_ARGUMENT, "hash-range sharding takes [n, 16] uint8 "
-                                  f"keys (16-byte keys only), got shape {tuple(keys.shape)}")
+                                  "keys, or [n, 24] at <= 12 bits/key, got shape "
+                                  f"{tuple(keys.shape)}")
         n = keys.shape[0]
         u = self.unit
         routed = self._buf("routed", u * n)[:u * n].view(n, u)
         if self.records:
             ws = self._buf("route_ws", int(L.tkv_amq_bloom_route_records_ws_bytes(n, self.world)))
-            abi.check(L.tkv_amq_bloom_route_records(_ptr(keys), n, _ptr(self.d_seg), self.n_blocks,
-                                                    self.hash_count, self.world, _ptr(routed),
-                                                    _ptr(self.counts), _ptr(ws), ws.numel(),
-                                                    _stream_handle()), "tkv_amq_bloom_route_records")
+            abi.check(L.tkv_amq_bloom_route_records_ex(_ptr(keys), kb, n, _ptr(self.d_seg), self.n_blocks,
+                                                       self.hash_count, self.world, _ptr(routed),
+                                                       _ptr(self.counts), _ptr(ws), ws.numel(),
+                                                       _stream_handle()), "tkv_amq_bloom_route_records_ex")
         else:
             ws = self._buf("route_ws", int(L.tkv_amq_bloom_route_ws_bytes(n, self.world)))
             abi.check(L.tkv_amq_bloom_route(_ptr(keys), n, _ptr(self.d_seg), self.n_blocks, self.world,
