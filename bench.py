@@ -3,7 +3,7 @@
 
   python bench.py [--gpus N] [--steps K] [--warmup W]
                   [--workload bloom10|bloom12|vqf12|probe10|probe_vqf12|bloom10k24|vqf12k24|
-                              bloom10var|vqf12var|bloom12big|bloom10mono|bloom12hash]
+                              bloom10var|vqf12var|bloom12big|bloom10mono|bloom10monok24|bloom12hash]
                   [--total-keys T]
 
 One step = one pass of the hot path over one batch: build every leaf filter of
@@ -57,6 +57,7 @@ WORKLOADS = {
     "bloom10k24": (0, 10, "Bloom @10 bits/key, 24-byte keys (TurtleKV default key size)"),
     "vqf12k24": (1, 12, "VQF @12 bits/key, 24-byte keys (TurtleKV default key size) in generation order"),
     "bloom10mono": (0, 10, "Bloom @10 bits/key, one monolithic filter per GPU"),
+    "bloom10monok24": (0, 10, "Bloom @10 bits/key, 24-byte keys, one monolithic filter per GPU"),
     "bloom10var": (0, 10, "Bloom @10 bits/key, variable-length keys (8-31 B)"),
     "bloom12hash": (0, 12, "Bloom @12 bits/key, one filter over all GPUs' keys, hash-range sharded"),
     "vqf12var": (1, 12, "VQF @12 bits/key, variable-length keys (8-31 B) in generation order"),
@@ -67,8 +68,8 @@ WORKLOADS = {
 HASH_SHARDED = {"bloom12hash"}
 # workloads whose one filter spans every key of the GPU (the monolithic
 # single-filter Bloom variant)
-MONOLITHIC = {"bloom10mono"}
-KEY_BYTES = {"bloom10k24": 24, "vqf12k24": 24, "bloom10var": 0, "vqf12var": 0}  # 0: variable length
+MONOLITHIC = {"bloom10mono", "bloom10monok24"}
+KEY_BYTES = {"bloom10k24": 24, "vqf12k24": 24, "bloom10var": 0, "vqf12var": 0, "bloom10monok24": 24}  # 0: variable length
 LEAF_KEYS = {"bloom12big": 200_000}  # default keys per leaf where it is not SEG_KEYS
 SWEEP_LEAVES = (64, 256, 1024)                   # + the whole batch
 
