@@ -23,6 +23,7 @@ if has bench; then
   timeout -k 10 300 python bench.py --workload vqf12k24 > $O/bench_vqf12k24.log 2>&1 || exit 8
   timeout -k 10 300 python bench.py --workload bloom12 --total-keys 1000000000 --steps 10 --no-e2e > $O/bench_bloom12_1B.log 2>&1 || exit 9
   timeout -k 10 300 python bench.py --workload bloom10mono > $O/bench_bloom10mono.log 2>&1 || exit 10
+  timeout -k 10 300 python bench.py --workload bloom10monok24 > $O/bench_bloom10monok24.log 2>&1 || exit 10
   timeout -k 10 300 python bench.py --workload bloom10var --no-e2e > $O/bench_bloom10var.log 2>&1 || exit 10
   timeout -k 10 300 python bench.py --workload bloom12hash > $O/bench_bloom12hash.log 2>&1 || exit 10
   timeout -k 10 300 python bench.py --workload vqf12var --no-e2e > $O/bench_vqf12var.log 2>&1 || exit 10
@@ -40,13 +41,13 @@ cd /tmp
 if has prof; then
   # kernel-trace stats of the exact default bench command, and of the other workloads
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_bloom10 -o run --output-format csv -- python3 $R/bench.py > $O/prof_bloom10.log 2>&1 || exit 11
-  for W in vqf12 probe10 probe_vqf12 bloom10mono bloom12hash vqf12var bloom10var bloom12big; do
+  for W in vqf12 probe10 probe_vqf12 bloom10mono bloom10monok24 bloom12hash vqf12var bloom10var bloom12big; do
     timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_$W -o run --output-format csv -- python3 $R/bench.py --workload $W --no-cpu-baseline --no-e2e > $O/prof_$W.log 2>&1 || exit 12
   done
 fi
 if has pmc; then
   # HBM traffic + VALU counters: one counter group per pass, --pmc only, no clock ramp
-  for W in ${PMC_WS:-bloom10 vqf12 bloom10mono bloom10k24 vqf12k24 bloom10var vqf12var bloom12big}; do
+  for W in ${PMC_WS:-bloom10 vqf12 bloom10mono bloom10monok24 bloom10k24 vqf12k24 bloom10var vqf12var bloom12big}; do
     for pass in "fetch:FETCH_SIZE" "write:WRITE_SIZE" "sq:SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" "valu:SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_INSTS_VALU GRBM_GUI_ACTIVE"; do
       name=${pass%%:*}; ctrs=${pass#*:}
       timeout -k 10 -s KILL 240 rocprofv3 --pmc $ctrs -d $O/pmc_${W}_$name -o run --output-format csv -- python3 $R/bench.py --workload $W --steps 3 --warmup 1 --no-cpu-baseline --no-e2e --no-verify --ramp-ms 0 > $O/pmc_${W}_$name.log 2>&1 || exit 13
