@@ -465,6 +465,7 @@ def main():
         e2e = end_to_end(torch, amq, kind, bpk, cap, counts, keys, sync=sync, reduce_max=red,
                          total_keys=total_keys, world=world)
 
+    comm = comm_info(torch, dist, dev) if pg else None
     if pg:
         dist.barrier()
     if rank != 0:
@@ -523,6 +524,8 @@ def main():
                      "alg_bytes_per_launch": alg_bytes},
         "cpu_baseline": base,
     }
+    if comm is not None:
+        line["comm"] = comm
     if verified is not None:
         line["verified"] = verified["ok"] and verified.get("all_ranks_ok", True)
         line["verify"] = verified
@@ -578,10 +581,14 @@ def valu_roofline(prof, n_keys, kernel_ms):
 # ---------------------------------------------------------------------------------------
 def bench_hash_sharded(args, torch, dist, amq, world, rank, dev, bpk, label, pg=False):
     """One Bloom filter over every rank's keys; rank r owns a contiguous byte range of its
-    bitmap.  A step = route (tkv_amq_bloom_route) + all-to-all of the keys (RCCL) + the rank's
-    range build (tkv_amq_bloom_build_range); the all-gather of the ranges is timed separately
-    (in-step with --allgather).  Rank 0 checks the gathered filter against a one-GPU build of
-    all keys, and that against the CPU oracle when it holds <= 200M keys."""
+    bitmap (turtle_kv_amd.dist.HashShardedBloom).  A step = route (every key hashed once into
+    its 12-byte bit record, ordered by owning part) + all-to-all of the records (RCCL) + the
+    rank's part builds; the all-gather of the ranges is timed separately (in-step with
+    --allgather).  Without a process group (one GPU, no launcher) the step is the range build
+    over the GPU's own keys, which makes the same records itself.  Rank 0 checks the gathered
+    filter against a one-GPU build of all keys, and that against the CPU oracle: the whole
+    filter up to 200M keys, beyond that the header and eight sampled tiles (the first, the last
+    and six seeded-random ones), the oracle hashing every key for them."""
     from turtle_kv_amd import dist as tdist
     strong = args.total_keys is not None
     n_local = args.total_keys // world if strong else args.keys_per_gpu
@@ -619,23 +626,22 @@ def bench_hash_sharded(args, torch, dist, amq, world, rank, dev, bpk, label, pg=
 
     # untimed breakdown of one step on this rank (HIP events on the current stream)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+    n_owned = n_local
     ev[0].record()
     if pg:
-        routed, sc = hs.route(keys)
+        routed, pc = hs.route(keys)
         ev[1].record()
-        owned = hs.exchange(routed, sc)
+        owned, sub = hs.exchange(routed, pc)
+        ev[2].record()
+        hs.build_owned(owned, sub)
+        n_owned = int(owned.shape[0])
     else:
         ev[1].record()
-        owned = keys
-    ev[2].record()
-    if pg:
-        hs.build_owned(owned)  # bit records (k <= 8) or keys, as routed
-    else:
-        hs.build_range(owned)
+        ev[2].record()
+        hs.local_build(keys)
     ev[3].record()
     torch.cuda.synchronize()
     route_ms, a2a_ms, build_ms = (ev[i].elapsed_time(ev[i + 1]) for i in range(3))
-    n_owned = int(owned.shape[0])
 
     allgather_ms = None
     if pg:
@@ -647,20 +653,11 @@ def bench_hash_sharded(args, torch, dist, amq, world, rank, dev, bpk, label, pg=
         allgather_ms = reduce_max(torch, dist, (time.perf_counter() - g0) / 3 * 1e3, coll_dev)
     filt = hs.allgather()
     torch.cuda.synchronize()
+    comm = comm_info(torch, dist, dev) if pg else None
 
     check = None
     if rank == 0 and not args.no_verify:
-        allk = amq.gen_keys16(42, 0, total, device=dev)
-        ref_plan = amq.plan_filters(0, [total], bpk)
-        ref = amq.build_all_filters(ref_plan, amq.KeyBatch.fixed(allk))
-        check = {"equal_to_one_gpu_build": bool(torch.equal(ref[:filt.numel()], filt))}
-        del allk
-        if total <= 200_000_000:
-            from oracle import oracle as O
-            O.build_oracle()
-            st, oref = O.bloom_build(O.gen_keys16(42, 0, total), total, bpk, src_page_id=0)
-            check["equal_to_oracle"] = st == 0 and oref.tobytes() == filt.cpu().numpy().tobytes()
-        check["ok"] = all(v for k, v in check.items())
+        check = verify_hash_sharded(torch, amq, filt, total, bpk, dev)
     if pg:
         flag = torch.tensor([1 if (check is None or check["ok"]) else 0], dtype=torch.int32,
                             device=coll_dev)
@@ -683,6 +680,9 @@ def bench_hash_sharded(args, torch, dist, amq, world, rank, dev, bpk, label, pg=
     ms_per_step = wall / args.steps * 1e3
     value = total * args.steps / wall / 1e6
     alg = n_local * 16 + (int(hs.payload_bytes) - 64) // world  # keys in, this rank's bitmap out
+    path = ("route -> all-to-all -> part builds" if pg else
+            ("range build from the keys" if hs.T <= tdist.KEY_RANGE_MAX_TILES else
+             "route -> part builds"))
     line = {
         "metric": f"{label} Mkeys/s (device-resident)",
         "value": round(value, 2), "unit": "Mkeys/s", "n_gpus": world, "steps": args.steps,
@@ -690,11 +690,13 @@ def bench_hash_sharded(args, torch, dist, amq, world, rank, dev, bpk, label, pg=
         "higher_is_better": True, "scaling": "strong" if strong else "weak", "vs_baseline": None,
         "dtype": "u64", "data": "synthetic (splitmix64 seed 42 keys generated on the device)",
         "config": {"workload": f"{label}: {total} x 16B keys, {n_local} per GPU, one filter of "
-                               f"{hs.n_blocks} blocks; rank r owns tiles [{hs.tile_begin}, ...)",
+                               f"{hs.n_blocks} blocks ({hs.T} tiles); rank r owns tiles "
+                               f"[r*{hs.g * hs.q}, ...) in {hs.g} part(s)",
                    "keys_per_gpu": n_local, "total_keys": total, "key_bytes": 16,
                    "bits_per_key": bpk, "filter": "bloom-blocked512, monolithic",
                    "parallelism": f"hash-range-sharded x{world}",
-                   "backend": args.backend if pg else None},
+                   "backend": args.backend if pg else None,
+                   "path": path, "units": "12-byte bit records" if hs.records else "16-byte keys"},
         "roofline": {"bound": "hbm", "achieved": round(alg / (ms_per_step * 1e-3) / 1e9, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(alg / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
@@ -705,10 +707,65 @@ def bench_hash_sharded(args, torch, dist, amq, world, rank, dev, bpk, label, pg=
                                     "range_build": round(build_ms, 4), "keys_owned": n_owned},
         "verified": check["ok"] if check else None, "verify": check,
     }
+    if comm is not None:
+        line["comm"] = comm
     if allgather_ms is not None:
         line["allgather_ms"] = round(allgather_ms, 3)
         line["build_plus_allgather_mkeys_s"] = round(total / ((ms_per_step + allgather_ms) * 1e-3) / 1e6, 2)
     print(json.dumps(line), flush=True)
+
+
+def verify_hash_sharded(torch, amq, filt, total, bpk, dev, full_oracle_max=200_000_000):
+    """The gathered hash-range sharded filter against a one-GPU tkv_amq_build of all keys and
+    against the CPU oracle (whole filter up to full_oracle_max keys, else header + 8 tiles)."""
+    from turtle_kv_amd import dist as tdist
+    allk = amq.gen_keys16(42, 0, total, device=dev)
+    ref_plan = amq.plan_filters(0, [total], bpk)
+    ref = amq.build_all_filters(ref_plan, amq.KeyBatch.fixed(allk))
+    check = {"equal_to_one_gpu_build": bool(torch.equal(ref[:filt.numel()], filt))}
+    del allk, ref
+    from oracle import oracle as O
+    O.build_oracle()
+    if total <= full_oracle_max:
+        st, oref = O.bloom_build(O.gen_keys16(42, 0, total), total, bpk, src_page_id=0)
+        check["equal_to_oracle"] = st == 0 and oref.tobytes() == filt.cpu().numpy().tobytes()
+    else:
+        nb = int(ref_plan.segs[0]["n_blocks"])
+        TB = tdist.BLOOM_TILE_BLOCKS
+        T = -(-nb // TB)
+        rng = np.random.default_rng(7)
+        tiles = sorted({0, T - 1, *[int(t) for t in rng.choice(T, size=min(6, T), replace=False)]})
+        wins = [(t * TB, min(nb, (t + 1) * TB)) for t in tiles]
+        cores, _ = host_cpu_share()
+        t0 = time.perf_counter()
+        st, got = O.bloom_sample_blocks(42, 0, total, bpk, wins, n_threads=cores)
+        dt = time.perf_counter() - t0
+        host = filt.cpu().numpy()
+        same = st == 0 and all(v.tobytes() == host[64 + 64 * a:64 + 64 * b].tobytes()
+                               for (a, b), v in got.items())
+        k = int(O.lib().tkvo_bloom_hash_count(bpk))
+        hdr = np.frombuffer(host[:64].tobytes(), dtype="<u8")
+        hdr_ok = (int(hdr[0]) == 0xCA6F49A0F3F8A4B0 and int(hdr[1]) == 512 * nb and int(hdr[2]) == 0
+                  and int(hdr[3]) == 0 and int(hdr[4]) == 8 * nb
+                  and int(hdr[5]) == nb | (k << 32) | (2 << 48) and int(hdr[6]) == total)
+        check["equal_to_oracle_sampled_tiles"] = bool(same and hdr_ok)
+        check["oracle_sample"] = {"tiles": tiles, "tile_blocks": TB, "of_tiles": T,
+                                  "keys_hashed": total, "threads": cores, "seconds": round(dt, 2)}
+    check["ok"] = all(v for k, v in check.items() if isinstance(v, bool))
+    return check
+
+
+def comm_info(torch, dist, dev):
+    """The process group as the ranks see it: the communicator's world size and backend and
+    every rank's bound device, gathered from the ranks themselves (an N-rank line shows that
+    RCCL saw N ranks on N devices)."""
+    p = torch.cuda.get_device_properties(dev)
+    mine = {"rank": dist.get_rank(), "device": dev.index, "uuid": str(getattr(p, "uuid", "")),
+            "pci_bus_id": getattr(p, "pci_bus_id", None), "host": socket.gethostname()}
+    everyone = [None] * dist.get_world_size()
+    dist.all_gather_object(everyone, mine)
+    return {"world_size": dist.get_world_size(), "backend": dist.get_backend(), "ranks": everyone,
+            "distinct_devices": len({(e["host"], e["uuid"], e["pci_bus_id"]) for e in everyone})}
 
 
 def cpu_baseline_monolithic(bpk, n):

@@ -187,14 +187,20 @@ int tkv_amq_build_check(int kind, const void* d_workspace, uint64_t workspace_by
 /* Hash-range sharding of ONE monolithic Bloom filter over several GPUs (BASELINE config 5,
  * SURVEY.md 8(e); no reference counterpart: the reference builds each filter on one CPU
  * thread, filter_builder.hpp:126-135).  The filter planned by tkv_amq_plan for the whole key
- * set (one segment of n_blocks blocks) is cut into T = ceil(n_blocks / 1024) tiles of 1024
- * blocks; part p of n_parts owns tiles [p*q, min((p+1)*q, T)), q = ceil(T / n_parts), i.e. a
- * contiguous byte range of the bitmap.  A key belongs to the tile of its block (h0).
+ * set (one segment of n_blocks blocks) is cut into T = ceil(n_blocks / tile_blocks) tiles of
+ * tkv_amq_bloom_tile_blocks() blocks (2048: one 128 KiB LDS image); part p of n_parts owns
+ * tiles [p*q, min((p+1)*q, T)), q = ceil(T / n_parts), i.e. a contiguous byte range of the
+ * bitmap.  A key belongs to the tile of its block (h0).  A rank may own several consecutive
+ * parts (its range is then their union, built part by part).
  *
  * tkv_amq_bloom_route: rank-local step 1.  Reorders this rank's n_keys 16-byte keys by owning
  * part into d_routed16 (part 0's keys first) and writes the per-part counts
  * (d_part_counts[n_parts], u32, device) -- the send counts of the all-to-all that follows.
  * d_seg is the whole filter's segment (device), n_blocks its n_blocks (host copy). */
+uint32_t tkv_amq_bloom_tile_blocks(void);
+/* the most tiles one range build takes: from records (records != 0; the record's tile field)
+ * or from 16-byte keys (the partition's LDS tile table) */
+uint32_t tkv_amq_bloom_range_max_tiles(int records);
 uint64_t tkv_amq_bloom_route_ws_bytes(uint64_t n_keys, uint32_t n_parts);
 int tkv_amq_bloom_route(const uint8_t* d_keys16, uint64_t n_keys, const tkv_amq_segment* d_seg,
                         uint32_t n_blocks, uint32_t n_parts, uint8_t* d_routed16,
@@ -207,7 +213,8 @@ int tkv_amq_bloom_route(const uint8_t* d_keys16, uint64_t n_keys, const tkv_amq_
  * where tkv_amq_build puts them, and writes the filter header too.  Bytes of other tiles are
  * not touched, so the ranks' ranges are disjoint and one all-gather of them is the filter.
  * An empty range (tile_begin == tile_end: a rank past the last tile when ceil(T/q) < ranks)
- * writes the header only.  Keys are 16 bytes (route and range build alike). */
+ * writes the header only.  Keys are 16 bytes (route and range build alike); a range holds at
+ * most tkv_amq_bloom_range_max_tiles(0) tiles. */
 uint64_t tkv_amq_bloom_build_range_ws_bytes(uint64_t n_keys, uint32_t tile_begin, uint32_t tile_end);
 int tkv_amq_bloom_build_range(const uint8_t* d_keys16, uint64_t n_keys, const tkv_amq_segment* d_seg,
                               uint32_t n_blocks, uint32_t tile_begin, uint32_t tile_end,
@@ -219,7 +226,10 @@ int tkv_amq_bloom_build_range(const uint8_t* d_keys16, uint64_t n_keys, const tk
  * once and writes its record (block in tile, the k bit indices, the tile relative to its
  * owner's first tile) into d_recs12 ordered by owner, so the all-to-all carries 12 bytes per key
  * instead of 16 and the owner does not hash again; tkv_amq_bloom_build_range_records builds the
- * owner's tiles from the records it received (at most 3,584 tiles per range). */
+ * owner's tiles from the records it received.  The record carries its tile relative to its
+ * part, so a part -- and a range built from records -- holds at most
+ * tkv_amq_bloom_range_max_tiles(1) tiles (8,192: 1 GiB of filter); a route with larger parts is
+ * refused (InvalidArgument). */
 uint64_t tkv_amq_bloom_route_records_ws_bytes(uint64_t n_keys, uint32_t n_parts);
 int tkv_amq_bloom_route_records(const uint8_t* d_keys16, uint64_t n_keys, const tkv_amq_segment* d_seg,
                                 uint32_t n_blocks, uint32_t hash_count, uint32_t n_parts,

@@ -92,6 +92,8 @@ def _load(path):
     L.tkvo_bloom_build_payload.argtypes = [vp, vp, u32, u64, u32, u64, vp, u64]
     L.tkvo_bloom_query_payload.restype = i32
     L.tkvo_bloom_query_payload.argtypes = [vp, vp, ctypes.c_size_t]
+    L.tkvo_bloom_sample_blocks_gen16.restype = i32
+    L.tkvo_bloom_sample_blocks_gen16.argtypes = [u64, u64, u64, u32, vp, vp, u32, vp, i32]
     L.tkvo_vqf_load_factor.restype = ctypes.c_double
     L.tkvo_vqf_load_factor.argtypes = [i32, u64]
     L.tkvo_vqf_required_size.restype = u64
@@ -142,6 +144,23 @@ def bloom_build(keys, n: int, bpk: int, src_page_id: int = 0, offsets=None, stri
     st = L.tkvo_bloom_build_payload(_p(keys), _p(offsets), stride, n, bpk, src_page_id,
                                        _p(out), cap)
     return st, out
+
+
+def bloom_sample_blocks(seed: int, first: int, n: int, bpk: int, windows, n_threads: int = 8):
+    """The 64-byte blocks of the block windows [(b0, b1), ...] (ascending, disjoint) of the
+    Bloom filter over gen_keys16(seed, first, n), without the key array or the whole filter.
+    Returns (status, {(b0, b1): bytes})."""
+    windows = sorted(windows)
+    b0 = np.ascontiguousarray([w[0] for w in windows], dtype=np.uint64)
+    b1 = np.ascontiguousarray([w[1] for w in windows], dtype=np.uint64)
+    out = np.zeros(int(64 * (b1 - b0).sum()), dtype=np.uint8)
+    st = lib().tkvo_bloom_sample_blocks_gen16(seed, first, n, bpk, _p(b0), _p(b1), len(windows),
+                                             _p(out), n_threads)
+    res, off = {}, 0
+    for (a, b) in windows:
+        res[(a, b)] = out[off:off + 64 * (b - a)]
+        off += 64 * (b - a)
+    return st, res
 
 
 def bloom_query(payload: np.ndarray, key: bytes) -> int:

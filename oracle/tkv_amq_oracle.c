@@ -280,6 +280,67 @@ int tkvo_bloom_query_payload(const uint8_t* payload, const uint8_t* key, size_t 
   return 1;
 }
 
+/* Sampled block windows of the Bloom filter over the n splitmix keys tkvo_gen_keys16(seed,
+ * first, n) would produce, without materialising the keys or the filter (the check of a
+ * filter too large to build on one host thread in a test's time, e.g. BASELINE config 5's
+ * 1B keys): every key is generated and its h0 computed; a key whose block falls in one of
+ * the windows [blk0[i], blk1[i]) (ascending, disjoint) has its k bits set there, exactly as
+ * tkvo_bloom_build_payload would.  out: the windows' 64-byte blocks concatenated, zeroed by
+ * the caller.  Keys are spread over n_threads threads in chunks; bits are ORed atomically. */
+typedef struct {
+  uint64_t seed, first, n;
+  uint32_t nb, k, n_win;
+  const uint64_t* blk0;
+  const uint64_t* blk1;
+  const uint64_t* wbase; /* first word of window i in out */
+  uint64_t* words;
+} sample_arg;
+
+#define SAMPLE_CHUNK (1u << 20)
+
+static void sample_chunk(par_ctx* c, uint32_t ci)
+{
+  const sample_arg* a = (const sample_arg*)c->arg;
+  const uint64_t b = (uint64_t)ci * SAMPLE_CHUNK;
+  const uint64_t e = b + SAMPLE_CHUNK < a->n ? b + SAMPLE_CHUNK : a->n;
+  for (uint64_t i = b; i < e; ++i) {
+    uint8_t key[16];
+    const uint64_t g = a->first + i;
+    wr64(key, tkvo_splitmix64_at(a->seed, 2 * g + 1));
+    wr64(key + 8, tkvo_splitmix64_at(a->seed, 2 * g + 2));
+    const uint64_t h0 = tkvo_xxh64(key, 16, tkvo_bloom_seed(0));
+    const uint64_t blk = (uint64_t)(((u128)h0 * a->nb) >> 64);
+    for (uint32_t w = 0; w < a->n_win; ++w) {
+      if (blk < a->blk0[w]) break;
+      if (blk >= a->blk1[w]) continue;
+      uint64_t* bw = a->words + a->wbase[w] + 8 * (blk - a->blk0[w]);
+      for (uint32_t j = 0; j < a->k; ++j) {
+        const uint64_t h = j == 0 ? h0 : tkvo_xxh64(key, 16, tkvo_bloom_seed(j));
+        const uint32_t bit = (uint32_t)(h & 511);
+        __atomic_fetch_or(bw + (bit >> 6), 1ull << (bit & 63), __ATOMIC_RELAXED);
+      }
+      break;
+    }
+  }
+}
+
+int tkvo_bloom_sample_blocks_gen16(uint64_t seed, uint64_t first, uint64_t n, uint32_t bpk,
+                                   const uint64_t* blk0, const uint64_t* blk1, uint32_t n_win,
+                                   uint8_t* out, int n_threads)
+{
+  if (bpk == 0 || bpk > 64 || n_win > 64) return TKVO_INVALID_ARGUMENT;
+  uint64_t wbase[64];
+  uint64_t words = 0;
+  for (uint32_t w = 0; w < n_win; ++w) {
+    if (blk1[w] < blk0[w] || (w && blk0[w] < blk1[w - 1])) return TKVO_INVALID_ARGUMENT;
+    wbase[w] = words;
+    words += 8 * (blk1[w] - blk0[w]);
+  }
+  sample_arg a = {seed, first, n, tkvo_bloom_block_count(n, bpk), tkvo_bloom_hash_count(bpk),
+                  n_win, blk0, blk1, wbase, (uint64_t*)out};
+  return par_run((uint32_t)((n + SAMPLE_CHUNK - 1) / SAMPLE_CHUNK), n_threads, sample_chunk, &a);
+}
+
 /* ------------------------------------------------------------------------------------
  * VQF (restates the vqf 0.2.4 operations called at tree/filter_builder.hpp:193-211 and
  * vqf_filter_page_view.hpp:113-125; upstream design: Pandey et al., SIGMOD'21).

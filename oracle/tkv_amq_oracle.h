@@ -59,6 +59,11 @@ int tkvo_bloom_build_payload(const uint8_t* keys, const uint64_t* offsets, uint3
                              uint64_t n, uint32_t bits_per_key, uint64_t src_page_id,
                              uint8_t* out_payload, uint64_t out_capacity);
 int tkvo_bloom_query_payload(const uint8_t* payload, const uint8_t* key, size_t len);
+/* the blocks of sampled windows [blk0[i], blk1[i]) of the filter over tkvo_gen_keys16(seed,
+ * first, n), keys generated and hashed on the fly (no key array, no whole filter) */
+int tkvo_bloom_sample_blocks_gen16(uint64_t seed, uint64_t first, uint64_t n, uint32_t bpk,
+                                   const uint64_t* blk0, const uint64_t* blk1, uint32_t n_win,
+                                   uint8_t* out, int n_threads);
 
 /* ---------------- VQF ---------------- */
 typedef struct tkvo_vqf_plan {

@@ -105,6 +105,27 @@ def test_batch_plan_layout(amq):
         amq.plan_filters(amq.BLOOM, [100000], 10, out_stride=20544)
 
 
+def test_hash_shard_constants_match_library(amq):
+    """turtle_kv_amd.dist's tile geometry is the library's (tkv_amq_bloom_tile_blocks and the
+    range builds' tile caps), and the monolithic workspace the plan asks for covers the
+    routed-part form beyond one partition's tile table (16 bytes per key of routed items plus
+    the part's regions and overflow lists)."""
+    from turtle_kv_amd import dist as tdist
+    L = amq.abi.lib()
+    assert L.tkv_amq_bloom_tile_blocks() == tdist.BLOOM_TILE_BLOCKS == 2048
+    assert L.tkv_amq_bloom_range_max_tiles(1) == tdist.RECORD_RANGE_MAX_TILES
+    assert L.tkv_amq_bloom_range_max_tiles(0) == tdist.KEY_RANGE_MAX_TILES
+    direct = amq.plan_filters(amq.BLOOM, [100_000_000], 10)
+    routed = amq.plan_filters(amq.BLOOM, [1_750_000_000], 12)
+    assert direct.workspace_bytes >= 16 * 100_000_000
+    assert routed.workspace_bytes >= 16 * 1_750_000_000 * 2
+    # a range build from records past 8,192 tiles, or from keys past 20,000, is refused
+    assert L.tkv_amq_bloom_build_range_records_ws_bytes(1000, 0, 8192) > 0
+    assert L.tkv_amq_bloom_build_range_records_ws_bytes(1000, 0, 8193) == 0
+    assert L.tkv_amq_bloom_build_range_ws_bytes(1000, 5, 20005) > 0
+    assert L.tkv_amq_bloom_build_range_ws_bytes(1000, 5, 20006) == 0
+
+
 def test_device_calls_fail_loudly_without_gpu(amq):
     if amq.abi.lib().tkv_amq_device_count() > 0:
         pytest.skip("a GPU is visible")

@@ -93,27 +93,73 @@ def test_shard_ranges_cover_all_leaves():
 def test_hash_shard_tiles_cover_the_filter():
     """Hash-range sharding (config 5 read literally): the ranks' tile ranges are contiguous,
     disjoint and cover every tile.  With ceil(T/q) < ranks the last ranks own an empty range
-    (T = 17 over 8 ranks: q = 3, ranks 6 and 7; 3 tiles over 8 ranks: ranks 3-7): they are
+    (T = 17 over 8 ranks: q = 3, ranks 6 and 7; 2 tiles over 8 ranks: ranks 2-7): they are
     accepted, and their range build writes the header only (GPU test
     test_gpu_hash_shard.py::test_empty_ranges_write_the_header)."""
     from turtle_kv_amd import abi
-    from turtle_kv_amd.dist import HashShardedBloom, hash_shard_tiles
-    for nb, world in [(1, 1), (1024, 1), (1025, 2), (93750, 8), (2_343_750, 8), (29297, 8),
-                      (17 * 1024, 8), (3000, 8)]:
+    from turtle_kv_amd.dist import BLOOM_TILE_BLOCKS as TB, HashShardedBloom, hash_shard_tiles
+    for nb, world in [(1, 1), (TB, 1), (TB + 1, 2), (93750, 8), (2_343_750, 8), (29297, 8),
+                      (17 * TB, 8), (3000, 8)]:
         T, q = hash_shard_tiles(nb, world)
-        assert T == -(-nb // 1024)
+        assert T == -(-nb // TB)
         ranges = [(min(T, r * q), min(T, (r + 1) * q)) for r in range(world)]
         assert ranges[0][0] == 0 and ranges[-1][1] == T
         assert all(a[1] == b[0] for a, b in zip(ranges, ranges[1:]))
-    T, q = hash_shard_tiles(17 * 1024, 8)
+    T, q = hash_shard_tiles(17 * TB, 8)
     assert (T, q) == (17, 3)
     empty = [r for r in range(8) if min(T, r * q) == min(T, (r + 1) * q)]
     assert empty == [6, 7]
-    hs = HashShardedBloom(100_000, 12, 8, 5, "cpu")   # 3 tiles over 8 ranks: rank 5 owns none
-    assert hs.tile_begin == hs.tile_end == 3
+    hs = HashShardedBloom(100_000, 12, 8, 5, "cpu")   # 2 tiles over 8 ranks: rank 5 owns none
+    assert hs.T == 2 and hs.tile_begin == hs.tile_end == 2
     with pytest.raises(abi.TkvAmqError, match="got shape"):
         hs.route(torch.zeros((10, 20), dtype=torch.uint8))   # 16- or 24-byte keys only
     hk = HashShardedBloom(100_000, 16, 8, 0, "cpu")         # k = 11: keys travel, 16 bytes only
     assert not hk.records
     with pytest.raises(abi.TkvAmqError, match="got shape"):
         hk.route(torch.zeros((10, 24), dtype=torch.uint8))
+    with pytest.raises(abi.TkvAmqError, match="got shape"):
+        hk.build_range(torch.zeros((10, 24), dtype=torch.uint8))   # the range build: 16 only
+
+
+def test_hash_shard_parts_per_rank():
+    """A rank's range is cut into g parts when it exceeds what one range build takes (8,192
+    tiles from 12-byte records, 20,000 from 16-byte keys): BASELINE config 5 (1B keys at
+    12 bits/key, 11,445 tiles) takes two parts on one rank and one part from two ranks up; every
+    part holds at most the cap, the parts of all ranks tile the filter, and rank r's range is
+    its parts' union."""
+    from turtle_kv_amd.dist import (KEY_RANGE_MAX_TILES, RECORD_RANGE_MAX_TILES, HashShardedBloom,
+                                    hash_shard_plan)
+    nb_1b = -(-1_000_000_000 * 12 // 512)
+    assert hash_shard_plan(nb_1b, 1) == (11445, 2, 5723)
+    assert hash_shard_plan(nb_1b, 2)[1:] == (1, 5723)
+    assert hash_shard_plan(nb_1b, 8)[1:] == (1, 1431)
+    assert hash_shard_plan(nb_1b, 1, records=False) == (11445, 1, 11445)
+    for nb in [1, 5000, nb_1b, 3 * nb_1b, 40_000_000 * 2048]:
+        for world in [1, 2, 3, 8]:
+            for rec in (True, False):
+                T, g, q = hash_shard_plan(nb, world, rec)
+                assert q <= (RECORD_RANGE_MAX_TILES if rec else KEY_RANGE_MAX_TILES)
+                parts = [(min(T, p * q), min(T, (p + 1) * q)) for p in range(world * g)]
+                assert parts[0][0] == 0 and parts[-1][1] == T
+                assert all(a[1] == b[0] for a, b in zip(parts, parts[1:]))
+    hs = HashShardedBloom(1_000_000_000, 12, 2, 1, "meta")
+    assert (hs.g, hs.q, hs.tile_begin, hs.tile_end) == (1, 5723, 5723, 11445)
+    assert hs.part_tiles(0) == (5723, 11445)
+
+
+def test_build_owned_regroups_parts():
+    """With g > 1 parts per rank the all-to-all delivers, per sender, that sender's units for
+    each of this rank's parts in order; build_owned hands part j all senders' pieces of it."""
+    from turtle_kv_amd.dist import HashShardedBloom
+    hs = HashShardedBloom.__new__(HashShardedBloom)
+    got = []
+    hs._build_part = lambda units, j: got.append((j, units.tolist()))
+    W, g = 3, 2
+    sub = torch.tensor([[2, 1], [0, 3], [1, 0]])     # sender s sent sub[s, j] units of part j
+    owned = torch.arange(int(sub.sum()))
+    hs.build_owned(owned, sub)
+    # sender 0: [0 1 | 2], sender 1: [ | 3 4 5], sender 2: [6 | ]
+    assert got == [(0, [0, 1, 6]), (1, [2, 3, 4, 5])]
+    got.clear()
+    hs.build_owned(owned[:5], torch.tensor([[5]]))
+    assert got == [(0, [0, 1, 2, 3, 4])]

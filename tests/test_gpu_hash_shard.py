@@ -57,7 +57,7 @@ def test_route_and_range_build_equal_monolithic(oracle, amq, torch, n_keys, bpk,
         keys[n_keys - dup:] = keys[n_keys // 3]
     plan = amq.plan_filters(0, [n_keys], bpk)
     nb = int(plan.segs[0]["n_blocks"])
-    assert 64 * nb > 64 * 1024, "must take the tiled monolithic build"
+    assert 64 * nb > 4 * 160 * 1024, "must take the tiled monolithic build"
     whole = amq.build_all_filters(plan, amq.KeyBatch.fixed(keys))
     routed, counts = _route(amq, torch, keys, plan, n_parts)
     assert counts.sum() == n_keys
@@ -89,7 +89,8 @@ def test_range_build_ignores_keys_outside_its_tiles(amq, torch):
     out = torch.zeros(plan.total_out_bytes, dtype=torch.uint8, device="cuda")
     _build_range(amq, torch, keys, plan, q, 2 * q, out)
     torch.cuda.synchronize()
-    lo, hi = 64 + 64 * 1024 * q, 64 + 64 * 1024 * 2 * q
+    from turtle_kv_amd.dist import BLOOM_TILE_BLOCKS as TB
+    lo, hi = 64 + 64 * TB * q, 64 + 64 * TB * 2 * q
     assert torch.equal(out[lo:hi], whole[lo:hi])
     assert torch.equal(out[:64], whole[:64])          # the header, from every range
     assert int(out[64:lo].count_nonzero()) == 0       # other ranges untouched
@@ -120,7 +121,7 @@ def test_empty_ranges_write_the_header(amq, torch):
     from the route, and their range build still writes the whole filter header, so every
     rank's assembled result (its own header + the gathered ranges) equals the one-GPU build."""
     from turtle_kv_amd.dist import hash_shard_tiles
-    n, world = 720_000, 8
+    n, world = 1_440_000, 8
     keys = amq.gen_keys16(13, 0, n)
     plan = amq.plan_filters(0, [n], 12)
     T, q = hash_shard_tiles(int(plan.segs[0]["n_blocks"]), world)
@@ -177,12 +178,12 @@ def _build_range_records(amq, torch, recs, plan, t0, t1, out):
 
 @pytest.mark.parametrize("n_keys,bpk,n_parts,dup", [(3_000_000, 12, 3, 0), (1_500_001, 10, 8, 0),
                                                    (700_000, 12, 1, 0), (2_000_000, 12, 4, 600_000),
-                                                   (720_000, 12, 8, 0), (900_000, 5, 2, 0)])
+                                                   (1_440_000, 12, 8, 0), (900_000, 5, 2, 0)])
 def test_route_records_and_range_build_equal_monolithic(oracle, amq, torch, n_keys, bpk, n_parts, dup):
     """The record form of hash-range sharding (k <= 8): every key hashed once by its sender into
     a 12-byte bit record with its tile relative to its owner; each owner builds its tiles from
     the records alone.  Equal to the one-GPU build and the oracle: k = 8, 7 and 3, duplicate
-    keys (one tile's regions overflow), ranks past the last tile (720K keys: 17 tiles over 8)."""
+    keys (one tile's regions overflow), ranks past the last tile (1.44M keys: 17 tiles over 8)."""
     from turtle_kv_amd.dist import hash_shard_tiles
     keys = amq.gen_keys16(21, 0, n_keys)
     if dup:

@@ -88,7 +88,7 @@ EXPORTS = [
     "tkv_amq_bloom_route_ws_bytes", "tkv_amq_bloom_route", "tkv_amq_bloom_build_range_ws_bytes",
     "tkv_amq_bloom_build_range", "tkv_amq_bloom_route_records_ws_bytes", "tkv_amq_bloom_route_records",
     "tkv_amq_bloom_build_range_records_ws_bytes", "tkv_amq_bloom_build_range_records",
-    "tkv_amq_bloom_route_records_ex",
+    "tkv_amq_bloom_route_records_ex", "tkv_amq_bloom_tile_blocks", "tkv_amq_bloom_range_max_tiles",
 ]
 
 # tkv_amq_key_view (libstdc++ std::string_view layout)
@@ -185,6 +185,11 @@ def lib(build_if_missing: bool = True):
         L.tkv_amq_bloom_build_range_records_ws_bytes.argtypes = [u64, u32, u32]
         L.tkv_amq_bloom_build_range_records.restype = i32
         L.tkv_amq_bloom_build_range_records.argtypes = [vp, u64, vp, u32, u32, u32, u32, vp, vp, u64, vp]
+    if hasattr(L, "tkv_amq_bloom_tile_blocks"):
+        L.tkv_amq_bloom_tile_blocks.restype = u32
+        L.tkv_amq_bloom_tile_blocks.argtypes = []
+        L.tkv_amq_bloom_range_max_tiles.restype = u32
+        L.tkv_amq_bloom_range_max_tiles.argtypes = [i32]
     _lib = L
     return L
 

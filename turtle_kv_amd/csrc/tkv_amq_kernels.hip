@@ -6,11 +6,12 @@
 //                        lane rounds shared), bits set in an LDS image of the whole filter with
 //                        ds_or_b32, image written out with 16-byte coalesced stores.  Other key
 //                        shapes: 24-byte lanes, or XxhShort for any key under 32 bytes.
-//   bloom_rec_*          one filter larger than LDS (the monolithic variant): each key hashed
-//                        once into a 12-byte bit record, records counting-sorted by 64 KiB
-//                        tile in LDS and appended to per-(tile, workgroup) regions, then each
-//                        tile built in LDS from its records (bloom_part_* / bloom_tile_build:
-//                        the count / scatter / hash-in-tile fallback for larger filters).
+//   bloom_part_* / bloom_tile   one filter larger than LDS (the monolithic variant, and a rank's
+//                        tile range of a hash-range sharded filter): each key hashed once into
+//                        a 12-byte bit record, ranked in its 128 KiB tile's run by an LDS
+//                        histogram and stored straight to its per-(tile, workgroup) region,
+//                        then each tile built in LDS from its records (route_*: the parts of
+//                        a filter beyond one partition's tile table, and hash-range shards).
 //   vqf_decide           one wave per segment replays the reference's insert order exactly
 //                        (power-of-two-choice decisions depend only on per-block counts, kept
 //                        in LDS); per 64-key chunk every conflict-free lane decides in the same
@@ -944,49 +945,93 @@ __global__ __launch_bounds__(256) void bloom_global_set(const uint8_t* __restric
 }
 
 // ---------------------------------------------------------------------------------------
-// Bloom build, monolithic filter (one filter larger than the LDS budget, 16-byte keys:
-// SURVEY.md 8(d)'s single-filter variant; the reference's build_bloom_filter_page over one
-// item range, tree/filter_builder.hpp:126-135).  The filter is cut into tiles of
-// kBloomTileBlocks 512-bit blocks (64 KiB, one LDS image each) and the keys are partitioned
-// by tile before each tile is built in LDS exactly like a leaf:
-//   bloom_part_count      P workgroups over contiguous key ranges: h0 -> tile, LDS
-//                         histogram, one row of H[P][n_tiles]
-//   bloom_part_scan_cols  per tile: exclusive scan of its column of H (each workgroup's
-//                         offset inside the tile's bucket) and the tile total
-//   bloom_part_scan_tiles exclusive scan of the tile totals (bucket bases)
-//   bloom_part_scatter    the same key ranges again: h0 -> tile, an LDS cursor gives the
-//                         key's slot in its tile's bucket; the 16-byte key is copied there
-//   bloom_tile_build      one 512-thread workgroup per tile: the bucket's keys through the
-//                         leaf kernel's k-hash LDS insert, then 16-byte stores of the image
-// The bits set do not depend on the order of keys inside a bucket, so the filter is
-// byte-identical to the leaf kernel's and the oracle's.  Device atomics (bloom_global_set,
-// one 4-byte memory-side atomic per bit) ran at 3.6 Gkeys/s on 100M keys.
+// Bloom build, monolithic filter: one filter larger than the window path takes (SURVEY.md
+// 8(d)'s single-filter variant, the reference's build_bloom_filter_page over one item range,
+// tree/filter_builder.hpp:126-135), and one rank's tile range of a hash-range sharded filter
+// (BASELINE config 5).  The filter is cut into tiles of kTileBlocks 512-bit blocks (128 KiB,
+// one LDS image each).  Every key is hashed once, where it is read, and what its tile needs of
+// the hashes -- its 12-byte bit record -- travels instead of the key:
+//   bloom_part      one 1024-thread workgroup per CU over a contiguous key range, in batches
+//                   of kPartBatch: each key is hashed into its record, its rank in its tile's
+//                   run of the batch comes from a returning ds_add on an LDS histogram (two
+//                   u16 counters per word), and the record is stored straight to its slot in
+//                   this workgroup's region of its tile (no LDS sort: the L2 merges a run's
+//                   records, which are written together).  Region (t, w) holds `cap` records
+//                   (mean + 6 sigma of a uniform hash); records beyond it go to the workgroup's
+//                   overflow list (LDS counter).  LDS per tile: two u16 histograms
+//                   (double-buffered over batches) and a u32 cursor, 8 bytes, so one pass takes
+//                   up to kDirectMaxTiles tiles.
+//   bloom_tile      one workgroup per tile: every region of the tile through ds_or into the
+//                   128 KiB image, then 16-byte stores.
+//   bloom_overflow  the overflow lists with device-scope atomicOr into the finished filter
+//                   (empty unless the keys are not spread by the hash, e.g. duplicates).
+// Partition sources: 16- and 24-byte keys (hashed here), 12-byte records routed by
+// tkv_amq_bloom_route_records (not hashed again; the tile relative to the part is in the
+// record), and, with k > 8, 16-byte keys as 16-byte records (the tile kernel hashes them).
+// A filter of more than kDirectMaxTiles tiles is first routed into parts of at most
+// kRecPartMaxTiles tiles (tkv_amq_bloom_route_records' kernels), and each part is built from
+// its records, its count read on the device.  The bits set do not depend on which kernel or
+// workgroup sets them, so the filter is byte-identical to the leaf kernel's and the oracle's.
+// Record: w0 = blk | b0 << 11 | b1 << 20 | tile[0:2] << 29
+//         w1 = b2 | b3 << 9 | b4 << 18 | tile[3:7] << 27
+//         w2 = b5 | b6 << 9 | b7 << 18 | tile[8:12] << 27      (b_j = b_0 for j >= k)
+// The tile field is the tile relative to the record's part (routed records); a partition's
+// own region records leave it unused.  Overflow entries are 16 bytes: the record and its
+// tile (relative to the build's first tile), or the 16-byte key.
 // ---------------------------------------------------------------------------------------
-constexpr uint32_t kBloomTileBlocks = 1024;     // 64 KiB LDS image per tile
-constexpr uint32_t kBloomPartMaxTiles = 32768;  // LDS histogram / cursors <= 128 KiB
-constexpr uint32_t kBloomPartMaxWgs = 1024;     // scatter workgroups (256 / 512 / 128 slower)
-constexpr uint32_t kRouteMaxParts = 2048;       // tkv_amq_bloom_route
-constexpr uint32_t kBloomTileThreads = 1024;    // 2 workgroups per CU (512: 6% slower)
-struct BloomPartGeom {
-  uint32_t P;         // partition workgroups
+constexpr uint32_t kTileBlocks = 2048;   // 128 KiB LDS image per tile
+constexpr uint32_t kTileShift = 11;
+constexpr uint32_t kTileThreads = 1024;  // one workgroup per CU
+constexpr uint32_t kPartThreads = 1024;
+constexpr uint32_t kPartU = 8;                              // items per thread per batch
+constexpr uint32_t kPartBatch = kPartThreads * kPartU;      // < 65536: u16 ranks
+constexpr uint32_t kPartMaxWgs = 256;
+constexpr uint32_t kDirectMaxTiles = 20000;                 // LDS: 8 bytes per tile
+constexpr uint32_t kRecPartMaxTiles = 8192;                 // a record's 13-bit tile field
+constexpr uint32_t kRouteMaxParts = 2048;                   // tkv_amq_bloom_route(_records)
+constexpr uint32_t kRouteMaxWgs = 1024;                     // route count / scatter workgroups
+
+__host__ __device__ constexpr inline uint32_t part_lds_bytes(uint32_t n_tiles)
+{
+  // H0, H1: (T+1)/2 words each; cursor: 2 * ((T+1)/2) words; the overflow counter
+  return 16u * ((n_tiles + 1) / 2) + 16u;
+}
+static_assert(part_lds_bytes(kDirectMaxTiles) <= 160 * 1024, "one workgroup per CU");
+static_assert(kPartBatch < 65536, "u16 ranks");
+
+enum PartSrc : int { kSrcKey16 = 0, kSrcKey24 = 1, kSrcRec12 = 2, kSrcRaw16 = 3 };
+
+struct PartGeom {
+  uint32_t P;        // partition workgroups
   uint32_t n_tiles;
-  uint32_t per;       // keys per partition workgroup
-  uint64_t h_words;   // P * n_tiles
-  uint64_t part_off;  // byte offset of the partitioned keys in the workspace
-  uint64_t bytes;     // workspace bytes
+  uint32_t per;      // items per partition workgroup at most (overflow list capacity)
+  uint32_t cap;      // records per (tile, workgroup) region
+  uint32_t rb;       // record bytes, 12 or 16
+  uint64_t counts_off;   // u32 [n_tiles][P]: records in each region
+  uint64_t ovf_n_off;    // u32 [P]: entries in each workgroup's overflow list
+  uint64_t regions_off;  // region (t, w) at regions_off + (t * P + w) * cap * rb
+  uint64_t ovf_off;      // workgroup w's overflow list at ovf_off + w * per * 16
+  uint64_t bytes;
 };
 
-__host__ __device__ inline BloomPartGeom bloom_part_geom(uint64_t n_keys, uint64_t nb)
+// n_max: items the build may receive (the overflow lists' capacity); n_exp: the expected
+// count (the regions' capacity; equal to n_max unless the count is only known on the device)
+inline PartGeom part_geom(uint64_t n_max, uint64_t n_exp, uint32_t n_tiles, uint32_t rb)
 {
-  BloomPartGeom g;
-  g.n_tiles = (uint32_t)((nb + kBloomTileBlocks - 1) / kBloomTileBlocks);
-  const uint64_t p = (n_keys + 4095) / 4096;
-  g.P = (uint32_t)(p < 1 ? 1 : (p > kBloomPartMaxWgs ? kBloomPartMaxWgs : p));
-  g.per = (uint32_t)((n_keys + g.P - 1) / g.P);
-  g.h_words = (uint64_t)g.P * g.n_tiles;
-  // [H: P x n_tiles u32][tile totals: n_tiles u32][bucket bases: n_tiles + 1 u32][keys]
-  g.part_off = (4 * (g.h_words + 2ull * g.n_tiles + 1) + 255) & ~255ull;
-  g.bytes = g.part_off + 16 * n_keys;
+  PartGeom g;
+  g.n_tiles = n_tiles ? n_tiles : 1;
+  g.rb = rb;
+  const uint64_t p = (n_exp + 32767) / 32768;
+  g.P = (uint32_t)(p < 1 ? 1 : (p > kPartMaxWgs ? kPartMaxWgs : p));
+  g.per = (uint32_t)((n_max + g.P - 1) / g.P);
+  const double e = (double)((n_exp + g.P - 1) / g.P) / g.n_tiles;
+  g.cap = ((uint32_t)(e + 6.0 * sqrt(e) + 16.0) + 15) & ~15u;
+  const uint64_t regions = (uint64_t)g.n_tiles * g.P;
+  g.counts_off = 256;
+  g.ovf_n_off = g.counts_off + 4 * regions;
+  g.regions_off = (g.ovf_n_off + 4ull * g.P + 255) & ~255ull;
+  g.ovf_off = g.regions_off + (uint64_t)rb * regions * g.cap;
+  g.bytes = g.ovf_off + 16ull * g.P * g.per;
   return g;
 }
 
@@ -994,12 +1039,12 @@ __device__ inline uint32_t bloom_tile_of(const uint4& kv, uint32_t nb)
 {
   const Xxh16 x((uint64_t)kv.x | ((uint64_t)kv.y << 32), (uint64_t)kv.z | ((uint64_t)kv.w << 32));
   const uint64_t h0 = x.finish(c_bloom.rhinit16[0]);
-  return (uint32_t)__umul64hi(h0, (uint64_t)nb) / kBloomTileBlocks;
+  return (uint32_t)__umul64hi(h0, (uint64_t)nb) >> kTileShift;
 }
 
 // 24-byte keys (TurtleKV's default key size, 8-byte aligned) where the hash-once paths take
-// them: the record partition of a monolithic filter and the hash-range route's count and
-// record passes.  (16-byte keys stay uint4.)
+// them: the partition of a monolithic filter and the hash-range route's count and record
+// passes.  (16-byte keys stay uint4.)
 struct Key24 {
   uint64_t w[3];
 };
@@ -1015,7 +1060,7 @@ __device__ inline uint32_t bloom_tile_of(const Key24& kv, uint32_t nb)
 {
   const XxhFixed<24> x(kv.w);
   const uint64_t h0 = x.finish(xxh_fixed_rc<24>(c_bloom.seed[0]));
-  return (uint32_t)__umul64hi(h0, (uint64_t)nb) / kBloomTileBlocks;
+  return (uint32_t)__umul64hi(h0, (uint64_t)nb) >> kTileShift;
 }
 
 // key i of a 16- or 24-byte key array
@@ -1026,80 +1071,122 @@ __device__ inline auto load_rec_key(const uint8_t* keys, uint32_t i)
   else return load_nt16(keys + 16ull * i);
 }
 
-// The window of a partition pass.  The whole monolithic filter: tile0 = 0, div = 1, keys
-// from the segment.  Hash-range sharding (tkv_amq_bloom_route / _build_range): the route
-// partitions a rank's keys by owner (div = tiles per part, output to `out`); a rank's range
-// build takes its routed keys [0, n) and the tiles [tile0, tile0 + n_tiles).
-struct PartWindow {
-  uint32_t tile0;  // global tile of local tile 0
-  uint32_t div;    // global tiles per local tile
-  uint32_t local;  // keys are [0, n_cap) of the key array, not the segment's range
-  uint32_t hdr;    // the first local tile also writes the filter header (every rank)
-  uint4* out;      // partitioned keys go here instead of the workspace
+__device__ inline void rec_pack(uint32_t blk, uint32_t tile, const uint32_t (&b)[8], uint32_t& w0,
+                                uint32_t& w1, uint32_t& w2)
+{
+  w0 = blk | b[0] << 11 | b[1] << 20 | (tile & 7u) << 29;
+  w1 = b[2] | b[3] << 9 | b[4] << 18 | ((tile >> 3) & 31u) << 27;
+  w2 = b[5] | b[6] << 9 | b[7] << 18 | ((tile >> 8) & 31u) << 27;
+}
+
+__device__ inline uint32_t rec_tile(uint32_t w0, uint32_t w1, uint32_t w2)
+{
+  return (w0 >> 29) | ((w1 >> 27) << 3) | ((w2 >> 27) << 8);
+}
+
+// a 16-byte key's block in the filter and its k <= 8 bit indices (b_j = b_0 for j >= k)
+template <int K>
+__device__ inline uint32_t rec_hash_bits(const uint4& kv, uint32_t nb, uint32_t k, uint32_t (&b)[8])
+{
+  const Xxh16 x((uint64_t)kv.x | ((uint64_t)kv.y << 32), (uint64_t)kv.z | ((uint64_t)kv.w << 32));
+  const uint64_t h0 = x.finish(c_bloom.rhinit16[0]);
+  b[0] = (uint32_t)h0 & 511u;
+#pragma unroll
+  for (uint32_t j = 1; j < 8; ++j) {
+    if (K != 0 ? j < (uint32_t)K : j < k) b[j] = x.finish_lo9(c_bloom.rhinit16[j]) & 511u;
+    else b[j] = b[0];
+  }
+  return (uint32_t)__umul64hi(h0, (uint64_t)nb);
+}
+
+// a 24-byte key's block and its bit indices (k > 8: the first eight; bloom_overflow sets the
+// others)
+template <int K>
+__device__ inline uint32_t rec_hash_bits(const Key24& kv, uint32_t nb, uint32_t k, uint32_t (&b)[8])
+{
+  const XxhFixed<24> x(kv.w);
+  const uint64_t h0 = x.finish(xxh_fixed_rc<24>(c_bloom.seed[0]));
+  b[0] = (uint32_t)h0 & 511u;
+#pragma unroll
+  for (uint32_t j = 1; j < 8; ++j) {
+    if (K != 0 ? j < (uint32_t)K : j < k) b[j] = x.finish_lo9(xxh_fixed_rc<24>(c_bloom.seed[j])) & 511u;
+    else b[j] = b[0];
+  }
+  return (uint32_t)__umul64hi(h0, (uint64_t)nb);
+}
+
+// ---------------------------------------------------------------------------------------
+// The route (hash-range sharding, and the parts of a filter beyond kDirectMaxTiles): part p
+// of n_parts owns tiles [p*q, (p+1)*q).  A count pass (h0 -> part, LDS histogram, one row of
+// H[P][n_parts] per workgroup), two scans (each workgroup's offset in each part's run, the
+// part bases), and a scatter pass over the same key ranges that writes each key -- or, with
+// k <= 8, its 12-byte bit record with its tile relative to its part -- to its slot.
+// ---------------------------------------------------------------------------------------
+struct RouteGeom {
+  uint32_t P;         // route workgroups
+  uint32_t n_parts;
+  uint32_t per;       // keys per route workgroup
+  uint64_t h_words;   // P * n_parts
+  uint64_t bytes;     // workspace bytes: [H][part totals][part bases (n_parts + 1)]
 };
 
-__host__ __device__ inline PartWindow whole_filter_window()
+inline RouteGeom route_geom(uint64_t n_keys, uint32_t n_parts)
 {
-  return PartWindow{0u, 1u, 0u, 0u, nullptr};
+  RouteGeom g;
+  g.n_parts = n_parts;
+  const uint64_t p = (n_keys + 4095) / 4096;
+  g.P = (uint32_t)(p < 1 ? 1 : (p > kRouteMaxWgs ? kRouteMaxWgs : p));
+  g.per = (uint32_t)((n_keys + g.P - 1) / g.P);
+  g.h_words = (uint64_t)g.P * n_parts;
+  g.bytes = (4 * (g.h_words + 2ull * n_parts + 1) + 255) & ~255ull;
+  return g;
 }
 
-// local tile of a key, or ~0 outside the window (below tile0 the subtraction wraps)
-template <class KV>
-__device__ inline uint32_t part_tile(const KV& kv, uint32_t nb, const PartWindow& pw,
-                                     uint32_t n_tiles)
-{
-  const uint32_t t = (bloom_tile_of(kv, nb) - pw.tile0) / pw.div;
-  return t < n_tiles ? t : ~0u;
-}
-
-// PASS 0: histogram; PASS 1: scatter.  Both walk the same key range in the same way.  KB = 24:
-// 24-byte keys, the histogram only (tkv_amq_bloom_route_records_ex's count pass)
+// PASS 0: histogram of the parts; PASS 1: the keys themselves to their slots (16-byte keys;
+// nothing when the filter's k < min_k: the monolithic build routes records up to k = 8).
+// Both walk the same key ranges in the same way.
 template <int PASS, uint32_t NT, int KB = 16>
-__global__ __launch_bounds__(NT) void bloom_part_keys(const uint4* __restrict__ keys,
-                                                       const tkv_amq_segment* __restrict__ segs,
-                                                       uint32_t* __restrict__ ws, uint32_t n_tiles,
-                                                       uint32_t per, uint64_t part_off,
-                                                       uint32_t n_cap, PartWindow pw)
+__global__ __launch_bounds__(NT) void route_keys(const uint8_t* __restrict__ keys,
+                                                 const tkv_amq_segment* __restrict__ segs,
+                                                 uint32_t* __restrict__ ws, uint32_t n_parts,
+                                                 uint32_t per, uint32_t n, uint32_t q,
+                                                 uint4* __restrict__ out, uint32_t min_k)
 {
-  extern __shared__ uint32_t s_tile[];
+  extern __shared__ uint32_t s_part[];
   const tkv_amq_segment sg = segs[0];
-  const uint32_t tid = threadIdx.x, w = blockIdx.x;
-  uint32_t* H = ws + (uint64_t)w * n_tiles;
-  const uint32_t* base = ws + (uint64_t)gridDim.x * n_tiles + n_tiles;
-  for (uint32_t t = tid; t < n_tiles; t += NT) s_tile[t] = PASS == 0 ? 0u : base[t] + H[t];
+  if (sg.hash_count < min_k) return;
+  const uint32_t tid = threadIdx.x, w = blockIdx.x, nb = sg.n_blocks;
+  uint32_t* H = ws + (uint64_t)w * n_parts;
+  const uint32_t* base = ws + (uint64_t)gridDim.x * n_parts + n_parts;
+  for (uint32_t t = tid; t < n_parts; t += NT) s_part[t] = PASS == 0 ? 0u : base[t] + H[t];
   __syncthreads();
-  // n_cap: keys the caller passed (the partition buffer holds that many)
-  const uint32_t n = pw.local ? n_cap : min(sg.n_keys, n_cap), nb = sg.n_blocks;
   const uint32_t b = min(n, w * per), e = min(n, b + per);
   static_assert(KB == 16 || (KB == 24 && PASS == 0), "24-byte keys: the count pass only");
-  const uint8_t* kp = reinterpret_cast<const uint8_t*>(keys) + (uint64_t)KB * (pw.local ? 0 : sg.key_begin);
-  uint4* part = pw.out ? pw.out : reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(ws) + part_off);
   constexpr int U = 4;
   for (uint32_t i0 = b; i0 < e; i0 += NT * U) {
-    decltype(load_rec_key<KB>(kp, 0)) kv[U];
+    decltype(load_rec_key<KB>(keys, 0)) kv[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint32_t i = i0 + u * NT + tid;
-      if (i < e) kv[u] = load_rec_key<KB>(kp, i);
+      if (i < e) kv[u] = load_rec_key<KB>(keys, i);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint32_t i = i0 + u * NT + tid;
       if (i < e) {
-        const uint32_t t = part_tile(kv[u], nb, pw, n_tiles);
-        if (t == ~0u) continue;
+        const uint32_t p = bloom_tile_of(kv[u], nb) / q;
+        if (p >= n_parts) continue;
         if constexpr (PASS == 0) {
-          atomicAdd(s_tile + t, 1u);
+          atomicAdd(s_part + p, 1u);
         } else if constexpr (KB == 16) {
-          const uint32_t slot = atomicAdd(s_tile + t, 1u);
-          part[slot] = kv[u];
+          out[atomicAdd(s_part + p, 1u)] = kv[u];
         }
       }
     }
   }
   if constexpr (PASS == 0) {
     __syncthreads();
-    for (uint32_t t = tid; t < n_tiles; t += NT) H[t] = s_tile[t];
+    for (uint32_t t = tid; t < n_parts; t += NT) H[t] = s_part[t];
   }
 }
 
@@ -1122,19 +1209,19 @@ __device__ inline uint32_t block_exclusive_scan256(uint32_t v, uint32_t* s, uint
   return r;
 }
 
-// One workgroup per tile: H[w][t] <- sum of H[w'][t] over w' < w; totals[t] <- column sum.
-__global__ __launch_bounds__(256) void bloom_part_scan_cols(uint32_t* __restrict__ ws, uint32_t P,
-                                                            uint32_t n_tiles)
+// One workgroup per part: H[w][p] <- sum of H[w'][p] over w' < w; totals[p] <- column sum.
+__global__ __launch_bounds__(256) void route_scan_cols(uint32_t* __restrict__ ws, uint32_t P,
+                                                       uint32_t n_parts)
 {
   __shared__ uint32_t s[256];
   const uint32_t t = blockIdx.x, tid = threadIdx.x;
-  constexpr uint32_t R = kBloomPartMaxWgs / 256;  // rows per thread
+  constexpr uint32_t R = kRouteMaxWgs / 256;  // rows per thread
   uint32_t v[R];
   uint32_t sum = 0;
 #pragma unroll
   for (uint32_t r = 0; r < R; ++r) {
     const uint32_t w = tid * R + r;
-    v[r] = w < P ? ws[(uint64_t)w * n_tiles + t] : 0u;
+    v[r] = w < P ? ws[(uint64_t)w * n_parts + t] : 0u;
     sum += v[r];
   }
   uint32_t total;
@@ -1142,22 +1229,22 @@ __global__ __launch_bounds__(256) void bloom_part_scan_cols(uint32_t* __restrict
 #pragma unroll
   for (uint32_t r = 0; r < R; ++r) {
     const uint32_t w = tid * R + r;
-    if (w < P) ws[(uint64_t)w * n_tiles + t] = run;
+    if (w < P) ws[(uint64_t)w * n_parts + t] = run;
     run += v[r];
   }
-  if (tid == 0) ws[(uint64_t)P * n_tiles + t] = total;
+  if (tid == 0) ws[(uint64_t)P * n_parts + t] = total;
 }
 
-// One workgroup: bases[t] = sum of totals[t'] over t' < t, bases[n_tiles] = key count.
-__global__ __launch_bounds__(256) void bloom_part_scan_tiles(uint32_t* __restrict__ ws, uint32_t P,
-                                                             uint32_t n_tiles)
+// One workgroup: bases[p] = sum of totals[p'] over p' < p, bases[n_parts] = key count.
+__global__ __launch_bounds__(256) void route_scan_parts(uint32_t* __restrict__ ws, uint32_t P,
+                                                        uint32_t n_parts)
 {
   __shared__ uint32_t s[256];
-  const uint32_t* tot = ws + (uint64_t)P * n_tiles;
-  uint32_t* base = ws + (uint64_t)P * n_tiles + n_tiles;
+  const uint32_t* tot = ws + (uint64_t)P * n_parts;
+  uint32_t* base = ws + (uint64_t)P * n_parts + n_parts;
   const uint32_t tid = threadIdx.x;
-  const uint32_t per = (n_tiles + 255) / 256;  // consecutive tiles per thread
-  const uint32_t t0 = min(n_tiles, tid * per), t1 = min(n_tiles, t0 + per);
+  const uint32_t per = (n_parts + 255) / 256;  // consecutive parts per thread
+  const uint32_t t0 = min(n_parts, tid * per), t1 = min(n_parts, t0 + per);
   uint32_t sum = 0;
   for (uint32_t t = t0; t < t1; ++t) sum += tot[t];
   uint32_t total;
@@ -1166,221 +1253,18 @@ __global__ __launch_bounds__(256) void bloom_part_scan_tiles(uint32_t* __restric
     base[t] = run;
     run += tot[t];
   }
-  if (tid == 0) base[n_tiles] = total;
+  if (tid == 0) base[n_parts] = total;
 }
 
-// One workgroup per tile of the monolithic filter (segment 0).
-template <uint32_t NT>
-__global__ __launch_bounds__(NT) void bloom_tile_build(
-    const tkv_amq_segment* __restrict__ segs, const uint32_t* __restrict__ ws, uint32_t P,
-    uint32_t n_tiles, uint64_t part_off, uint8_t* __restrict__ out, PartWindow pw)
-{
-  extern __shared__ uint32_t s_bits[];
-  const tkv_amq_segment sg = segs[0];
-  const uint32_t t = blockIdx.x, tid = threadIdx.x;
-  const uint32_t nb = sg.n_blocks, k = sg.hash_count;
-  const uint32_t first = (pw.tile0 + t) * kBloomTileBlocks;
-  const uint32_t tb = min(kBloomTileBlocks, nb - first);
-  for (uint32_t w = tid; w < tb * 16; w += NT) s_bits[w] = 0;
-  __syncthreads();
-  const uint32_t* base = ws + (uint64_t)P * n_tiles + n_tiles;
-  const uint32_t kb = base[t], ke = base[t + 1];
-  const uint4* kp = reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(ws) + part_off) + kb;
-  if (k == 7) bloom_keys16_lds<7, NT>(kp, ke - kb, nb, k, s_bits, first);
-  else if (k == 8) bloom_keys16_lds<8, NT>(kp, ke - kb, nb, k, s_bits, first);
-  else bloom_keys16_lds<0, NT>(kp, ke - kb, nb, k, s_bits, first);
-  __syncthreads();
-  uint8_t* payload = out + sg.out_offset;
-  const bool hdr = t == 0 && (pw.tile0 == 0 || pw.hdr);
-  if (hdr && tid < 4) write_bloom_header(payload, sg, tid);
-  else if (hdr && tid < 8) write_page_header(out, sg, kLayoutBloom, tid - 4);
-  uint4* dst = reinterpret_cast<uint4*>(payload + kBloomHeader + 64ull * first);
-  const uint4* src = reinterpret_cast<const uint4*>(s_bits);
-  for (uint32_t q = tid; q < tb * 4; q += NT) dst[q] = src[q];
-}
-
-// ---------------------------------------------------------------------------------------
-// Monolithic Bloom, hash-once record path (filters of <= kRecMaxTiles tiles).  The k hashes
-// of a key are computed once, where the key is read, and what a tile needs of them travels
-// instead of the key:
-//   bloom_rec_partition  one 1024-thread workgroup per CU over a contiguous key range, in
-//                        batches: every key is hashed into a 12-byte bit record (block in
-//                        tile, k <= 8 bit indices, tile id); the batch is counting-sorted by
-//                        tile in LDS and each tile's run is appended to this workgroup's
-//                        region of that tile.  No count pass, no global atomics: regions
-//                        have a fixed capacity (mean + 6 sigma of a uniform hash), and
-//                        records beyond it go to the workgroup's overflow list.
-//   bloom_rec_tile       one workgroup per tile: every workgroup's region of the tile
-//                        through ds_or into the 64 KiB LDS image, then 16-byte stores.
-//   bloom_rec_overflow   the overflow lists (empty unless the keys are not spread by the
-//                        hash, e.g. duplicates) with device-scope atomicOr into the filter.
-// With k > 8 the records are the 16-byte keys themselves (batches of 4096) and the tile
-// kernel hashes them.  The bits set do not depend on which kernel or workgroup sets them,
-// so the filter is byte-identical to the leaf kernel's and the oracle's.
-// Record (k <= 8): w0 = blk | b0 << 10 | b1 << 19 | tile[0:3] << 28,
-//                  w1 = b2 | b3 << 9 | b4 << 18 | tile[4:8] << 27,
-//                  w2 = b5 | b6 << 9 | b7 << 18 | tile[9:13] << 27   (b_j = b_0 for j >= k)
-// ---------------------------------------------------------------------------------------
-constexpr uint32_t kRecThreads = 1024;
-constexpr uint32_t kRecBatchBits = 8192;  // keys per batch, 12-byte records (3 LDS planes)
-constexpr uint32_t kRecBatchKeys = 4096;  // keys per batch, 16-byte keys (4 planes + tile ids)
-constexpr uint32_t kRecMaxTiles = 3584;
-constexpr uint32_t kRecMaxWgs = 256;
-constexpr uint32_t kRecPlaneBytes = 12 * kRecBatchBits;  // = 20 * kRecBatchKeys + 16 KiB
-constexpr uint32_t kRecTileThreads = 1024;
-static_assert(20 * kRecBatchKeys <= kRecPlaneBytes, "LDS planes");
-
-__host__ __device__ constexpr inline uint32_t bloom_rec_lds_bytes(uint32_t n_tiles)
-{
-  return kRecPlaneBytes + 16 * n_tiles + 4 * (kRecThreads / 64 + 1);
-}
-static_assert(kRecPlaneBytes + 16 * kRecMaxTiles + 4 * 17 <= 160 * 1024, "one workgroup per CU");
-
-struct BloomRecGeom {
-  uint32_t P;        // partition workgroups
-  uint32_t n_tiles;
-  uint32_t per;      // keys per partition workgroup
-  uint32_t cap;      // records per (tile, workgroup) region
-  uint64_t counts_off;   // u32 [n_tiles][P]: records in each region
-  uint64_t ovf_n_off;    // u32 [P]: records in each workgroup's overflow list
-  uint64_t regions_off;  // region (t, w) at regions_off + (t * P + w) * cap * 16
-  uint64_t ovf_off;      // workgroup w's overflow list at ovf_off + w * per * 16
-  uint64_t bytes;
-};
-
-// regions sized for 16-byte records (the device picks 12 or 16 by k; the host does not know k)
-inline BloomRecGeom bloom_rec_geom(uint64_t n_keys, uint64_t nb)
-{
-  BloomRecGeom g;
-  g.n_tiles = (uint32_t)((nb + kBloomTileBlocks - 1) / kBloomTileBlocks);
-  const uint64_t p = (n_keys + 32767) / 32768;
-  g.P = (uint32_t)(p < 1 ? 1 : (p > kRecMaxWgs ? kRecMaxWgs : p));
-  g.per = (uint32_t)((n_keys + g.P - 1) / g.P);
-  const double e = (double)g.per / g.n_tiles;
-  g.cap = ((uint32_t)(e + 6.0 * sqrt(e) + 16.0) + 7) & ~7u;
-  const uint64_t regions = (uint64_t)g.n_tiles * g.P;
-  g.counts_off = 256;
-  g.ovf_n_off = g.counts_off + 4 * regions;
-  g.regions_off = (g.ovf_n_off + 4ull * g.P + 255) & ~255ull;
-  g.ovf_off = g.regions_off + 16ull * regions * g.cap;
-  g.bytes = g.ovf_off + 16ull * g.P * g.per;
-  return g;
-}
-
-
-// Per-batch tile bookkeeping of bloom_rec_partition (n <= 4 * kRecThreads tiles; thread i owns
-// tiles 4i..4i+3): cursor[t] += prev[t] (the previous batch's run lengths), prev[t] = 0 (the
-// next batch's histogram), start[t] = exclusive scan of cur[t].  Returns the batch's record
-// count.  Two LDS barriers inside.
-__device__ inline uint32_t rec_scan(const uint32_t* cur, uint32_t* prev, uint32_t* start,
-                                    uint32_t* cursor, uint32_t n, uint32_t* wsum)
-{
-  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-  uint32_t x[4], s = 0;
-#pragma unroll
-  for (uint32_t j = 0; j < 4; ++j) {
-    const uint32_t i = 4 * tid + j;
-    x[j] = 0;
-    if (i < n) {
-      x[j] = cur[i];
-      cursor[i] += prev[i];
-      prev[i] = 0;
-    }
-    s += x[j];
-  }
-  uint32_t inc = s;  // inclusive scan over the wave
-#pragma unroll
-  for (uint32_t d = 1; d < 64; d <<= 1) {
-    const uint32_t y = __shfl_up(inc, d, 64);
-    if (lane >= d) inc += y;
-  }
-  if (lane == 63) wsum[wave] = inc;
-  lds_barrier();
-  uint32_t before = 0, total = 0;
-#pragma unroll
-  for (uint32_t q = 0; q < kRecThreads / 64; ++q) {
-    const uint32_t t = wsum[q];
-    before += q < wave ? t : 0u;
-    total += t;
-  }
-  uint32_t run = before + inc - s;
-#pragma unroll
-  for (uint32_t j = 0; j < 4; ++j) {
-    const uint32_t i = 4 * tid + j;
-    if (i < n) start[i] = run;
-    run += x[j];
-  }
-  lds_barrier();  // start / cursor complete; wsum is reused by the next call
-  return total;
-}
-
-__device__ inline void rec_pack(uint32_t blk, uint32_t tile, const uint32_t (&b)[8], uint32_t& w0,
-                                uint32_t& w1, uint32_t& w2)
-{
-  w0 = blk | b[0] << 10 | b[1] << 19 | (tile & 15u) << 28;
-  w1 = b[2] | b[3] << 9 | b[4] << 18 | ((tile >> 4) & 31u) << 27;
-  w2 = b[5] | b[6] << 9 | b[7] << 18 | ((tile >> 9) & 31u) << 27;
-}
-
-__device__ inline uint32_t rec_tile(uint32_t w0, uint32_t w1, uint32_t w2)
-{
-  return (w0 >> 28) | ((w1 >> 27) << 4) | ((w2 >> 27) << 9);
-}
-
-// a 16-byte key's block in the filter and its k <= 8 bit indices (b_j = b_0 for j >= k)
-template <int K>
-__device__ inline uint32_t rec_hash_bits(const uint4& kv, uint32_t nb, uint32_t k, uint32_t (&b)[8])
-{
-  const Xxh16 x((uint64_t)kv.x | ((uint64_t)kv.y << 32), (uint64_t)kv.z | ((uint64_t)kv.w << 32));
-  const uint64_t h0 = x.finish(c_bloom.rhinit16[0]);
-  b[0] = (uint32_t)h0 & 511u;
-#pragma unroll
-  for (uint32_t j = 1; j < 8; ++j) {
-    if (K != 0 ? j < (uint32_t)K : j < k) b[j] = x.finish_lo9(c_bloom.rhinit16[j]) & 511u;
-    else b[j] = b[0];
-  }
-  return (uint32_t)__umul64hi(h0, (uint64_t)nb);
-}
-
-// a 24-byte key's block and its bit indices (k > 8: the first eight; bloom_rec_overflow sets
-// the others)
-template <int K>
-__device__ inline uint32_t rec_hash_bits(const Key24& kv, uint32_t nb, uint32_t k, uint32_t (&b)[8])
-{
-  const XxhFixed<24> x(kv.w);
-  const uint64_t h0 = x.finish(xxh_fixed_rc<24>(c_bloom.seed[0]));
-  b[0] = (uint32_t)h0 & 511u;
-#pragma unroll
-  for (uint32_t j = 1; j < 8; ++j) {
-    if (K != 0 ? j < (uint32_t)K : j < k) b[j] = x.finish_lo9(xxh_fixed_rc<24>(c_bloom.seed[j])) & 511u;
-    else b[j] = b[0];
-  }
-  return (uint32_t)__umul64hi(h0, (uint64_t)nb);
-}
-
-// one key of the record path: local tile (~0 outside the window), block in tile, bit record
-template <int K, class KV>
-__device__ inline uint32_t rec_hash(const KV& kv, uint32_t nb, uint32_t k, uint32_t tile0,
-                                    uint32_t n_tiles, uint32_t& w0, uint32_t& w1, uint32_t& w2)
-{
-  uint32_t b[8];
-  const uint32_t blk = rec_hash_bits<K>(kv, nb, k, b);
-  const uint32_t t = blk / kBloomTileBlocks - tile0;  // wraps below the window
-  rec_pack(blk & (kBloomTileBlocks - 1), t, b, w0, w1, w2);
-  return t < n_tiles ? t : ~0u;
-}
-
-// tkv_amq_bloom_route_records' scatter pass: the same key ranges and slots as
-// bloom_part_keys<1> (after the same count pass), but each key leaves as its 12-byte bit record
-// (rec_pack) with its tile relative to its owner's first tile (owner = tile / q): k <= 8 only.
+// the route's record scatter pass (k <= 8): the same key ranges and slots as route_keys<1>
+// (after the same count pass), each key leaving as its 12-byte bit record with its tile
+// relative to its part's first tile
 template <uint32_t NT, int K, int KB>
-__device__ void bloom_route_recs_body(const uint8_t* __restrict__ keys, const tkv_amq_segment& sg,
-                                      uint32_t* __restrict__ ws, uint32_t n_parts, uint32_t per,
-                                      uint32_t n_cap, uint32_t q, uint32_t* __restrict__ out,
-                                      uint32_t* s_tile)
+__device__ void route_recs_body(const uint8_t* __restrict__ keys, const tkv_amq_segment& sg,
+                                uint32_t n_parts, uint32_t per, uint32_t n, uint32_t q,
+                                uint32_t* __restrict__ out, uint32_t* s_part)
 {
   const uint32_t tid = threadIdx.x, w = blockIdx.x, nb = sg.n_blocks, k = sg.hash_count;
-  const uint32_t n = n_cap;
   const uint32_t b = min(n, w * per), e = min(n, b + per);
   constexpr int U = 4;
   for (uint32_t i0 = b; i0 < e; i0 += NT * U) {
@@ -1395,13 +1279,12 @@ __device__ void bloom_route_recs_body(const uint8_t* __restrict__ keys, const tk
       const uint32_t i = i0 + u * NT + tid;
       if (i >= e) continue;
       uint32_t bits[8], r0, r1, r2;
-      // global tile of the key, then its owner and its tile within the owner's range
       const uint32_t blk = rec_hash_bits<K>(kv[u], nb, k, bits);
-      const uint32_t tg = blk / kBloomTileBlocks;
-      const uint32_t owner = tg / q;
-      if (owner >= n_parts) continue;
-      rec_pack(blk & (kBloomTileBlocks - 1), tg - owner * q, bits, r0, r1, r2);
-      const uint32_t slot = atomicAdd(s_tile + owner, 1u);
+      const uint32_t tg = blk >> kTileShift;
+      const uint32_t p = tg / q;
+      if (p >= n_parts) continue;
+      rec_pack(blk & (kTileBlocks - 1), tg - p * q, bits, r0, r1, r2);
+      const uint32_t slot = atomicAdd(s_part + p, 1u);
       uint3 v;
       v.x = r0;
       v.y = r1;
@@ -1412,226 +1295,247 @@ __device__ void bloom_route_recs_body(const uint8_t* __restrict__ keys, const tk
 }
 
 template <uint32_t NT, int KB>
-__global__ __launch_bounds__(NT) void bloom_route_recs(const uint8_t* __restrict__ keys,
-                                                        const tkv_amq_segment* __restrict__ segs,
-                                                        uint32_t* __restrict__ ws, uint32_t n_parts,
-                                                        uint32_t per, uint32_t n_cap, uint32_t q,
-                                                        uint32_t* __restrict__ out)
+__global__ __launch_bounds__(NT) void route_recs(const uint8_t* __restrict__ keys,
+                                                 const tkv_amq_segment* __restrict__ segs,
+                                                 uint32_t* __restrict__ ws, uint32_t n_parts,
+                                                 uint32_t per, uint32_t n, uint32_t q,
+                                                 uint32_t* __restrict__ out)
 {
-  extern __shared__ uint32_t s_tile[];
+  extern __shared__ uint32_t s_part[];
   const tkv_amq_segment sg = segs[0];
   const uint32_t tid = threadIdx.x, w = blockIdx.x;
   const uint32_t* H = ws + (uint64_t)w * n_parts;
   const uint32_t* base = ws + (uint64_t)gridDim.x * n_parts + n_parts;
-  for (uint32_t t = tid; t < n_parts; t += NT) s_tile[t] = base[t] + H[t];
+  for (uint32_t t = tid; t < n_parts; t += NT) s_part[t] = base[t] + H[t];
   __syncthreads();
   const uint32_t k = sg.hash_count;
   if (k == 0 || k > 8) return;  // (the ABI refuses k > 8: a record holds 8 bit indices)
-  if (k == 7) bloom_route_recs_body<NT, 7, KB>(keys, sg, ws, n_parts, per, n_cap, q, out, s_tile);
-  else if (k == 8) bloom_route_recs_body<NT, 8, KB>(keys, sg, ws, n_parts, per, n_cap, q, out, s_tile);
-  else bloom_route_recs_body<NT, 0, KB>(keys, sg, ws, n_parts, per, n_cap, q, out, s_tile);
+  if (k == 7) route_recs_body<NT, 7, KB>(keys, sg, n_parts, per, n, q, out, s_part);
+  else if (k == 8) route_recs_body<NT, 8, KB>(keys, sg, n_parts, per, n, q, out, s_part);
+  else route_recs_body<NT, 0, KB>(keys, sg, n_parts, per, n, q, out, s_part);
 }
 
-
-// 16-byte keys (k > 8): the record is the key; only its tile is computed here
-__device__ inline uint32_t rec_key_tile(const uint4& kv, uint32_t nb, uint32_t tile0, uint32_t n_tiles)
-{
-  const uint32_t t = bloom_tile_of(kv, nb) - tile0;
-  return t < n_tiles ? t : ~0u;
-}
-
-struct RecArgs {
-  const uint4* keys;  // the window's keys [0, n) (from_seg: the segment's keys, n capped by it)
-  uint32_t n;
-  uint32_t tile0;     // global tile of local tile 0
+// ---------------------------------------------------------------------------------------
+// partition, tile build, overflow
+// ---------------------------------------------------------------------------------------
+struct PartArgs {
+  const uint8_t* src;  // keys (16 or 24 bytes), routed 12-byte records, or routed 16-byte keys
+  uint32_t n;          // items [0, n) of src (from_seg: the segment's keys, n capped by it)
+  uint32_t tile0;      // global tile of local tile 0
   uint32_t from_seg;
+  uint32_t kb;         // key bytes of hashed keys, 16 or 24 (24 with k > 8: the first eight bits
+                       // in the records, the others set by bloom_overflow from the keys)
+  const uint32_t* cnt; // routed parts built on the device: items = cnt[part] at the offset
+  uint32_t part;       // sum(cnt[0..part)) of src (n and from_seg unused)
   uint8_t* ws;
-  BloomRecGeom g;
-  const uint32_t* recs;  // instead of keys: 12-byte bit records with local tiles (hash-range
-                         // shards, tkv_amq_bloom_route_records), n of them
-  uint32_t kb;           // key bytes, 16 or 24 (24: bit records for any k, the first eight
-                         // bits in the records, the others set by bloom_rec_overflow)
+  PartGeom g;
 };
 
-// batches of B keys, U = B / kRecThreads per thread; RAW: 16-byte keys instead of bit records.
-// Per batch: hash (the next batch's keys are then loaded, in flight until its hash), LDS
-// barrier, scan (two), place into the planes, LDS barrier, write out.  The histogram is
-// double-buffered, so no barrier is needed after the write-out: the next batch's hash touches
-// only the other histogram, and its scan comes after a barrier.
-// one 12-byte record of a.recs (records input: no hashing, the tile is in the record)
-__device__ inline uint4 load_rec12(const uint32_t* recs, uint32_t i)
+__device__ inline uint4 load_rec12(const uint8_t* recs, uint32_t i)
 {
   const uint3 r = reinterpret_cast<const uint3*>(recs)[i];
   return make_uint4(r.x, r.y, r.z, 0u);
 }
 
-template <int K, bool RAW, bool RECIN = false, int KB = 16>
-__device__ void bloom_rec_partition_body(const tkv_amq_segment& sg, const RecArgs& a, uint32_t* lds)
+// items [b, e) of the build's source and its base pointer (SRC: item bytes)
+__device__ inline void part_items(const tkv_amq_segment& sg, const PartArgs& a, uint32_t item_bytes,
+                                  const uint8_t*& src, uint32_t& n)
 {
-  static_assert(!(RAW && RECIN), "records carry k <= 8 bit indices");
-  static_assert(KB == 16 || (!RAW && !RECIN), "24-byte keys leave as bit records");
-  constexpr uint32_t B = RAW ? kRecBatchKeys : kRecBatchBits;
-  constexpr uint32_t U = B / kRecThreads;
-  constexpr uint32_t RB = RAW ? 16 : 12;  // record bytes
+  if (a.cnt) {
+    uint64_t off = 0;
+    for (uint32_t p = 0; p < a.part; ++p) off += a.cnt[p];
+    n = a.cnt[a.part];
+    src = a.src + (uint64_t)item_bytes * off;
+  } else {
+    n = a.from_seg ? min(a.n, sg.n_keys) : a.n;
+    src = a.src + (uint64_t)item_bytes * (a.from_seg ? sg.key_begin : 0);
+  }
+}
+
+// Per batch: hash U items per thread into records and ranks (the next batch's items are then
+// loaded, in flight until its hash), LDS barrier, the previous batch's run lengths added to the
+// cursors (and its histogram cleared for the batch after), LDS barrier, every record stored to
+// its slot.  Every lane issues the same loads and stores per batch (clamped loads; lanes
+// without a record store to a sink in the workspace header), so the compiler's wait for a
+// load never also waits for the stores.
+template <int K, int SRC>
+__device__ void part_body(const tkv_amq_segment& sg, const PartArgs& a, uint32_t* lds)
+{
+  constexpr bool RAW = SRC == kSrcRaw16;
+  // 16-byte records hold four words per item: half the items per batch
+  constexpr uint32_t RB = RAW ? 16 : 12, U = RAW ? kPartU / 2 : kPartU, NT = kPartThreads, B = U * NT;
+  constexpr uint32_t IB = SRC == kSrcKey24 ? 24 : (SRC == kSrcRec12 ? 12 : 16);  // item bytes
   const uint32_t tid = threadIdx.x, w = blockIdx.x, P = a.g.P, T = a.g.n_tiles, cap = a.g.cap;
   const uint32_t nb = sg.n_blocks, k = sg.hash_count;
-  uint32_t* pl[5];
-#pragma unroll
-  for (uint32_t j = 0; j < 5; ++j) pl[j] = lds + j * B;  // planes (RAW: 4 key words + tile)
-  uint32_t* hist2 = lds + kRecPlaneBytes / 4;  // two histograms
-  uint32_t* start = hist2 + 2 * T;
-  uint32_t* cursor = start + T;
-  uint32_t* wsum = cursor + T;  // 16 wave sums + the overflow count
-  uint32_t* ovf_n = wsum + kRecThreads / 64;
-  for (uint32_t t = tid; t < T; t += kRecThreads) {
-    hist2[t] = 0;
-    hist2[T + t] = 0;
-    cursor[t] = 0;
+  const uint32_t HW = (T + 1) >> 1;
+  uint32_t* H0 = lds;
+  uint32_t* H1 = lds + HW;
+  uint32_t* cursor = lds + 2 * HW;
+  uint32_t* ovf_n = cursor + 2 * HW;
+  for (uint32_t i = tid; i < 2 * HW; i += NT) {
+    lds[i] = 0;
+    cursor[i] = 0;
   }
   if (tid == 0) *ovf_n = 0;
   __syncthreads();
-  const uint32_t n = a.from_seg ? min(a.n, sg.n_keys) : a.n;
-  const uint8_t* keys = reinterpret_cast<const uint8_t*>(a.keys) + (uint64_t)KB * (a.from_seg ? sg.key_begin : 0);
-  const uint32_t kb = min(n, w * a.g.per), ke = min(n, kb + a.g.per);
+  const uint8_t* src;
+  uint32_t n;
+  part_items(sg, a, IB, src, n);
+  const uint32_t per = a.cnt ? (n + P - 1) / P : a.g.per;
+  const uint32_t kb = min(n, w * per), ke = min(n, kb + per);
   uint8_t* regions = a.ws + a.g.regions_off;
   uint8_t* ovf = a.ws + a.g.ovf_off + (uint64_t)w * a.g.per * 16;
-  // Loads are clamped, not skipped, and every lane stores once per record slot (lanes with
-  // nothing to write hit a sink in the workspace header): a fixed count of memory operations
-  // per batch, so the compiler's wait for a key load never also waits for the stores.
   uint8_t* const sink = a.ws;
-  const uint32_t last_key = ke > 0 ? ke - 1 : 0;
-  using KV = typename std::conditional<KB == 24, Key24, uint4>::type;
-  KV kv[U];
-  auto load_in = [&](uint32_t i) -> KV {
-    if constexpr (RECIN) return load_rec12(a.recs, i);
-    else return load_rec_key<KB>(keys, i);
+  const uint32_t last_item = ke > 0 ? ke - 1 : 0;
+  using In = typename std::conditional<SRC == kSrcKey24, Key24, uint4>::type;
+  auto load_in = [&](uint32_t i) -> In {
+    if constexpr (SRC == kSrcRec12) return load_rec12(src, i);
+    else if constexpr (SRC == kSrcKey24) return load_key24(src, i);
+    else return load_nt16(src + 16ull * i);
   };
+  In in[U];
 #pragma unroll
-  for (uint32_t u = 0; u < U; ++u) kv[u] = load_in(min(kb + u * kRecThreads + tid, last_key));
-  uint32_t parity = 0;
-  for (uint32_t b0 = kb; b0 < ke; b0 += B, parity ^= 1) {
-    uint32_t* hist = hist2 + parity * T;
-    uint32_t* prev = hist2 + (parity ^ 1) * T;
-    // per key: its record and its rank in the tile's run (~0: no record); the tile of a bit
-    // record is in the record (fewer live registers while the next batch loads)
-    uint32_t tl[RAW ? U : 1], rk[U], r0[U], r1[U], r2[U], r3[RAW ? U : 1];
+  for (uint32_t u = 0; u < U; ++u) in[u] = load_in(min(kb + u * NT + tid, last_item));
+  uint32_t par = 0;
+  for (uint32_t b0 = kb; b0 < ke; b0 += B, par ^= 1) {
+    uint32_t* hist = par ? H1 : H0;
+    uint32_t* prev = par ? H0 : H1;
+    // per item: its record and (tile << 16 | rank in the tile's run), ~0: no record
+    uint32_t r0[U], r1[U], r2[U], r3[RAW ? U : 1], tr[U];
 #pragma unroll
     for (uint32_t u = 0; u < U; ++u) {
-      const uint32_t i = b0 + u * kRecThreads + tid;
-      uint32_t t;
-      if constexpr (RAW) {
-        t = tl[u] = i < ke ? rec_key_tile(kv[u], nb, a.tile0, T) : ~0u;
-        r0[u] = kv[u].x;
-        r1[u] = kv[u].y;
-        r2[u] = kv[u].z;
-        r3[u] = kv[u].w;
-      } else if constexpr (RECIN) {
-        r0[u] = kv[u].x;
-        r1[u] = kv[u].y;
-        r2[u] = kv[u].z;
-        t = rec_tile(r0[u], r1[u], r2[u]);
-        t = t < T ? t : ~0u;
-      } else {
-        t = i < ke ? rec_hash<K>(kv[u], nb, k, a.tile0, T, r0[u], r1[u], r2[u]) : ~0u;
+      const uint32_t i = b0 + u * NT + tid;
+      // (under a branch: the hashes of the U items are not interleaved by the scheduler,
+      // whose register demand would then spill)
+      uint32_t t = ~0u;
+      if (i < ke) {
+        if constexpr (RAW) {
+          t = bloom_tile_of(in[u], nb) - a.tile0;  // wraps below the window
+          r0[u] = in[u].x;
+          r1[u] = in[u].y;
+          r2[u] = in[u].z;
+          r3[u] = in[u].w;
+        } else if constexpr (SRC == kSrcRec12) {
+          r0[u] = in[u].x;
+          r1[u] = in[u].y;
+          r2[u] = in[u].z;
+          t = rec_tile(r0[u], r1[u], r2[u]);
+        } else {
+          uint32_t bits[8];
+          const uint32_t blk = rec_hash_bits<K>(in[u], nb, k, bits);
+          t = (blk >> kTileShift) - a.tile0;
+          rec_pack(blk & (kTileBlocks - 1), t, bits, r0[u], r1[u], r2[u]);
+        }
       }
-      if (i >= ke) t = ~0u;  // a clamped load past the range
-      rk[u] = t != ~0u ? atomicAdd(hist + t, 1u) : ~0u;
+      if (t >= T) {
+        tr[u] = ~0u;
+      } else {
+        const uint32_t sh = (t & 1u) << 4;
+        const uint32_t rank = (atomicAdd(hist + (t >> 1), 1u << sh) >> sh) & 0xffffu;
+        tr[u] = t << 16 | rank;
+      }
     }
 #pragma unroll
-    for (uint32_t u = 0; u < U; ++u)  // the next batch's keys
-      kv[u] = load_in(min(b0 + B + u * kRecThreads + tid, last_key));
+    for (uint32_t u = 0; u < U; ++u)  // the next batch's items
+      in[u] = load_in(min(b0 + B + u * NT + tid, last_item));
     lds_barrier();
-    const uint32_t total = rec_scan(hist, prev, start, cursor, T, wsum);
-#pragma unroll
-    for (uint32_t u = 0; u < U; ++u) {
-      if (rk[u] == ~0u) continue;
-      uint32_t t;
-      if constexpr (RAW) t = tl[u];
-      else t = rec_tile(r0[u], r1[u], r2[u]);
-      const uint32_t pos = start[t] + rk[u];
-      pl[0][pos] = r0[u];
-      pl[1][pos] = r1[u];
-      pl[2][pos] = r2[u];
-      if constexpr (RAW) {
-        pl[3][pos] = r3[u];
-        pl[4][pos] = tl[u];
+    // the previous batch's run lengths into the cursors; its histogram is the next batch's
+    for (uint32_t j = tid; j < HW; j += NT) {
+      const uint32_t x = prev[j];
+      if (x) {
+        cursor[2 * j] += x & 0xffffu;
+        cursor[2 * j + 1] += x >> 16;
+        prev[j] = 0;
       }
     }
     lds_barrier();
-    // each tile's run goes to the end of this workgroup's region of the tile
 #pragma unroll
     for (uint32_t u = 0; u < U; ++u) {
-      const uint32_t j0 = u * kRecThreads + tid;
-      const bool v = j0 < total;
-      const uint32_t j = v ? j0 : 0u;
-      const uint32_t x0 = pl[0][j], x1 = pl[1][j], x2 = pl[2][j];
-      uint32_t x3 = 0, t;
-      if constexpr (RAW) {
-        x3 = pl[3][j];
-        t = pl[4][j];
-      } else {
-        t = rec_tile(x0, x1, x2);
-      }
-      t = v ? t : 0u;
-      const uint32_t c = cursor[t] + (j - start[t]);
       uint8_t* dst = sink;
-      if (v) {
-        if (c < cap) dst = regions + ((uint64_t)t * P + w) * cap * 16 + (uint64_t)c * RB;
-        else dst = ovf + 16ull * atomicAdd(ovf_n, 1u);  // LDS atomic, this workgroup's list
+      bool of = false;
+      if (tr[u] != ~0u) {
+        const uint32_t t = tr[u] >> 16;
+        const uint32_t c = cursor[t] + (tr[u] & 0xffffu);
+        if (c < cap) {
+          dst = regions + ((uint64_t)t * P + w) * cap * a.g.rb + (uint64_t)c * RB;
+        } else {
+          dst = ovf + 16ull * atomicAdd(ovf_n, 1u);  // LDS atomic, this workgroup's list
+          of = true;
+        }
       }
-      uint32_t* d = reinterpret_cast<uint32_t*>(dst);
       if constexpr (RAW) {
-        *reinterpret_cast<uint4*>(d) = make_uint4(x0, x1, x2, x3);
+        *reinterpret_cast<uint4*>(dst) = make_uint4(r0[u], r1[u], r2[u], r3[u]);
+      } else if (of) {  // rare (a region full): the entry carries its tile
+        *reinterpret_cast<uint4*>(dst) = make_uint4(r0[u], r1[u], r2[u], tr[u] >> 16);
       } else {
-        d[0] = x0;
-        d[1] = x1;
-        d[2] = x2;
+        uint3 v;
+        v.x = r0[u];
+        v.y = r1[u];
+        v.z = r2[u];
+        *reinterpret_cast<uint3*>(dst) = v;
       }
     }
   }
   __syncthreads();
-  // the last batch's run lengths (its histogram is the one the loop's last scan read)
-  const uint32_t* last = hist2 + (parity ^ 1) * T;
+  // the last batch's run lengths (its histogram is the one the loop's last batch counted into)
+  const uint32_t* last = par ? H0 : H1;
   uint32_t* counts = reinterpret_cast<uint32_t*>(a.ws + a.g.counts_off);
-  for (uint32_t t = tid; t < T; t += kRecThreads)
-    counts[(uint64_t)t * P + w] = min(cursor[t] + last[t], cap);
+  for (uint32_t t = tid; t < T; t += NT)
+    counts[(uint64_t)t * P + w] = min(cursor[t] + ((last[t >> 1] >> ((t & 1u) << 4)) & 0xffffu), cap);
   if (tid == 0) reinterpret_cast<uint32_t*>(a.ws + a.g.ovf_n_off)[w] = *ovf_n;
 }
 
-__global__ __launch_bounds__(kRecThreads) void bloom_rec_partition(const tkv_amq_segment* __restrict__ segs,
-                                                                   RecArgs a)
+// 16-byte keys: bit records for k <= 8, the keys themselves above
+__global__ __launch_bounds__(kPartThreads) void bloom_part_keys16(const tkv_amq_segment* __restrict__ segs,
+                                                                  PartArgs a)
 {
-  extern __shared__ __attribute__((aligned(16))) uint32_t s_rec[];
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_part[];
   const tkv_amq_segment sg = segs[0];
   const uint32_t k = sg.hash_count;
   if (k == 0) return;
-  if (a.recs) {
-    if (k <= 8) bloom_rec_partition_body<0, false, true>(sg, a, s_rec);
-  } else if (k == 7) bloom_rec_partition_body<7, false>(sg, a, s_rec);
-  else if (k == 8) bloom_rec_partition_body<8, false>(sg, a, s_rec);
-  else if (k < 8) bloom_rec_partition_body<0, false>(sg, a, s_rec);
-  else bloom_rec_partition_body<0, true>(sg, a, s_rec);
+  if (k == 7) part_body<7, kSrcKey16>(sg, a, s_part);
+  else if (k == 8) part_body<8, kSrcKey16>(sg, a, s_part);
+  else if (k < 8) part_body<0, kSrcKey16>(sg, a, s_part);
+  else part_body<0, kSrcRaw16>(sg, a, s_part);
 }
 
 // 24-byte keys (a kernel of its own: their six key words per prefetched key would raise the
-// 16-byte kernel's register count)
-__global__ __launch_bounds__(kRecThreads) void bloom_rec_partition24(const tkv_amq_segment* __restrict__ segs,
-                                                                     RecArgs a)
+// 16-byte kernel's register count): always bit records (k > 8: the first eight bits)
+__global__ __launch_bounds__(kPartThreads) void bloom_part_keys24(const tkv_amq_segment* __restrict__ segs,
+                                                                  PartArgs a)
 {
-  extern __shared__ __attribute__((aligned(16))) uint32_t s_rec[];
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_part[];
   const tkv_amq_segment sg = segs[0];
   const uint32_t k = sg.hash_count;
   if (k == 0) return;
-  if (k == 7) bloom_rec_partition_body<7, false, false, 24>(sg, a, s_rec);
-  else if (k == 8) bloom_rec_partition_body<8, false, false, 24>(sg, a, s_rec);
-  else bloom_rec_partition_body<0, false, false, 24>(sg, a, s_rec);
+  if (k == 7) part_body<7, kSrcKey24>(sg, a, s_part);
+  else if (k == 8) part_body<8, kSrcKey24>(sg, a, s_part);
+  else part_body<0, kSrcKey24>(sg, a, s_part);
+}
+
+// routed items: 12-byte bit records for k <= 8, 16-byte keys above (tkv_amq_bloom_route)
+__global__ __launch_bounds__(kPartThreads) void bloom_part_routed(const tkv_amq_segment* __restrict__ segs,
+                                                                  PartArgs a)
+{
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_part[];
+  const tkv_amq_segment sg = segs[0];
+  const uint32_t k = sg.hash_count;
+  if (k == 0) return;
+  if (k <= 8) part_body<0, kSrcRec12>(sg, a, s_part);
+  else part_body<0, kSrcRaw16>(sg, a, s_part);
+}
+
+// the tile and overflow kernels' records are 16-byte keys when the partition had them
+__device__ inline bool part_raw(const tkv_amq_segment& sg, const PartArgs& a)
+{
+  return sg.hash_count > 8 && a.kb != 24;
 }
 
 template <int K>
 __device__ inline void rec_insert(uint32_t* img, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t k)
 {
-  uint32_t* blk = img + 16 * (w0 & (kBloomTileBlocks - 1));
-  const uint32_t b[8] = {w0 >> 10, w0 >> 19, w1, w1 >> 9, w1 >> 18, w2, w2 >> 9, w2 >> 18};
+  uint32_t* blk = img + 16 * (w0 & (kTileBlocks - 1));
+  const uint32_t b[8] = {w0 >> 11, w0 >> 20, w1, w1 >> 9, w1 >> 18, w2, w2 >> 9, w2 >> 18};
 #pragma unroll
   for (uint32_t j = 0; j < 8; ++j)
     if (K != 0 ? j < (uint32_t)K : j < k) lds_set_bit(blk, b[j]);
@@ -1642,24 +1546,24 @@ __device__ inline void rec_insert(uint32_t* img, uint32_t w0, uint32_t w1, uint3
 // loads the next piece before it inserts the current one (two register sets, unrolled by two:
 // no copy of an in-flight load), so every wave has one piece in flight at all times.
 template <int K, bool RAW>
-__device__ void bloom_rec_tile_body(const tkv_amq_segment& sg, const RecArgs& a, uint32_t* img,
-                                    uint32_t t)
+__device__ void tile_body(const tkv_amq_segment& sg, const PartArgs& a, uint32_t* img, uint32_t t)
 {
-  constexpr uint32_t RB = RAW ? 16 : 12, NW = kRecTileThreads / 64, V = 4, PIECE = 64 * V;
+  constexpr uint32_t RB = RAW ? 16 : 12, NW = kTileThreads / 64, V = 4, PIECE = 64 * V;
   // wave-uniform in an SGPR: region counts are scalar loads (lgkmcnt), so waiting for one
   // never waits for the record loads in flight
   const uint32_t lane = threadIdx.x & 63u, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t P = a.g.P, cap = a.g.cap;
-  const uint32_t k = sg.hash_count, nb = sg.n_blocks, first = (a.tile0 + t) * kBloomTileBlocks;
+  const uint32_t k = sg.hash_count, nb = sg.n_blocks, first = (a.tile0 + t) * kTileBlocks;
   const uint32_t* counts = reinterpret_cast<const uint32_t*>(a.ws + a.g.counts_off) + (uint64_t)t * P;
-  const uint8_t* regions = a.ws + a.g.regions_off + (uint64_t)t * P * cap * 16;
+  const uint64_t rstride = (uint64_t)cap * a.g.rb;  // bytes per region
+  const uint8_t* regions = a.ws + a.g.regions_off + (uint64_t)t * P * rstride;
   struct Piece {
     uint32_t w, i0, c;  // region, first record, records in the region
     uint32_t x[V][4];
   };
   auto count = [&](uint32_t w) { return w < P ? counts[w] : 0u; };
   auto load = [&](Piece& q) {
-    const uint8_t* reg = q.w < P ? regions + (uint64_t)q.w * cap * 16 : a.ws;
+    const uint8_t* reg = q.w < P ? regions + (uint64_t)q.w * rstride : a.ws;
     const uint32_t lastr = q.c ? q.c - 1 : 0u;
 #pragma unroll
     for (uint32_t v = 0; v < V; ++v) {
@@ -1668,7 +1572,8 @@ __device__ void bloom_rec_tile_body(const tkv_amq_segment& sg, const RecArgs& a,
         const uint4 e = *reinterpret_cast<const uint4*>(p);
         q.x[v][0] = e.x; q.x[v][1] = e.y; q.x[v][2] = e.z; q.x[v][3] = e.w;
       } else {
-        q.x[v][0] = p[0]; q.x[v][1] = p[1]; q.x[v][2] = p[2]; q.x[v][3] = 0;
+        const uint3 e = *reinterpret_cast<const uint3*>(p);
+        q.x[v][0] = e.x; q.x[v][1] = e.y; q.x[v][2] = e.z; q.x[v][3] = 0;
       }
     }
   };
@@ -1707,22 +1612,23 @@ __device__ void bloom_rec_tile_body(const tkv_amq_segment& sg, const RecArgs& a,
   }
 }
 
-__global__ __launch_bounds__(kRecTileThreads) void bloom_rec_tile(const tkv_amq_segment* __restrict__ segs,
-                                                                  RecArgs a, uint8_t* __restrict__ out,
-                                                                  uint32_t hdr_always)
+__global__ __launch_bounds__(kTileThreads) void bloom_tile(const tkv_amq_segment* __restrict__ segs,
+                                                           PartArgs a, uint8_t* __restrict__ out,
+                                                           uint32_t hdr_always)
 {
-  extern __shared__ uint32_t s_img[];
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_img[];
   const tkv_amq_segment sg = segs[0];
   const uint32_t t = blockIdx.x, tid = threadIdx.x, k = sg.hash_count;
   if (k == 0) return;
-  const uint32_t first = (a.tile0 + t) * kBloomTileBlocks;
-  const uint32_t tb = min(kBloomTileBlocks, sg.n_blocks - first);
-  for (uint32_t w = tid; w < tb * 16; w += kRecTileThreads) s_img[w] = 0;
+  const bool raw = part_raw(sg, a);
+  const uint32_t first = (a.tile0 + t) * kTileBlocks;
+  const uint32_t tb = min(kTileBlocks, sg.n_blocks - first);
+  for (uint32_t w = tid; w < tb * 16; w += kTileThreads) s_img[w] = 0;
   __syncthreads();
-  if (k == 7) bloom_rec_tile_body<7, false>(sg, a, s_img, t);
-  else if (k == 8) bloom_rec_tile_body<8, false>(sg, a, s_img, t);
-  else if (k < 8 || a.kb == 24) bloom_rec_tile_body<0, false>(sg, a, s_img, t);  // (24: 8 bits)
-  else bloom_rec_tile_body<0, true>(sg, a, s_img, t);
+  if (raw) tile_body<0, true>(sg, a, s_img, t);
+  else if (k == 7) tile_body<7, false>(sg, a, s_img, t);
+  else if (k == 8) tile_body<8, false>(sg, a, s_img, t);
+  else tile_body<0, false>(sg, a, s_img, t);  // (k > 8 with 24-byte keys: eight bits)
   __syncthreads();
   uint8_t* payload = out + sg.out_offset;
   const bool hdr = t == 0 && (a.tile0 == 0 || hdr_always);
@@ -1730,7 +1636,7 @@ __global__ __launch_bounds__(kRecTileThreads) void bloom_rec_tile(const tkv_amq_
   else if (hdr && tid < 8) write_page_header(out, sg, kLayoutBloom, tid - 4);
   uint4* dst = reinterpret_cast<uint4*>(payload + kBloomHeader + 64ull * first);
   const uint4* src = reinterpret_cast<const uint4*>(s_img);
-  for (uint32_t q = tid; q < tb * 4; q += kRecTileThreads) dst[q] = src[q];
+  for (uint32_t q = tid; q < tb * 4; q += kTileThreads) dst[q] = src[q];
 }
 
 // the filter header alone (a hash-range shard that owns no tile still returns a whole header)
@@ -1745,26 +1651,29 @@ __global__ __launch_bounds__(64) void bloom_header_only(const tkv_amq_segment* _
 }
 
 // one workgroup per partition workgroup's overflow list; device-scope atomics into the filter
-// (runs after bloom_rec_tile has stored every tile).  24-byte keys with k > 8 (bits_per_key
-// >= 13): the bits past the eighth of the workgroup's keys, also with atomics.
-__global__ __launch_bounds__(256) void bloom_rec_overflow(const tkv_amq_segment* __restrict__ segs,
-                                                          RecArgs a, uint8_t* __restrict__ out)
+// (runs after bloom_tile has stored every tile).  24-byte keys with k > 8 (bits_per_key >= 13):
+// the bits past the eighth of the workgroup's keys, also with atomics.
+__global__ __launch_bounds__(256) void bloom_overflow(const tkv_amq_segment* __restrict__ segs,
+                                                      PartArgs a, uint8_t* __restrict__ out)
 {
   const tkv_amq_segment sg = segs[0];
   const uint32_t k = sg.hash_count, w = blockIdx.x;
   if (k == 0) return;
+  const bool raw = part_raw(sg, a);
   const uint32_t n = reinterpret_cast<const uint32_t*>(a.ws + a.g.ovf_n_off)[w];
   const uint8_t* list = a.ws + a.g.ovf_off + (uint64_t)w * a.g.per * 16;
   uint32_t* words = reinterpret_cast<uint32_t*>(out + sg.out_offset + kBloomHeader);
-  if (a.kb == 24 && k > 8 && !a.recs) {
+  if (a.kb == 24 && k > 8 && !a.cnt) {
+    // (routed parts come from records, which the route refuses above eight bits)
     const uint32_t nk = a.from_seg ? min(a.n, sg.n_keys) : a.n;
-    const uint8_t* keys = reinterpret_cast<const uint8_t*>(a.keys) + 24ull * (a.from_seg ? sg.key_begin : 0);
-    const uint32_t kb = min(nk, w * a.g.per), ke = min(nk, kb + a.g.per);
+    const uint8_t* keys = a.src + 24ull * (a.from_seg ? sg.key_begin : 0);
+    const uint32_t per = a.g.per;
+    const uint32_t kb = min(nk, w * per), ke = min(nk, kb + per);
     for (uint32_t i = kb + threadIdx.x; i < ke; i += 256) {
       const XxhFixed<24> x(load_key24(keys, i).w);
       const uint64_t h0 = x.finish(xxh_fixed_rc<24>(c_bloom.seed[0]));
       const uint32_t blk = (uint32_t)__umul64hi(h0, (uint64_t)sg.n_blocks);
-      if (blk / kBloomTileBlocks - a.tile0 >= a.g.n_tiles) continue;  // (outside the window)
+      if ((blk >> kTileShift) - a.tile0 >= a.g.n_tiles) continue;  // (outside the window)
       uint32_t* bw = words + 16ull * blk;
       for (uint32_t j = 8; j < k; ++j) {
         const uint32_t bj = x.finish_lo9(xxh_fixed_rc<24>(c_bloom.seed[j])) & 511u;
@@ -1774,28 +1683,24 @@ __global__ __launch_bounds__(256) void bloom_rec_overflow(const tkv_amq_segment*
   }
   for (uint32_t i = threadIdx.x; i < n; i += 256) {
     const uint4 q = *reinterpret_cast<const uint4*>(list + 16ull * i);
-    uint32_t* blk;
-    uint32_t b[8];
-    uint32_t kk = k < 8 ? k : 8u;
-    if (k <= 8 || a.kb == 24) {
-      const uint32_t tile = rec_tile(q.x, q.y, q.z);
-      blk = words + 16ull * ((uint64_t)(a.tile0 + tile) * kBloomTileBlocks + (q.x & (kBloomTileBlocks - 1)));
-      b[0] = q.x >> 10; b[1] = q.x >> 19; b[2] = q.y; b[3] = q.y >> 9;
-      b[4] = q.y >> 18; b[5] = q.z; b[6] = q.z >> 9; b[7] = q.z >> 18;
+    if (!raw) {
+      const uint64_t blk = (uint64_t)(a.tile0 + q.w) * kTileBlocks + (q.x & (kTileBlocks - 1));
+      uint32_t* bw = words + 16ull * blk;
+      const uint32_t b[8] = {q.x >> 11, q.x >> 20, q.y, q.y >> 9, q.y >> 18, q.z, q.z >> 9, q.z >> 18};
+      const uint32_t kk = k < 8 ? k : 8u;
+      for (uint32_t j = 0; j < kk; ++j) {
+        const uint32_t bj = b[j] & 511u;
+        atomicOr(bw + (bj >> 5), 1u << (bj & 31u));
+      }
     } else {
       const Xxh16 x((uint64_t)q.x | ((uint64_t)q.y << 32), (uint64_t)q.z | ((uint64_t)q.w << 32));
       const uint64_t h0 = x.finish(c_bloom.rhinit16[0]);
-      blk = words + 16 * (uint64_t)__umul64hi(h0, (uint64_t)sg.n_blocks);
-      atomicOr(blk + ((h0 & 511u) >> 5), 1u << (h0 & 31u));
+      uint32_t* bw = words + 16 * (uint64_t)__umul64hi(h0, (uint64_t)sg.n_blocks);
+      atomicOr(bw + ((h0 & 511u) >> 5), 1u << (h0 & 31u));
       for (uint32_t j = 1; j < k; ++j) {
         const uint32_t bj = x.finish_lo9(c_bloom.rhinit16[j]) & 511u;
-        atomicOr(blk + (bj >> 5), 1u << (bj & 31u));
+        atomicOr(bw + (bj >> 5), 1u << (bj & 31u));
       }
-      kk = 0;
-    }
-    for (uint32_t j = 0; j < kk; ++j) {
-      const uint32_t bj = b[j] & 511u;
-      atomicOr(blk + (bj >> 5), 1u << (bj & 31u));
     }
   }
 }
@@ -4225,97 +4130,143 @@ inline void once_per_device(std::once_flag (&flags)[kMaxDevices], Fn&& fn)
   std::call_once(flags[dev], fn);
 }
 
-// Kernel attributes of the partitioned monolithic build (dynamic LDS above 64 KiB).
-inline void set_part_attributes()
+// Kernel attributes of the monolithic build (dynamic LDS above 64 KiB).
+inline void set_mono_attributes()
 {
   static std::once_flag lds_attr[kMaxDevices];
   once_per_device(lds_attr, [] {
-    const int cap = (int)(4 * kBloomPartMaxTiles);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&bloom_part_keys<0, 256>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, cap);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&bloom_part_keys<1, 256>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, cap);
-  });
-}
-
-// count -> scans -> scatter -> tile build over the window `pw` (the whole filter, or one
-// rank's tile range of a hash-range sharded filter)
-inline void launch_partitioned_build(const BloomPartGeom& pg, hipStream_t s, const uint4* k4,
-                                     const tkv_amq_segment* d_segs, uint32_t* w, uint32_t nk,
-                                     const PartWindow& pw, uint8_t* d_out)
-{
-  const size_t hl = 4ull * pg.n_tiles;
-  hipLaunchKernelGGL((bloom_part_keys<0, 256>), dim3(pg.P), dim3(256), hl, s, k4, d_segs, w,
-                     pg.n_tiles, pg.per, pg.part_off, nk, pw);
-  hipLaunchKernelGGL(bloom_part_scan_cols, dim3(pg.n_tiles), dim3(256), 0, s, w, pg.P, pg.n_tiles);
-  hipLaunchKernelGGL(bloom_part_scan_tiles, dim3(1), dim3(256), 0, s, w, pg.P, pg.n_tiles);
-  hipLaunchKernelGGL((bloom_part_keys<1, 256>), dim3(pg.P), dim3(256), hl, s, k4, d_segs, w,
-                     pg.n_tiles, pg.per, pg.part_off, nk, pw);
-  hipLaunchKernelGGL(bloom_tile_build<kBloomTileThreads>, dim3(pg.n_tiles), dim3(kBloomTileThreads),
-                     64ull * kBloomTileBlocks, s, d_segs, w, pg.P, pg.n_tiles, pg.part_off, d_out,
-                     pw);
-}
-
-// the hash-once record path takes a monolithic filter of <= kRecMaxTiles tiles
-inline bool bloom_rec_eligible(uint64_t n_blocks, uint64_t n_keys)
-{
-  return div_up(n_blocks, kBloomTileBlocks) <= kRecMaxTiles && n_keys <= 0xffffffffull;
-}
-
-// partition -> tiles -> overflow over keys [0, n) (from_seg: the segment's own keys) into
-// tiles [tile0, tile0 + g.n_tiles)
-inline void launch_rec_build(const BloomRecGeom& g, hipStream_t s, const uint4* keys, uint32_t n,
-                             uint32_t tile0, uint32_t from_seg, uint32_t hdr_always,
-                             const tkv_amq_segment* d_segs, uint8_t* ws, uint8_t* d_out,
-                             const uint32_t* recs = nullptr, uint32_t key_bytes = 16)
-{
-  static std::once_flag lds_attr[kMaxDevices];
-  once_per_device(lds_attr, [] {
-    for (const void* f : {reinterpret_cast<const void*>(&bloom_rec_partition),
-                          reinterpret_cast<const void*>(&bloom_rec_partition24)})
+    for (const void* f : {reinterpret_cast<const void*>(&bloom_part_keys16),
+                          reinterpret_cast<const void*>(&bloom_part_keys24),
+                          reinterpret_cast<const void*>(&bloom_part_routed)})
       (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)bloom_rec_lds_bytes(kRecMaxTiles));
+                                (int)part_lds_bytes(kDirectMaxTiles));
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&bloom_tile),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)(64 * kTileBlocks));
   });
-  const RecArgs a{keys, n, tile0, from_seg, ws, g, recs, key_bytes};
-  if (key_bytes == 24 && !recs)
-    hipLaunchKernelGGL(bloom_rec_partition24, dim3(g.P), dim3(kRecThreads), bloom_rec_lds_bytes(g.n_tiles),
-                       s, d_segs, a);
+}
+
+inline uint32_t filter_tiles(uint64_t n_blocks) { return (uint32_t)div_up(n_blocks, kTileBlocks); }
+
+inline uint64_t align256(uint64_t x) { return (x + 255) & ~255ull; }
+
+// partition -> tiles -> overflow.  src: kSrcKey16 / kSrcKey24 (keys, hashed), or kSrcRec12 for
+// routed items (records, or 16-byte keys when k > 8)
+inline void launch_part_build(int src, const PartArgs& a, hipStream_t s, const tkv_amq_segment* d_segs,
+                              uint8_t* d_out, uint32_t hdr_always)
+{
+  set_mono_attributes();
+  const size_t lds = part_lds_bytes(a.g.n_tiles);
+  const dim3 grid(a.g.P), block(kPartThreads);
+  if (src == kSrcKey24) hipLaunchKernelGGL(bloom_part_keys24, grid, block, lds, s, d_segs, a);
+  else if (src == kSrcKey16) hipLaunchKernelGGL(bloom_part_keys16, grid, block, lds, s, d_segs, a);
+  else hipLaunchKernelGGL(bloom_part_routed, grid, block, lds, s, d_segs, a);
+  hipLaunchKernelGGL(bloom_tile, dim3(a.g.n_tiles), dim3(kTileThreads), 64ull * kTileBlocks, s, d_segs, a,
+                     d_out, hdr_always);
+  hipLaunchKernelGGL(bloom_overflow, dim3(a.g.P), dim3(256), 0, s, d_segs, a, d_out);
+}
+
+// The route of n keys (16 or 24 bytes) into g.n_parts parts of q tiles: the count pass, the two
+// scans, then the scatter of the 12-byte records (out_recs; route_recs writes nothing for
+// k > 8) and/or of the 16-byte keys themselves (out_keys; nothing for k < min_k).  The part
+// totals are left at ws + g.P * n_parts (u32).
+inline void launch_route(const RouteGeom& g, hipStream_t s, const uint8_t* keys, uint32_t kb, uint32_t n,
+                         const tkv_amq_segment* d_seg, uint32_t q, uint32_t* ws, uint8_t* out_keys,
+                         uint32_t min_k, uint8_t* out_recs)
+{
+  const size_t hl = 4ull * g.n_parts;
+  const dim3 grid(g.P), block(256);
+  if (kb == 24)
+    hipLaunchKernelGGL((route_keys<0, 256, 24>), grid, block, hl, s, keys, d_seg, ws, g.n_parts, g.per, n,
+                       q, nullptr, 0u);
   else
-    hipLaunchKernelGGL(bloom_rec_partition, dim3(g.P), dim3(kRecThreads), bloom_rec_lds_bytes(g.n_tiles),
-                       s, d_segs, a);
-  hipLaunchKernelGGL(bloom_rec_tile, dim3(g.n_tiles), dim3(kRecTileThreads), 64ull * kBloomTileBlocks,
-                     s, d_segs, a, d_out, hdr_always);
-  hipLaunchKernelGGL(bloom_rec_overflow, dim3(g.P), dim3(256), 0, s, d_segs, a, d_out);
+    hipLaunchKernelGGL((route_keys<0, 256, 16>), grid, block, hl, s, keys, d_seg, ws, g.n_parts, g.per, n,
+                       q, nullptr, 0u);
+  hipLaunchKernelGGL(route_scan_cols, dim3(g.n_parts), dim3(256), 0, s, ws, g.P, g.n_parts);
+  hipLaunchKernelGGL(route_scan_parts, dim3(1), dim3(256), 0, s, ws, g.P, g.n_parts);
+  if (out_recs) {
+    uint32_t* r = reinterpret_cast<uint32_t*>(out_recs);
+    if (kb == 24)
+      hipLaunchKernelGGL((route_recs<256, 24>), grid, block, hl, s, keys, d_seg, ws, g.n_parts, g.per, n, q, r);
+    else
+      hipLaunchKernelGGL((route_recs<256, 16>), grid, block, hl, s, keys, d_seg, ws, g.n_parts, g.per, n, q, r);
+  }
+  if (out_keys && kb == 16)
+    hipLaunchKernelGGL((route_keys<1, 256, 16>), grid, block, hl, s, keys, d_seg, ws, g.n_parts, g.per, n,
+                       q, reinterpret_cast<uint4*>(out_keys), min_k);
 }
 
-// Hash-range sharding (BASELINE config 5): T = ceil(n_blocks / tile) tiles, q = ceil(T / parts)
-// per part; part p owns tiles [p * q, min((p + 1) * q, T)).
-inline uint32_t shard_tiles_per_part(uint32_t n_blocks, uint32_t n_parts)
+// The monolithic build of one filter (a one-leaf tkv_amq_build batch beyond the window path):
+// up to kDirectMaxTiles tiles the partition reads the keys; beyond, the keys are first routed
+// into g parts of at most kRecPartMaxTiles tiles -- as 12-byte records (k <= 8) or as
+// themselves (16-byte keys, k > 8) -- and the parts are built one after another, each
+// partition reading its part's count on the device.  The host does not know k (the plan lives
+// on the device), so the workspace is sized for 16-byte region slots and routed items.
+struct MonoPlan {
+  uint32_t T, g, q;  // tiles, parts, tiles per part
+  RouteGeom rg;
+  uint64_t items_off, part_off;
+  PartGeom pg;       // a part of q tiles (every part's own geometry is no larger)
+  uint64_t bytes;
+};
+
+inline MonoPlan mono_plan(uint64_t n_keys, uint64_t n_blocks)
 {
-  const uint32_t T = (uint32_t)div_up(n_blocks, kBloomTileBlocks);
-  return (uint32_t)div_up(T, n_parts);
+  MonoPlan m{};
+  m.T = filter_tiles(n_blocks);
+  if (m.T <= kDirectMaxTiles) {
+    m.g = 1;
+    m.q = m.T;
+    m.pg = part_geom(n_keys, n_keys, m.T, 16);
+    m.bytes = m.pg.bytes;
+    return m;
+  }
+  m.g = (uint32_t)div_up(m.T, kRecPartMaxTiles);
+  m.q = (uint32_t)div_up(m.T, m.g);
+  m.rg = route_geom(n_keys, m.g);
+  m.items_off = align256(m.rg.bytes);
+  m.part_off = align256(m.items_off + 16ull * n_keys);
+  m.pg = part_geom(n_keys, div_up(n_keys, m.g), m.q, 16);
+  m.bytes = m.part_off + m.pg.bytes;
+  return m;
 }
 
-// the route is an unstaged partition (exact runs, no padding) into n_parts buckets
-inline BloomPartGeom bloom_route_geom(uint64_t n_keys, uint32_t n_parts)
+// k of a one-leaf Bloom plan from its key and block counts (the host-side plan is gone by the
+// time tkv_amq_build runs; for n >= 512 keys one bits-per-key value gives n_blocks); 0 if none
+inline uint32_t bloom_k_of(uint64_t n_keys, uint64_t n_blocks)
 {
-  BloomPartGeom g;
-  g.n_tiles = n_parts;
-  const uint64_t p = (n_keys + 4095) / 4096;
-  g.P = (uint32_t)(p < 1 ? 1 : (p > kBloomPartMaxWgs ? kBloomPartMaxWgs : p));
-  g.per = (uint32_t)((n_keys + g.P - 1) / g.P);
-  g.h_words = (uint64_t)g.P * n_parts;
-  g.part_off = (4 * (g.h_words + 2ull * n_parts + 1) + 255) & ~255ull;
-  g.bytes = g.part_off;
-  return g;
+  for (uint32_t b = 1; b <= 64; ++b) {
+    const uint64_t nb = div_up(n_keys * b, 512);
+    if ((nb == 0 ? 1 : nb) == n_blocks) return bloom_hash_count(b);
+  }
+  return 0;
 }
 
-// a one-filter Bloom batch too large for one LDS image takes the tiled, partitioned build
-// (it needs a workspace of bloom_part_geom(n_keys, n_blocks).bytes and 16-byte keys)
+// keys [0, n) of segment 0 (kb 16 or 24); with g > 1 and 24-byte keys k must be <= 8
+inline void launch_mono(const MonoPlan& m, hipStream_t s, const uint8_t* keys, uint32_t kb, uint32_t n,
+                        const tkv_amq_segment* d_segs, uint8_t* ws, uint8_t* d_out)
+{
+  if (m.g == 1) {
+    const PartArgs a{keys, n, 0u, 1u, kb, nullptr, 0u, ws, m.pg};
+    launch_part_build(kb == 24 ? kSrcKey24 : kSrcKey16, a, s, d_segs, d_out, 0u);
+    return;
+  }
+  uint32_t* rws = reinterpret_cast<uint32_t*>(ws);
+  uint8_t* items = ws + m.items_off;
+  launch_route(m.rg, s, keys, kb, n, d_segs, m.q, rws, kb == 16 ? items : nullptr, 9u, items);
+  const uint32_t* cnt = rws + (uint64_t)m.rg.P * m.g;  // the part totals
+  for (uint32_t j = 0; j < m.g; ++j) {
+    const uint32_t t0 = j * m.q, tn = m.T - t0 < m.q ? m.T - t0 : m.q;
+    const PartArgs a{items, 0u, t0, 0u, 16u, cnt, j, ws + m.part_off,
+                     part_geom(n, div_up(n, m.g), tn, 16)};
+    launch_part_build(kSrcRec12, a, s, d_segs, d_out, 0u);
+  }
+}
+
+// a one-filter Bloom batch too large for one LDS image takes the monolithic build (it needs a
+// workspace of mono_plan(n_keys, n_blocks).bytes and 16- or 24-byte keys)
 inline bool bloom_partitioned(uint32_t n_segs, uint64_t max_blocks, uint64_t n_keys)
 {
-  return n_segs == 1 && 64 * max_blocks > kBloomLeafLdsBudget && n_keys <= 0xffffffffull &&
-         div_up(max_blocks, kBloomTileBlocks) <= kBloomPartMaxTiles;
+  return n_segs == 1 && 64 * max_blocks > kBloomLeafLdsBudget && n_keys <= 0xffffffffull;
 }
 
 }  // namespace
@@ -4513,9 +4464,7 @@ int tkv_amq_plan(int kind, const uint64_t* counts, const uint64_t* src_ids, uint
       *ws_bytes = bloom_split_ws_bytes(n_segs, bloom_window_parts(n_segs, key_begin, max_blocks),
                                        max_blocks);
     else if (kind == TKV_AMQ_BLOOM && bloom_partitioned(n_segs, max_blocks, key_begin))
-      *ws_bytes = bloom_rec_eligible(max_blocks, key_begin)  // 16-byte keys
-                      ? bloom_rec_geom(key_begin, max_blocks).bytes
-                      : bloom_part_geom(key_begin, max_blocks).bytes;
+      *ws_bytes = mono_plan(key_begin, max_blocks).bytes;
     else if (kind == TKV_AMQ_BLOOM)
       *ws_bytes = bloom_split_ws_bytes(n_segs, bloom_split_parts(n_segs, key_begin, max_blocks),
                                        max_blocks);
@@ -4594,13 +4543,15 @@ int tkv_amq_build(int kind, const uint8_t* keys, const uint64_t* offs, uint32_t 
                          parts, chunks, w, img, d_out);
       return hipGetLastError() == hipSuccess ? TKV_AMQ_OK : TKV_AMQ_INTERNAL;
     }
-    // one filter beyond the window path: 16-byte keys take the record path or the key
-    // partition, 24-byte keys the record path (the keys hashed once either way)
+    // one filter beyond the window path: 16- and 24-byte keys take the monolithic build (each
+    // key hashed once); 24-byte keys with k > 8 only up to kDirectMaxTiles tiles (their records
+    // hold eight bits, and the others are set from the keys, which the route does not carry)
     const int mono_mode = build_key_mode(keys, offs, stride);
     const bool mono_part = bloom_partitioned(n_segs, max_blocks, n_keys) && d_ws;
-    const bool mono16 = mono_part && mode == kKey16;
-    const bool mono24 = mono_part && mono_mode == kKey24 && bloom_rec_eligible(max_blocks, n_keys) &&
-                        ws_bytes >= bloom_rec_geom(n_keys, max_blocks).bytes;
+    const MonoPlan mp = mono_plan(n_keys, max_blocks);
+    const bool mono16 = mono_part && mode == kKey16 && ws_bytes >= mp.bytes;
+    const bool mono24 = mono_part && mono_mode == kKey24 && ws_bytes >= mp.bytes &&
+                        (mp.g == 1 || bloom_k_of(n_keys, max_blocks) <= 8);
     if (bloom_window_path(n_segs, max_blocks, mono16 || mono24)) {
       // leaves beyond one CU's LDS: windows of the image, parts of the keys
       const uint32_t W = bloom_window_count(max_blocks), wblk = bloom_window_blocks(max_blocks);
@@ -4660,26 +4611,15 @@ int tkv_amq_build(int kind, const uint8_t* keys, const uint64_t* offs, uint32_t 
         launch_bloom_lds<256>(bmode, mode, n_segs, lds, s, keys, offs, stride, d_segs, d_out);
       return hipGetLastError() == hipSuccess ? TKV_AMQ_OK : TKV_AMQ_INTERNAL;
     }
-    const BloomPartGeom pg = bloom_part_geom(n_keys, max_blocks);
-    const bool mono = mono16;
-    if (mono24) {
-      launch_rec_build(bloom_rec_geom(n_keys, max_blocks), s, reinterpret_cast<const uint4*>(keys),
-                       (uint32_t)n_keys, 0u, 1u, 0u, d_segs, static_cast<uint8_t*>(d_ws), d_out, nullptr, 24u);
-    } else if (mono && bloom_rec_eligible(max_blocks, n_keys) &&
-        ws_bytes >= bloom_rec_geom(n_keys, max_blocks).bytes) {
-      // one monolithic filter: hash once into bit records partitioned by tile, build the tiles
-      launch_rec_build(bloom_rec_geom(n_keys, max_blocks), s, reinterpret_cast<const uint4*>(keys),
-                       (uint32_t)n_keys, 0u, 1u, 0u, d_segs, static_cast<uint8_t*>(d_ws), d_out);
-    } else if (mono && ws_bytes >= pg.bytes) {
-      // one monolithic filter: partition the keys by tile, build every tile in LDS
-      set_part_attributes();
-      launch_partitioned_build(pg, s, reinterpret_cast<const uint4*>(keys), d_segs,
-                               static_cast<uint32_t*>(d_ws), (uint32_t)n_keys, whole_filter_window(),
-                               d_out);
+    if (mono16 || mono24) {
+      // one monolithic filter: every key hashed once into its bit record, records partitioned
+      // by tile (routed into parts first beyond kDirectMaxTiles tiles), tiles built in LDS
+      launch_mono(mp, s, keys, mono24 ? 24u : 16u, (uint32_t)n_keys, d_segs, static_cast<uint8_t*>(d_ws),
+                  d_out);
     } else {
       // fewer than kBloomSpreadSegs leaves, leaves beyond the LDS budget in a multi-leaf batch,
-      // or a monolithic filter whose keys are neither 16 nor 24 bytes (or of more than
-      // kRecMaxTiles tiles with 24-byte keys): device atomics
+      // or a monolithic filter whose keys are neither 16 nor 24 bytes (or 24-byte keys with
+      // k > 8 beyond kDirectMaxTiles tiles): device atomics
       const dim3 g1(n_segs), b(256);
       hipLaunchKernelGGL(bloom_global_init, g1, b, 0, s, d_segs, d_out);
       const uint32_t g2 = (uint32_t)(div_up(n_keys, 256) < 8192 ? div_up(n_keys, 256) : 8192);
@@ -4884,10 +4824,17 @@ int tkv_amq_build(int kind, const uint8_t* keys, const uint64_t* offs, uint32_t 
   return hipGetLastError() == hipSuccess ? TKV_AMQ_OK : TKV_AMQ_INTERNAL;
 }
 
+uint32_t tkv_amq_bloom_tile_blocks(void) { return kTileBlocks; }
+
+uint32_t tkv_amq_bloom_range_max_tiles(int records)
+{
+  return records ? kRecPartMaxTiles : kDirectMaxTiles;
+}
+
 uint64_t tkv_amq_bloom_route_ws_bytes(uint64_t n_keys, uint32_t n_parts)
 {
   if (n_parts == 0 || n_parts > kRouteMaxParts) return 0;
-  return bloom_route_geom(n_keys, n_parts).bytes;
+  return route_geom(n_keys, n_parts).bytes;
 }
 
 int tkv_amq_bloom_route(const uint8_t* d_keys16, uint64_t n_keys, const tkv_amq_segment* d_seg,
@@ -4901,23 +4848,13 @@ int tkv_amq_bloom_route(const uint8_t* d_keys16, uint64_t n_keys, const tkv_amq_
   if (n_keys && (!d_keys16 || !d_routed16 || (reinterpret_cast<uintptr_t>(d_keys16) & 15) ||
                  (reinterpret_cast<uintptr_t>(d_routed16) & 15)))
     return TKV_AMQ_INVALID_ARGUMENT;
-  const BloomPartGeom g = bloom_route_geom(n_keys, n_parts);
+  const RouteGeom g = route_geom(n_keys, n_parts);
   if (!d_ws || ws_bytes < g.bytes) return TKV_AMQ_INVALID_ARGUMENT;
   const hipStream_t s = as_stream(stream);
   uint32_t* w = static_cast<uint32_t*>(d_ws);
-  set_part_attributes();
-  const PartWindow pw{0u, shard_tiles_per_part(n_blocks, n_parts), 1u, 0u,
-                      reinterpret_cast<uint4*>(d_routed16)};
-  const uint4* k4 = reinterpret_cast<const uint4*>(d_keys16);
-  const size_t hl = 4ull * n_parts;
-  const uint32_t nk = (uint32_t)n_keys;
-  hipLaunchKernelGGL((bloom_part_keys<0, 256>), dim3(g.P), dim3(256), hl, s, k4, d_seg, w, n_parts,
-                     g.per, g.part_off, nk, pw);
-  hipLaunchKernelGGL(bloom_part_scan_cols, dim3(n_parts), dim3(256), 0, s, w, g.P, n_parts);
-  hipLaunchKernelGGL(bloom_part_scan_tiles, dim3(1), dim3(256), 0, s, w, g.P, n_parts);
-  hipLaunchKernelGGL((bloom_part_keys<1, 256>), dim3(g.P), dim3(256), hl, s, k4, d_seg, w, n_parts,
-                     g.per, g.part_off, nk, pw);
-  // the per-part totals bloom_part_scan_cols left after the histogram
+  const uint32_t q = (uint32_t)div_up(filter_tiles(n_blocks), n_parts);
+  launch_route(g, s, d_keys16, 16, (uint32_t)n_keys, d_seg, q, w, d_routed16, 0u, nullptr);
+  // the per-part totals route_scan_cols left after the histogram
   if (hipMemcpyAsync(d_part_counts, w + g.h_words, 4ull * n_parts, hipMemcpyDeviceToDevice, s) !=
       hipSuccess)
     return TKV_AMQ_INTERNAL;
@@ -4947,34 +4884,18 @@ int tkv_amq_bloom_route_records_ex(const uint8_t* d_keys, uint32_t key_bytes, ui
   if (n_parts == 0 || n_parts > kRouteMaxParts || n_blocks == 0 || !d_seg || !d_part_counts ||
       n_keys > 0xffffffffull || hash_count == 0 || hash_count > 8 || (key_bytes != 16 && key_bytes != 24))
     return TKV_AMQ_INVALID_ARGUMENT;
+  // a record's tile field holds the tile relative to its part: parts of <= kRecPartMaxTiles
+  const uint32_t q = (uint32_t)div_up(filter_tiles(n_blocks), n_parts);
+  if (q > kRecPartMaxTiles) return TKV_AMQ_INVALID_ARGUMENT;
   const uintptr_t kalign = key_bytes == 16 ? 15 : 7;
   if (n_keys && (!d_keys || !d_recs12 || (reinterpret_cast<uintptr_t>(d_keys) & kalign) ||
                  (reinterpret_cast<uintptr_t>(d_recs12) & 3)))
     return TKV_AMQ_INVALID_ARGUMENT;
-  const BloomPartGeom g = bloom_route_geom(n_keys, n_parts);
+  const RouteGeom g = route_geom(n_keys, n_parts);
   if (!d_ws || ws_bytes < g.bytes) return TKV_AMQ_INVALID_ARGUMENT;
   const hipStream_t s = as_stream(stream);
   uint32_t* w = static_cast<uint32_t*>(d_ws);
-  set_part_attributes();
-  const uint32_t q = shard_tiles_per_part(n_blocks, n_parts);
-  const PartWindow pw{0u, q, 1u, 0u, nullptr};
-  const uint4* k4 = reinterpret_cast<const uint4*>(d_keys);
-  const size_t hl = 4ull * n_parts;
-  const uint32_t nk = (uint32_t)n_keys;
-  if (key_bytes == 24)
-    hipLaunchKernelGGL((bloom_part_keys<0, 256, 24>), dim3(g.P), dim3(256), hl, s, k4, d_seg, w, n_parts,
-                       g.per, g.part_off, nk, pw);
-  else
-    hipLaunchKernelGGL((bloom_part_keys<0, 256>), dim3(g.P), dim3(256), hl, s, k4, d_seg, w, n_parts,
-                       g.per, g.part_off, nk, pw);
-  hipLaunchKernelGGL(bloom_part_scan_cols, dim3(n_parts), dim3(256), 0, s, w, g.P, n_parts);
-  hipLaunchKernelGGL(bloom_part_scan_tiles, dim3(1), dim3(256), 0, s, w, g.P, n_parts);
-  if (key_bytes == 24)
-    hipLaunchKernelGGL((bloom_route_recs<256, 24>), dim3(g.P), dim3(256), hl, s, d_keys, d_seg, w, n_parts,
-                       g.per, nk, q, reinterpret_cast<uint32_t*>(d_recs12));
-  else
-    hipLaunchKernelGGL((bloom_route_recs<256, 16>), dim3(g.P), dim3(256), hl, s, d_keys, d_seg, w, n_parts,
-                       g.per, nk, q, reinterpret_cast<uint32_t*>(d_recs12));
+  launch_route(g, s, d_keys, key_bytes, (uint32_t)n_keys, d_seg, q, w, nullptr, 0u, d_recs12);
   if (hipMemcpyAsync(d_part_counts, w + g.h_words, 4ull * n_parts, hipMemcpyDeviceToDevice, s) !=
       hipSuccess)
     return TKV_AMQ_INTERNAL;
@@ -4983,8 +4904,8 @@ int tkv_amq_bloom_route_records_ex(const uint8_t* d_keys, uint32_t key_bytes, ui
 
 uint64_t tkv_amq_bloom_build_range_records_ws_bytes(uint64_t n_recs, uint32_t tile_begin, uint32_t tile_end)
 {
-  if (tile_end <= tile_begin || tile_end - tile_begin > kRecMaxTiles || n_recs > 0xffffffffull) return 0;
-  return bloom_rec_geom(n_recs, (uint64_t)(tile_end - tile_begin) * kBloomTileBlocks).bytes;
+  if (tile_end <= tile_begin || tile_end - tile_begin > kRecPartMaxTiles || n_recs > 0xffffffffull) return 0;
+  return part_geom(n_recs, n_recs, tile_end - tile_begin, 12).bytes;
 }
 
 int tkv_amq_bloom_build_range_records(const uint8_t* d_recs12, uint64_t n_recs, const tkv_amq_segment* d_seg,
@@ -4993,9 +4914,9 @@ int tkv_amq_bloom_build_range_records(const uint8_t* d_recs12, uint64_t n_recs, 
                                       void* stream)
 {
   if (tkv_amq_device_count() == 0) return TKV_AMQ_UNAVAILABLE;
-  const uint32_t T = (uint32_t)div_up(n_blocks, kBloomTileBlocks);
+  const uint32_t T = filter_tiles(n_blocks);
   if (!d_seg || !d_out || n_blocks == 0 || tile_begin > tile_end || tile_end > T ||
-      tile_end - tile_begin > kRecMaxTiles || n_recs > 0xffffffffull || hash_count == 0 ||
+      tile_end - tile_begin > kRecPartMaxTiles || n_recs > 0xffffffffull || hash_count == 0 ||
       hash_count > 8)
     return TKV_AMQ_INVALID_ARGUMENT;
   if (n_recs && (!d_recs12 || (reinterpret_cast<uintptr_t>(d_recs12) & 3))) return TKV_AMQ_INVALID_ARGUMENT;
@@ -5003,18 +4924,17 @@ int tkv_amq_bloom_build_range_records(const uint8_t* d_recs12, uint64_t n_recs, 
     hipLaunchKernelGGL(bloom_header_only, dim3(1), dim3(64), 0, as_stream(stream), d_seg, d_out);
     return hipGetLastError() == hipSuccess ? TKV_AMQ_OK : TKV_AMQ_INTERNAL;
   }
-  const BloomRecGeom g = bloom_rec_geom(n_recs, (uint64_t)(tile_end - tile_begin) * kBloomTileBlocks);
+  const PartGeom g = part_geom(n_recs, n_recs, tile_end - tile_begin, 12);
   if (!d_ws || ws_bytes < g.bytes) return TKV_AMQ_INVALID_ARGUMENT;
-  launch_rec_build(g, as_stream(stream), nullptr, (uint32_t)n_recs, tile_begin, 0u, 1u, d_seg,
-                   static_cast<uint8_t*>(d_ws), d_out, reinterpret_cast<const uint32_t*>(d_recs12));
+  const PartArgs a{d_recs12, (uint32_t)n_recs, tile_begin, 0u, 16u, nullptr, 0u, static_cast<uint8_t*>(d_ws), g};
+  launch_part_build(kSrcRec12, a, as_stream(stream), d_seg, d_out, 1u);
   return hipGetLastError() == hipSuccess ? TKV_AMQ_OK : TKV_AMQ_INTERNAL;
 }
 
 uint64_t tkv_amq_bloom_build_range_ws_bytes(uint64_t n_keys, uint32_t tile_begin, uint32_t tile_end)
 {
-  if (tile_end <= tile_begin || tile_end - tile_begin > kBloomPartMaxTiles) return 0;
-  const uint64_t nb = (uint64_t)(tile_end - tile_begin) * kBloomTileBlocks;
-  return bloom_rec_eligible(nb, n_keys) ? bloom_rec_geom(n_keys, nb).bytes : bloom_part_geom(n_keys, nb).bytes;
+  if (tile_end <= tile_begin || tile_end - tile_begin > kDirectMaxTiles || n_keys > 0xffffffffull) return 0;
+  return part_geom(n_keys, n_keys, tile_end - tile_begin, 16).bytes;
 }
 
 int tkv_amq_bloom_build_range(const uint8_t* d_keys16, uint64_t n_keys, const tkv_amq_segment* d_seg,
@@ -5022,9 +4942,9 @@ int tkv_amq_bloom_build_range(const uint8_t* d_keys16, uint64_t n_keys, const tk
                               uint8_t* d_out, void* d_ws, uint64_t ws_bytes, void* stream)
 {
   if (tkv_amq_device_count() == 0) return TKV_AMQ_UNAVAILABLE;
-  const uint32_t T = (uint32_t)div_up(n_blocks, kBloomTileBlocks);
+  const uint32_t T = filter_tiles(n_blocks);
   if (!d_seg || !d_out || n_blocks == 0 || tile_begin > tile_end || tile_end > T ||
-      tile_end - tile_begin > kBloomPartMaxTiles || n_keys > 0xffffffffull)
+      tile_end - tile_begin > kDirectMaxTiles || n_keys > 0xffffffffull)
     return TKV_AMQ_INVALID_ARGUMENT;
   if (n_keys && (!d_keys16 || (reinterpret_cast<uintptr_t>(d_keys16) & 15)))
     return TKV_AMQ_INVALID_ARGUMENT;
@@ -5034,21 +4954,10 @@ int tkv_amq_bloom_build_range(const uint8_t* d_keys16, uint64_t n_keys, const tk
     hipLaunchKernelGGL(bloom_header_only, dim3(1), dim3(64), 0, as_stream(stream), d_seg, d_out);
     return hipGetLastError() == hipSuccess ? TKV_AMQ_OK : TKV_AMQ_INTERNAL;
   }
-  const uint64_t nb = (uint64_t)(tile_end - tile_begin) * kBloomTileBlocks;
-  if (d_ws && bloom_rec_eligible(nb, n_keys)) {
-    const BloomRecGeom g = bloom_rec_geom(n_keys, nb);
-    if (ws_bytes >= g.bytes) {
-      launch_rec_build(g, as_stream(stream), reinterpret_cast<const uint4*>(d_keys16), (uint32_t)n_keys,
-                       tile_begin, 0u, 1u, d_seg, static_cast<uint8_t*>(d_ws), d_out);
-      return hipGetLastError() == hipSuccess ? TKV_AMQ_OK : TKV_AMQ_INTERNAL;
-    }
-  }
-  const BloomPartGeom pg = bloom_part_geom(n_keys, nb);
-  if (!d_ws || ws_bytes < pg.bytes) return TKV_AMQ_INVALID_ARGUMENT;
-  set_part_attributes();
-  const PartWindow pw{tile_begin, 1u, 1u, 1u, nullptr};
-  launch_partitioned_build(pg, as_stream(stream), reinterpret_cast<const uint4*>(d_keys16), d_seg,
-                           static_cast<uint32_t*>(d_ws), (uint32_t)n_keys, pw, d_out);
+  const PartGeom g = part_geom(n_keys, n_keys, tile_end - tile_begin, 16);
+  if (!d_ws || ws_bytes < g.bytes) return TKV_AMQ_INVALID_ARGUMENT;
+  const PartArgs a{d_keys16, (uint32_t)n_keys, tile_begin, 0u, 16u, nullptr, 0u, static_cast<uint8_t*>(d_ws), g};
+  launch_part_build(kSrcKey16, a, as_stream(stream), d_seg, d_out, 1u);
   return hipGetLastError() == hipSuccess ? TKV_AMQ_OK : TKV_AMQ_INTERNAL;
 }
 

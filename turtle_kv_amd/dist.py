@@ -88,17 +88,39 @@ def allgather_filters(local, gathered=None, group=None):
 # "1B keys, Bloom @12, hash-range sharded across 8 GPUs, RCCL all-gather").  Unlike the leaf
 # filters above, keys must move: every key's bits fall in the 64-byte block its h0 selects, so
 # a rank can only build its byte range of the bitmap from the keys whose blocks fall there.
-# Steps per build: route (reorder the rank's keys by owning rank: tkv_amq_bloom_route_records
-# hashes each key once and ships its 12-byte bit record, k <= 8; tkv_amq_bloom_route ships the
-# 16-byte key otherwise), one all-to-all of them (RCCL over xGMI), the rank's tile range built in
-# LDS (tkv_amq_bloom_build_range_records / _build_range), then the all-gather of the bitmap
-# ranges.
+# The filter's T tiles (tkv_amq_bloom_tile_blocks() blocks each) are cut into world * g parts
+# of q tiles; rank r owns the g consecutive parts [r*g, (r+1)*g), a contiguous byte range of
+# the bitmap.  g = 1 unless a rank's range exceeds what one range build takes from records
+# (8,192 tiles: 1 GiB of filter per rank).  Steps per build, the same at every world size:
+#   route     reorder the rank's keys by part (tkv_amq_bloom_route_records hashes each key once
+#             and ships its 12-byte bit record, k <= 8; tkv_amq_bloom_route ships the 16-byte
+#             key otherwise);
+#   exchange  one all-to-all of them (RCCL over xGMI; at world size 1 a local copy);
+#   build     each owned part built from its records (tkv_amq_bloom_build_range_records /
+#             _build_range), part after part;
+#   gather    the all-gather of the bitmap ranges.
+# Without a process group (one GPU, no launcher) a filter of at most 20,000 tiles skips the
+# route: the range build reads the keys and makes the same records itself.
 # ---------------------------------------------------------------------------------------
-BLOOM_TILE_BLOCKS = 1024  # blocks per tile, as tkv_amq_bloom_route / _build_range cut them
+BLOOM_TILE_BLOCKS = 2048        # tkv_amq_bloom_tile_blocks()
+RECORD_RANGE_MAX_TILES = 8192   # tkv_amq_bloom_range_max_tiles(1): a record's tile field
+KEY_RANGE_MAX_TILES = 20000     # tkv_amq_bloom_range_max_tiles(0): the partition's tile table
+
+
+def hash_shard_plan(n_blocks: int, world: int, records: bool = True) -> tuple[int, int, int]:
+    """(T, g, q): the filter's tiles, the parts per rank and the tiles per part; part p owns
+    tiles [p*q, min((p+1)*q, T)) and rank r parts [r*g, (r+1)*g)."""
+    T = -(-int(n_blocks) // BLOOM_TILE_BLOCKS)
+    per_rank = -(-T // world)
+    cap = RECORD_RANGE_MAX_TILES if records else KEY_RANGE_MAX_TILES
+    g = max(1, -(-per_rank // cap))
+    q = -(-T // (world * g))
+    return T, g, q
 
 
 def hash_shard_tiles(n_blocks: int, world: int) -> tuple[int, int]:
-    """(T, q): the filter's tiles and the tiles per rank; rank r owns [r*q, min((r+1)*q, T))."""
+    """(T, q): the filter's tiles and the tiles per part when each of `world` parts is one
+    range build (the ABI's tkv_amq_bloom_route with n_parts = world)."""
     T = -(-int(n_blocks) // BLOOM_TILE_BLOCKS)
     return T, -(-T // world)
 
@@ -119,25 +141,26 @@ class HashShardedBloom:
         seg = self.plan.segs[0]
         self.n_blocks = int(seg["n_blocks"])
         self.payload_bytes = int(seg["payload_bytes"])
-        T, q = hash_shard_tiles(self.n_blocks, world)
-        # ranks past ceil(T / q) own no tile (e.g. T = 17 over 8 ranks: q = 3, ranks 6 and 7):
-        # they route and exchange keys like the others, and their range build writes only the
-        # filter header
-        self.tile_begin, self.tile_end = min(T, rank * q), min(T, (rank + 1) * q)
-        self.slice_bytes = q * BLOOM_TILE_BLOCKS * 64
+        # k <= 8 (bits_per_key <= 12): 12-byte bit records travel instead of the 16-byte keys,
+        # hashed once by their sender (tkv_amq_bloom_route_records); the owner's range builds
+        # read them without hashing
+        self.hash_count = int(seg["hash_count"])
+        self.records = self.hash_count <= 8
+        self.unit = 12 if self.records else 16  # bytes per routed key
+        self.T, self.g, self.q = hash_shard_plan(self.n_blocks, world, self.records)
+        self.n_parts = world * self.g
+        # ranks past the last tile (e.g. T = 17 over 8 ranks: q = 3, ranks 6 and 7) route and
+        # exchange keys like the others, and their range build writes only the filter header
+        self.tile_begin = min(self.T, rank * self.g * self.q)
+        self.tile_end = min(self.T, (rank + 1) * self.g * self.q)
+        self.slice_bytes = self.g * self.q * BLOOM_TILE_BLOCKS * 64
         # the payload layout of tkv_amq_build (64-byte header, then the blocks), padded so every
         # rank's range is a slice of slice_bytes
         self.out = torch.zeros(64 + world * self.slice_bytes, dtype=torch.uint8, device=self.dev)
         self.gathered = torch.empty(world * self.slice_bytes, dtype=torch.uint8, device=self.dev)
         self.d_seg = self.plan.device_segs(self.dev)
-        self.counts = torch.zeros(world, dtype=torch.int32, device=self.dev)
+        self.counts = torch.zeros(self.n_parts, dtype=torch.int32, device=self.dev)
         self._bufs = {}
-        # k <= 8 (bits_per_key <= 12): 12-byte bit records travel instead of the 16-byte keys,
-        # hashed once by their sender (tkv_amq_bloom_route_records); the owner's range build
-        # reads them without hashing (a range of <= 3,584 tiles: the record path's table)
-        self.hash_count = int(seg["hash_count"])
-        self.records = self.hash_count <= 8 and q <= 3584
-        self.unit = 12 if self.records else 16  # bytes per routed key
 
     def _buf(self, name, nbytes):
         import torch
@@ -147,9 +170,14 @@ class HashShardedBloom:
             self._bufs[name] = b
         return b
 
+    def part_tiles(self, j: int) -> tuple[int, int]:
+        """Tiles of this rank's j-th part."""
+        b = min(self.T, self.tile_begin + j * self.q)
+        return b, min(self.tile_end, b + self.q)
+
     def route(self, keys):
         """keys [n, 16] (or [n, 24] with bit records) uint8 on the device -> (routed [n, unit],
-        send counts per rank, int64)."""
+        per-part counts [n_parts], int64 on the device)."""
         import torch
         from . import abi
         from .filters import _ptr, _stream_handle
@@ -165,31 +193,34 @@ class HashShardedBloom:
         n = keys.shape[0]
         u = self.unit
         routed = self._buf("routed", u * n)[:u * n].view(n, u)
+        P = self.n_parts
         if self.records:
-            ws = self._buf("route_ws", int(L.tkv_amq_bloom_route_records_ws_bytes(n, self.world)))
+            ws = self._buf("route_ws", int(L.tkv_amq_bloom_route_records_ws_bytes(n, P)))
             abi.check(L.tkv_amq_bloom_route_records_ex(_ptr(keys), kb, n, _ptr(self.d_seg), self.n_blocks,
-                                                       self.hash_count, self.world, _ptr(routed),
+                                                       self.hash_count, P, _ptr(routed),
                                                        _ptr(self.counts), _ptr(ws), ws.numel(),
                                                        _stream_handle()), "tkv_amq_bloom_route_records_ex")
         else:
-            ws = self._buf("route_ws", int(L.tkv_amq_bloom_route_ws_bytes(n, self.world)))
-            abi.check(L.tkv_amq_bloom_route(_ptr(keys), n, _ptr(self.d_seg), self.n_blocks, self.world,
+            ws = self._buf("route_ws", int(L.tkv_amq_bloom_route_ws_bytes(n, P)))
+            abi.check(L.tkv_amq_bloom_route(_ptr(keys), n, _ptr(self.d_seg), self.n_blocks, P,
                                             _ptr(routed), _ptr(self.counts), _ptr(ws), ws.numel(),
                                             _stream_handle()), "tkv_amq_bloom_route")
         return routed, self.counts.to(dtype=torch.int64)
 
-    def exchange(self, routed, send_counts):
-        """All-to-all of the routed units (bit records or keys): returns the [m, unit] units
-        this rank owns."""
+    def exchange(self, routed, part_counts):
+        """All-to-all of the routed units (bit records or keys).  Returns (owned [m, unit],
+        sub [world, g]): the units this rank owns, sender after sender, each sender's ordered
+        by part, and how many each sender sent for each of this rank's parts."""
         import torch
         import torch.distributed as dist
-        u = self.unit
+        u, W, g = self.unit, self.world, self.g
         gloo = dist.get_backend(self.group) != "nccl"
-        sc = send_counts.cpu() if gloo else send_counts
-        rc = torch.empty_like(sc)
-        dist.all_to_all_single(rc, sc, group=self.group)
-        send = [int(x) * u for x in sc.tolist()]
-        recv = [int(x) * u for x in rc.tolist()]
+        pc = part_counts.cpu() if gloo else part_counts
+        sub = torch.empty_like(pc)
+        dist.all_to_all_single(sub, pc, group=self.group)  # [W*g] -> [sender][part]
+        sub = sub.cpu().view(W, g)
+        send = [int(x) * u for x in part_counts.cpu().view(W, g).sum(1).tolist()]
+        recv = [int(x) * u for x in sub.sum(1).tolist()]
         m = sum(recv) // u
         out = self._buf("recv", u * m)[:u * m]
         src = routed.reshape(-1)
@@ -199,41 +230,62 @@ class HashShardedBloom:
             out.copy_(host)
         else:
             dist.all_to_all_single(out, src, recv, send, group=self.group)
-        return out.view(m, u)
+        return out.view(m, u), sub
 
-    def build_range(self, owned):
-        """This rank's tile range of the filter from the keys it owns (into self.out)."""
+    def build_range(self, owned, t0=None, t1=None):
+        """Tiles [t0, t1) (default: this rank's range) of the filter from 16-byte keys."""
         from . import abi
         from .filters import _ptr, _stream_handle
         L = abi.lib()
+        t0 = self.tile_begin if t0 is None else t0
+        t1 = self.tile_end if t1 is None else t1
+        if owned.dim() != 2 or owned.shape[1] != 16:
+            raise abi.TkvAmqError(abi.INVALID_ARGUMENT, "the range build takes [n, 16] uint8 keys, "
+                                  f"got shape {tuple(owned.shape)}")
         m = owned.shape[0]
-        ws = self._buf("build_ws", int(L.tkv_amq_bloom_build_range_ws_bytes(m, self.tile_begin,
-                                                                             self.tile_end)))
-        abi.check(L.tkv_amq_bloom_build_range(_ptr(owned), m, _ptr(self.d_seg), self.n_blocks,
-                                              self.tile_begin, self.tile_end, _ptr(self.out),
-                                              _ptr(ws), ws.numel(), _stream_handle()),
+        ws = self._buf("build_ws", int(L.tkv_amq_bloom_build_range_ws_bytes(m, t0, t1)))
+        abi.check(L.tkv_amq_bloom_build_range(_ptr(owned), m, _ptr(self.d_seg), self.n_blocks, t0, t1,
+                                              _ptr(self.out), _ptr(ws), ws.numel(), _stream_handle()),
                   "tkv_amq_bloom_build_range")
 
-    def build_range_records(self, recs):
-        """This rank's tile range of the filter from the bit records it owns (into self.out)."""
+    def build_range_records(self, recs, t0=None, t1=None):
+        """Tiles [t0, t1) (default: this rank's range) of the filter from bit records."""
         from . import abi
         from .filters import _ptr, _stream_handle
         L = abi.lib()
+        t0 = self.tile_begin if t0 is None else t0
+        t1 = self.tile_end if t1 is None else t1
         m = recs.shape[0]
-        ws = self._buf("build_ws", int(L.tkv_amq_bloom_build_range_records_ws_bytes(
-            m, self.tile_begin, self.tile_end)))
-        abi.check(L.tkv_amq_bloom_build_range_records(_ptr(recs), m, _ptr(self.d_seg), self.n_blocks,
-                                                      self.hash_count, self.tile_begin, self.tile_end,
+        ws = self._buf("build_ws", int(L.tkv_amq_bloom_build_range_records_ws_bytes(m, t0, t1)))
+        abi.check(L.tkv_amq_bloom_build_range_records(_ptr(recs) if m else None, m, _ptr(self.d_seg),
+                                                      self.n_blocks, self.hash_count, t0, t1,
                                                       _ptr(self.out), _ptr(ws), ws.numel(),
                                                       _stream_handle()),
                   "tkv_amq_bloom_build_range_records")
 
-    def build_owned(self, owned):
-        """The range build from what exchange() returned (records or keys)."""
+    def _build_part(self, units, j):
+        t0, t1 = self.part_tiles(j)
         if self.records:
-            self.build_range_records(owned)
+            self.build_range_records(units, t0, t1)
         else:
-            self.build_range(owned)
+            self.build_range(units, t0, t1)
+
+    def build_owned(self, owned, sub):
+        """This rank's parts from what exchange() returned: part j's units are, for every
+        sender, the sub[sender, j] units after that sender's parts < j."""
+        import torch
+        W, g = sub.shape
+        if g == 1:
+            self._build_part(owned, 0)
+            return
+        counts = sub.reshape(-1).tolist()
+        starts = [0]
+        for c in counts:
+            starts.append(starts[-1] + int(c))
+        for j in range(g):
+            pieces = [owned[starts[s * g + j]:starts[s * g + j] + int(counts[s * g + j])] for s in range(W)]
+            part = pieces[0] if W == 1 else torch.cat(pieces)
+            self._build_part(part, j)
 
     @property
     def _collective(self) -> bool:
@@ -243,12 +295,17 @@ class HashShardedBloom:
         return self.world > 1 or (dist.is_available() and dist.is_initialized())
 
     def local_build(self, keys):
-        """route + exchange + range build: after it, this rank's byte range of the bitmap is final."""
+        """route + exchange + part builds: after it, this rank's byte range of the bitmap is
+        final."""
         if not self._collective:
-            self.build_range(keys)
+            if keys.dim() == 2 and keys.shape[1] == 16 and self.T <= KEY_RANGE_MAX_TILES:
+                self.build_range(keys, 0, self.T)  # the partition makes the records itself
+                return
+            routed, pc = self.route(keys)  # (checks the key shape)
+            self.build_owned(routed, pc.cpu().view(1, self.g))
             return
-        routed, sc = self.route(keys)
-        self.build_owned(self.exchange(routed, sc))
+        routed, pc = self.route(keys)
+        self.build_owned(*self.exchange(routed, pc))
 
     def allgather(self):
         """Every rank's bitmap range -> the whole filter payload (header + bitmap) on every rank.
