@@ -198,7 +198,7 @@ def cpu_baseline(kind, bpk, cap, keys_host, counts, threads, leaf_keys=SEG_KEYS)
         out = np.empty(int(sizes.sum()), np.uint8)
         t0 = time.perf_counter()
         st, _ = O.build_segments(kind, keys_host, sb, bpk, offs, sizes, 0, n_threads=nthr,
-                                 out=out, L=L)
+                                 out=out, L=L, baseline=kind == 1)
         dt = time.perf_counter() - t0
         assert st == 0, st
         return int(sb[-1]), dt
@@ -217,8 +217,10 @@ def cpu_baseline(kind, bpk, cap, keys_host, counts, threads, leaf_keys=SEG_KEYS)
     used = min(threads, ns)  # one filter per thread at a time
     res = {"value": round(nk / dt / 1e6, 2), "unit": "Mkeys/s", "cores": used,
            "kind": "port",
-           "sample": f"{ns} leaves x {leaf_keys} keys ({nk} keys) of the same workload, C oracle "
-                     f"(oracle/tkv_amq_oracle.c, "
+           "sample": f"{ns} leaves x {leaf_keys} keys ({nk} keys) of the same workload, "
+                     + ("BMI2 VQF build (oracle/tkv_amq_baseline.c: pdep/tzcnt select, POPCNT, "
+                        "unrolled XXH64; byte-equal to the oracle) " if kind == 1 else "C oracle ")
+                     + f"(oracle/tkv_amq_oracle.c, "
                      f"{'-O3 -march=native -mbmi2 -mavx2' if native else '-O3 -march=x86-64-v3 (native build failed)'}), "
                      f"{used} threads, {dt:.2f} s wall",
            "host": share,

@@ -198,8 +198,8 @@ int tkv_amq_build_check(int kind, const void* d_workspace, uint64_t workspace_by
  * (d_part_counts[n_parts], u32, device) -- the send counts of the all-to-all that follows.
  * d_seg is the whole filter's segment (device), n_blocks its n_blocks (host copy). */
 uint32_t tkv_amq_bloom_tile_blocks(void);
-/* the most tiles one range build takes: from records (records != 0; the record's tile field)
- * or from 16-byte keys (the partition's LDS tile table) */
+/* the most tiles one range build takes, from records (records != 0) or from 16-byte keys: the
+ * partition's LDS tile table (6,400 tiles) */
 uint32_t tkv_amq_bloom_range_max_tiles(int records);
 uint64_t tkv_amq_bloom_route_ws_bytes(uint64_t n_keys, uint32_t n_parts);
 int tkv_amq_bloom_route(const uint8_t* d_keys16, uint64_t n_keys, const tkv_amq_segment* d_seg,
@@ -228,8 +228,8 @@ int tkv_amq_bloom_build_range(const uint8_t* d_keys16, uint64_t n_keys, const tk
  * instead of 16 and the owner does not hash again; tkv_amq_bloom_build_range_records builds the
  * owner's tiles from the records it received.  The record carries its tile relative to its
  * part, so a part -- and a range built from records -- holds at most
- * tkv_amq_bloom_range_max_tiles(1) tiles (8,192: 1 GiB of filter); a route with larger parts is
- * refused (InvalidArgument). */
+ * tkv_amq_bloom_range_max_tiles(1) tiles (6,400: 800 MiB of filter); a route with larger parts
+ * is refused (InvalidArgument). */
 uint64_t tkv_amq_bloom_route_records_ws_bytes(uint64_t n_keys, uint32_t n_parts);
 int tkv_amq_bloom_route_records(const uint8_t* d_keys16, uint64_t n_keys, const tkv_amq_segment* d_seg,
                                 uint32_t n_blocks, uint32_t hash_count, uint32_t n_parts,

@@ -111,6 +111,10 @@ def _load(path):
     L.tkvo_tree_filter_bits_per_key.argtypes = [u64, i32]
     L.tkvo_build_segments.restype = i32
     L.tkvo_build_segments.argtypes = [i32, vp, vp, u32, u32, vp, vp, vp, vp, i32]
+    L.tkvb_vqf_build_payload16.restype = i32
+    L.tkvb_vqf_build_payload16.argtypes = [vp, u64, u64, u64, vp, u64]
+    L.tkvb_vqf_build_segments.restype = i32
+    L.tkvb_vqf_build_segments.argtypes = [vp, vp, u32, u32, vp, vp, vp, vp, i32]
     L.tkvo_probe_segments.restype = i32
     L.tkvo_probe_segments.argtypes = [i32, vp, vp, vp, vp, u64, vp, i32]
     return L
@@ -183,6 +187,14 @@ def vqf_build(keys, n: int, bpk: int, payload_capacity: int, src_page_id: int = 
     return st, out, pl
 
 
+def vqf_build_baseline(keys16, n: int, bpk: int, payload_capacity: int, src_page_id: int = 0,
+                       L=None):
+    """tkv_amq_baseline.c's BMI2 VQF build (the CPU baseline bench.py times)."""
+    out = np.zeros(payload_capacity, dtype=np.uint8)
+    st = (L or lib()).tkvb_vqf_build_payload16(_p(keys16), n, bpk, src_page_id, _p(out), payload_capacity)
+    return st, out
+
+
 def vqf_is_present(payload: np.ndarray, hash_val: int) -> int:
     return lib().tkvo_vqf_is_present_payload(_p(payload), hash_val)
 
@@ -190,12 +202,18 @@ def vqf_is_present(payload: np.ndarray, hash_val: int) -> int:
 def build_segments(kind: int, keys16: np.ndarray, seg_begin: np.ndarray, bpk: int,
                    out_offset: np.ndarray, out_capacity: np.ndarray, total_bytes: int,
                    src_page_id: np.ndarray | None = None, n_threads: int = 8,
-                   out: np.ndarray | None = None, L=None):
+                   out: np.ndarray | None = None, L=None, baseline: bool = False):
+    """The oracle over a batch of 16-byte-key leaves (baseline=True, VQF: the BMI2 baseline)."""
     seg_begin = np.ascontiguousarray(seg_begin, dtype=np.uint64)
     out_offset = np.ascontiguousarray(out_offset, dtype=np.uint64)
     out_capacity = np.ascontiguousarray(out_capacity, dtype=np.uint64)
     if out is None:
         out = np.zeros(total_bytes, dtype=np.uint8)
+    if kind == VQF and baseline:
+        st = (L or lib()).tkvb_vqf_build_segments(_p(keys16), _p(seg_begin), len(seg_begin) - 1, bpk,
+                                                  _p(src_page_id), _p(out), _p(out_offset),
+                                                  _p(out_capacity), n_threads)
+        return st, out
     st = (L or lib()).tkvo_build_segments(kind, _p(keys16), _p(seg_begin), len(seg_begin) - 1, bpk,
                                    _p(src_page_id), _p(out), _p(out_offset), _p(out_capacity),
                                    n_threads)

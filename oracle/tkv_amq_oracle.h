@@ -105,6 +105,15 @@ int tkvo_probe_segments(int kind, const uint8_t* filters, const uint64_t* out_of
                         const uint8_t* queries16, const uint32_t* query_seg, uint64_t n_queries,
                         uint8_t* result, int n_threads);
 
+/* tkv_amq_baseline.c: the VQF build as an optimised CPU build runs it (BMI2 pdep/tzcnt select,
+ * POPCNT, unrolled 16-byte XXH64, multiply-high remainder) -- the cpu_baseline bench.py times;
+ * byte-identical to tkvo_vqf_build_payload for 16-byte keys */
+int tkvb_vqf_build_payload16(const uint8_t* keys, uint64_t n, uint64_t bpk, uint64_t src_page_id,
+                             uint8_t* out, uint64_t cap);
+int tkvb_vqf_build_segments(const uint8_t* keys16, const uint64_t* seg_begin, uint32_t n_segs,
+                            uint32_t bpk, const uint64_t* src_page_id, uint8_t* out,
+                            const uint64_t* out_offset, const uint64_t* out_capacity, int n_threads);
+
 #ifdef __cplusplus
 }
 #endif

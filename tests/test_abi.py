@@ -119,11 +119,11 @@ def test_hash_shard_constants_match_library(amq):
     routed = amq.plan_filters(amq.BLOOM, [1_750_000_000], 12)
     assert direct.workspace_bytes >= 16 * 100_000_000
     assert routed.workspace_bytes >= 16 * 1_750_000_000 * 2
-    # a range build from records past 8,192 tiles, or from keys past 20,000, is refused
-    assert L.tkv_amq_bloom_build_range_records_ws_bytes(1000, 0, 8192) > 0
-    assert L.tkv_amq_bloom_build_range_records_ws_bytes(1000, 0, 8193) == 0
-    assert L.tkv_amq_bloom_build_range_ws_bytes(1000, 5, 20005) > 0
-    assert L.tkv_amq_bloom_build_range_ws_bytes(1000, 5, 20006) == 0
+    # a range build past 6,400 tiles (the partition's LDS tile table) is refused
+    assert L.tkv_amq_bloom_build_range_records_ws_bytes(1000, 0, 6400) > 0
+    assert L.tkv_amq_bloom_build_range_records_ws_bytes(1000, 0, 6401) == 0
+    assert L.tkv_amq_bloom_build_range_ws_bytes(1000, 5, 6405) > 0
+    assert L.tkv_amq_bloom_build_range_ws_bytes(1000, 5, 6406) == 0
 
 
 def test_device_calls_fail_loudly_without_gpu(amq):

@@ -122,8 +122,8 @@ def test_hash_shard_tiles_cover_the_filter():
 
 
 def test_hash_shard_parts_per_rank():
-    """A rank's range is cut into g parts when it exceeds what one range build takes (8,192
-    tiles from 12-byte records, 20,000 from 16-byte keys): BASELINE config 5 (1B keys at
+    """A rank's range is cut into g parts when it exceeds what one range build takes (6,400
+    tiles, the partition's LDS tile table): BASELINE config 5 (1B keys at
     12 bits/key, 11,445 tiles) takes two parts on one rank and one part from two ranks up; every
     part holds at most the cap, the parts of all ranks tile the filter, and rank r's range is
     its parts' union."""
@@ -133,7 +133,7 @@ def test_hash_shard_parts_per_rank():
     assert hash_shard_plan(nb_1b, 1) == (11445, 2, 5723)
     assert hash_shard_plan(nb_1b, 2)[1:] == (1, 5723)
     assert hash_shard_plan(nb_1b, 8)[1:] == (1, 1431)
-    assert hash_shard_plan(nb_1b, 1, records=False) == (11445, 1, 11445)
+    assert hash_shard_plan(nb_1b, 1, records=False) == (11445, 2, 5723)
     for nb in [1, 5000, nb_1b, 3 * nb_1b, 40_000_000 * 2048]:
         for world in [1, 2, 3, 8]:
             for rec in (True, False):

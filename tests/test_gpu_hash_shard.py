@@ -264,3 +264,19 @@ def test_route_records_refuse_k_above_8(amq, torch):
                                        int(plan.segs[0]["n_blocks"]), 11, 2, _ptr(recs), _ptr(counts),
                                        _ptr(ws), ws.numel(), _stream_handle())
     assert st == amq.abi.INVALID_ARGUMENT
+
+
+@pytest.mark.parametrize("n_keys,bpk", [(1_200_000, 12), (700_000, 10)])
+def test_hash_sharded_world1_24_byte_keys(oracle, amq, torch, n_keys, bpk):
+    """HashShardedBloom without a process group (the first thing a caller tries) with [n, 24]
+    keys: the range build reads 16-byte keys only, so the keys go through the record route
+    (tkv_amq_bloom_route_records_ex) and the part builds; the filter equals the oracle's.
+    Before round 4 such keys were read as 16-byte keys at a 16-byte stride."""
+    from turtle_kv_amd.dist import HashShardedBloom
+    rng = np.random.default_rng(n_keys)
+    kn = rng.integers(0, 256, (n_keys, 24), dtype=np.uint8)
+    hs = HashShardedBloom(n_keys, bpk, 1, 0, "cuda")
+    filt = hs.build(torch.from_numpy(kn).cuda())
+    torch.cuda.synchronize()
+    st, ref = oracle.bloom_build(kn, n_keys, bpk, src_page_id=0, stride=24)
+    assert st == 0 and filt.cpu().numpy().tobytes() == ref.tobytes()

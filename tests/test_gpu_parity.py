@@ -540,14 +540,14 @@ def sampled_tiles_equal_oracle(oracle, out, n, bpk, seed, n_random=6):
     return T
 
 
-@pytest.mark.parametrize("n,bpk,parts", [(108_000_000, 10, 1), (1_750_000_000, 12, 3),
-                                         (700_000_000, 64, 6)])
+@pytest.mark.parametrize("n,bpk,parts", [(108_000_000, 10, 1), (1_750_000_000, 12, 4),
+                                         (700_000_000, 64, 7)])
 def test_bloom_monolithic_large_sampled_oracle(oracle, amq, torch, n, bpk, parts):
     """Full-size monolithic filters against the oracle on eight sampled tiles and the header:
     108M keys at 10 bits/key (1,030 tiles: the partition reads the keys), 1.75B keys at 12
-    bits/key (20,028 tiles, beyond one partition's 20,000-tile table: routed as 12-byte records
-    into 3 parts, each built from its records, its count read on the device) and 700M keys at
-    64 bits/key (42,725 tiles, k = 44: the 16-byte keys themselves routed into 6 parts)."""
+    bits/key (20,028 tiles, beyond one partition's 6,400-tile table: routed as 12-byte records
+    into 4 parts, each built from its records, its count read on the device) and 700M keys at
+    64 bits/key (42,725 tiles, k = 44: the 16-byte keys themselves routed into 7 parts)."""
     from turtle_kv_amd import abi
     L = abi.lib()
     seed = 16
@@ -564,358 +564,6 @@ def test_bloom_monolithic_large_sampled_oracle(oracle, amq, torch, n, bpk, parts
     assert sampled_tiles_equal_oracle(oracle, out, n, bpk, seed) == T
     del out
     torch.cuda.empty_cache()
-
-
-@pytest.mark.parametrize("shape", ["k16", "k24", "var"])
-def test_bloom_leaf_kernel_widths(oracle, amq, torch, n_leaves, shape):
-    """Below 1024 leaves each leaf's keys are split over several workgroups whose images are
-    ORed by the last one (bloom_build_split); from 1024 leaves one workgroup per leaf
-    (bloom_build_lds).  Both, every key shape, ragged leaves, against the oracle (sampled)."""
-    rng = np.random.default_rng(n_leaves)
-    counts = [int(c) for c in rng.integers(0, 3000, n_leaves)]
-    counts[0], counts[1], counts[-1] = 0, 16384, 1
-    n = sum(counts)
-    offs = None
-    if shape == "k16":
-        keys, stride = oracle.gen_keys16(42, 0, n), 16
-    elif shape == "k24":
-        keys, stride = rng.integers(0, 256, (n, 24), dtype=np.uint8), 24
-    else:
-        lens = rng.integers(0, 40, n)
-        keys, stride = rng.integers(0, 256, int(lens.sum()), dtype=np.uint8), 0
-        offs = np.zeros(n + 1, np.int64)
-        offs[1:] = np.cumsum(lens)
-    plan, out = gpu_build(amq, torch, 0, torch.from_numpy(keys).cuda(), counts, 10,
-                          offsets_t=None if offs is None else torch.from_numpy(offs).cuda())
-    sb = seg_bounds(counts)
-    for s in sorted({0, 1, n_leaves - 1, *rng.integers(0, n_leaves, 12).tolist()}):
-        b, c = int(sb[s]), counts[s]
-        if offs is None:
-            st, ref = oracle.bloom_build(keys[b:], c, 10, src_page_id=s, stride=stride)
-        else:
-            o = (offs[b:b + c + 1] - offs[b]).astype(np.uint64)
-            st, ref = oracle.bloom_build(keys[int(offs[b]):], c, 10, src_page_id=s, offsets=o, stride=0)
-        assert st == 0
-        assert segment_bytes(plan, out, s) == ref.tobytes(), f"leaf {s}"
-
-
-@pytest.mark.parametrize("counts", [[16384], [16384, 9000, 1, 0, 52000], [3000] * 200,
-                                    [100000], [120000, 700, 0, 5]])
-def test_bloom_split_matches_unsplit(oracle, amq, torch, counts):
-    """The split build (workspace given) and the one-workgroup / atomic builds (no workspace)
-    write the same bytes; the split one also equals the oracle (a 52K-key leaf: a 64 KiB
-    image; 100K- and 120K-key leaves: 125 and 150 KB images, up to the 160 KB the split parts
-    take in LDS)."""
-    keys = oracle.gen_keys16(9, 0, sum(counts))
-    kt = torch.from_numpy(keys).cuda()
-    plan = amq.plan_filters(0, counts, 10)
-    assert plan.workspace_bytes > 0
-    a = amq.build_all_filters(plan, amq.KeyBatch.fixed(kt))
-    L, F = amq.abi.lib(), amq.filters
-    b = torch.zeros_like(a)
-    st = L.tkv_amq_build(0, F._ptr(kt), None, 16, kt.shape[0], F._ptr(plan.device_segs()), plan.n_segs,
-                         plan.max_seg_blocks, F._ptr(b), None, 0, F._stream_handle())
-    assert st == 0
-    torch.cuda.synchronize()
-    an, bn = a.cpu().numpy(), b.cpu().numpy()
-    sb = seg_bounds(counts)
-    for s in range(len(counts)):
-        assert segment_bytes(plan, an, s) == segment_bytes(plan, bn, s), f"leaf {s}"
-        st, ref = oracle.bloom_build(keys[int(sb[s]):], counts[s], 10, src_page_id=s)
-        assert segment_bytes(plan, an, s) == ref.tobytes(), f"leaf {s}"
-
-
-def sorted_keys(oracle, seed, counts):
-    keys = oracle.gen_keys16(seed, 0, sum(counts))
-    oracle.sort_segments(keys, seg_bounds(counts))
-    return keys
-
-
-@pytest.mark.parametrize("bpk,cap", [(12, 32704), (13, 32704), (16, 32704), (22, 65472),
-                                     (24, 65472), (32, 65472), (12, 16320), (12, 8128)])
-def test_vqf_parity(oracle, amq, torch, bpk, cap):
-    counts = RAGGED
-    keys = sorted_keys(oracle, 42, counts)
-    src = [500 + i for i in range(len(counts))]
-    ref = oracle_per_segment(oracle, 1, keys, counts, bpk, cap=cap, src=src)
-    plan, out = gpu_build(amq, torch, 1, torch.from_numpy(keys).cuda(), counts, bpk, cap=cap,
-                          src=src)
-    assert_same(plan, out, ref)
-
-
-@pytest.mark.parametrize("bpk,cap", [(22, 65472), (32, 16320)])
-def test_vqf_parity_fused_16bit_tags(oracle, amq, torch, bpk, cap):
-    """16-bit tags (and, at 32 bpk in 16 KB pages, 8-bit truncated and 16-bit leaves in one
-    batch) through the fused LDS place path: every leaf small enough that the batch's LDS
-    image fits."""
-    counts = [8000, 777, 5000, 1, 0, 64, 7000]
-    keys = sorted_keys(oracle, 43, counts)
-    src = [900 + i for i in range(len(counts))]
-    ref = oracle_per_segment(oracle, 1, keys, counts, bpk, cap=cap, src=src)
-    plan, out = gpu_build(amq, torch, 1, torch.from_numpy(keys).cuda(), counts, bpk, cap=cap,
-                          src=src)
-    assert plan.max_seg_blocks * 132 <= 80 * 1024, "batch should take the fused place"
-    assert 16 in set(plan.segs["tag_bits"].tolist())
-    assert_same(plan, out, ref)
-
-
-def test_vqf_config1_sha256(oracle, amq, torch):
-    g = json.load(open(os.path.join(GOLDEN, "filters.json")))["config1_vqf12_1M"]
-    n = g["n_keys"]
-    counts = [S] * (n // S) + [n % S]
-    keys = sorted_keys(oracle, 42, counts)
-    plan = amq.plan_filters(1, counts, 12, payload_capacity=32704, out_stride=32704)
-    out = amq.build_all_filters(plan, amq.KeyBatch.fixed(torch.from_numpy(keys).cuda()))
-    o = out.cpu().numpy()
-    # the golden buffer has zero tails after each payload; the GPU writes payloads only
-    for s in range(plan.n_segs):
-        seg = plan.segs[s]
-        o[int(seg["out_offset"]) + int(seg["payload_bytes"]):int(seg["out_offset"]) + 32704] = 0
-    assert hashlib.sha256(o.tobytes()).hexdigest() == g["sha256"]
-
-
-def test_vqf_unsorted_and_duplicate_keys(oracle, amq, torch):
-    # insertion order matters for VQF: unsorted input and duplicate keys must still match
-    counts = [16384, 9000]
-    keys = oracle.gen_keys16(77, 0, sum(counts))
-    keys[100:200] = keys[0:100]
-    ref = oracle_per_segment(oracle, 1, keys, counts, 12)
-    plan, out = gpu_build(amq, torch, 1, torch.from_numpy(keys).cuda(), counts, 12)
-    assert_same(plan, out, ref)
-
-
-@pytest.mark.parametrize("n_leaves", [40, 768, 769, 4097])
-@pytest.mark.parametrize("shape", ["k16", "k24", "k20", "var"])
-def test_vqf_decide_paths(oracle, amq, torch, n_leaves, shape):
-    """Batches of up to 768 leaves (4,096 for keys read where they are hashed: 20-byte and
-    variable-length ones) take vqf_decide_ring (producer waves locate and match each 64-key
-    chunk, one decider wave replays the insertion order), larger ones vqf_decide (one wave
-    per leaf); 16- and 24-byte keys are loaded ahead of their hash.  8- and 16-bit tags (12 / 22 bits per key), leaves of <= 512 and
-    > 512 blocks (the producers' 9- and 11-bit matches, vqf_decide's LDS lane-mask table past
-    512 blocks; a 30000-key leaf of ~740 blocks, placed in LDS), 4- and 8-byte key records,
-    ragged leaves, every key shape, sampled against the oracle.  (The unfused place and the
-    ballot matches: test_vqf_leaf_beyond_ring_blocks.)"""
-    rng = np.random.default_rng(1000 + n_leaves)
-    counts = [int(c) for c in rng.integers(0, 3000, n_leaves)]
-    counts[0], counts[1], counts[2], counts[-1] = 0, 16384, 30000, 1
-    n = sum(counts)
-    offs = None
-    if shape == "k16":
-        keys, stride = oracle.gen_keys16(5, 0, n), 16
-    elif shape in ("k24", "k20"):
-        stride = int(shape[1:])
-        keys = rng.integers(0, 256, (n, stride), dtype=np.uint8)
-    else:  # >= 6 bytes: duplicates of very short keys would overflow a block (as in the oracle)
-        lens = rng.integers(6, 40, n)
-        keys, stride = rng.integers(0, 256, int(lens.sum()), dtype=np.uint8), 0
-        offs = np.zeros(n + 1, np.int64)
-        offs[1:] = np.cumsum(lens)
-    sb = seg_bounds(counts)
-    for bpk in (12, 22):
-        # (4,097 random leaves hold one whose 16-bit filter overflows -- vqf_insert fails in the
-        # oracle too, as in the reference; the leaves compared are those the oracle builds)
-        plan, out = gpu_build(amq, torch, 1, torch.from_numpy(keys).cuda(), counts, bpk, cap=65472,
-                              offsets_t=None if offs is None else torch.from_numpy(offs).cuda(),
-                              check=n_leaves < 4097)
-        if bpk == 12:
-            assert plan.segs["n_blocks"][2] > 512 and plan.segs["n_blocks"][1] <= 512
-        else:
-            assert plan.segs["n_blocks"][1] > 512 and 16 in set(plan.segs["tag_bits"].tolist())
-        for s in sorted({0, 1, 2, n_leaves - 1, *rng.integers(0, n_leaves, 10).tolist()}):
-            b, c = int(sb[s]), counts[s]
-            if offs is None:
-                st, ref, p = oracle.vqf_build(keys[b:], c, bpk, 65472, src_page_id=s, stride=stride)
-            else:
-                o = (offs[b:b + c + 1] - offs[b]).astype(np.uint64)
-                st, ref, p = oracle.vqf_build(keys[int(offs[b]):], c, bpk, 65472, src_page_id=s,
-                                              offsets=o, stride=0)
-            if st != 0 and n_leaves == 4097:
-                continue
-            assert st == 0
-            assert segment_bytes(plan, out, s) == ref[:p.payload_used].tobytes(), f"bpk {bpk} leaf {s}"
-
-
-@pytest.mark.parametrize("n_leaves", [1, 256, 257, 512])
-@pytest.mark.parametrize("edge", ["b402", "tbl", "ring512", "ring960", "plain961"])
-@pytest.mark.parametrize("bpk", [12, 22])
-def test_vqf_ring_place_classes(oracle, amq, torch, n_leaves, edge, bpk):
-    """Batches of <= 256 leaves whose largest leaf has <= 884 blocks take vqf_ring_place
-    (decide and place in one workgroup per leaf, entries straight into the LDS image; <= 512
-    blocks: the producers' LDS match tables), batches of up to 512 leaves of <= 420 blocks two
-    such workgroups per CU (b402: the bench layout's 16K-key leaves), others vqf_decide_ring +
-    vqf_place_fused.  The batch's largest leaf sits at each threshold (512 / 513 / 960 / 961
-    blocks in 64 KiB pages), 8- and 16-bit tags; byte-equal to the oracle."""
-    big = {12: {"b402": 16384, "tbl": 20889, "ring512": 20890, "ring960": 39167, "plain961": 39168},
-           22: {"b402": 9000, "tbl": 11729, "ring512": 11730, "ring960": 21992, "plain961": 21993}}[bpk][edge]
-    rng = np.random.default_rng(7 + n_leaves)
-    counts = [big] + [int(c) for c in rng.integers(0, 3000, n_leaves - 1)]
-    if n_leaves > 2:
-        counts[1] = 0
-    keys = oracle.gen_keys16(9, 0, sum(counts))
-    plan, out = gpu_build(amq, torch, 1, torch.from_numpy(keys).cuda(), counts, bpk, cap=65472)
-    want = {"b402": None, "tbl": 512, "ring512": 513, "ring960": 960, "plain961": 961}[edge]
-    if want is not None:
-        assert int(plan.segs["n_blocks"].max()) == want
-    else:
-        assert int(plan.segs["n_blocks"].max()) <= 420
-    sb = seg_bounds(counts)
-    for s in sorted({0, n_leaves - 1, *rng.integers(0, n_leaves, 4).tolist()}):
-        st, ref, p = oracle.vqf_build(keys[int(sb[s]):], counts[s], bpk, 65472, src_page_id=s)
-        assert st == 0
-        assert segment_bytes(plan, out, s) == ref[:p.payload_used].tobytes(), f"leaf {s}"
-
-
-@pytest.mark.parametrize("big", [100000, 260000])
-@pytest.mark.parametrize("n_leaves", [4, 800])
-@pytest.mark.parametrize("bpk", [12, 22])
-def test_vqf_leaf_beyond_ring_blocks(oracle, amq, torch, n_leaves, big, bpk):
-    """A 100000-key leaf in 1 MiB pages has 2451 blocks: more than the ring kernel's count
-    table holds, so its wave 0 runs vqf_decide_body (block-id ballots, no LDS match table);
-    in a batch of 800 leaves vqf_decide does the same.  Its LDS place is split over two
-    workgroups per leaf; a 260000-key leaf (6373 blocks, beyond four) takes the unfused
-    scatter + place.  At 22 bits/key: 16-bit tags, 4365 / 11349 blocks."""
-    counts = [big, 500, 0, 16384] + [300] * (n_leaves - 4)
-    keys = oracle.gen_keys16(6, 0, sum(counts))
-    plan, out = gpu_build(amq, torch, 1, torch.from_numpy(keys).cuda(), counts, bpk, cap=1 << 20)
-    assert plan.segs["n_blocks"][0] > 2048 and plan.segs["hash_val_shift"][0] == 0
-    assert (plan.segs["n_blocks"][0] > 4964) == (big == 260000)
-    sb = seg_bounds(counts)
-    for s in sorted({0, 1, 2, 3, n_leaves - 1}):
-        st, ref, p = oracle.vqf_build(keys[int(sb[s]):], counts[s], bpk, 1 << 20, src_page_id=s)
-        assert st == 0
-        assert segment_bytes(plan, out, s) == ref[:p.payload_used].tobytes(), f"leaf {s}"
-
-
-@pytest.mark.parametrize("big,bpk,cap", [(700_000, 12, 4 << 20), (700_000, 22, 4 << 20),
-                                         (7_000_000, 12, 16 << 20)])
-def test_vqf_huge_leaf(oracle, amq, torch, big, bpk, cap):
-    """Leaves past vqf_decide's u32 LDS count table (16,384 blocks), which round 2 refused:
-    a 700K-key leaf (17,157 blocks at 12 bits/key, 30,553 with 16-bit tags at 22) keeps u8
-    counts in LDS; a 7M-key leaf (171,569 blocks) keeps them in the workspace's block records
-    (agent-scope atomics).  Both are placed by the multi-workgroup unfused place, in a batch
-    with small leaves, and must equal the oracle byte for byte."""
-    counts = [big, 500, 0, 16384] if big < 1_000_000 else [big, 3000]
-    keys = oracle.gen_keys16(8, 0, sum(counts))
-    plan, out = gpu_build(amq, torch, 1, torch.from_numpy(keys).cuda(), counts, bpk, cap=cap)
-    nb = int(plan.segs["n_blocks"][0])
-    assert nb > 16384 and (nb > 160 * 1024) == (big > 1_000_000)
-    sb = seg_bounds(counts)
-    for s in range(len(counts)):
-        st, ref, p = oracle.vqf_build(keys[int(sb[s]):], counts[s], bpk, cap, src_page_id=s)
-        assert st == 0
-        assert segment_bytes(plan, out, s) == ref[:p.payload_used].tobytes(), f"leaf {s}"
-
-
-def probe_inputs(oracle, n_keys, counts, n_miss):
-    hits = np.arange(n_keys)
-    seg_of = np.repeat(np.arange(len(counts)), counts)
-    miss = oracle.gen_keys16(43, 0, n_miss)
-    rng = np.random.default_rng(44)
-    miss_seg = rng.integers(0, len(counts), n_miss)
-    return hits, seg_of, miss, miss_seg
-
-
-@pytest.mark.parametrize("kind,bpk", [(0, 10), (0, 12), (1, 12), (1, 24)])
-def test_probe_parity(oracle, amq, torch, kind, bpk):
-    counts = [S] * 8 + [8448, 0, 5]
-    keys = sorted_keys(oracle, 42, counts) if kind else oracle.gen_keys16(42, 0, sum(counts))
-    cap = 65472
-    plan = amq.plan_filters(kind, counts, bpk, payload_capacity=cap if kind else 0)
-    filt = amq.build_all_filters(plan, amq.KeyBatch.fixed(torch.from_numpy(keys).cuda()))
-    n = sum(counts)
-    _, seg_of, miss, miss_seg = probe_inputs(oracle, n, counts, 200000)
-    q = np.concatenate([keys, miss])
-    qs = np.concatenate([seg_of, miss_seg]).astype(np.uint32)
-    res = amq.probe_filters(plan, filt, amq.KeyBatch.fixed(torch.from_numpy(q).cuda()),
-                            torch.from_numpy(qs.astype(np.int32)).cuda()).cpu().numpy()
-    # oracle probe over the GPU-built filter bytes (which equal the oracle's, tested above)
-    st, ref = oracle.probe_segments(kind, filt.cpu().numpy(), plan.segs["out_offset"], q, qs)
-    assert st == 0
-    assert np.array_equal(res, ref)
-    assert res[:n].all(), "false negative"
-    fpr = res[n:].mean()
-    assert fpr < (0.02 if kind == 0 else 0.01)
-    if kind == 1:
-        hv = amq.vqf_hash_val(amq.KeyBatch.fixed(torch.from_numpy(q).cuda()))
-        res2 = amq.vqf_probe_hashed(plan, filt, hv, torch.from_numpy(qs.astype(np.int32)).cuda())
-        assert np.array_equal(res2.cpu().numpy(), ref)
-
-
-def test_vqf_hash_matches_xxhash(amq, torch):
-    import xxhash
-    keys = [ln.strip().encode() for ln in open(os.path.join(GOLDEN, "workload_e_keys.txt")) if ln.strip()]
-    kb = amq.KeyBatch.from_host(keys[:1000])
-    h = amq.vqf_hash_val(kb).cpu().numpy().view(np.uint64)
-    assert [int(x) for x in h] == [xxhash.xxh64_intdigest(k, VQF_SEED) for k in keys[:1000]]
-    h16 = amq.vqf_hash_val(amq.KeyBatch.fixed(amq.gen_keys16(1, 0, 1000))).cpu().numpy().view(np.uint64)
-    k16 = amq.gen_keys16(1, 0, 1000).cpu().numpy()
-    assert [int(x) for x in h16] == [xxhash.xxh64_intdigest(k.tobytes(), VQF_SEED) for k in k16]
-
-
-@pytest.mark.parametrize("n,bpk,seed", [(600000, 10, 8), (3000000, 10, 9), (1500000, 12, 10),
-                                         (1100000, 5, 11), (90000, 64, 12)])
-def test_bloom_monolithic_partitioned(oracle, amq, torch, n, bpk, seed):
-    """One filter of 16-byte keys larger than four LDS windows (640 KB; smaller ones take the
-    window path, tests/test_gpu_window.py): the hash-once record path (bloom_part_keys16 /
-    bloom_tile), byte-identical to the oracle.  Covers a ragged last tile, k = 7 / 8 /
-    generic <= 8 (12-byte bit records) and k = 44 (the keys themselves are partitioned and
-    hashed per tile), and 29 tiles over 92 partition workgroups."""
-    keys = oracle.gen_keys16(seed, 0, n)
-    ref = oracle_per_segment(oracle, 0, keys, [n], bpk)
-    plan, out = gpu_build(amq, torch, 0, torch.from_numpy(keys).cuda(), [n], bpk)
-    assert plan.max_seg_blocks * 64 > 160 * 1024
-    assert plan.workspace_bytes >= 16 * n  # the partitioned path's workspace
-    assert_same(plan, out, ref)
-
-
-@pytest.mark.parametrize("n,bpk,dup", [(600000, 10, 0), (1500000, 12, 0), (1100000, 5, 0),
-                                       (400000, 14, 0), (90000, 64, 0), (700000, 10, 200000),
-                                       (450000, 14, 150000)])
-def test_bloom_monolithic_k24(oracle, amq, torch, n, bpk, dup):
-    """One filter of 24-byte keys (TurtleKV's default key size) beyond four windows: the record
-    path's own partition kernel (bloom_part_keys24) hashes each key once into a 12-byte bit
-    record; k > 8 (14 and 64 bits/key) keeps the first eight bits in the records and
-    bloom_overflow sets the others; duplicates overflow the regions of one tile.
-    Byte-identical to the oracle (round 2: device atomics)."""
-    rng = np.random.default_rng(n + bpk)
-    keys = rng.integers(0, 256, (n, 24), dtype=np.uint8)
-    if dup:
-        keys[n - dup:] = keys[n // 3]
-    ref = oracle_per_segment(oracle, 0, keys, [n], bpk, stride=24)
-    plan, out = gpu_build(amq, torch, 0, torch.from_numpy(keys).cuda(), [n], bpk)
-    assert plan.max_seg_blocks * 64 > 4 * 160 * 1024
-    assert_same(plan, out, ref)
-
-
-def test_bloom_monolithic_duplicate_keys(oracle, amq, torch):
-    """Every key identical (one tile receives the whole batch: its regions overflow and the
-    overflow lists are applied with device atomics) and a few distinct ones."""
-    n = 200000
-    keys = np.repeat(oracle.gen_keys16(13, 0, 1), n, axis=0)
-    keys[::50000] = oracle.gen_keys16(14, 0, len(keys[::50000]))
-    ref = oracle_per_segment(oracle, 0, keys, [n], 10)
-    plan, out = gpu_build(amq, torch, 0, torch.from_numpy(keys).cuda(), [n], 10)
-    assert_same(plan, out, ref)
-
-
-@pytest.mark.parametrize("n,bpk", [(108_000_000, 10), (30_000_000, 64)])
-def test_bloom_monolithic_large_matches_atomic_path(amq, torch, n, bpk):
-    """Full-size monolithic filters against the device-atomic path for the same keys (planned
-    as a two-leaf batch, which routes the big leaf through bloom_global_set): 108M keys at 10
-    bits/key (2,060 tiles, the record path) and 30M keys at 64 bits/key (3,663 tiles, beyond
-    the record path's 3,584: the count / scatter / hash-in-tile path)."""
-    keys = amq.KeyBatch.fixed(amq.gen_keys16(16, 0, n + 1))
-    mono = amq.plan_filters(0, [n], bpk)
-    tiles = -(-mono.max_seg_blocks // 1024)
-    assert (tiles > 3584) == (bpk == 64)
-    kb = amq.KeyBatch.fixed(keys.data[:n])
-    a = amq.build_all_filters(mono, kb)
-    two = amq.plan_filters(0, [n, 1], bpk)
-    assert two.workspace_bytes == 0
-    b = amq.build_all_filters(two, keys)
-    pa = int(mono.segs[0]["payload_bytes"])
-    assert int(two.segs[0]["payload_bytes"]) == pa
-    assert torch.equal(a[:pa], b[:pa])
 
 
 @pytest.mark.parametrize("shape", ["k16", "k24", "var"])

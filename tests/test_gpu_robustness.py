@@ -52,6 +52,34 @@ def test_vqf_block_overflow_is_reported(oracle, amq, torch):
     assert out.cpu().numpy()[:pl.payload_used].tobytes() == ref[:pl.payload_used].tobytes()
 
 
+@pytest.mark.parametrize("n_leaves", [1, 64, 300, 800])
+def test_vqf_failed_build_then_clean_build_on_one_workspace(oracle, amq, torch, n_leaves):
+    """No memset precedes a VQF build: every decide-class kernel rewrites each leaf's nelts
+    word (flags included).  A batch with one overflowing leaf reports Internal; the next,
+    clean batch on the same workspace must report OK and equal the oracle.  1 / 64 leaves:
+    vqf_ring_place; 300: its two-per-CU form; 800: vqf_decide."""
+    bad = overflow_keys(oracle)
+    rest = [oracle.gen_keys16(4000 + i, 0, 500) for i in range(n_leaves - 1)]
+    counts = [len(bad)] + [500] * (n_leaves - 1)
+    keys = np.concatenate([bad] + rest) if rest else bad
+    plan = amq.plan_filters(amq.VQF, counts, 12, payload_capacity=32704)
+    ws = torch.empty(plan.workspace_bytes, dtype=torch.uint8, device="cuda")
+    with pytest.raises(amq.TkvAmqError) as e:
+        amq.build_all_filters(plan, amq.KeyBatch.fixed(torch.from_numpy(keys).cuda()), workspace=ws)
+    assert e.value.status == amq.abi.INTERNAL
+    good = keys.copy()
+    good[:len(bad)] = oracle.gen_keys16(999, 0, len(bad))
+    out = amq.build_all_filters(plan, amq.KeyBatch.fixed(torch.from_numpy(good).cuda()), workspace=ws)
+    o = out.cpu().numpy()
+    sb = np.concatenate([[0], np.cumsum(counts)])
+    for s in (0, n_leaves - 1):
+        st, ref, pl = oracle.vqf_build(good[sb[s]:], counts[s], 12, 32704, src_page_id=s)
+        seg = plan.segs[s]
+        assert st == 0
+        assert o[int(seg["out_offset"]):int(seg["out_offset"]) + pl.payload_used].tobytes() == \
+            ref[:pl.payload_used].tobytes()
+
+
 @pytest.mark.parametrize("kind", [0, 1])
 def test_concurrent_streams_two_threads(oracle, amq, torch, kind):
     """The ABI is called concurrently from worker threads (build_all_pages); each call on its

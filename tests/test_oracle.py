@@ -150,3 +150,48 @@ def test_bloom_no_false_negatives_variable_keys(oracle):
     st, b = oracle.bloom_build(blob, len(ks), 10, offsets=offs)
     assert st == 0
     assert all(oracle.bloom_query(b, k) == 1 for k in ks)
+
+
+@pytest.mark.parametrize("n,bpk,cap", [(16384, 12, 32704), (8448, 12, 32704), (20000, 22, 131072),
+                                       (5000, 30, 32704), (60000, 12, 32704), (1, 12, 32704),
+                                       (0, 12, 32704), (700, 64, 32704)])
+def test_vqf_bmi2_baseline(oracle, n, bpk, cap):
+    """The CPU baseline bench.py times for VQF (oracle/tkv_amq_baseline.c: BMI2 select, POPCNT,
+    unrolled XXH64 -- the instructions the reference's -mbmi2 -mavx2 build of vqf 0.2.4 uses,
+    CMakeLists.txt:46-48) writes the literal oracle's bytes: 8- and 16-bit tags, hash
+    truncation (60,000 keys on a 32 KiB page), one and zero keys, and the batched form."""
+    keys = oracle.gen_keys16(100 + n, 0, max(n, 1))
+    st, ref, pl = oracle.vqf_build(keys, n, bpk, cap)
+    sb, got = oracle.vqf_build_baseline(keys, n, bpk, cap)
+    assert st == sb == 0
+    assert got[:pl.payload_used].tobytes() == ref[:pl.payload_used].tobytes()
+    counts = [4000, 0, 16384, 777]
+    allk = oracle.gen_keys16(7, 0, sum(counts))
+    seg = np.concatenate([[0], np.cumsum(counts)]).astype(np.uint64)
+    off = np.arange(len(counts), dtype=np.uint64) * 32768
+    capa = np.full(len(counts), 32704, np.uint64)
+    s1, a = oracle.build_segments(1, allk, seg, 12, off, capa, 32768 * len(counts), n_threads=3)
+    s2, b = oracle.build_segments(1, allk, seg, 12, off, capa, 32768 * len(counts), n_threads=3,
+                                  baseline=True)
+    assert s1 == s2 == 0 and np.array_equal(a, b)
+
+
+def test_vqf_bmi2_baseline_overflow(oracle):
+    """A block overflow (keys whose primary and alternate buckets fall in block 0 of a 2-block
+    filter) fails the baseline as it fails the oracle (vqf_insert, filter_builder.hpp:211)."""
+    seed = 0x9D0924DC03E79A75
+    out, i = [], 0
+    while len(out) < 50:
+        k = oracle.gen_keys16(1234, i, 1)[0]
+        i += 1
+        h = oracle.xxh64(k.tobytes(), seed)
+        tag = h & 0xFF
+        if (h >> 8) % 160 < 80 and ((h ^ ((tag * 0x5BD1E995) & ((1 << 64) - 1))) >> 8) % 160 < 80:
+            out.append(k)
+    keys = np.stack(out)
+    st, _, _ = oracle.vqf_build(keys, 50, 12, 32704)
+    sb, _ = oracle.vqf_build_baseline(keys, 50, 12, 32704)
+    assert st == sb == 13
+    st, ref, pl = oracle.vqf_build(keys[:48].copy(), 48, 12, 32704)
+    sb, got = oracle.vqf_build_baseline(keys[:48].copy(), 48, 12, 32704)
+    assert st == sb == 0 and got[:pl.payload_used].tobytes() == ref[:pl.payload_used].tobytes()

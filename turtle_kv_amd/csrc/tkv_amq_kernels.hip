@@ -28,6 +28,7 @@
 // No MFMA anywhere: this is hashing and bit-set, not a contraction.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <mutex>
 #include <type_traits>
 #include <vector>
@@ -952,15 +953,15 @@ __global__ __launch_bounds__(256) void bloom_global_set(const uint8_t* __restric
 // one LDS image each).  Every key is hashed once, where it is read, and what its tile needs of
 // the hashes -- its 12-byte bit record -- travels instead of the key:
 //   bloom_part      one 1024-thread workgroup per CU over a contiguous key range, in batches
-//                   of kPartBatch: each key is hashed into its record, its rank in its tile's
-//                   run of the batch comes from a returning ds_add on an LDS histogram (two
-//                   u16 counters per word), and the record is stored straight to its slot in
-//                   this workgroup's region of its tile (no LDS sort: the L2 merges a run's
-//                   records, which are written together).  Region (t, w) holds `cap` records
-//                   (mean + 6 sigma of a uniform hash); records beyond it go to the workgroup's
-//                   overflow list (LDS counter).  LDS per tile: two u16 histograms
-//                   (double-buffered over batches) and a u32 cursor, 8 bytes, so one pass takes
-//                   up to kDirectMaxTiles tiles.
+//                   of kPartBatch: each key is hashed into its record and ranked in its tile's
+//                   run of the batch by a returning ds_add on an LDS histogram (two u16
+//                   counters per word); the batch is counting-sorted by tile in LDS planes and
+//                   each tile's run is appended to this workgroup's region of that tile, so a
+//                   store instruction writes a few long runs.  Region (t, w) holds `cap`
+//                   records (mean + 6 sigma of a uniform hash); records beyond it go to the
+//                   workgroup's overflow list (LDS counter).  LDS per tile beside the planes:
+//                   two u16 histograms (double-buffered over batches), the u16 run starts and
+//                   a u32 cursor, 10 bytes, so one pass takes up to kDirectMaxTiles tiles.
 //   bloom_tile      one workgroup per tile: every region of the tile through ds_or into the
 //                   128 KiB image, then 16-byte stores.
 //   bloom_overflow  the overflow lists with device-scope atomicOr into the finished filter
@@ -986,17 +987,20 @@ constexpr uint32_t kPartThreads = 1024;
 constexpr uint32_t kPartU = 8;                              // items per thread per batch
 constexpr uint32_t kPartBatch = kPartThreads * kPartU;      // < 65536: u16 ranks
 constexpr uint32_t kPartMaxWgs = 256;
-constexpr uint32_t kDirectMaxTiles = 20000;                 // LDS: 8 bytes per tile
-constexpr uint32_t kRecPartMaxTiles = 8192;                 // a record's 13-bit tile field
+constexpr uint32_t kPartPlaneBytes = 12 * kPartBatch;       // the batch's records, sorted by tile
+constexpr uint32_t kDirectMaxTiles = 6400;                  // LDS: 10 bytes per tile beside the planes
+constexpr uint32_t kRecPartMaxTiles = kDirectMaxTiles;      // (< 2^13: a record's tile field)
 constexpr uint32_t kRouteMaxParts = 2048;                   // tkv_amq_bloom_route(_records)
 constexpr uint32_t kRouteMaxWgs = 1024;                     // route count / scatter workgroups
 
 __host__ __device__ constexpr inline uint32_t part_lds_bytes(uint32_t n_tiles)
 {
-  // H0, H1: (T+1)/2 words each; cursor: 2 * ((T+1)/2) words; the overflow counter
-  return 16u * ((n_tiles + 1) / 2) + 16u;
+  // the planes; H0, H1, start: (T+1)/2 words each (u16 pairs); cursor: 2 * ((T+1)/2) words;
+  // 16 wave sums and the overflow counter
+  return kPartPlaneBytes + 20u * ((n_tiles + 1) / 2) + 4u * (kPartThreads / 64 + 1);
 }
 static_assert(part_lds_bytes(kDirectMaxTiles) <= 160 * 1024, "one workgroup per CU");
+static_assert(kRecPartMaxTiles <= 8192, "a record's 13-bit tile field");
 static_assert(kPartBatch < 65536, "u16 ranks");
 
 enum PartSrc : int { kSrcKey16 = 0, kSrcKey24 = 1, kSrcRec12 = 2, kSrcRaw16 = 3 };
@@ -1329,6 +1333,7 @@ struct PartArgs {
   uint32_t part;       // sum(cnt[0..part)) of src (n and from_seg unused)
   uint8_t* ws;
   PartGeom g;
+  uint32_t src_kind;   // PartSrc of the partition (kSrcRec12: routed items), for bloom_overflow
 };
 
 __device__ inline uint4 load_rec12(const uint8_t* recs, uint32_t i)
@@ -1352,28 +1357,86 @@ __device__ inline void part_items(const tkv_amq_segment& sg, const PartArgs& a, 
   }
 }
 
-// Per batch: hash U items per thread into records and ranks (the next batch's items are then
-// loaded, in flight until its hash), LDS barrier, the previous batch's run lengths added to the
-// cursors (and its histogram cleared for the batch after), LDS barrier, every record stored to
-// its slot.  Every lane issues the same loads and stores per batch (clamped loads; lanes
-// without a record store to a sink in the workspace header), so the compiler's wait for a
-// load never also waits for the stores.
+// Per-batch tile bookkeeping of part_body over the tiles' packed u16 counters (word j holds
+// tiles 2j and 2j+1; thread i owns words [i*c, (i+1)*c)): cursor[t] += prev[t] (the previous
+// batch's run lengths), prev[t] = 0 (the next batch's histogram), start[t] = exclusive scan of
+// cur[t].  Returns the batch's record count.  Two LDS barriers inside.
+__device__ inline uint32_t part_scan(const uint32_t* cur, uint32_t* prev, uint32_t* start,
+                                     uint32_t* cursor, uint32_t HW, uint32_t* wsum)
+{
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  const uint32_t c = (HW + kPartThreads - 1) / kPartThreads;
+  const uint32_t j0 = min(HW, tid * c), j1 = min(HW, j0 + c);
+  uint32_t s = 0;
+  for (uint32_t j = j0; j < j1; ++j) {
+    const uint32_t x = cur[j], y = prev[j];
+    if (y) {
+      cursor[2 * j] += y & 0xffffu;
+      cursor[2 * j + 1] += y >> 16;
+      prev[j] = 0;
+    }
+    s += (x & 0xffffu) + (x >> 16);
+  }
+  uint32_t inc = s;  // inclusive scan over the wave
+#pragma unroll
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const uint32_t v = __shfl_up(inc, d, 64);
+    if (lane >= d) inc += v;
+  }
+  if (lane == 63) wsum[wave] = inc;
+  lds_barrier();
+  uint32_t before = 0, total = 0;
+#pragma unroll
+  for (uint32_t q = 0; q < kPartThreads / 64; ++q) {
+    const uint32_t t = wsum[q];
+    before += q < wave ? t : 0u;
+    total += t;
+  }
+  uint32_t run = before + inc - s;
+  for (uint32_t j = j0; j < j1; ++j) {
+    const uint32_t x = cur[j], lo = x & 0xffffu;
+    start[j] = run | (run + lo) << 16;
+    run += lo + (x >> 16);
+  }
+  lds_barrier();  // start / cursor complete; wsum is reused by the next call
+  return total;
+}
+
+__device__ inline uint32_t lds_u16(const uint32_t* words, uint32_t t)
+{
+  return (words[t >> 1] >> ((t & 1u) << 4)) & 0xffffu;
+}
+
+// Per batch: hash U items per thread into records, each ranked in its tile's run by a
+// returning ds_add on the packed histogram (the next batch's items are then loaded, in flight
+// until its hash); LDS barrier; scan (two barriers); every record placed at its sorted position
+// in the LDS planes; LDS barrier; the planes written out in order, each tile's run to the end
+// of this workgroup's region of the tile, so a store instruction covers a few long runs (the L2
+// merges them into whole lines) instead of 64 scattered records.  Every lane issues the same
+// loads and stores per batch (clamped loads; lanes without a record store to a sink in the
+// workspace header).  Overflow entries are the records themselves (their tile is in the
+// record: T <= kDirectMaxTiles < 2^13) or, RAW, the 16-byte keys.
 template <int K, int SRC>
 __device__ void part_body(const tkv_amq_segment& sg, const PartArgs& a, uint32_t* lds)
 {
   constexpr bool RAW = SRC == kSrcRaw16;
-  // 16-byte records hold four words per item: half the items per batch
+  // 16-byte records: four key words and the tile per item in LDS, half the items per batch
   constexpr uint32_t RB = RAW ? 16 : 12, U = RAW ? kPartU / 2 : kPartU, NT = kPartThreads, B = U * NT;
+  constexpr uint32_t NPL = RAW ? 5 : 3;  // LDS planes
+  static_assert(NPL * B * 4 <= kPartPlaneBytes, "planes");
   constexpr uint32_t IB = SRC == kSrcKey24 ? 24 : (SRC == kSrcRec12 ? 12 : 16);  // item bytes
   const uint32_t tid = threadIdx.x, w = blockIdx.x, P = a.g.P, T = a.g.n_tiles, cap = a.g.cap;
   const uint32_t nb = sg.n_blocks, k = sg.hash_count;
   const uint32_t HW = (T + 1) >> 1;
-  uint32_t* H0 = lds;
-  uint32_t* H1 = lds + HW;
-  uint32_t* cursor = lds + 2 * HW;
-  uint32_t* ovf_n = cursor + 2 * HW;
+  uint32_t* pl = lds;  // plane j at pl + j * B
+  uint32_t* H0 = lds + kPartPlaneBytes / 4;
+  uint32_t* H1 = H0 + HW;
+  uint32_t* start = H1 + HW;
+  uint32_t* cursor = start + HW;
+  uint32_t* wsum = cursor + 2 * HW;  // 16 wave sums
+  uint32_t* ovf_n = wsum + NT / 64;
   for (uint32_t i = tid; i < 2 * HW; i += NT) {
-    lds[i] = 0;
+    H0[i] = 0;  // (H0 and H1)
     cursor[i] = 0;
   }
   if (tid == 0) *ovf_n = 0;
@@ -1383,9 +1446,7 @@ __device__ void part_body(const tkv_amq_segment& sg, const PartArgs& a, uint32_t
   part_items(sg, a, IB, src, n);
   const uint32_t per = a.cnt ? (n + P - 1) / P : a.g.per;
   const uint32_t kb = min(n, w * per), ke = min(n, kb + per);
-  uint8_t* regions = a.ws + a.g.regions_off;
-  uint8_t* ovf = a.ws + a.g.ovf_off + (uint64_t)w * a.g.per * 16;
-  uint8_t* const sink = a.ws;
+  const uint64_t ovf_base = a.g.ovf_off + (uint64_t)w * a.g.per * 16;
   const uint32_t last_item = ke > 0 ? ke - 1 : 0;
   using In = typename std::conditional<SRC == kSrcKey24, Key24, uint4>::type;
   auto load_in = [&](uint32_t i) -> In {
@@ -1439,40 +1500,48 @@ __device__ void part_body(const tkv_amq_segment& sg, const PartArgs& a, uint32_t
     for (uint32_t u = 0; u < U; ++u)  // the next batch's items
       in[u] = load_in(min(b0 + B + u * NT + tid, last_item));
     lds_barrier();
-    // the previous batch's run lengths into the cursors; its histogram is the next batch's
-    for (uint32_t j = tid; j < HW; j += NT) {
-      const uint32_t x = prev[j];
-      if (x) {
-        cursor[2 * j] += x & 0xffffu;
-        cursor[2 * j + 1] += x >> 16;
-        prev[j] = 0;
+    const uint32_t total = part_scan(hist, prev, start, cursor, HW, wsum);
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u) {
+      if (tr[u] == ~0u) continue;
+      const uint32_t t = tr[u] >> 16;
+      const uint32_t pos = lds_u16(start, t) + (tr[u] & 0xffffu);
+      pl[pos] = r0[u];
+      pl[B + pos] = r1[u];
+      pl[2 * B + pos] = r2[u];
+      if constexpr (RAW) {
+        pl[3 * B + pos] = r3[u];
+        pl[4 * B + pos] = t;
       }
     }
     lds_barrier();
 #pragma unroll
     for (uint32_t u = 0; u < U; ++u) {
-      uint8_t* dst = sink;
-      bool of = false;
-      if (tr[u] != ~0u) {
-        const uint32_t t = tr[u] >> 16;
-        const uint32_t c = cursor[t] + (tr[u] & 0xffffu);
-        if (c < cap) {
-          dst = regions + ((uint64_t)t * P + w) * cap * a.g.rb + (uint64_t)c * RB;
-        } else {
-          dst = ovf + 16ull * atomicAdd(ovf_n, 1u);  // LDS atomic, this workgroup's list
-          of = true;
-        }
-      }
+      const uint32_t j0 = u * NT + tid;
+      const bool v = j0 < total;
+      const uint32_t j = v ? j0 : 0u;
+      const uint32_t x0 = pl[j], x1 = pl[B + j], x2 = pl[2 * B + j];
+      uint32_t x3 = 0, t;
       if constexpr (RAW) {
-        *reinterpret_cast<uint4*>(dst) = make_uint4(r0[u], r1[u], r2[u], r3[u]);
-      } else if (of) {  // rare (a region full): the entry carries its tile
-        *reinterpret_cast<uint4*>(dst) = make_uint4(r0[u], r1[u], r2[u], tr[u] >> 16);
+        x3 = pl[3 * B + j];
+        t = pl[4 * B + j];
       } else {
-        uint3 v;
-        v.x = r0[u];
-        v.y = r1[u];
-        v.z = r2[u];
-        *reinterpret_cast<uint3*>(dst) = v;
+        t = rec_tile(x0, x1, x2);
+      }
+      t = v ? t : 0u;
+      const uint32_t c = cursor[t] + (j - lds_u16(start, t));
+      uint64_t off = 0;  // the sink
+      if (v) {
+        if (c < cap) off = a.g.regions_off + ((uint64_t)t * P + w) * cap * a.g.rb + (uint64_t)c * RB;
+        else off = ovf_base + (uint64_t)RB * atomicAdd(ovf_n, 1u);  // LDS atomic: this workgroup's list
+      }
+      uint32_t* d = reinterpret_cast<uint32_t*>(a.ws + off);
+      if constexpr (RAW) {
+        *reinterpret_cast<uint4*>(d) = make_uint4(x0, x1, x2, x3);
+      } else {
+        d[0] = x0;
+        d[1] = x1;
+        d[2] = x2;
       }
     }
   }
@@ -1481,7 +1550,7 @@ __device__ void part_body(const tkv_amq_segment& sg, const PartArgs& a, uint32_t
   const uint32_t* last = par ? H0 : H1;
   uint32_t* counts = reinterpret_cast<uint32_t*>(a.ws + a.g.counts_off);
   for (uint32_t t = tid; t < T; t += NT)
-    counts[(uint64_t)t * P + w] = min(cursor[t] + ((last[t >> 1] >> ((t & 1u) << 4)) & 0xffffu), cap);
+    counts[(uint64_t)t * P + w] = min(cursor[t] + lds_u16(last, t), cap);
   if (tid == 0) reinterpret_cast<uint32_t*>(a.ws + a.g.ovf_n_off)[w] = *ovf_n;
 }
 
@@ -1651,28 +1720,30 @@ __global__ __launch_bounds__(64) void bloom_header_only(const tkv_amq_segment* _
 }
 
 // one workgroup per partition workgroup's overflow list; device-scope atomics into the filter
-// (runs after bloom_tile has stored every tile).  24-byte keys with k > 8 (bits_per_key >= 13):
-// the bits past the eighth of the workgroup's keys, also with atomics.
+// (runs after bloom_tile has stored every tile).  An entry is a record whose region was full
+// (the 16-byte key itself when the records were keys).  24-byte keys with k > 8 (bits_per_key
+// >= 13): the bits past the eighth of the workgroup's keys, also with atomics.
 __global__ __launch_bounds__(256) void bloom_overflow(const tkv_amq_segment* __restrict__ segs,
                                                       PartArgs a, uint8_t* __restrict__ out)
 {
   const tkv_amq_segment sg = segs[0];
-  const uint32_t k = sg.hash_count, w = blockIdx.x;
+  const uint32_t k = sg.hash_count, w = blockIdx.x, nb = sg.n_blocks;
   if (k == 0) return;
   const bool raw = part_raw(sg, a);
   const uint32_t n = reinterpret_cast<const uint32_t*>(a.ws + a.g.ovf_n_off)[w];
   const uint8_t* list = a.ws + a.g.ovf_off + (uint64_t)w * a.g.per * 16;
   uint32_t* words = reinterpret_cast<uint32_t*>(out + sg.out_offset + kBloomHeader);
-  if (a.kb == 24 && k > 8 && !a.cnt) {
-    // (routed parts come from records, which the route refuses above eight bits)
-    const uint32_t nk = a.from_seg ? min(a.n, sg.n_keys) : a.n;
-    const uint8_t* keys = a.src + 24ull * (a.from_seg ? sg.key_begin : 0);
+  const uint32_t ib = a.src_kind == kSrcKey24 ? 24 : (a.src_kind == kSrcRec12 ? (raw ? 16 : 12) : 16);
+  const uint8_t* src;
+  uint32_t n_items;
+  part_items(sg, a, ib, src, n_items);
+  if (a.src_kind == kSrcKey24 && k > 8) {
     const uint32_t per = a.g.per;
-    const uint32_t kb = min(nk, w * per), ke = min(nk, kb + per);
+    const uint32_t kb = min(n_items, w * per), ke = min(n_items, kb + per);
     for (uint32_t i = kb + threadIdx.x; i < ke; i += 256) {
-      const XxhFixed<24> x(load_key24(keys, i).w);
+      const XxhFixed<24> x(load_key24(src, i).w);
       const uint64_t h0 = x.finish(xxh_fixed_rc<24>(c_bloom.seed[0]));
-      const uint32_t blk = (uint32_t)__umul64hi(h0, (uint64_t)sg.n_blocks);
+      const uint32_t blk = (uint32_t)__umul64hi(h0, (uint64_t)nb);
       if ((blk >> kTileShift) - a.tile0 >= a.g.n_tiles) continue;  // (outside the window)
       uint32_t* bw = words + 16ull * blk;
       for (uint32_t j = 8; j < k; ++j) {
@@ -1681,26 +1752,28 @@ __global__ __launch_bounds__(256) void bloom_overflow(const tkv_amq_segment* __r
       }
     }
   }
-  for (uint32_t i = threadIdx.x; i < n; i += 256) {
-    const uint4 q = *reinterpret_cast<const uint4*>(list + 16ull * i);
-    if (!raw) {
-      const uint64_t blk = (uint64_t)(a.tile0 + q.w) * kTileBlocks + (q.x & (kTileBlocks - 1));
-      uint32_t* bw = words + 16ull * blk;
-      const uint32_t b[8] = {q.x >> 11, q.x >> 20, q.y, q.y >> 9, q.y >> 18, q.z, q.z >> 9, q.z >> 18};
-      const uint32_t kk = k < 8 ? k : 8u;
-      for (uint32_t j = 0; j < kk; ++j) {
-        const uint32_t bj = b[j] & 511u;
-        atomicOr(bw + (bj >> 5), 1u << (bj & 31u));
-      }
-    } else {
+  for (uint32_t e = threadIdx.x; e < n; e += 256) {
+    if (raw) {
+      const uint4 q = *reinterpret_cast<const uint4*>(list + 16ull * e);
       const Xxh16 x((uint64_t)q.x | ((uint64_t)q.y << 32), (uint64_t)q.z | ((uint64_t)q.w << 32));
       const uint64_t h0 = x.finish(c_bloom.rhinit16[0]);
-      uint32_t* bw = words + 16 * (uint64_t)__umul64hi(h0, (uint64_t)sg.n_blocks);
+      uint32_t* bw = words + 16 * (uint64_t)__umul64hi(h0, (uint64_t)nb);
       atomicOr(bw + ((h0 & 511u) >> 5), 1u << (h0 & 31u));
       for (uint32_t j = 1; j < k; ++j) {
         const uint32_t bj = x.finish_lo9(c_bloom.rhinit16[j]) & 511u;
         atomicOr(bw + (bj >> 5), 1u << (bj & 31u));
       }
+      continue;
+    }
+    // a record whose region was full (its tile relative to the build's first tile is in it)
+    const uint3 r = *reinterpret_cast<const uint3*>(list + 12ull * e);
+    const uint64_t blk = (uint64_t)(a.tile0 + rec_tile(r.x, r.y, r.z)) * kTileBlocks + (r.x & (kTileBlocks - 1));
+    const uint32_t b[8] = {r.x >> 11, r.x >> 20, r.y, r.y >> 9, r.y >> 18, r.z, r.z >> 9, r.z >> 18};
+    uint32_t* bw = words + 16ull * blk;
+    const uint32_t kk = k < 8 ? k : 8u;
+    for (uint32_t j = 0; j < kk; ++j) {
+      const uint32_t bj = b[j] & 511u;
+      atomicOr(bw + (bj >> 5), 1u << (bj & 31u));
     }
   }
 }
@@ -2005,7 +2078,14 @@ __device__ inline bool vqf_ws_ok(const tkv_amq_segment* segs, uint32_t n_segs, u
 }
 
 // the first thing every decide workgroup does: the build's leaf count for tkv_amq_build_check
-// (the header lies inside the part of the workspace the host checks)
+// (the header lies inside the part of the workspace the host checks).
+// INVARIANT (no memset precedes a VQF build): every decide-class kernel (vqf_decide,
+// vqf_decide_big, vqf_decide_ring, vqf_ring_place) calls this for every leaf and then writes
+// that leaf's nelts word -- flags included -- on every path, including the early exits
+// (vqf_ws_ok's short-workspace flag, bits_per_key 0); tkv_amq_build's max_blocks == 0 path
+// clears the header word itself.  A kernel that skipped either would let tkv_amq_build_check,
+// LeafBatcher and HostFilterPipeline read a previous build's flags
+// (test_gpu_robustness.py::test_vqf_failed_build_then_clean_build_on_one_workspace).
 __device__ inline void vqf_mark_build(VqfWorkspace ws, uint32_t n_segs)
 {
   if (threadIdx.x == 0) ws.hdr[1] = n_segs;
@@ -4151,10 +4231,11 @@ inline uint64_t align256(uint64_t x) { return (x + 255) & ~255ull; }
 
 // partition -> tiles -> overflow.  src: kSrcKey16 / kSrcKey24 (keys, hashed), or kSrcRec12 for
 // routed items (records, or 16-byte keys when k > 8)
-inline void launch_part_build(int src, const PartArgs& a, hipStream_t s, const tkv_amq_segment* d_segs,
+inline void launch_part_build(int src, PartArgs a, hipStream_t s, const tkv_amq_segment* d_segs,
                               uint8_t* d_out, uint32_t hdr_always)
 {
   set_mono_attributes();
+  a.src_kind = (uint32_t)src;
   const size_t lds = part_lds_bytes(a.g.n_tiles);
   const dim3 grid(a.g.P), block(kPartThreads);
   if (src == kSrcKey24) hipLaunchKernelGGL(bloom_part_keys24, grid, block, lds, s, d_segs, a);
@@ -4458,13 +4539,18 @@ int tkv_amq_plan(int kind, const uint64_t* counts, const uint64_t* src_ids, uint
     *ws_bytes = 0;
     if (kind == TKV_AMQ_VQF && bpk != 0)
       *ws_bytes = vqf_temp_offset(n_segs) + kVqfTempStride * block_base + 8 * key_begin + 64;
-    // (the window path for one 16-byte-key filter above kWinMonoMax windows is not taken: the
-    // monolithic workspace below; any other window batch, its partial images)
+    // (the window path for one 16- or 24-byte-key filter above kWinMonoMax windows is not
+    // taken: the monolithic workspace below; any other window batch, its partial images.  The
+    // plan does not know the key shape, so a single filter of kWinMonoMax+1 .. kWinMaxWindows
+    // windows gets the larger of the two: other key shapes take the window path with it)
+    const uint64_t win_ws =
+        kind == TKV_AMQ_BLOOM && bpk != 0 && bloom_window_path(n_segs, max_blocks, false)
+            ? bloom_split_ws_bytes(n_segs, bloom_window_parts(n_segs, key_begin, max_blocks), max_blocks)
+            : 0;
     if (kind == TKV_AMQ_BLOOM && bpk != 0 && bloom_window_path(n_segs, max_blocks, true))
-      *ws_bytes = bloom_split_ws_bytes(n_segs, bloom_window_parts(n_segs, key_begin, max_blocks),
-                                       max_blocks);
+      *ws_bytes = win_ws;
     else if (kind == TKV_AMQ_BLOOM && bloom_partitioned(n_segs, max_blocks, key_begin))
-      *ws_bytes = mono_plan(key_begin, max_blocks).bytes;
+      *ws_bytes = std::max(mono_plan(key_begin, max_blocks).bytes, win_ws);
     else if (kind == TKV_AMQ_BLOOM)
       *ws_bytes = bloom_split_ws_bytes(n_segs, bloom_split_parts(n_segs, key_begin, max_blocks),
                                        max_blocks);

@@ -90,8 +90,8 @@ def allgather_filters(local, gathered=None, group=None):
 # a rank can only build its byte range of the bitmap from the keys whose blocks fall there.
 # The filter's T tiles (tkv_amq_bloom_tile_blocks() blocks each) are cut into world * g parts
 # of q tiles; rank r owns the g consecutive parts [r*g, (r+1)*g), a contiguous byte range of
-# the bitmap.  g = 1 unless a rank's range exceeds what one range build takes from records
-# (8,192 tiles: 1 GiB of filter per rank).  Steps per build, the same at every world size:
+# the bitmap.  g = 1 unless a rank's range exceeds what one range build takes (6,400 tiles:
+# 800 MiB of filter per rank).  Steps per build, the same at every world size:
 #   route     reorder the rank's keys by part (tkv_amq_bloom_route_records hashes each key once
 #             and ships its 12-byte bit record, k <= 8; tkv_amq_bloom_route ships the 16-byte
 #             key otherwise);
@@ -99,12 +99,12 @@ def allgather_filters(local, gathered=None, group=None):
 #   build     each owned part built from its records (tkv_amq_bloom_build_range_records /
 #             _build_range), part after part;
 #   gather    the all-gather of the bitmap ranges.
-# Without a process group (one GPU, no launcher) a filter of at most 20,000 tiles skips the
+# Without a process group (one GPU, no launcher) a filter of at most 6,400 tiles skips the
 # route: the range build reads the keys and makes the same records itself.
 # ---------------------------------------------------------------------------------------
 BLOOM_TILE_BLOCKS = 2048        # tkv_amq_bloom_tile_blocks()
-RECORD_RANGE_MAX_TILES = 8192   # tkv_amq_bloom_range_max_tiles(1): a record's tile field
-KEY_RANGE_MAX_TILES = 20000     # tkv_amq_bloom_range_max_tiles(0): the partition's tile table
+RECORD_RANGE_MAX_TILES = 6400   # tkv_amq_bloom_range_max_tiles(1): the partition's tile table
+KEY_RANGE_MAX_TILES = 6400      # tkv_amq_bloom_range_max_tiles(0)
 
 
 def hash_shard_plan(n_blocks: int, world: int, records: bool = True) -> tuple[int, int, int]:

@@ -927,18 +927,24 @@ class HostFilterPipeline:
         for p in self.plans:
             p.device_segs(self.dev)
         self.s_in, self.s_run, self.s_out = (torch.cuda.Stream(self.dev) for _ in range(3))
-        self.fail = torch.zeros(1, dtype=torch.int32, device=self.dev)
+        # failed leaves by cause: [0] inserts that overflowed a block (TKV_AMQ_VQF_FLAG_OVERFLOW,
+        # bit 31), [1] a workspace smaller than the plan (TKV_AMQ_VQF_FLAG_WORKSPACE, bit 30)
+        self.fail = torch.zeros(2, dtype=torch.int32, device=self.dev)
         torch.cuda.synchronize(self.dev)
 
     def new_host_output(self):
         return _torch().empty(self.plan.total_out_bytes, dtype=_torch().uint8, pin_memory=True)
 
     def _fold_flags(self, slot: int, chunk) -> None:
-        """Add the chunk's failed-leaf count (the flag bits 30/31 of each leaf's nelts word in
-        the VQF workspace, tkv_amq_build_check's source) to self.fail, on the device."""
+        """Add the chunk's failed-leaf counts (the flag bits of each leaf's nelts word in the VQF
+        workspace, tkv_amq_build_check's source) to self.fail, on the device: bit 31 (an insert
+        overflowed its block) and bit 30 (the workspace was short) counted apart, so each is
+        reported as tkv_amq_build_check reports it."""
+        torch = _torch()
         b0, b1 = chunk
-        w = self.d_ws[slot][64:64 + 4 * (b1 - b0)].view(_torch().int32)
-        self.fail.add_(((w >> 30) != 0).sum(dtype=_torch().int32))
+        w = self.d_ws[slot][64:64 + 4 * (b1 - b0)].view(torch.int32)
+        self.fail[0].add_((w < 0).sum(dtype=torch.int32))                  # bit 31
+        self.fail[1].add_((((w >> 30) & 1) != 0).sum(dtype=torch.int32))  # bit 30
 
     def run_views(self, views, host_out=None, view_stride: int = 16, n_threads: int = 16,
                   check: bool = True):
@@ -1025,7 +1031,11 @@ class HostFilterPipeline:
         self.s_out.synchronize()
         if check and self.kind == VQF:
             self.s_run.synchronize()
-            if int(self.fail.item()) != 0:
+            overflow, short_ws = (int(x) for x in self.fail.tolist())
+            if short_ws:  # as tkv_amq_build_check: the plan's workspace was not given
+                raise TkvAmqError(abi.INVALID_ARGUMENT, f"vqf build: workspace smaller than the plan "
+                                                        f"({short_ws} leaves)")
+            if overflow:
                 raise TkvAmqError(abi.INTERNAL, "vqf_insert (filter_builder.hpp:211)")
         if check or self.kind == BLOOM:
             record_filter_metrics(self.plan, (time.perf_counter() - t_run) * 1e6)
