@@ -89,6 +89,11 @@ def parse():
                          "ranks by leaf range (BASELINE config 5: --workload bloom12 "
                          "--total-keys 1000000000)")
     ap.add_argument("--allgather", action="store_true", help="time the RCCL all-gather in-step")
+    ap.add_argument("--chunks", type=int, default=1,
+                    help="with a process group: build each rank's leaves in this many rounds of "
+                         "block-cyclic leaf chunks and all-gather round c on a communication "
+                         "stream while round c+1 builds (the gather inside the timed step; "
+                         "turtle_kv_amd.dist.PipelinedLeafGather)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="process-group backend for N > 1 (nccl = RCCL; gloo only to rehearse "
                          "the multi-rank logic on one GPU)")
@@ -271,6 +276,9 @@ def main():
     kind, bpk, label = WORKLOADS[args.workload]
     if args.workload in HASH_SHARDED:
         return bench_hash_sharded(args, torch, dist, amq, world, rank, dev, bpk, label, pg)
+    if args.chunks > 1:
+        return bench_pipelined_gather(args, torch, dist, amq, world, rank, dev, kind, bpk, label,
+                                      pg)
     # the VQF payload capacity is the default TreeOptions' filter page at this bits/key
     # (tree/tree_options.hpp:177-220): 32 KiB pages, 32,704 payload bytes at 12 bits/key
     cap = (amq.TreeOptions(kind).set_filter_bits_per_key(bpk).filter_page_payload_size()
@@ -579,6 +587,121 @@ def valu_roofline(prof, n_keys, kernel_ms):
 
 
 # ---------------------------------------------------------------------------------------
+# leaf build with the all-gather pipelined into the step (--chunks K)
+# ---------------------------------------------------------------------------------------
+def bench_pipelined_gather(args, torch, dist, amq, world, rank, dev, kind, bpk, label, pg):
+    """The north star's multi-GPU step with the all-gather inside it: the checkpoint's leaves
+    are dealt to the ranks in block-cyclic chunks of Q leaves (round c of rank r = leaves
+    [(c*W + r)*Q, (c*W + r + 1)*Q)), each rank builds its K rounds one after the other on the
+    compute stream and all-gathers round c on a communication stream while round c + 1 builds,
+    so every rank ends the step holding the whole leaf-ordered filter array.  The step costs
+    about max(build, gather) + one round's gather; `breakdown_ms` times build-only and
+    gather-only steps beside it.  Rank 0 checks the gathered array against a one-GPU build of
+    every leaf (itself checked against the oracle by the plain leaf line)."""
+    from turtle_kv_amd import dist as tdist
+    if not pg:
+        raise SystemExit("bench.py: --chunks needs a process group (a launcher, or --gpus N > 1)")
+    if args.workload.startswith("probe") or args.workload in MONOLITHIC or \
+            KEY_BYTES.get(args.workload, 16) != 16:
+        raise SystemExit("bench.py: --chunks pipelines the leaf build of 16-byte keys "
+                         "(bloom10, bloom12, vqf12, bloom12big)")
+    cap = (amq.TreeOptions(kind).set_filter_bits_per_key(bpk).filter_page_payload_size()
+           if kind == amq.VQF else 0)
+    strong = args.total_keys is not None
+    leaf_keys = args.leaf_keys or LEAF_KEYS.get(args.workload, SEG_KEYS)
+    all_counts = (segment_counts(args.total_keys, leaf_keys) if strong
+                  else segment_counts(args.keys_per_gpu, leaf_keys) * world)
+    n_leaves = len(all_counts)
+    per_rank = -(-n_leaves // world)
+    q = -(-per_rank // args.chunks)
+    stride = tdist.leaf_stride(kind, bpk, max(all_counts), cap)
+    pl = tdist.PipelinedLeafGather(kind, all_counts, bpk, world, rank, stride, q, dev,
+                                   payload_capacity=cap)
+    batches = []
+    n = 0
+    for (b, e), (k0, k1) in zip(pl.rounds, pl.key_ranges()):
+        if k1 == k0:
+            batches.append(None)
+            continue
+        keys = amq.gen_keys16(42, k0, k1 - k0, device=dev)
+        if kind == 1:
+            keys = sort_segments_device(torch, keys, all_counts[b:e])
+        batches.append(amq.KeyBatch.fixed(keys))
+        n += k1 - k0
+    total_keys = sum(all_counts)
+    coll_dev = dev if args.backend == "nccl" else "cpu"
+
+    def timed(steps, **kw):
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            pl.step(batches, **kw)
+        torch.cuda.synchronize()
+        dist.barrier()
+        return reduce_max(torch, dist, time.perf_counter() - t0, coll_dev)
+
+    ramp0 = time.perf_counter()
+    n_ramp = 0
+    while (time.perf_counter() - ramp0) * 1e3 < args.ramp_ms:
+        pl.step(batches)
+        n_ramp += 1
+        torch.cuda.synchronize()
+    for _ in range(args.warmup):
+        pl.step(batches)
+    torch.cuda.synchronize()
+    wall = timed(args.steps)
+    ms_per_step = wall / args.steps * 1e3
+    reps = max(1, min(5, args.steps))
+    build_ms = timed(reps, gather=False) / reps * 1e3
+    gather_ms = timed(reps, build=False) / reps * 1e3
+
+    pl.step(batches)  # the checked array: one more full step
+    torch.cuda.synchronize()
+    gather_ok = None
+    if rank == 0 and not args.no_verify:
+        gather_ok = verify_gather(torch, amq, kind, bpk, cap, all_counts, stride, pl.filters(), 16,
+                                  dev)
+    flag = torch.tensor([0 if gather_ok is False else 1], dtype=torch.int32, device=coll_dev)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    if not bool(flag.item()):
+        raise SystemExit("bench.py: the pipelined all-gather's array differs from a one-GPU build")
+    comm = comm_info(torch, dist, dev)
+    dist.barrier()
+    dist.destroy_process_group()
+    if rank != 0:
+        return
+    line = {
+        "metric": f"{label} Mkeys/s incl. all-gather (device-resident)",
+        "value": round(total_keys * args.steps / wall / 1e6, 2), "unit": "Mkeys/s",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ramp_steps": n_ramp,
+        "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+        "scaling": "strong" if strong else "weak", "vs_baseline": None, "dtype": "u64",
+        "data": "synthetic (splitmix64 seed 42 keys generated on the device)",
+        "config": {"workload": f"{label}: {total_keys} x 16B keys in {n_leaves} {leaf_keys}-key "
+                               f"leaves, block-cyclic chunks of {q} leaves, {len(pl.rounds)} "
+                               f"rounds per rank, every rank gathers the whole array",
+                   "keys_per_gpu": n, "total_keys": total_keys, "key_bytes": 16,
+                   "leaf_keys": leaf_keys, "bits_per_key": bpk,
+                   "filter": "bloom-blocked512" if kind == 0 else "vqf",
+                   "payload_capacity": cap or None, "parallelism": f"leaf-sharded x{world}",
+                   "backend": args.backend, "chunk_leaves": q, "rounds": len(pl.rounds)},
+        "roofline": None,
+        "cpu_baseline": None,
+        "breakdown_ms": {"build_only": round(build_ms, 4), "gather_only": round(gather_ms, 4),
+                         "pipelined": round(ms_per_step, 4),
+                         "sum_of_parts": round(build_ms + gather_ms, 4),
+                         "max_of_parts": round(max(build_ms, gather_ms), 4)},
+        "allgather_bytes_in_per_gpu": (world - 1) * len(pl.rounds) * pl.round_bytes,
+        "gather_verified": gather_ok,
+        "comm": comm,
+        "note": "roofline and cpu_baseline are the plain leaf line's (same build kernels); this "
+                "line measures the gather overlap",
+    }
+    print(json.dumps(line), flush=True)
+
+
+# ---------------------------------------------------------------------------------------
 # hash-range sharded monolithic Bloom (BASELINE config 5 read literally)
 # ---------------------------------------------------------------------------------------
 def bench_hash_sharded(args, torch, dist, amq, world, rank, dev, bpk, label, pg=False):
@@ -859,9 +982,10 @@ def verify_gather(torch, amq, kind, bpk, cap, all_counts, stride, gathered, key_
     allk = amq.gen_keys16(42, 0, sum(all_counts), device=dev)
     if kind == 1:
         allk = sort_segments_device(torch, allk, all_counts)
-    full = torch.zeros(gathered.numel(), dtype=torch.uint8, device=dev)
+    full = torch.zeros(max(gathered.numel(), full_plan.total_out_bytes), dtype=torch.uint8,
+                       device=dev)
     amq.build_all_filters(full_plan, amq.KeyBatch.fixed(allk), out=full[:full_plan.total_out_bytes])
-    ok = bool(torch.equal(full, gathered))
+    ok = bool(torch.equal(full[:gathered.numel()], gathered))
     del full, allk
     return ok
 

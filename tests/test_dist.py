@@ -163,3 +163,70 @@ def test_build_owned_regroups_parts():
     got.clear()
     hs.build_owned(owned[:5], torch.tensor([[5]]))
     assert got == [(0, [0, 1, 2, 3, 4])]
+
+
+def test_cyclic_rounds_cover_leaves_in_order():
+    """Round c of every rank, concatenated rank by rank, is one contiguous leaf range, and the
+    rounds in order cover every leaf once: what lets each round's all-gather land in place."""
+    from turtle_kv_amd import dist as tdist
+    for n, world, q in [(10, 2, 2), (10, 3, 1), (6104, 8, 191), (7, 8, 1), (0, 2, 4), (5, 2, 8)]:
+        per = [tdist.cyclic_rounds(n, world, r, q) for r in range(world)]
+        assert len({len(p) for p in per}) == 1
+        flat = [rng for c in range(len(per[0])) for r in range(world) for rng in [per[r][c]]]
+        pos = 0
+        for b, e in flat:
+            assert b == pos or b == e == n
+            pos = e
+            assert e - b <= q
+        assert pos == n
+
+
+def cyclic_worker(rank, world, port, kind, q_leaves, result_q):
+    """Rank r builds its block-cyclic rounds (the oracle standing in for the GPU build) and
+    all-gathers round c into bytes [c*W*Q*stride, (c+1)*W*Q*stride) of the array, as
+    PipelinedLeafGather does on its communication stream."""
+    import sys
+    sys.path.insert(0, ROOT)
+    from oracle import oracle as O
+    from turtle_kv_amd import dist as tdist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    counts = [4096] * 9 + [1000]
+    bpk, cap = (10, 0) if kind == 0 else (12, 16320)
+    keys = O.gen_keys16(42, 0, sum(counts))
+    sb = np.concatenate([[0], np.cumsum(counts)])
+    if kind == 1:
+        O.sort_segments(keys, sb.astype(np.uint64))
+    stride = tdist.leaf_stride(kind, bpk, max(counts), cap)
+    rounds = tdist.cyclic_rounds(len(counts), world, rank, q_leaves)
+    rb = q_leaves * stride
+    gathered = torch.zeros(len(rounds) * world * rb, dtype=torch.uint8)
+    for c, (b, e) in enumerate(rounds):
+        local = np.zeros(rb, np.uint8)
+        if e > b:
+            local = oracle_build(O, kind, keys[sb[b]:sb[e]], counts[b:e], bpk, cap, stride,
+                                 range(b, e), q_leaves)
+        tdist.allgather_filters(torch.from_numpy(local), gathered[c * world * rb:(c + 1) * world * rb])
+    if rank == 0:
+        full = oracle_build(O, kind, keys, counts, bpk, cap, stride, range(len(counts)),
+                            len(counts))
+        result_q.put(bool(np.array_equal(gathered.numpy()[:len(counts) * stride], full)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("kind,world,q", [(0, 2, 2), (1, 2, 3), (0, 3, 1)])
+def test_cyclic_round_allgather(kind, world, q):
+    """The pipelined all-gather's layout: rounds gathered one by one give the leaf-ordered
+    array a single-process build writes (ragged last round, ranks with empty rounds)."""
+    ctx = mp.get_context("spawn")
+    rq = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=cyclic_worker, args=(r, world, port, kind, q, rq))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    assert rq.get(timeout=5) is True

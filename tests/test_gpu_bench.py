@@ -158,3 +158,32 @@ def test_bench_nccl_world1(workload):
     else:
         assert d["verify"]["equal_to_one_gpu_build"] and d["verify"]["equal_to_oracle"]
         assert d["step_breakdown_rank0_ms"]["keys_owned"] == 2_000_000
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("workload,extra", [("bloom10", ["--keys-per-gpu", "2000000"]),
+                                            ("vqf12", ["--keys-per-gpu", "2000000"]),
+                                            ("bloom12", ["--total-keys", "3000001"])])
+def test_bench_pipelined_gather_gloo(workload, extra):
+    """--chunks: two gloo ranks build their block-cyclic rounds and all-gather each round on
+    the communication stream while the next builds; rank 0 finds the gathered array equal to
+    a one-GPU build of every leaf (strong scaling: ragged rounds, an empty last slot)."""
+    r = run_bench("--gpus", "2", "--backend", "gloo", "--workload", workload, "--chunks", "3",
+                  *extra, *SMALL)
+    assert r.returncode == 0, r.stderr[-4000:]
+    d = last_json(r)
+    assert d["n_gpus"] == 2 and d["gather_verified"] is True
+    assert d["config"]["rounds"] == 3 and d["comm"]["world_size"] == 2
+    b = d["breakdown_ms"]
+    assert b["build_only"] > 0 and b["gather_only"] > 0 and b["pipelined"] > 0
+
+
+@pytest.mark.gpu
+def test_bench_pipelined_gather_nccl_world1():
+    """The same step over RCCL at world size 1: all_gather_into_tensor per round on the
+    communication stream, the gathered array checked against a one-GPU build."""
+    r = run_launched("--workload", "bloom10", "--keys-per-gpu", "2000000", "--chunks", "4", *SMALL)
+    assert r.returncode == 0, r.stderr[-4000:]
+    d = last_json(r)
+    assert d["n_gpus"] == 1 and d["config"]["backend"] == "nccl" and d["gather_verified"] is True
+    assert d["config"]["rounds"] == 4

@@ -84,6 +84,90 @@ def allgather_filters(local, gathered=None, group=None):
 
 
 # ---------------------------------------------------------------------------------------
+# The all-gather overlapped with the build.  A contiguous leaf range per rank can only be
+# gathered once the whole range is built (all_gather_into_tensor lands rank r's bytes at r's
+# offset).  With block-cyclic ownership -- in round c rank r owns leaves [(c*W + r)*Q,
+# (c*W + r + 1)*Q) -- round c's slots of all ranks are one contiguous piece of the leaf-ordered
+# array, so each round is gathered straight into place on a communication stream while the
+# next round builds: the step costs about max(build, gather) instead of their sum.
+# ---------------------------------------------------------------------------------------
+def cyclic_rounds(n_leaves: int, world: int, rank: int, chunk_leaves: int) -> list[tuple[int, int]]:
+    """Rank `rank`'s leaf range in each round (empty ranges past the last leaf)."""
+    q = max(1, int(chunk_leaves))
+    rounds = -(-int(n_leaves) // (world * q)) if n_leaves else 0
+    return [(min(n_leaves, (c * world + rank) * q), min(n_leaves, (c * world + rank + 1) * q))
+            for c in range(rounds)]
+
+
+class PipelinedLeafGather:
+    """One rank's side of a checkpoint build whose filter array is all-gathered round by round
+    while the next round builds (leaf s at s * stride of `gathered` on every rank, as
+    allgather_filters gives).  `step(key_batches)` builds and gathers every round."""
+
+    def __init__(self, kind: int, leaf_key_counts, bits_per_key: int, world: int, rank: int,
+                 stride: int, chunk_leaves: int, device, payload_capacity: int = 0, group=None):
+        import torch
+        from .filters import plan_filters
+        counts = np.asarray(leaf_key_counts, dtype=np.int64)
+        self.world, self.rank, self.group, self.dev = world, rank, group, torch.device(device)
+        self.stride, self.q = stride, max(1, int(chunk_leaves))
+        self.n_leaves = len(counts)
+        self.key_begin = np.concatenate([[0], np.cumsum(counts)])
+        self.rounds = cyclic_rounds(self.n_leaves, world, rank, self.q)
+        self.plans = []
+        for b, e in self.rounds:
+            if b == e:  # past the last leaf: this rank's slots of the round stay zero
+                self.plans.append(None)
+                continue
+            p = plan_filters(kind, counts[b:e].astype(np.uint64), bits_per_key,
+                             payload_capacity=payload_capacity, out_stride=stride,
+                             src_page_ids=np.arange(b, e, dtype=np.uint64))
+            self.plans.append(p)
+        R = len(self.rounds)
+        self.round_bytes = self.q * stride
+        self.local = torch.zeros(max(1, R) * self.round_bytes, dtype=torch.uint8, device=self.dev)
+        self.gathered = torch.zeros(max(1, R) * world * self.round_bytes, dtype=torch.uint8,
+                                    device=self.dev)
+        ws = max((p.workspace_bytes for p in self.plans if p is not None), default=0)
+        self.ws = torch.empty(max(ws, 1), dtype=torch.uint8, device=self.dev)
+        self.comm = torch.cuda.Stream(device=self.dev)
+
+    def key_ranges(self) -> list[tuple[int, int]]:
+        """Global key index range of each round's leaves (keys are laid out leaf after leaf)."""
+        return [(int(self.key_begin[b]), int(self.key_begin[e])) for b, e in self.rounds]
+
+    def _gather(self, c: int):
+        rb, W = self.round_bytes, self.world
+        allgather_filters(self.local[c * rb:(c + 1) * rb], self.gathered[c * W * rb:(c + 1) * W * rb],
+                          self.group)
+
+    def step(self, key_batches, build: bool = True, gather: bool = True):
+        """Build round c on the current stream; gather it on the communication stream once
+        its build is done, while round c + 1 builds.  Returns when the current stream has
+        every gathered byte (the next step may rebuild the slots)."""
+        import torch
+        from .filters import build_all_filters
+        cur = torch.cuda.current_stream(self.dev)
+        self.comm.wait_stream(cur)  # the previous step's readers of `gathered` are done
+        rb = self.round_bytes
+        for c, kb in enumerate(key_batches):
+            if build and self.plans[c] is not None:
+                build_all_filters(self.plans[c], kb, out=self.local[c * rb:(c + 1) * rb],
+                                  workspace=self.ws, check=False)
+            if gather:
+                ev = torch.cuda.Event()
+                ev.record(cur)
+                with torch.cuda.stream(self.comm):
+                    self.comm.wait_event(ev)
+                    self._gather(c)
+        cur.wait_stream(self.comm)
+
+    def filters(self):
+        """The gathered leaf-ordered array (leaf s at s * stride), trimmed to the leaves."""
+        return self.gathered[:self.n_leaves * self.stride]
+
+
+# ---------------------------------------------------------------------------------------
 # Hash-range sharding of ONE monolithic Bloom filter (BASELINE config 5 read literally:
 # "1B keys, Bloom @12, hash-range sharded across 8 GPUs, RCCL all-gather").  Unlike the leaf
 # filters above, keys must move: every key's bits fall in the 64-byte block its h0 selects, so
