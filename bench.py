@@ -94,6 +94,9 @@ def parse():
                          "block-cyclic leaf chunks and all-gather round c on a communication "
                          "stream while round c+1 builds (the gather inside the timed step; "
                          "turtle_kv_amd.dist.PipelinedLeafGather)")
+    ap.add_argument("--pipeline-rounds", type=int, default=4,
+                    help="N > 1 leaf lines: rounds per rank of the pipelined build + all-gather "
+                         "figure (build_plus_allgather_pipelined)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="process-group backend for N > 1 (nccl = RCCL; gloo only to rehearse "
                          "the multi-rank logic on one GPU)")
@@ -459,6 +462,17 @@ def main():
             gather_ok = verify_gather(torch, amq, kind, bpk, cap, all_counts, stride, gathered,
                                       key_bytes, dev)
 
+    # the north star's whole step with the all-gather overlapped (untimed by `value`): the same
+    # leaves dealt in block-cyclic rounds, round c gathered on a communication stream while
+    # round c + 1 builds (turtle_kv_amd.dist.PipelinedLeafGather; bench --chunks K times it alone)
+    pipelined = None
+    if (pg and world > 1 and not probe and key_bytes == 16 and args.workload not in MONOLITHIC
+            and not args.allgather):
+        del gathered
+        torch.cuda.empty_cache()
+        pipelined = pipelined_figure(torch, dist, amq, tdist, kind, bpk, cap, all_counts, world,
+                                     rank, stride, dev, coll_dev, args.pipeline_rounds)
+
     sweep = None
     if rank == 0 and world == 1 and not probe and args.sweep and \
             args.workload not in MONOLITHIC and len(counts) > SWEEP_LEAVES[0]:
@@ -549,6 +563,9 @@ def main():
         line["build_plus_allgather_mkeys_s"] = round(units / ((ms_per_step + allgather_ms) * 1e-3) / 1e6, 2)
     if gather_ok is not None:
         line["gather_verified"] = gather_ok
+    if pipelined is not None:
+        pipelined["mkeys_s"] = round(units / (pipelined["ms_per_step"] * 1e-3) / 1e6, 2)
+        line["build_plus_allgather_pipelined"] = pipelined
     if sweep is not None:
         line["batch_sweep"] = sweep
     if e2e is not None:
@@ -584,6 +601,42 @@ def valu_roofline(prof, n_keys, kernel_ms):
     if prof.get("valu_busy_frac") is not None:
         r["valu_busy_frac_pmc"] = prof["valu_busy_frac"]
     return r
+
+
+def pipelined_figure(torch, dist, amq, tdist, kind, bpk, cap, all_counts, world, rank, stride, dev,
+                     coll_dev, rounds, reps=5):
+    """Max over ranks of the pipelined build + all-gather step time (PipelinedLeafGather,
+    `rounds` rounds per rank) after one untimed step.  (bench --chunks K runs the same step as
+    its timed step and checks the array it gathers.)"""
+    per_rank = -(-len(all_counts) // world)
+    q = -(-per_rank // max(1, rounds))
+    pl = tdist.PipelinedLeafGather(kind, all_counts, bpk, world, rank, stride, q, dev,
+                                   payload_capacity=cap)
+    batches = []
+    for (b, e), (k0, k1) in zip(pl.rounds, pl.key_ranges()):
+        if k1 == k0:
+            batches.append(None)
+            continue
+        keys = amq.gen_keys16(42, k0, k1 - k0, device=dev)
+        if kind == 1:
+            keys = sort_segments_device(torch, keys, all_counts[b:e])
+        batches.append(amq.KeyBatch.fixed(keys))
+    pl.step(batches)
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        pl.step(batches)
+    torch.cuda.synchronize()
+    dist.barrier()
+    ms = reduce_max(torch, dist, (time.perf_counter() - t0) / reps * 1e3, coll_dev)
+    out = {"ms_per_step": round(ms, 4), "rounds": len(pl.rounds), "chunk_leaves": q,
+           "reps": reps, "note": "block-cyclic rounds, round c all-gathered on a communication "
+                                 "stream while round c+1 builds; every rank ends the step with "
+                                 "the whole array (bench --chunks verifies it)"}
+    del pl, batches
+    torch.cuda.empty_cache()
+    return out
 
 
 # ---------------------------------------------------------------------------------------

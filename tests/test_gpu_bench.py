@@ -123,6 +123,7 @@ def test_bench_two_ranks_gloo_host_legs():
     b = d["cpu_baseline"]
     assert b and b["value"] > 0 and b["cores"] >= 1 and "rank 0" in b["note"]
     assert d["allgather_bytes_in_per_gpu"] > 0
+    assert d["build_plus_allgather_pipelined"]["ms_per_step"] > 0
 
 
 def run_launched(*args, timeout=400):
