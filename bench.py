@@ -1039,6 +1039,11 @@ def verify_gather(torch, amq, kind, bpk, cap, all_counts, stride, gathered, key_
                        device=dev)
     amq.build_all_filters(full_plan, amq.KeyBatch.fixed(allk), out=full[:full_plan.total_out_bytes])
     ok = bool(torch.equal(full[:gathered.numel()], gathered))
+    if not ok and stride:
+        bad = torch.nonzero(full[:gathered.numel()] != gathered).flatten()
+        leaves = sorted({int(x) // stride for x in bad[:4096].tolist()})
+        print(f"verify_gather: {bad.numel()} bytes differ, in leaves {leaves[:16]} "
+              f"(first byte {int(bad[0])})", file=sys.stderr, flush=True)
     del full, allk
     return ok
 

@@ -384,6 +384,50 @@ def test_vqf_ring_place_classes(oracle, amq, torch, n_leaves, edge, bpk):
         assert segment_bytes(plan, out, s) == ref[:p.payload_used].tobytes(), f"leaf {s}"
 
 
+@pytest.mark.parametrize("shape", ["k16", "k24", "var"])
+@pytest.mark.parametrize("bpk", [12, 22])
+@pytest.mark.parametrize("cap", [65472, 8128])
+def test_vqf_ring_edges(oracle, amq, torch, shape, bpk, cap):
+    """vqf_ring_place on the leaves where a decider step changes kind: 30 keys in one block
+    (no key ever reaches the alternate-choice threshold), 40 keys in one block (the threshold
+    is reached inside the first 64-key chunk; two blocks each at 16-bit tags), 1 and 0 keys,
+    700, a 16,384-key leaf; 8- and 16-bit tags; in 8 KiB pages (cap 8128) the larger leaves
+    keep only masked keys (hash_val_shift > 0); 16-, 24-byte and variable-length keys.
+    Byte-equal to the oracle.  (The round-4 parallel-prefix variant of the ring,
+    tools/patches/r04_vqf_loc_prefix_tile_loop.patch, was checked with these leaves.)"""
+    counts = [30, 40, 1, 0, 700, 16384, 5000]
+    n = sum(counts)
+    rng = np.random.default_rng(11)
+    offs = None
+    if shape == "k16":
+        keys, stride = oracle.gen_keys16(12, 0, n), 16
+    elif shape == "k24":
+        keys, stride = rng.integers(0, 256, (n, 24), dtype=np.uint8), 24
+    else:
+        lens = rng.integers(6, 40, n)
+        keys, stride = rng.integers(0, 256, int(lens.sum()), dtype=np.uint8), 0
+        offs = np.zeros(n + 1, np.int64)
+        offs[1:] = np.cumsum(lens)
+    plan, out = gpu_build(amq, torch, 1, torch.from_numpy(keys).cuda(), counts, bpk, cap=cap,
+                          offsets_t=None if offs is None else torch.from_numpy(offs).cuda())
+    assert int(plan.segs["n_blocks"][:2].max()) <= 2  # (one block at 8-bit tags, two at 16)
+    if cap == 8128:
+        assert int(plan.segs["hash_val_shift"][5]) > 0
+    if bpk == 22:
+        assert 16 in set(plan.segs["tag_bits"].tolist())
+    sb = seg_bounds(counts)
+    for s in range(len(counts)):
+        b, c = int(sb[s]), counts[s]
+        if offs is None:
+            st, ref, p = oracle.vqf_build(keys[b:], c, bpk, cap, src_page_id=s, stride=stride)
+        else:
+            o = (offs[b:b + c + 1] - offs[b]).astype(np.uint64)
+            st, ref, p = oracle.vqf_build(keys[int(offs[b]):], c, bpk, cap, src_page_id=s,
+                                          offsets=o, stride=0)
+        assert st == 0
+        assert segment_bytes(plan, out, s) == ref[:p.payload_used].tobytes(), f"leaf {s}"
+
+
 @pytest.mark.parametrize("big", [100000, 260000])
 @pytest.mark.parametrize("n_leaves", [4, 800])
 @pytest.mark.parametrize("bpk", [12, 22])
