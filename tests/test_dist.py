@@ -122,29 +122,28 @@ def test_hash_shard_tiles_cover_the_filter():
 
 
 def test_hash_shard_parts_per_rank():
-    """A rank's range is cut into g parts when it exceeds what one range build takes (6,400
-    tiles, the partition's LDS tile table): BASELINE config 5 (1B keys at
-    12 bits/key, 11,445 tiles) takes two parts on one rank and one part from two ranks up; every
-    part holds at most the cap, the parts of all ranks tile the filter, and rank r's range is
-    its parts' union."""
-    from turtle_kv_amd.dist import (KEY_RANGE_MAX_TILES, RECORD_RANGE_MAX_TILES, HashShardedBloom,
-                                    hash_shard_plan)
+    """A rank's range is cut into g parts of at most 1,600 tiles (ROUTED_PART_TILES, under the
+    6,400 of one range build's LDS tile table): BASELINE config 5 (1B keys at 12 bits/key,
+    11,445 tiles) builds parts of 1,431 tiles at every N -- 8 on one rank, 4 each on two, 1 each
+    on eight; the parts of all ranks tile the filter, and rank r's range is its parts' union."""
+    from turtle_kv_amd.dist import ROUTED_PART_TILES, HashShardedBloom, hash_shard_plan
     nb_1b = -(-1_000_000_000 * 12 // 512)
-    assert hash_shard_plan(nb_1b, 1) == (11445, 2, 5723)
-    assert hash_shard_plan(nb_1b, 2)[1:] == (1, 5723)
+    assert hash_shard_plan(nb_1b, 1) == (11445, 8, 1431)
+    assert hash_shard_plan(nb_1b, 2)[1:] == (4, 1431)
+    assert hash_shard_plan(nb_1b, 4)[1:] == (2, 1431)
     assert hash_shard_plan(nb_1b, 8)[1:] == (1, 1431)
-    assert hash_shard_plan(nb_1b, 1, records=False) == (11445, 2, 5723)
+    assert hash_shard_plan(nb_1b, 1, records=False) == (11445, 8, 1431)
     for nb in [1, 5000, nb_1b, 3 * nb_1b, 40_000_000 * 2048]:
         for world in [1, 2, 3, 8]:
             for rec in (True, False):
                 T, g, q = hash_shard_plan(nb, world, rec)
-                assert q <= (RECORD_RANGE_MAX_TILES if rec else KEY_RANGE_MAX_TILES)
+                assert q <= ROUTED_PART_TILES
                 parts = [(min(T, p * q), min(T, (p + 1) * q)) for p in range(world * g)]
                 assert parts[0][0] == 0 and parts[-1][1] == T
                 assert all(a[1] == b[0] for a, b in zip(parts, parts[1:]))
     hs = HashShardedBloom(1_000_000_000, 12, 2, 1, "meta")
-    assert (hs.g, hs.q, hs.tile_begin, hs.tile_end) == (1, 5723, 5723, 11445)
-    assert hs.part_tiles(0) == (5723, 11445)
+    assert (hs.g, hs.q, hs.tile_begin, hs.tile_end) == (4, 1431, 5724, 11445)
+    assert hs.part_tiles(0) == (5724, 7155) and hs.part_tiles(3) == (10017, 11445)
 
 
 def test_build_owned_regroups_parts():

@@ -4303,6 +4303,13 @@ struct MonoPlan {
   uint64_t bytes;
 };
 
+// Tiles per routed part (a filter past kDirectMaxTiles): the fewer tiles a partition spreads
+// a batch over, the longer each tile's run per store (fewer partial-line writes).  1B keys at
+// 12 bits/key: 8 parts of 1,431 tiles, the parts an 8-rank hash-range build gives each rank
+// (turtle_kv_amd.dist.ROUTED_PART_TILES)
+constexpr uint32_t kRoutePartTiles = 1600;
+static_assert(kRoutePartTiles <= kRecPartMaxTiles, "");
+
 inline MonoPlan mono_plan(uint64_t n_keys, uint64_t n_blocks)
 {
   MonoPlan m{};
@@ -4314,7 +4321,7 @@ inline MonoPlan mono_plan(uint64_t n_keys, uint64_t n_blocks)
     m.bytes = m.pg.bytes;
     return m;
   }
-  m.g = (uint32_t)div_up(m.T, kRecPartMaxTiles);
+  m.g = (uint32_t)div_up(m.T, kRoutePartTiles);
   m.q = (uint32_t)div_up(m.T, m.g);
   m.rg = route_geom(n_keys, m.g);
   m.items_off = align256(m.rg.bytes);
