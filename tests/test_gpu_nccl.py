@@ -58,9 +58,10 @@ def child():
     keys = amq.gen_keys16(7, 0, n)
     hs = tdist.HashShardedBloom(n, 12, 1, 0, dev)
     routed, sc = hs.route(keys)
-    owned = hs.exchange(routed, sc)
+    owned, sub = hs.exchange(routed, sc)
     # one rank: the all-to-all of the 12-byte bit records (k = 8 at 12 bits/key) is a copy
-    res["exchange_identity"] = bool(hs.records and owned.shape == (n, 12) and torch.equal(owned, routed))
+    res["exchange_identity"] = bool(hs.records and owned.shape == (n, 12) and torch.equal(owned, routed)
+                                    and tuple(sub.shape) == (1, hs.g) and int(sub.sum()) == n)
     filt = hs.build(keys)
     torch.cuda.synchronize()
     whole = amq.build_all_filters(amq.plan_filters(0, [n], 12), amq.KeyBatch.fixed(keys))
