@@ -17,8 +17,8 @@ KERNELS = {  # kernel-name substrings of one step (pmc_summary sums them)
     "bloom10": "bloom_build_lds", "bloom12": "bloom_build_lds", "bloom10k24": "bloom_build_lds",
     "bloom10var": "bloom_build_lds", "vqf12": "vqf_decide<,vqf_place_fused",
     "vqf12k24": "vqf_decide<,vqf_place_fused", "vqf12var": "vqf_decide<,vqf_place_fused",
-    "bloom10mono": "bloom_rec_partition,bloom_rec_tile,bloom_rec_overflow",
-    "bloom10monok24": "bloom_rec_partition24,bloom_rec_tile,bloom_rec_overflow",
+    "bloom10mono": "bloom_part_keys16,bloom_tile,bloom_overflow",
+    "bloom10monok24": "bloom_part_keys24,bloom_tile,bloom_overflow",
     "bloom12big": "bloom_build_window,bloom_split_merge",
     "probe10": "bloom_probe", "probe_vqf12": "vqf_probe",
 }
