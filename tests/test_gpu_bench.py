@@ -188,3 +188,19 @@ def test_bench_pipelined_gather_nccl_world1():
     d = last_json(r)
     assert d["n_gpus"] == 1 and d["config"]["backend"] == "nccl" and d["gather_verified"] is True
     assert d["config"]["rounds"] == 4
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("workload", ["probe10", "probe_vqf12"])
+def test_bench_probe_full_size(workload):
+    """Config 4 at its own size in the GPU suite: 200M shuffled hit/miss lookups against the
+    100M-key build, every answer equal to the oracle's over the GPU-built filter bytes, so the
+    FPRs are equal; no false negatives."""
+    r = run_bench("--workload", workload, "--steps", "3", "--warmup", "1", "--ramp-ms", "0",
+                  "--no-e2e", "--no-cpu-baseline", timeout=600)
+    assert r.returncode == 0, r.stderr[-4000:]
+    d = last_json(r)
+    p = d["probe"]
+    assert p["lookups"] == 200_000_000 and p["hits_all_true"] is True
+    assert p["results_equal_oracle"] is True and d["verified"] is True
+    assert p["fpr_oracle"] == p["false_positive_rate"]
