@@ -470,8 +470,13 @@ def main():
             and not args.allgather):
         del gathered
         torch.cuda.empty_cache()
-        pipelined = pipelined_figure(torch, dist, amq, tdist, kind, bpk, cap, all_counts, world,
-                                     rank, stride, dev, coll_dev, args.pipeline_rounds)
+        try:
+            pipelined = pipelined_figure(torch, dist, amq, tdist, kind, bpk, cap, all_counts,
+                                         world, rank, stride, dev, coll_dev, args.pipeline_rounds)
+        except Exception as e:  # an extra figure: it must not cost the timed line
+            pipelined = {"error": f"{type(e).__name__}: {e}"[:400]}
+            torch.cuda.synchronize()
+            dist.barrier()
 
     sweep = None
     if rank == 0 and world == 1 and not probe and args.sweep and \
@@ -563,8 +568,9 @@ def main():
         line["build_plus_allgather_mkeys_s"] = round(units / ((ms_per_step + allgather_ms) * 1e-3) / 1e6, 2)
     if gather_ok is not None:
         line["gather_verified"] = gather_ok
-    if pipelined is not None:
+    if pipelined is not None and "ms_per_step" in pipelined:
         pipelined["mkeys_s"] = round(units / (pipelined["ms_per_step"] * 1e-3) / 1e6, 2)
+    if pipelined is not None:
         line["build_plus_allgather_pipelined"] = pipelined
     if sweep is not None:
         line["batch_sweep"] = sweep
