@@ -2578,6 +2578,9 @@ __device__ inline void vqf_decide_dispatch(const uint8_t* keys, const uint64_t* 
   }
 }
 
+// (74 VGPRs, 6 waves per SIMD.  Forcing 7 or 8 waves per SIMD spills -- 12 / 48 bytes per
+// lane for 16-byte keys -- and ran slower: 498 -> 544 / 546 us per 100M keys, variable-length
+// keys 986 -> 1241 / 1590 us; profiles/r04/experiments/vqf_decide_waves_per_eu.txt)
 template <int MODE>
 __global__ __launch_bounds__(64) void vqf_decide(const uint8_t* __restrict__ keys,
                                                  const uint64_t* __restrict__ offs, uint32_t stride,
