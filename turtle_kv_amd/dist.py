@@ -147,6 +147,8 @@ class PipelinedLeafGather:
         every gathered byte (the next step may rebuild the slots)."""
         import torch
         from .filters import build_all_filters
+        if len(key_batches) != len(self.rounds):
+            raise ValueError(f"{len(key_batches)} key batches for {len(self.rounds)} rounds")
         cur = torch.cuda.current_stream(self.dev)
         self.comm.wait_stream(cur)  # the previous step's readers of `gathered` are done
         rb = self.round_bytes
