@@ -780,6 +780,12 @@ def bench_hash_sharded(args, torch, dist, amq, world, rank, dev, bpk, label, pg=
     keys = amq.gen_keys16(42, rank * n_local, n_local, device=dev)
     hs = tdist.HashShardedBloom(total, bpk, world, rank, dev)
 
+    def progress(msg):  # long runs (1B keys) report their stages on stderr
+        if rank == 0:
+            print(f"bench.py bloom12hash: {msg}", file=sys.stderr, flush=True)
+
+    progress(f"{n_local} keys per rank generated; ramp")
+
     def step():
         hs.local_build(keys)
         if args.allgather and pg:
@@ -794,6 +800,7 @@ def bench_hash_sharded(args, torch, dist, amq, world, rank, dev, bpk, label, pg=
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    progress(f"ramp ({n_ramp} steps) and warmup done")
     coll_dev = dev if args.backend == "nccl" else "cpu"
     if pg:
         dist.barrier()
@@ -807,6 +814,7 @@ def bench_hash_sharded(args, torch, dist, amq, world, rank, dev, bpk, label, pg=
     wall = time.perf_counter() - t0
     if pg:
         wall = reduce_max(torch, dist, wall, coll_dev)
+    progress(f"{args.steps} timed steps: {wall / args.steps * 1e3:.3f} ms per step")
 
     # untimed breakdown of one step on this rank (HIP events on the current stream)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
@@ -837,6 +845,7 @@ def bench_hash_sharded(args, torch, dist, amq, world, rank, dev, bpk, label, pg=
         allgather_ms = reduce_max(torch, dist, (time.perf_counter() - g0) / 3 * 1e3, coll_dev)
     filt = hs.allgather()
     torch.cuda.synchronize()
+    progress("breakdown and all-gather done; verifying")
     comm = comm_info(torch, dist, dev) if pg else None
 
     check = None

@@ -17,7 +17,7 @@ fi
 if has rccl1; then
   timeout -k 10 600 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
       --master-addr 127.0.0.1 --master-port 29511 bench.py --workload bloom12hash \
-      --total-keys 1000000000 --steps 10 --no-cpu-baseline > $O/bench_bloom12hash_1B_rccl1.log 2>&1 || exit 3
+      --total-keys 1000000000 --steps 5 --no-cpu-baseline > $O/bench_bloom12hash_1B_rccl1.log 2>&1 || exit 3
 fi
 if has gloo8; then
   timeout -k 10 1000 python -u bench.py --gpus 8 --backend gloo --workload bloom12hash \
