@@ -311,15 +311,15 @@ class HashShardedBloom:
         send = [int(x) * u for x in part_counts.cpu().view(W, g).sum(1).tolist()]
         recv = [int(x) * u for x in sub.sum(1).tolist()]
         m = sum(recv) // u
-        out = self._buf("recv", u * m)[:u * m]
         src = routed.reshape(-1)
+        if W == 1:  # every unit is this rank's own: nothing moves
+            return src[:u * m].view(m, u), sub
+        out = self._buf("recv", u * m)[:u * m]
         # this rank's own units are a device copy, not a message to itself (at world size 1 RCCL
         # moved 12 GB of records to the rank itself at under 1 GB/s)
         r = self.rank
         so, ro = sum(send[:r]), sum(recv[:r])
         out[ro:ro + recv[r]].copy_(src[so:so + send[r]])
-        if W == 1:
-            return out.view(m, u), sub
         if gloo:  # CPU rehearsal: stage through host memory
             host = torch.empty(u * m, dtype=torch.uint8)
             dist.all_to_all_single(host, src.cpu(), recv, send, group=self.group)
