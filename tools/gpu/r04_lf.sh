@@ -7,7 +7,7 @@ mkdir -p $O
 for L in main $LIBS; do
   n=$(basename $L .so)
   if [ $L = main ]; then unset TKV_AMQ_LIB; else export TKV_AMQ_LIB=$L; fi
-  timeout -k 10 400 python -u -m pytest -q --timeout 300 --timeout-method thread tests/test_gpu_parity.py -k "monolithic and not large" > $O/t_$n.log 2>&1; rc=$?
+  timeout -k 10 400 python -u -m pytest -q --timeout 300 --timeout-method thread tests/test_gpu_parity.py tests/test_gpu_hash_shard.py -k "monolithic or hash" > $O/t_$n.log 2>&1; rc=$?
   echo "## $n tests rc=$rc"; tail -1 $O/t_$n.log; [ $rc -gt 1 ] && exit 3
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_$n -o p --output-format csv -- \
       python -u bench.py --workload bloom10mono --steps 20 --no-e2e --no-cpu-baseline --no-verify > $O/mono_$n.log 2>&1 || exit 4
