@@ -141,10 +141,12 @@ class PipelinedLeafGather:
         allgather_filters(self.local[c * rb:(c + 1) * rb], self.gathered[c * W * rb:(c + 1) * W * rb],
                           self.group)
 
-    def step(self, key_batches, build: bool = True, gather: bool = True):
+    def step(self, key_batches, build: bool = True, gather: bool = True, check: bool = False):
         """Build round c on the current stream; gather it on the communication stream once
-        its build is done, while round c + 1 builds.  Returns when the current stream has
-        every gathered byte (the next step may rebuild the slots)."""
+        its build is done, while round c + 1 builds.  On return the current stream is ordered
+        after every gather: work queued on it next sees the whole array (and may rebuild the
+        slots).  check=True synchronises after each round's build to report VQF insert
+        failures (build_all_filters' check); the default keeps the step asynchronous."""
         import torch
         from .filters import build_all_filters
         if len(key_batches) != len(self.rounds):
@@ -155,7 +157,7 @@ class PipelinedLeafGather:
         for c, kb in enumerate(key_batches):
             if build and self.plans[c] is not None:
                 build_all_filters(self.plans[c], kb, out=self.local[c * rb:(c + 1) * rb],
-                                  workspace=self.ws, check=False)
+                                  workspace=self.ws, check=check)
             if gather:
                 ev = torch.cuda.Event()
                 ev.record(cur)
