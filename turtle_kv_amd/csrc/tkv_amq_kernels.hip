@@ -4063,8 +4063,9 @@ constexpr uint32_t kBloomLdsBudget = 64 * 1024;  // dynamic LDS a launch gets wi
 // keys at 10 bits/key; TurtleKV leaves of small items reach ~80K keys): one workgroup per
 // leaf from kBloomSpreadSegs leaves, the split build below kBloomSplitSegs.  Images above
 // kBloomWideLds take 1024-thread workgroups (fewer than five 256-thread workgroups would fit
-// a CU).  A single larger filter takes the tiled monolithic build (64 KiB tiles); anything
-// else beyond kBloomLeafLdsBudget, device atomics.
+// a CU).  Larger leaves take the window path (up to 16 windows of LDS); a single larger filter
+// of 16- or 24-byte keys the tiled monolithic build (128 KiB tiles); anything else, device
+// atomics.
 constexpr uint32_t kBloomLeafLdsBudget = 160 * 1024;
 constexpr uint32_t kBloomWideLds = 32 * 1024;
 // The LDS build runs one workgroup per leaf, so a batch of a few leaves (the per-leaf call
