@@ -71,7 +71,9 @@ __constant__ BloomSeeds c_bloom = make_bloom_seeds();
 // ---------------------------------------------------------------------------------------
 // kKey24: fixed 24-byte keys, 8-byte aligned (Bloom build fast path; other kernels hash them
 // through the generic fixed-stride path)
-enum KeyMode : int { kKey16 = 0, kKeyFixed = 1, kKeyVar = 2, kKey24 = 3 };
+// kKeyLoc: not a key shape -- the small-batch VQF path's located keys (vqf_locate_keys writes
+// one 8-byte record per key: vqf_loc_encode), read by vqf_ring_place in place of the keys
+enum KeyMode : int { kKey16 = 0, kKeyFixed = 1, kKeyVar = 2, kKey24 = 3, kKeyLoc = 4 };
 
 typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
 
@@ -2193,12 +2195,17 @@ struct VqfKeyBuf<kKeyVar> {
   uint64_t noff;
   uint32_t nlen;
 };
+template <>
+struct VqfKeyBuf<kKeyLoc> {
+  uint2 v;  // the key's located record (vqf_loc_encode)
+};
 template <int MODE>
 constexpr bool kVqfPrefetch = MODE == kKey16 || MODE == kKey24 || MODE == kKeyVar;
-// vqf_decide_ring's producers prefetch 16- and 24-byte keys only (three rotating buffers of
-// variable-length keys would cost the ring kernel its three workgroups per CU)
+// vqf_decide_ring's producers prefetch 16- and 24-byte keys (and located records) only (three
+// rotating buffers of variable-length keys would cost the ring kernel its three workgroups
+// per CU)
 template <int MODE>
-constexpr bool kVqfRingPrefetch = MODE == kKey16 || MODE == kKey24;
+constexpr bool kVqfRingPrefetch = MODE == kKey16 || MODE == kKey24 || MODE == kKeyLoc;
 
 // the bytes of the key whose offsets `prev` holds, and the offsets of key gi_next.  Every lane
 // issues the same loads (clamped to a safe address when the key is shorter: the offsets
@@ -2227,6 +2234,8 @@ __device__ inline void vqf_load_key(const uint8_t* __restrict__ keys, uint64_t g
     const uint64_t* p = reinterpret_cast<const uint64_t*>(keys) + 3 * gi;
 #pragma unroll
     for (int i = 0; i < 3; ++i) kb.w[i] = p[i];
+  } else if constexpr (MODE == kKeyLoc) {
+    kb.v = reinterpret_cast<const uint2*>(keys)[gi];
   }
 }
 
@@ -2288,6 +2297,30 @@ __device__ inline void vqf_locate_alt(const VqfLoc& l, uint64_t R, uint64_t magi
   ab = ai / C::kBuckets;
   ao = ai - ab * C::kBuckets;
 }
+
+// A located key (kKeyLoc; leaves of <= 2,048 blocks): x = primary block | alternate block << 11
+// | primary bucket offset << 22 | kept << 31, y = tag | alternate bucket offset << 16
+template <int T>
+__device__ inline uint2 vqf_loc_encode(uint64_t h, const tkv_amq_segment& sg)
+{
+  using C = Vqf<T>;
+  const uint64_t R = (uint64_t)sg.n_blocks * C::kBuckets;
+  const VqfLoc l = vqf_locate<T>(h, true, ~0ull << sg.hash_val_shift, R, sg.mod_magic);
+  uint32_t ab, ao;
+  vqf_locate_alt<T>(l, R, sg.mod_magic, ab, ao);
+  return make_uint2(l.pb | ab << 11 | l.po << 22 | (l.kept ? 1u << 31 : 0u), l.tag | ao << 16);
+}
+__device__ inline void vqf_loc_decode(uint2 r, bool valid, VqfLoc& l, uint32_t& ab, uint32_t& ao)
+{
+  l.h = 0;
+  l.pb = r.x & 2047u;
+  ab = (r.x >> 11) & 2047u;
+  l.po = (r.x >> 22) & 127u;
+  l.kept = valid && (r.x >> 31) != 0;
+  l.tag = r.y & 0xffffu;
+  ao = r.y >> 16;
+}
+constexpr uint32_t kVqfLocMaxBlocks = 2048;
 
 // Exact replay of the reference insert order (build_vqf_filter<T>, filter_builder.hpp:204-214)
 // for one leaf, 64 keys per step.  The power-of-two-choice decision of key i depends only on
@@ -2778,8 +2811,14 @@ __device__ __attribute__((always_inline)) void vqf_ring_produce(const uint8_t* _
   auto produce = [&](uint32_t q, KB& kv) {
     const uint32_t i = q * 64 + lane;
     const bool valid = i < n;
+    VqfLoc l;
+    uint32_t ab, ao;
+    if constexpr (MODE == kKeyLoc) {
+      vqf_loc_decode(kv.v, valid, l, ab, ao);
+      load(q + kDepth * kStep, kv);
+    } else {
     uint64_t h = 0;
-    if constexpr (kVqfRingPrefetch<MODE>) {
+    if constexpr (MODE == kKey16 || MODE == kKey24) {
       h = valid ? vqf_key_hash<MODE>(keys, offs, stride, sg.key_begin + i, kv) : 0;
     } else if constexpr (MODE == kKeyVar) {
       const uint64_t gi = sg.key_begin + min(i, n - 1), o0 = offs[gi];
@@ -2802,9 +2841,9 @@ __device__ __attribute__((always_inline)) void vqf_ring_produce(const uint8_t* _
       h = valid ? hash_key<MODE>(keys, offs, stride, sg.key_begin + i, kVqfHashSeed) : 0;
     }
     load(q + kDepth * kStep, kv);
-    const VqfLoc l = vqf_locate<T>(h, valid, mask, R, magic);
-    uint32_t ab, ao;
+    l = vqf_locate<T>(h, valid, mask, R, magic);
     vqf_locate_alt<T>(l, R, magic, ab, ao);
+    }
     const uint64_t keptmask = __ballot(l.kept);
     uint32_t pp_lo = (uint32_t)keptmask, pp_hi = (uint32_t)(keptmask >> 32);
     uint32_t pa_lo = pp_lo, pa_hi = pp_hi, ap_lo = pp_lo, ap_hi = pp_hi, aa_lo = pp_lo, aa_hi = pp_hi;
@@ -3663,6 +3702,17 @@ __global__ __launch_bounds__(NT) void vqf_place_fused(const tkv_amq_segment* __r
 // LDS: ring | ready/freed | counts [cnt_words] | image [nb x 33 dwords] | sink | nelts.
 // ---------------------------------------------------------------------------------------
 constexpr uint32_t kRingPlaceMaxSegs = 256;
+// vqf_locate_keys before vqf_ring_place up to this many leaves (variable-length keys, other
+// fixed sizes): measured crossovers, past which the chip is busy enough that hashing inside the
+// producers, overlapped with the decider, beats writing and re-reading 8-byte located records
+#ifndef TKV_EXP_LOC_VAR_SEGS
+#define TKV_EXP_LOC_VAR_SEGS 64
+#endif
+#ifndef TKV_EXP_LOC_FIXED_SEGS
+#define TKV_EXP_LOC_FIXED_SEGS 32
+#endif
+constexpr uint32_t kVqfLocMaxSegsVar = TKV_EXP_LOC_VAR_SEGS;
+constexpr uint32_t kVqfLocMaxSegsFixed = TKV_EXP_LOC_FIXED_SEGS;
 __host__ __device__ inline uint32_t ring_place_cnt_words(uint32_t max_nb)
 {
   return (max_nb + 1 + 3) & ~3u;  // + the dummy block
@@ -3690,6 +3740,7 @@ constexpr uint32_t kRingPlace2MaxBlocks =
 static_assert(ring_place_lds_bytes(kRingPlace2MaxBlocks, kRingPlace2Slots, false) <= 80 * 1024,
               "two vqf_ring_place workgroups per CU");
 static_assert(kRingPlace2MaxBlocks == 420, "(DESIGN.md and test_vqf_ring_place_classes quote it)");
+static_assert(kRingPlaceMaxBlocks < kVqfLocMaxBlocks, "located records hold 11-bit block ids");
 
 template <int T, int MODE, int NBITS, uint32_t NS>
 __device__ __attribute__((always_inline)) void vqf_ring_place_body(const uint8_t* keys, const uint64_t* offs, uint32_t stride,
@@ -3722,9 +3773,43 @@ __device__ __attribute__((always_inline)) void vqf_ring_place_body(const uint8_t
   diag_stamp(2);
 }
 
+// every key of a small batch hashed and located on the whole chip, ahead of vqf_ring_place
+// (kKeyLoc): the hashing leaves the ring's CU, whose producers then only read the records
+template <int MODE>
+__global__ __launch_bounds__(256) void vqf_locate_keys(const uint8_t* __restrict__ keys,
+                                                       const uint64_t* __restrict__ offs, uint32_t stride,
+                                                       const tkv_amq_segment* __restrict__ segs,
+                                                       void* ws_base, uint64_t ws_bytes, uint32_t n_segs,
+                                                       uint64_t n_keys)
+{
+  const uint64_t gi = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (gi >= n_keys) return;
+  // the key's leaf: the last with key_begin <= gi (leaves lie in key order)
+  uint32_t lo = 0, hi = n_segs;
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) / 2;
+    if (segs[mid].key_begin <= gi) lo = mid;
+    else hi = mid;
+  }
+  const tkv_amq_segment sg = segs[lo];
+  if (gi >= sg.key_begin + sg.n_keys || (sg.tag_bits != 8 && sg.tag_bits != 16)) return;
+  const VqfWorkspace ws = vqf_workspace(ws_base, n_segs);
+  if (!vqf_ws_ok(segs, n_segs, ws_bytes, ws, ~0u)) return;  // (vqf_ring_place flags the leaf)
+  uint64_t h;
+  if constexpr (MODE == kKey16 || MODE == kKey24) {
+    VqfKeyBuf<MODE> kb;
+    vqf_load_key<MODE>(keys, gi, kb);
+    h = vqf_key_hash<MODE>(keys, offs, stride, gi, kb);
+  } else {
+    h = hash_key<MODE>(keys, offs, stride, gi, kVqfHashSeed);
+  }
+  reinterpret_cast<uint2*>(vqf_records(ws, segs, n_segs))[gi] =
+      sg.tag_bits == 8 ? vqf_loc_encode<8>(h, sg) : vqf_loc_encode<16>(h, sg);
+}
+
 template <int MODE, uint32_t NS>
 __global__ __launch_bounds__(kRingThreads) void vqf_ring_place(
-    const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint32_t stride,
+    const uint8_t* keys, const uint64_t* __restrict__ offs, uint32_t stride,
     const tkv_amq_segment* __restrict__ segs, void* ws_base, uint64_t ws_bytes, uint32_t n_segs,
     uint8_t* __restrict__ out, uint32_t cnt_words, uint32_t tbl)
 {
@@ -3735,6 +3820,8 @@ __global__ __launch_bounds__(kRingThreads) void vqf_ring_place(
   if (!vqf_ws_ok(segs, n_segs, ws_bytes, ws, blockIdx.x)) return;
   const uint64_t key_end = vqf_key_end<MODE>(offs, segs, n_segs);
   const uint32_t nb = sg.n_blocks;  // <= kRingPlaceMaxBlocks (tkv_amq_build)
+  // kKeyLoc: the located records vqf_locate_keys wrote, where vqf_decide_ring writes its records
+  if constexpr (MODE == kKeyLoc) keys = reinterpret_cast<const uint8_t*>(vqf_records(ws, segs, n_segs));
   if (sg.tag_bits == 8) {
     if (nb <= 512) vqf_ring_place_body<8, MODE, 9, NS>(keys, offs, stride, sg, blockIdx.x, ws, out, s_ring, cnt_words, tbl != 0, key_end);
     else vqf_ring_place_body<8, MODE, 10, NS>(keys, offs, stride, sg, blockIdx.x, ws, out, s_ring, cnt_words, tbl != 0, key_end);
@@ -4838,16 +4925,34 @@ int tkv_amq_build(int kind, const uint8_t* keys, const uint64_t* offs, uint32_t 
                             reinterpret_cast<const void*>(&vqf_ring_place<kKey16, kRingPlace2Slots>),
                             reinterpret_cast<const void*>(&vqf_ring_place<kKey24, kRingPlace2Slots>),
                             reinterpret_cast<const void*>(&vqf_ring_place<kKeyFixed, kRingPlace2Slots>),
-                            reinterpret_cast<const void*>(&vqf_ring_place<kKeyVar, kRingPlace2Slots>)})
+                            reinterpret_cast<const void*>(&vqf_ring_place<kKeyVar, kRingPlace2Slots>),
+                            reinterpret_cast<const void*>(&vqf_ring_place<kKeyLoc, kRingPlaceSlots>),
+                            reinterpret_cast<const void*>(&vqf_ring_place<kKeyLoc, kRingPlace2Slots>)})
         (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     });
     const dim3 g(n_segs), b(kRingThreads);
     const uint32_t cw = ring_place_cnt_words(max_blocks);
     const uint32_t tbl = rp1 && max_blocks <= kRingTblBlocks;  // (ring_place_lds_bytes sizes them)
     const size_t rl = rp1 ? ring_place_lds_bytes(max_blocks) : ring_place_lds_bytes(max_blocks, kRingPlace2Slots, false);
+    // keys read where they are hashed (other than 16 or 24 bytes: the producers, not the
+    // decider, set a lone leaf's time): every key hashed and located on the whole chip first
+    // (vqf_locate_keys), the ring's producers then read 8-byte located records
+    const bool loc = !prefetched && n_segs <= (mode == kKeyVar ? kVqfLocMaxSegsVar : kVqfLocMaxSegsFixed);
+    if (loc && n_keys > 0) {
+      const dim3 lg((uint32_t)div_up(n_keys, 256)), lb(256);
+      if (mode == kKeyFixed)
+        hipLaunchKernelGGL(vqf_locate_keys<kKeyFixed>, lg, lb, 0, s, keys, offs, stride, d_segs, d_ws, ws_bytes, n_segs,
+                           n_keys);
+      else
+        hipLaunchKernelGGL(vqf_locate_keys<kKeyVar>, lg, lb, 0, s, keys, offs, stride, d_segs, d_ws, ws_bytes, n_segs,
+                           n_keys);
+    }
 #define TKV_RING_PLACE(NS)                                                                              \
   do {                                                                                                  \
-    if (vmode == kKey16)                                                                                \
+    if (loc)                                                                                            \
+      hipLaunchKernelGGL((vqf_ring_place<kKeyLoc, NS>), g, b, rl, s, nullptr, nullptr, 0, d_segs, d_ws,   \
+                         ws_bytes, n_segs, d_out, cw, tbl);                                             \
+    else if (vmode == kKey16)                                                                           \
       hipLaunchKernelGGL((vqf_ring_place<kKey16, NS>), g, b, rl, s, keys, offs, stride, d_segs, d_ws,     \
                          ws_bytes, n_segs, d_out, cw, tbl);                                             \
     else if (vmode == kKey24)                                                                           \
