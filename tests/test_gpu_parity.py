@@ -384,7 +384,7 @@ def test_vqf_ring_place_classes(oracle, amq, torch, n_leaves, edge, bpk):
         assert segment_bytes(plan, out, s) == ref[:p.payload_used].tobytes(), f"leaf {s}"
 
 
-@pytest.mark.parametrize("shape", ["k16", "k24", "var"])
+@pytest.mark.parametrize("shape", ["k16", "k24", "k20", "var"])
 @pytest.mark.parametrize("bpk", [12, 22])
 @pytest.mark.parametrize("cap", [65472, 8128])
 def test_vqf_ring_edges(oracle, amq, torch, shape, bpk, cap):
@@ -392,8 +392,8 @@ def test_vqf_ring_edges(oracle, amq, torch, shape, bpk, cap):
     (no key ever reaches the alternate-choice threshold), 40 keys in one block (the threshold
     is reached inside the first 64-key chunk; two blocks each at 16-bit tags), 1 and 0 keys,
     700, a 16,384-key leaf; 8- and 16-bit tags; in 8 KiB pages (cap 8128) the larger leaves
-    keep only masked keys (hash_val_shift > 0); 16-, 24-byte and variable-length keys.
-    Byte-equal to the oracle.  (The round-4 parallel-prefix variant of the ring,
+    keep only masked keys (hash_val_shift > 0); 16-, 24-, 20-byte and variable-length keys
+    (the last two through vqf_locate_keys' located records).  Byte-equal to the oracle.  (The round-4 parallel-prefix variant of the ring,
     tools/patches/r04_vqf_loc_prefix_tile_loop.patch, was checked with these leaves.)"""
     counts = [30, 40, 1, 0, 700, 16384, 5000]
     n = sum(counts)
@@ -401,8 +401,9 @@ def test_vqf_ring_edges(oracle, amq, torch, shape, bpk, cap):
     offs = None
     if shape == "k16":
         keys, stride = oracle.gen_keys16(12, 0, n), 16
-    elif shape == "k24":
-        keys, stride = rng.integers(0, 256, (n, 24), dtype=np.uint8), 24
+    elif shape in ("k24", "k20"):
+        stride = int(shape[1:])
+        keys = rng.integers(0, 256, (n, stride), dtype=np.uint8)
     else:
         lens = rng.integers(6, 40, n)
         keys, stride = rng.integers(0, 256, int(lens.sum()), dtype=np.uint8), 0
@@ -423,6 +424,38 @@ def test_vqf_ring_edges(oracle, amq, torch, shape, bpk, cap):
         else:
             o = (offs[b:b + c + 1] - offs[b]).astype(np.uint64)
             st, ref, p = oracle.vqf_build(keys[int(offs[b]):], c, bpk, cap, src_page_id=s,
+                                          offsets=o, stride=0)
+        assert st == 0
+        assert segment_bytes(plan, out, s) == ref[:p.payload_used].tobytes(), f"leaf {s}"
+
+
+@pytest.mark.parametrize("shape,n_leaves", [("var", 64), ("var", 65), ("k20", 32), ("k20", 33)])
+def test_vqf_located_keys_threshold(oracle, amq, torch, shape, n_leaves):
+    """Either side of the leaf counts up to which small VQF batches of variable-length (64)
+    and 20-byte (32) keys are hashed and located on the whole chip before vqf_ring_place
+    (kVqfLocMaxSegsVar/Fixed): ragged leaves, byte-equal to the oracle on a sample."""
+    rng = np.random.default_rng(n_leaves)
+    counts = rng.integers(0, 3000, n_leaves).tolist()
+    counts[1] = 0
+    n = sum(counts)
+    offs = None
+    if shape == "k20":
+        keys, stride = rng.integers(0, 256, (n, 20), dtype=np.uint8), 20
+    else:
+        lens = rng.integers(1, 48, n)
+        keys, stride = rng.integers(0, 256, int(lens.sum()), dtype=np.uint8), 0
+        offs = np.zeros(n + 1, np.int64)
+        offs[1:] = np.cumsum(lens)
+    plan, out = gpu_build(amq, torch, 1, torch.from_numpy(keys).cuda(), counts, 12, cap=65472,
+                          offsets_t=None if offs is None else torch.from_numpy(offs).cuda())
+    sb = seg_bounds(counts)
+    for s in sorted({0, 1, n_leaves - 1, *rng.integers(0, n_leaves, 5).tolist()}):
+        b, c = int(sb[s]), counts[s]
+        if offs is None:
+            st, ref, p = oracle.vqf_build(keys[b:], c, 12, 65472, src_page_id=s, stride=stride)
+        else:
+            o = (offs[b:b + c + 1] - offs[b]).astype(np.uint64)
+            st, ref, p = oracle.vqf_build(keys[int(offs[b]):], c, 12, 65472, src_page_id=s,
                                           offsets=o, stride=0)
         assert st == 0
         assert segment_bytes(plan, out, s) == ref[:p.payload_used].tobytes(), f"leaf {s}"
