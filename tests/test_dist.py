@@ -122,28 +122,30 @@ def test_hash_shard_tiles_cover_the_filter():
 
 
 def test_hash_shard_parts_per_rank():
-    """A rank's range is cut into g parts of at most 1,600 tiles (ROUTED_PART_TILES, under the
-    6,400 of one range build's LDS tile table): BASELINE config 5 (1B keys at 12 bits/key,
-    11,445 tiles) builds parts of 1,431 tiles at every N -- 8 on one rank, 4 each on two, 1 each
-    on eight; the parts of all ranks tile the filter, and rank r's range is its parts' union."""
-    from turtle_kv_amd.dist import ROUTED_PART_TILES, HashShardedBloom, hash_shard_plan
+    """A rank's range is cut into g parts of at most 256 tiles of bit records
+    (ROUTED_PART_TILES) or 1,600 of routed keys (ROUTED_KEY_PART_TILES), under the 6,400 of one
+    range build's LDS tile table: BASELINE config 5 (1B keys at 12 bits/key, 11,445 tiles)
+    builds 45 parts of 255 tiles on one rank, 23 of 249 on each of two, 6 of 239 on each of eight; the
+    parts of all ranks tile the filter, and rank r's range is its parts' union."""
+    from turtle_kv_amd.dist import (ROUTED_KEY_PART_TILES, ROUTED_PART_TILES, HashShardedBloom,
+                                    hash_shard_plan)
     nb_1b = -(-1_000_000_000 * 12 // 512)
-    assert hash_shard_plan(nb_1b, 1) == (11445, 8, 1431)
-    assert hash_shard_plan(nb_1b, 2)[1:] == (4, 1431)
-    assert hash_shard_plan(nb_1b, 4)[1:] == (2, 1431)
-    assert hash_shard_plan(nb_1b, 8)[1:] == (1, 1431)
+    assert hash_shard_plan(nb_1b, 1) == (11445, 45, 255)
+    assert hash_shard_plan(nb_1b, 2)[1:] == (23, 249)
+    assert hash_shard_plan(nb_1b, 4)[1:] == (12, 239)
+    assert hash_shard_plan(nb_1b, 8)[1:] == (6, 239)
     assert hash_shard_plan(nb_1b, 1, records=False) == (11445, 8, 1431)
     for nb in [1, 5000, nb_1b, 3 * nb_1b, 40_000_000 * 2048]:
         for world in [1, 2, 3, 8]:
             for rec in (True, False):
                 T, g, q = hash_shard_plan(nb, world, rec)
-                assert q <= ROUTED_PART_TILES
+                assert q <= (ROUTED_PART_TILES if rec else ROUTED_KEY_PART_TILES)
                 parts = [(min(T, p * q), min(T, (p + 1) * q)) for p in range(world * g)]
                 assert parts[0][0] == 0 and parts[-1][1] == T
                 assert all(a[1] == b[0] for a, b in zip(parts, parts[1:]))
     hs = HashShardedBloom(1_000_000_000, 12, 2, 1, "meta")
-    assert (hs.g, hs.q, hs.tile_begin, hs.tile_end) == (4, 1431, 5724, 11445)
-    assert hs.part_tiles(0) == (5724, 7155) and hs.part_tiles(3) == (10017, 11445)
+    assert (hs.g, hs.q, hs.tile_begin, hs.tile_end) == (23, 249, 5727, 11445)
+    assert hs.part_tiles(0) == (5727, 5976) and hs.part_tiles(22) == (11205, 11445)
 
 
 def test_build_owned_regroups_parts():

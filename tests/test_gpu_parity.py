@@ -617,13 +617,13 @@ def sampled_tiles_equal_oracle(oracle, out, n, bpk, seed, n_random=6):
     return T
 
 
-@pytest.mark.parametrize("n,bpk,parts", [(108_000_000, 10, 1), (1_750_000_000, 12, 13),
+@pytest.mark.parametrize("n,bpk,parts", [(108_000_000, 10, 1), (1_750_000_000, 12, 79),
                                          (700_000_000, 64, 27)])
 def test_bloom_monolithic_large_sampled_oracle(oracle, amq, torch, n, bpk, parts):
     """Full-size monolithic filters against the oracle on eight sampled tiles and the header:
     108M keys at 10 bits/key (1,030 tiles: the partition reads the keys), 1.75B keys at 12
     bits/key (20,028 tiles, beyond one partition's 6,400-tile table: routed as 12-byte records
-    into 13 parts of <= 1,600 tiles, each built from its records, its count read on the device)
+    into 79 parts of <= 256 tiles, each built from its records, its count read on the device)
     and 700M keys at 64 bits/key (42,725 tiles, k = 44: the 16-byte keys themselves routed into
     27 parts)."""
     from turtle_kv_amd import abi
@@ -634,8 +634,8 @@ def test_bloom_monolithic_large_sampled_oracle(oracle, amq, torch, n, bpk, parts
     direct = T <= int(L.tkv_amq_bloom_range_max_tiles(0))
     assert direct == (parts == 1)
     if not direct:
-        from turtle_kv_amd.dist import ROUTED_PART_TILES
-        assert -(-T // ROUTED_PART_TILES) == parts
+        from turtle_kv_amd.dist import ROUTED_KEY_PART_TILES, ROUTED_PART_TILES
+        assert -(-T // (ROUTED_PART_TILES if bpk <= 12 else ROUTED_KEY_PART_TILES)) == parts
     keys = amq.gen_keys16(seed, 0, n)
     out = amq.build_all_filters(plan, amq.KeyBatch.fixed(keys))
     del keys

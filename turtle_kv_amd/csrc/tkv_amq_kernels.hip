@@ -4395,11 +4395,17 @@ struct MonoPlan {
 };
 
 // Tiles per routed part (a filter past kDirectMaxTiles): the fewer tiles a partition spreads
-// a batch over, the longer each tile's run per store (fewer partial-line writes).  1B keys at
-// 12 bits/key: 8 parts of 1,431 tiles, the parts an 8-rank hash-range build gives each rank
-// (turtle_kv_amd.dist.ROUTED_PART_TILES)
-constexpr uint32_t kRoutePartTiles = 1600;
-static_assert(kRoutePartTiles <= kRecPartMaxTiles, "");
+// a batch over, the longer each tile's run per store (fewer partial-line writes), until the
+// route's scatter over that many parts pays more than the part builds save; and at most one
+// tile per CU, so a part's tile kernel runs in one round.  Bit records (k <= 8), 1B keys at 12
+// bits/key on one GPU: 1,431-tile parts 36.7 Gkeys/s, 800 39.2, 400 40.4, 294 39.8, 255 42.6,
+// 229 41.9, 198 41.5, 127 37.1, 100 33.6 (profiles/r04/part_tiles/).  16-byte keys routed as
+// themselves (k > 8) keep 1,600.  (turtle_kv_amd.dist.ROUTED_PART_TILES, ROUTED_KEY_PART_TILES)
+constexpr uint32_t kRoutePartTiles = 256;
+constexpr uint32_t kRouteKeyPartTiles = 1600;
+static_assert(kRoutePartTiles <= kRecPartMaxTiles && kRouteKeyPartTiles <= kRecPartMaxTiles, "");
+
+inline uint32_t bloom_k_of(uint64_t n_keys, uint64_t n_blocks);
 
 inline MonoPlan mono_plan(uint64_t n_keys, uint64_t n_blocks)
 {
@@ -4412,7 +4418,8 @@ inline MonoPlan mono_plan(uint64_t n_keys, uint64_t n_blocks)
     m.bytes = m.pg.bytes;
     return m;
   }
-  m.g = (uint32_t)div_up(m.T, kRoutePartTiles);
+  const uint32_t k = bloom_k_of(n_keys, n_blocks);  // (0: unknown -- any part size is exact)
+  m.g = (uint32_t)div_up(m.T, k >= 1 && k <= 8 ? kRoutePartTiles : kRouteKeyPartTiles);
   m.q = (uint32_t)div_up(m.T, m.g);
   m.rg = route_geom(n_keys, m.g);
   m.items_off = align256(m.rg.bytes);

@@ -193,17 +193,22 @@ class PipelinedLeafGather:
 BLOOM_TILE_BLOCKS = 2048        # tkv_amq_bloom_tile_blocks()
 RECORD_RANGE_MAX_TILES = 6400   # tkv_amq_bloom_range_max_tiles(1): the partition's tile table
 KEY_RANGE_MAX_TILES = 6400      # tkv_amq_bloom_range_max_tiles(0)
-ROUTED_PART_TILES = 1600        # the library's kRoutePartTiles: tiles per routed part
+ROUTED_PART_TILES = 256         # the library's kRoutePartTiles: tiles per part of bit records
+ROUTED_KEY_PART_TILES = 1600    # kRouteKeyPartTiles: tiles per part of routed 16-byte keys
 
 
 def hash_shard_plan(n_blocks: int, world: int, records: bool = True) -> tuple[int, int, int]:
     """(T, g, q): the filter's tiles, the parts per rank and the tiles per part; part p owns
     tiles [p*q, min((p+1)*q, T)) and rank r parts [r*g, (r+1)*g).  Parts hold at most
-    ROUTED_PART_TILES tiles (the library's kRoutePartTiles), well under what one range build
-    takes: BASELINE config 5 (1B keys at 12 bits/key) builds parts of 1,431 tiles at every N."""
+    ROUTED_PART_TILES tiles of bit records (ROUTED_KEY_PART_TILES of routed keys), well under
+    what one range build takes: the fewer tiles a part build spreads a batch of records over,
+    the longer its stores' runs, and at most one tile per CU (kRoutePartTiles).  BASELINE
+    config 5 (1B keys at 12 bits/key, 11,445 tiles) builds 45 parts of 255 tiles on one GPU,
+    6 of 239 on each of eight."""
     T = -(-int(n_blocks) // BLOOM_TILE_BLOCKS)
     per_rank = -(-T // world)
-    cap = min(ROUTED_PART_TILES, RECORD_RANGE_MAX_TILES if records else KEY_RANGE_MAX_TILES)
+    cap = (min(ROUTED_PART_TILES, RECORD_RANGE_MAX_TILES) if records
+           else min(ROUTED_KEY_PART_TILES, KEY_RANGE_MAX_TILES))
     g = max(1, -(-per_rank // cap))
     q = -(-T // (world * g))
     return T, g, q
