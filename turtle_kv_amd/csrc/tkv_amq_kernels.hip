@@ -993,7 +993,10 @@ constexpr uint32_t kPartPlaneBytes = 12 * kPartBatch;       // the batch's recor
 constexpr uint32_t kDirectMaxTiles = 6400;                  // LDS: 10 bytes per tile beside the planes
 constexpr uint32_t kRecPartMaxTiles = kDirectMaxTiles;      // (< 2^13: a record's tile field)
 constexpr uint32_t kRouteMaxParts = 2048;                   // tkv_amq_bloom_route(_records)
-constexpr uint32_t kRouteMaxWgs = 1024;                     // route count / scatter workgroups
+#ifndef TKV_EXP_ROUTE_WGS
+#define TKV_EXP_ROUTE_WGS 1024
+#endif
+constexpr uint32_t kRouteMaxWgs = TKV_EXP_ROUTE_WGS;        // route count / scatter workgroups
 
 __host__ __device__ constexpr inline uint32_t part_lds_bytes(uint32_t n_tiles)
 {
