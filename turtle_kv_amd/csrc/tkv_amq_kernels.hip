@@ -994,7 +994,7 @@ constexpr uint32_t kDirectMaxTiles = 6400;                  // LDS: 10 bytes per
 constexpr uint32_t kRecPartMaxTiles = kDirectMaxTiles;      // (< 2^13: a record's tile field)
 constexpr uint32_t kRouteMaxParts = 2048;                   // tkv_amq_bloom_route(_records)
 #ifndef TKV_EXP_ROUTE_WGS
-#define TKV_EXP_ROUTE_WGS 1024
+#define TKV_EXP_ROUTE_WGS 1792
 #endif
 constexpr uint32_t kRouteMaxWgs = TKV_EXP_ROUTE_WGS;        // route count / scatter workgroups
 
