@@ -16,9 +16,10 @@ must equal --gpus.  The RCCL all-gather of the filter array (north star) is time
 after the timed region and reported as `allgather_ms` (`--allgather` puts it inside the
 timed step instead); rank 0 then checks the gathered array against a single-process build.
 
-After the timed region every rank byte-compares a sample of its leaves (first, last, the
-partial leaf, 8 seeded-random ones) with the CPU oracle built from independently generated
-keys ("verified"); probe workloads compare all 200M answers with the oracle's ("fpr_oracle").
+After the timed region every rank byte-compares ALL of its leaves with the CPU oracle built
+from independently generated keys ("verified"; "verify": leaves_checked == of_leaves); probe
+workloads compare all 200M answers with the oracle's ("fpr_oracle"); the hash-range sharded
+filter (config 5) is compared whole with a multithreaded oracle build of all keys.
 
 The printed JSON line carries `roofline` (dominant kernel, HIP events on the build stream,
 algorithmic bytes), `valu_roofline` (the bound the build kernels sit on: PMC VALU instructions
@@ -89,6 +90,9 @@ def parse():
                          "ranks by leaf range (BASELINE config 5: --workload bloom12 "
                          "--total-keys 1000000000)")
     ap.add_argument("--allgather", action="store_true", help="time the RCCL all-gather in-step")
+    ap.add_argument("--no-step-allgather", action="store_true",
+                    help="bloom12hash: time the all-gather of the filter's rounds after the "
+                         "step instead of pipelined inside it")
     ap.add_argument("--chunks", type=int, default=1,
                     help="with a process group: build each rank's leaves in this many rounds of "
                          "block-cyclic leaf chunks and all-gather round c on a communication "
@@ -112,6 +116,9 @@ def parse():
                     help="also time the build over the first 64 / 256 / 1024 leaves (batch-size "
                          "curve; off by default so that a kernel-trace profile of the default "
                          "command averages the timed launches only)")
+    ap.add_argument("--experiment-lib", action="store_true",
+                    help="allow TKV_AMQ_LIB (an experiment build of the library) for kernel A/B "
+                         "timing")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="CPU baseline threads (0: every core this process may use)")
     return ap.parse_args()
@@ -244,6 +251,11 @@ def cpu_baseline(kind, bpk, cap, keys_host, counts, threads, leaf_keys=SEG_KEYS)
 # ---------------------------------------------------------------------------------------
 def main():
     args = parse()
+    if os.environ.get("TKV_AMQ_LIB") and not args.experiment_lib:
+        raise SystemExit("bench.py: TKV_AMQ_LIB names an experiment library; pass "
+                         "--experiment-lib to time it (its line is not the shipped library's)")
+    if args.experiment_lib:
+        os.environ["TKV_AMQ_EXPERIMENT"] = "1"
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -364,7 +376,7 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    if not probe and kind == 1 and not os.environ.get("TKV_AMQ_LIB"):  # (experiment libs skip it)
+    if not probe and kind == 1:
         amq.abi.check(amq.abi.lib().tkv_amq_build_check(kind, amq.filters._ptr(ws),
                                                         ws.numel(),
                                                         amq.filters._stream_handle()), "vqf build")
@@ -402,8 +414,8 @@ def main():
                                                  and not args.no_cpu_baseline))
             ok = True
         else:
-            verified = verify_sample(torch, kind, bpk, cap, plan, keys, offsets, out, key_bytes,
-                                     shard, rank, leaf_keys)
+            verified = verify_all_leaves(torch, kind, bpk, cap, plan, keys, offsets, out,
+                                         key_bytes, shard, host_cpu_share()[0])
             ok = verified["ok"]
         if pg:
             flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=coll_dev)
@@ -764,21 +776,24 @@ def bench_pipelined_gather(args, torch, dist, amq, world, rank, dev, kind, bpk, 
 # hash-range sharded monolithic Bloom (BASELINE config 5 read literally)
 # ---------------------------------------------------------------------------------------
 def bench_hash_sharded(args, torch, dist, amq, world, rank, dev, bpk, label, pg=False):
-    """One Bloom filter over every rank's keys; rank r owns a contiguous byte range of its
-    bitmap (turtle_kv_amd.dist.HashShardedBloom).  A step = route (every key hashed once into
-    its 12-byte bit record, ordered by owning part) + all-to-all of the records (RCCL) + the
-    rank's part builds; the all-gather of the ranges is timed separately (in-step with
-    --allgather).  Without a process group (one GPU, no launcher) the step is the range build
-    over the GPU's own keys, which makes the same records itself.  Rank 0 checks the gathered
-    filter against a one-GPU build of all keys, and that against the CPU oracle: the whole
-    filter up to 200M keys, beyond that the header and eight sampled tiles (the first, the last
-    and six seeded-random ones), the oracle hashing every key for them."""
+    """One Bloom filter over every rank's keys; rank r owns parts r, r + N, r + 2N, ... of its
+    bitmap (turtle_kv_amd.dist.HashShardedBloom).  A step, pipelined over a compute and a
+    communication stream: route the rank's keys in K chunks (every key hashed once into its
+    12-byte bit record, counting-sorted by part into fixed-capacity blocks) -> all-to-all of
+    chunk c's blocks while chunk c + 1 routes (RCCL, equal splits, no host synchronisation) ->
+    build each owned part from the blocks received -> all-gather round j (part j of every
+    rank, one contiguous range) in place while part j + 1 builds.  With --no-step-allgather the
+    gather is timed separately.  Without a process group (one GPU, no launcher) the step is the
+    route and the part builds.  Rank 0 checks the whole gathered filter against the CPU oracle
+    (every key hashed on every host thread) after the timed region."""
     from turtle_kv_amd import dist as tdist
     strong = args.total_keys is not None
     n_local = args.total_keys // world if strong else args.keys_per_gpu
     total = n_local * world
+    chunks = args.chunks if args.chunks > 1 else (4 if world > 1 else 1)
     keys = amq.gen_keys16(42, rank * n_local, n_local, device=dev)
-    hs = tdist.HashShardedBloom(total, bpk, world, rank, dev)
+    hs = tdist.HashShardedBloom(total, bpk, world, rank, dev, chunks=chunks)
+    gather_in_step = pg and not args.no_step_allgather
 
     def progress(msg):  # long runs (1B keys) report their stages on stderr
         if rank == 0:
@@ -787,9 +802,7 @@ def bench_hash_sharded(args, torch, dist, amq, world, rank, dev, bpk, label, pg=
     progress(f"{n_local} keys per rank generated; ramp")
 
     def step():
-        hs.local_build(keys)
-        if args.allgather and pg:
-            hs.allgather()
+        hs.step(keys, gather=gather_in_step)
 
     ramp0 = time.perf_counter()
     n_ramp = 0
@@ -815,35 +828,50 @@ def bench_hash_sharded(args, torch, dist, amq, world, rank, dev, bpk, label, pg=
     if pg:
         wall = reduce_max(torch, dist, wall, coll_dev)
     progress(f"{args.steps} timed steps: {wall / args.steps * 1e3:.3f} ms per step")
+    lost = hs.lost()  # blocks that needed more overflow room than they have (not for hashed keys)
 
-    # untimed breakdown of one step on this rank (HIP events on the current stream)
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
-    n_owned = n_local
-    ev[0].record()
+    # untimed breakdown: the stages one after another on rank 0 (HIP events on the current
+    # stream; each stage's collectives on the current stream, not overlapped)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(5)]
     if pg:
-        routed, pc = hs.route(keys)
-        ev[1].record()
-        owned, sub = hs.exchange(routed, pc)
-        ev[2].record()
-        hs.build_owned(owned, sub)
-        n_owned = int(owned.shape[0])
-    else:
-        ev[1].record()
-        ev[2].record()
-        hs.local_build(keys)
-    ev[3].record()
+        dist.barrier()
     torch.cuda.synchronize()
-    route_ms, a2a_ms, build_ms = (ev[i].elapsed_time(ev[i + 1]) for i in range(3))
+    ev[0].record()
+    if not hs.records:
+        hs.step(keys, gather=False)
+        ev[1].record()
+        ev[2].record()
+        ev[3].record()
+    else:
+        for c in range(hs.chunks):
+            hs.route_chunk(keys, c)
+        ev[1].record()
+        if pg and world > 1:
+            for c in range(hs.chunks):
+                hs.exchange_chunk(c)
+        ev[2].record()
+        for j in range(hs.g):
+            hs.build_part(j)
+        ev[3].record()
+    if pg:
+        if hs.records:
+            for j in range(hs.g):
+                hs.gather_round(j)
+        else:
+            hs.allgather()
+    ev[4].record()
+    torch.cuda.synchronize()
+    route_ms, a2a_ms, build_ms, gather_ms = (ev[i].elapsed_time(ev[i + 1]) for i in range(4))
 
     allgather_ms = None
-    if pg:
+    if pg and not gather_in_step:
         dist.barrier()
         g0 = time.perf_counter()
         for _ in range(3):
             hs.allgather()
         torch.cuda.synchronize()
         allgather_ms = reduce_max(torch, dist, (time.perf_counter() - g0) / 3 * 1e3, coll_dev)
-    filt = hs.allgather()
+    filt = hs.filter() if hs.records else hs.allgather()
     torch.cuda.synchronize()
     progress("breakdown and all-gather done; verifying")
     comm = comm_info(torch, dist, dev) if pg else None
@@ -852,14 +880,15 @@ def bench_hash_sharded(args, torch, dist, amq, world, rank, dev, bpk, label, pg=
     if rank == 0 and not args.no_verify:
         check = verify_hash_sharded(torch, amq, filt, total, bpk, dev)
     if pg:
-        flag = torch.tensor([1 if (check is None or check["ok"]) else 0], dtype=torch.int32,
-                            device=coll_dev)
+        flag = torch.tensor([1 if (check is None or check["ok"]) and not lost else 0],
+                            dtype=torch.int32, device=coll_dev)
         dist.all_reduce(flag, op=dist.ReduceOp.MIN)
         ok = bool(flag.item())
     else:
-        ok = check is None or check["ok"]
+        ok = (check is None or check["ok"]) and not lost
     if not ok:
-        raise SystemExit(f"bench.py: hash-sharded filter differs: {check}")
+        raise SystemExit(f"bench.py: hash-sharded filter differs (or its blocks lost overflow "
+                         f"entries: {lost}): {check}")
     if pg:
         dist.barrier()
     if rank != 0:
@@ -873,9 +902,13 @@ def bench_hash_sharded(args, torch, dist, amq, world, rank, dev, bpk, label, pg=
     ms_per_step = wall / args.steps * 1e3
     value = total * args.steps / wall / 1e6
     alg = n_local * 16 + (int(hs.payload_bytes) - 64) // world  # keys in, this rank's bitmap out
-    path = ("route -> all-to-all -> part builds" if pg else
-            ("range build from the keys" if hs.T <= tdist.KEY_RANGE_MAX_TILES else
-             "route -> part builds"))
+    if gather_in_step:
+        path = f"route ({chunks} chunks) -> all-to-all -> part builds -> all-gather, pipelined"
+    elif pg:
+        path = f"route ({chunks} chunks) -> all-to-all -> part builds, pipelined"
+    else:
+        path = f"route ({chunks} chunk(s)) -> part builds"
+    rp = getattr(hs, "rp", None)
     line = {
         "metric": f"{label} Mkeys/s (device-resident)",
         "value": round(value, 2), "unit": "Mkeys/s", "n_gpus": world, "steps": args.steps,
@@ -883,23 +916,33 @@ def bench_hash_sharded(args, torch, dist, amq, world, rank, dev, bpk, label, pg=
         "higher_is_better": True, "scaling": "strong" if strong else "weak", "vs_baseline": None,
         "dtype": "u64", "data": "synthetic (splitmix64 seed 42 keys generated on the device)",
         "config": {"workload": f"{label}: {total} x 16B keys, {n_local} per GPU, one filter of "
-                               f"{hs.n_blocks} blocks ({hs.T} tiles); rank r owns tiles "
-                               f"[r*{hs.g * hs.q}, ...) in {hs.g} part(s)",
+                               f"{hs.n_blocks} blocks ({hs.T} tiles) in {world * hs.g} parts of "
+                               f"{hs.q} tiles; rank r owns parts r, r + {world}, ...",
                    "keys_per_gpu": n_local, "total_keys": total, "key_bytes": 16,
                    "bits_per_key": bpk, "filter": "bloom-blocked512, monolithic",
                    "parallelism": f"hash-range-sharded x{world}",
-                   "backend": args.backend if pg else None,
+                   "backend": args.backend if pg else None, "chunks": chunks,
+                   "allgather_in_step": bool(gather_in_step),
                    "path": path, "units": "12-byte bit records" if hs.records else "16-byte keys"},
         "roofline": {"bound": "hbm", "achieved": round(alg / (ms_per_step * 1e-3) / 1e9, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(alg / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                     "traffic": None, "kernel_ms": round(build_ms, 4), "alg_bytes_per_launch": alg,
-                     "note": "whole step on rank 0 (route + all-to-all + range build)"},
+                     "traffic": load_profile(f"bloom12hash{'1B' if total >= 1_000_000_000 else ''}")
+                                .get("hbm_bytes_per_launch"),
+                     "alg_bytes_per_launch": alg,
+                     "note": "whole step on rank 0; traffic: PMC bytes of the step's kernels"},
         "cpu_baseline": base,
         "step_breakdown_rank0_ms": {"route": round(route_ms, 4), "all_to_all": round(a2a_ms, 4),
-                                    "range_build": round(build_ms, 4), "keys_owned": n_owned},
+                                    "part_builds": round(build_ms, 4),
+                                    "allgather": round(gather_ms, 4),
+                                    "note": "the stages run one after another (untimed by value)"},
         "verified": check["ok"] if check else None, "verify": check,
     }
+    if rp is not None:
+        line["route_plan"] = {"route_wgs": rp.route_wgs, "region_cap": rp.region_cap,
+                              "block_bytes": rp.block_bytes, "ovf_cap": rp.ovf_cap,
+                              "exchanged_bytes_per_rank": (world - 1) * chunks * rp.block_bytes,
+                              "overflow_lost": lost}
     if comm is not None:
         line["comm"] = comm
     if allgather_ms is not None:
@@ -908,43 +951,34 @@ def bench_hash_sharded(args, torch, dist, amq, world, rank, dev, bpk, label, pg=
     print(json.dumps(line), flush=True)
 
 
-def verify_hash_sharded(torch, amq, filt, total, bpk, dev, full_oracle_max=200_000_000):
-    """The gathered hash-range sharded filter against a one-GPU tkv_amq_build of all keys and
-    against the CPU oracle (whole filter up to full_oracle_max keys, else header + 8 tiles)."""
-    from turtle_kv_amd import dist as tdist
-    allk = amq.gen_keys16(42, 0, total, device=dev)
-    ref_plan = amq.plan_filters(0, [total], bpk)
-    ref = amq.build_all_filters(ref_plan, amq.KeyBatch.fixed(allk))
-    check = {"equal_to_one_gpu_build": bool(torch.equal(ref[:filt.numel()], filt))}
-    del allk, ref
+def verify_hash_sharded(torch, amq, filt, total, bpk, dev):
+    """The gathered hash-range sharded filter against the CPU oracle, WHOLE: the oracle generates
+    all `total` keys, hashes each one and sets its bits in one host bitmap on every host thread
+    (oracle.bloom_sample_blocks with the single window [0, block_count); ~10 s for config 5's
+    1B keys on 16 threads), and the header is checked field by field."""
     from oracle import oracle as O
     O.build_oracle()
-    if total <= full_oracle_max:
-        st, oref = O.bloom_build(O.gen_keys16(42, 0, total), total, bpk, src_page_id=0)
-        check["equal_to_oracle"] = st == 0 and oref.tobytes() == filt.cpu().numpy().tobytes()
-    else:
-        nb = int(ref_plan.segs[0]["n_blocks"])
-        TB = tdist.BLOOM_TILE_BLOCKS
-        T = -(-nb // TB)
-        rng = np.random.default_rng(7)
-        tiles = sorted({0, T - 1, *[int(t) for t in rng.choice(T, size=min(6, T), replace=False)]})
-        wins = [(t * TB, min(nb, (t + 1) * TB)) for t in tiles]
-        cores, _ = host_cpu_share()
-        t0 = time.perf_counter()
-        st, got = O.bloom_sample_blocks(42, 0, total, bpk, wins, n_threads=cores)
-        dt = time.perf_counter() - t0
-        host = filt.cpu().numpy()
-        same = st == 0 and all(v.tobytes() == host[64 + 64 * a:64 + 64 * b].tobytes()
-                               for (a, b), v in got.items())
-        k = int(O.lib().tkvo_bloom_hash_count(bpk))
-        hdr = np.frombuffer(host[:64].tobytes(), dtype="<u8")
-        hdr_ok = (int(hdr[0]) == 0xCA6F49A0F3F8A4B0 and int(hdr[1]) == 512 * nb and int(hdr[2]) == 0
-                  and int(hdr[3]) == 0 and int(hdr[4]) == 8 * nb
-                  and int(hdr[5]) == nb | (k << 32) | (2 << 48) and int(hdr[6]) == total)
-        check["equal_to_oracle_sampled_tiles"] = bool(same and hdr_ok)
-        check["oracle_sample"] = {"tiles": tiles, "tile_blocks": TB, "of_tiles": T,
-                                  "keys_hashed": total, "threads": cores, "seconds": round(dt, 2)}
-    check["ok"] = all(v for k, v in check.items() if isinstance(v, bool))
+    nb = int(O.lib().tkvo_bloom_block_count(total, bpk))
+    cores, _ = host_cpu_share()
+    t0 = time.perf_counter()
+    st, got = O.bloom_sample_blocks(42, 0, total, bpk, [(0, nb)], n_threads=cores)
+    dt = time.perf_counter() - t0
+    host = filt.cpu().numpy()
+    ref = got[(0, nb)]
+    body_ok = st == 0 and host.size == 64 + ref.size and np.array_equal(host[64:], ref)
+    k = int(O.lib().tkvo_bloom_hash_count(bpk))
+    hdr = np.frombuffer(host[:64].tobytes(), dtype="<u8")
+    hdr_ok = (int(hdr[0]) == 0xCA6F49A0F3F8A4B0 and int(hdr[1]) == 512 * nb and int(hdr[2]) == 0
+              and int(hdr[3]) == 0 and int(hdr[4]) == 8 * nb
+              and int(hdr[5]) == nb | (k << 32) | (2 << 48) and int(hdr[6]) == total)
+    check = {"equal_to_oracle": bool(body_ok and hdr_ok), "header_ok": bool(hdr_ok),
+             "oracle_whole_filter": {"blocks": nb, "bytes": 64 + 64 * nb, "keys_hashed": total,
+                                     "threads": cores, "seconds": round(dt, 2)}}
+    if not body_ok and st == 0 and host.size == 64 + ref.size:
+        d = np.nonzero(host[64:] != ref)[0]
+        check["differing_tiles"] = sorted({int(x) // (64 * 2048) for x in d[:100000]})[:16]
+        check["bytes_differing"] = int(d.size)
+    check["ok"] = check["equal_to_oracle"]
     return check
 
 
@@ -981,64 +1015,61 @@ def cpu_baseline_monolithic(bpk, n):
 # ---------------------------------------------------------------------------------------
 # verification of the timed output (untimed, oracle = the checker)
 # ---------------------------------------------------------------------------------------
-def sample_leaves(n_leaves, counts, rank, leaf_keys):
-    rng = np.random.default_rng(45 + rank)
-    pick = {0, n_leaves - 1}
-    partial = [i for i, c in enumerate(counts) if c != leaf_keys]
-    pick.update(partial[:1])
-    pick.update(int(x) for x in rng.integers(0, n_leaves, min(8, n_leaves)))
-    return sorted(pick)
-
-
-def verify_sample(torch, kind, bpk, cap, plan, keys, offsets, out, key_bytes, shard, rank,
-                  leaf_keys):
-    """Byte-compare a sample of this rank's leaves with the CPU oracle.  16-byte keys are
-    regenerated on the host by the oracle (so the device key generator and, for VQF, the
-    device sort are checked too); other key shapes are copied from the device."""
+def verify_all_leaves(torch, kind, bpk, cap, plan, keys, offsets, out, key_bytes, shard, threads):
+    """Byte-compare EVERY leaf of this rank's timed output with the CPU oracle (SURVEY.md 8(c):
+    whole-output parity at the bench's own size).  16-byte keys are regenerated on the host by
+    the oracle and, for VQF, sorted there (so the device key generator and the device sort are
+    checked too: `keys_equal_oracle`); other key shapes are copied from the device.  The
+    oracle builds all leaves on `threads` host threads (tkvo_build_segments_ex) into an array
+    laid out like the device's, and the two arrays are compared whole: every payload byte and
+    the never-written slack between payloads."""
     from oracle import oracle as O
     O.build_oracle()
-    counts = plan.segs["n_keys"].astype(np.int64)
-    leaves = sample_leaves(len(counts), counts, rank, leaf_keys)
+    t0 = time.perf_counter()
+    segs = plan.segs
+    counts = segs["n_keys"].astype(np.uint64)
+    sb = np.concatenate([[0], np.cumsum(counts)]).astype(np.uint64)
+    n = int(sb[-1])
+    res = {"against": ("CPU oracle (oracle/tkv_amq_oracle.c) on oracle-generated keys"
+                       if key_bytes == 16 else "CPU oracle on the device keys")}
+    offs = None
+    if key_bytes == 16:
+        kh = O.gen_keys16(42, shard.key_begin, n)
+        if kind == 1:
+            O.sort_segments(kh, sb, n_threads=threads)
+        res["keys_equal_oracle"] = bool(np.array_equal(kh, keys[:n].cpu().numpy()))
+        stride = 16
+    elif key_bytes == 0:
+        kh = keys.cpu().numpy()
+        offs = offsets.cpu().numpy().astype(np.uint64)
+        stride = 0
+    else:
+        kh = keys.cpu().numpy()
+        stride = key_bytes
+    got = out.cpu().numpy()
+    caps = (np.full(len(counts), cap, np.uint64) if kind == 1
+            else segs["payload_bytes"].astype(np.uint64))
+    ref = np.zeros(len(got) + int(cap or 0), np.uint8)
+    st = O.build_segments_ex(kind, kh if len(kh) else np.zeros(16, np.uint8), offs, stride, sb, bpk,
+                             segs["out_offset"], caps, ref, src_page_id=segs["src_page_id"],
+                             n_threads=threads)
+    del kh
     bad = []
-    keys_checked = 0
-    for s in leaves:
-        seg = plan.segs[s]
-        kb0, c = int(seg["key_begin"]), int(seg["n_keys"])
-        src = int(seg["src_page_id"])
-        o_off = None
-        if key_bytes == 16:
-            kh = O.gen_keys16(42, shard.key_begin + kb0, c)
-            if kind == 1:
-                O.sort_segments(kh, np.array([0, c], dtype=np.uint64), n_threads=1)
-            if not np.array_equal(kh, keys[kb0:kb0 + c].cpu().numpy()):
-                bad.append({"leaf": s, "what": "device keys differ from the oracle's"})
-                continue
-            stride = 16
-        elif key_bytes == 0:
-            o = offsets[kb0:kb0 + c + 1].cpu().numpy()
-            kh = keys[int(o[0]):int(o[-1])].cpu().numpy() if c else np.zeros(1, np.uint8)
-            o_off = (o - o[0]).astype(np.uint64)
-            stride = 0
-        else:
-            kh = keys[kb0:kb0 + c].cpu().numpy()
-            stride = key_bytes
-        if kind == 0:
-            st, ref = O.bloom_build(kh, c, bpk, src_page_id=src, offsets=o_off, stride=stride)
-            ref = ref.tobytes()
-        else:
-            st, ref, pl = O.vqf_build(kh, c, bpk, cap, src_page_id=src, offsets=o_off, stride=stride)
-            ref = ref[:pl.payload_used].tobytes()
-        if st != 0:
-            bad.append({"leaf": s, "what": f"oracle status {st}"})
-            continue
-        off, nbytes = int(seg["out_offset"]), int(seg["payload_bytes"])
-        got = out[off:off + nbytes].cpu().numpy().tobytes()
-        keys_checked += c
-        if got != ref:
-            bad.append({"leaf": s, "what": "filter bytes differ"})
-    return {"ok": not bad, "leaves": leaves, "keys": keys_checked,
-            "against": "CPU oracle (oracle/tkv_amq_oracle.c) on oracle-generated keys"
-                       if key_bytes == 16 else "CPU oracle on the device keys", "mismatches": bad}
+    if st != 0:
+        bad.append(f"oracle status {st}")
+    else:
+        ref = ref[:len(got)]
+        if not np.array_equal(got, ref):
+            diff = np.nonzero(got != ref)[0]
+            ends = (segs["out_offset"] + segs["payload_bytes"]).astype(np.int64)
+            leaves = np.unique(np.searchsorted(ends, diff[:1_000_000], side="right"))
+            bad = [int(x) for x in leaves[:16]]
+            res["bytes_differing"] = int(diff.size)
+    res.update({"ok": not bad and res.get("keys_equal_oracle", True),
+                "leaves_checked": int(len(counts)), "of_leaves": int(len(counts)), "keys": n,
+                "mismatched_leaves": bad, "threads": threads,
+                "seconds": round(time.perf_counter() - t0, 2)})
+    return res
 
 
 def verify_gather(torch, amq, kind, bpk, cap, all_counts, stride, gathered, key_bytes, dev):
@@ -1141,7 +1172,7 @@ def sort_segments_device(torch, keys, counts, chunk_keys=1 << 23):
     past leaf ~2007 on this ROCm build (argsort and repeat_interleave alone check out at
     100M, tools/gpu/diag_torch_sort.py; the failing op was not isolated).  Chunked, the
     result equals the oracle's sort at full size (tests/test_gpu_scale.py), and the bench
-    re-checks sampled leaves against oracle-generated keys after every run (verify_sample)."""
+    re-checks every leaf against oracle-generated keys after every run (verify_all_leaves)."""
     out = torch.empty_like(keys)
     b = 0
     i = 0

@@ -111,6 +111,8 @@ def _load(path):
     L.tkvo_tree_filter_bits_per_key.argtypes = [u64, i32]
     L.tkvo_build_segments.restype = i32
     L.tkvo_build_segments.argtypes = [i32, vp, vp, u32, u32, vp, vp, vp, vp, i32]
+    L.tkvo_build_segments_ex.restype = i32
+    L.tkvo_build_segments_ex.argtypes = [i32, vp, vp, u32, vp, u32, u32, vp, vp, vp, vp, i32]
     L.tkvb_vqf_build_payload16.restype = i32
     L.tkvb_vqf_build_payload16.argtypes = [vp, u64, u64, u64, vp, u64]
     L.tkvb_vqf_build_segments.restype = i32
@@ -218,6 +220,24 @@ def build_segments(kind: int, keys16: np.ndarray, seg_begin: np.ndarray, bpk: in
                                    _p(src_page_id), _p(out), _p(out_offset), _p(out_capacity),
                                    n_threads)
     return st, out
+
+
+def build_segments_ex(kind: int, keys: np.ndarray, offsets: np.ndarray | None, stride: int,
+                      seg_begin: np.ndarray, bpk: int, out_offset: np.ndarray,
+                      out_capacity: np.ndarray, out: np.ndarray,
+                      src_page_id: np.ndarray | None = None, n_threads: int = 8):
+    """The oracle over a batch of leaves of any key shape (fixed `stride`, or variable-length
+    keys through `offsets`, indexed by global key), into `out` at out_offset."""
+    seg_begin = np.ascontiguousarray(seg_begin, dtype=np.uint64)
+    out_offset = np.ascontiguousarray(out_offset, dtype=np.uint64)
+    out_capacity = np.ascontiguousarray(out_capacity, dtype=np.uint64)
+    if offsets is not None:
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+    if src_page_id is not None:
+        src_page_id = np.ascontiguousarray(src_page_id, dtype=np.uint64)
+    return lib().tkvo_build_segments_ex(kind, _p(keys), _p(offsets), stride, _p(seg_begin),
+                                        len(seg_begin) - 1, bpk, _p(src_page_id), _p(out),
+                                        _p(out_offset), _p(out_capacity), n_threads)
 
 
 def probe_segments(kind: int, filters: np.ndarray, out_offset: np.ndarray,

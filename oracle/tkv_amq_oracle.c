@@ -286,7 +286,9 @@ int tkvo_bloom_query_payload(const uint8_t* payload, const uint8_t* key, size_t 
  * 1B keys): every key is generated and its h0 computed; a key whose block falls in one of
  * the windows [blk0[i], blk1[i]) (ascending, disjoint) has its k bits set there, exactly as
  * tkvo_bloom_build_payload would.  out: the windows' 64-byte blocks concatenated, zeroed by
- * the caller.  Keys are spread over n_threads threads in chunks; bits are ORed atomically. */
+ * the caller.  Keys are spread over n_threads threads in chunks; bits are ORed atomically.
+ * One window [0, block_count) is the whole filter: the multithreaded whole-filter check of
+ * BASELINE config 5 (1B keys) against the GPU build. */
 typedef struct {
   uint64_t seed, first, n;
   uint32_t nb, k, n_win;
@@ -310,16 +312,19 @@ static void sample_chunk(par_ctx* c, uint32_t ci)
     wr64(key + 8, tkvo_splitmix64_at(a->seed, 2 * g + 2));
     const uint64_t h0 = tkvo_xxh64(key, 16, tkvo_bloom_seed(0));
     const uint64_t blk = (uint64_t)(((u128)h0 * a->nb) >> 64);
-    for (uint32_t w = 0; w < a->n_win; ++w) {
-      if (blk < a->blk0[w]) break;
-      if (blk >= a->blk1[w]) continue;
-      uint64_t* bw = a->words + a->wbase[w] + 8 * (blk - a->blk0[w]);
-      for (uint32_t j = 0; j < a->k; ++j) {
-        const uint64_t h = j == 0 ? h0 : tkvo_xxh64(key, 16, tkvo_bloom_seed(j));
-        const uint32_t bit = (uint32_t)(h & 511);
-        __atomic_fetch_or(bw + (bit >> 6), 1ull << (bit & 63), __ATOMIC_RELAXED);
-      }
-      break;
+    /* the last window starting at or before blk (binary search: windows are ascending) */
+    uint32_t lo = 0, hi = a->n_win;
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) / 2;
+      if (a->blk0[mid] <= blk) lo = mid;
+      else hi = mid;
+    }
+    if (a->n_win == 0 || blk < a->blk0[lo] || blk >= a->blk1[lo]) continue;
+    uint64_t* bw = a->words + a->wbase[lo] + 8 * (blk - a->blk0[lo]);
+    for (uint32_t j = 0; j < a->k; ++j) {
+      const uint64_t h = j == 0 ? h0 : tkvo_xxh64(key, 16, tkvo_bloom_seed(j));
+      const uint32_t bit = (uint32_t)(h & 511);
+      __atomic_fetch_or(bw + (bit >> 6), 1ull << (bit & 63), __ATOMIC_RELAXED);
     }
   }
 }
@@ -328,17 +333,23 @@ int tkvo_bloom_sample_blocks_gen16(uint64_t seed, uint64_t first, uint64_t n, ui
                                    const uint64_t* blk0, const uint64_t* blk1, uint32_t n_win,
                                    uint8_t* out, int n_threads)
 {
-  if (bpk == 0 || bpk > 64 || n_win > 64) return TKVO_INVALID_ARGUMENT;
-  uint64_t wbase[64];
+  if (bpk == 0 || bpk > 64 || n_win > TKVO_SAMPLE_MAX_WINDOWS) return TKVO_INVALID_ARGUMENT;
+  uint64_t* wbase = (uint64_t*)malloc(sizeof(uint64_t) * (n_win ? n_win : 1));
+  if (!wbase) return TKVO_RESOURCE_EXHAUSTED;
   uint64_t words = 0;
   for (uint32_t w = 0; w < n_win; ++w) {
-    if (blk1[w] < blk0[w] || (w && blk0[w] < blk1[w - 1])) return TKVO_INVALID_ARGUMENT;
+    if (blk1[w] < blk0[w] || (w && blk0[w] < blk1[w - 1])) {
+      free(wbase);
+      return TKVO_INVALID_ARGUMENT;
+    }
     wbase[w] = words;
     words += 8 * (blk1[w] - blk0[w]);
   }
   sample_arg a = {seed, first, n, tkvo_bloom_block_count(n, bpk), tkvo_bloom_hash_count(bpk),
                   n_win, blk0, blk1, wbase, (uint64_t*)out};
-  return par_run((uint32_t)((n + SAMPLE_CHUNK - 1) / SAMPLE_CHUNK), n_threads, sample_chunk, &a);
+  const int st = par_run((uint32_t)((n + SAMPLE_CHUNK - 1) / SAMPLE_CHUNK), n_threads, sample_chunk, &a);
+  free(wbase);
+  return st;
 }
 
 /* ------------------------------------------------------------------------------------
@@ -597,6 +608,8 @@ int tkvo_vqf_is_present_payload(const uint8_t* payload, uint64_t hash)
 typedef struct {
   int kind;
   const uint8_t* keys;
+  const uint64_t* offsets; /* variable-length keys (key i = keys[offsets[i], offsets[i+1])) */
+  uint32_t stride;         /* fixed-size keys (offsets == NULL) */
   const uint64_t* seg_begin;
   uint32_t bpk;
   const uint64_t* src;
@@ -610,13 +623,14 @@ static void build_one(par_ctx* c, uint32_t s)
   build_arg* a = (build_arg*)c->arg;
   const uint64_t b = a->seg_begin[s], e = a->seg_begin[s + 1];
   const uint64_t src = a->src ? a->src[s] : s;
+  /* leaf s's keys: a pointer at its first key (fixed size), or its offsets (variable) */
+  const uint8_t* k = a->offsets ? a->keys : a->keys + (uint64_t)a->stride * b;
+  const uint64_t* o = a->offsets ? a->offsets + b : NULL;
   int st;
   if (a->kind == 0)
-    st = tkvo_bloom_build_payload(a->keys + 16 * b, NULL, 16, e - b, a->bpk, src,
-                                  a->out + a->off[s], a->cap[s]);
+    st = tkvo_bloom_build_payload(k, o, a->stride, e - b, a->bpk, src, a->out + a->off[s], a->cap[s]);
   else
-    st = tkvo_vqf_build_payload(a->keys + 16 * b, NULL, 16, e - b, a->bpk, src,
-                                a->out + a->off[s], a->cap[s], NULL);
+    st = tkvo_vqf_build_payload(k, o, a->stride, e - b, a->bpk, src, a->out + a->off[s], a->cap[s], NULL);
   if (st != TKVO_OK) __atomic_store_n(&c->status, st, __ATOMIC_RELAXED);
 }
 
@@ -625,7 +639,16 @@ int tkvo_build_segments(int kind, const uint8_t* keys16, const uint64_t* seg_beg
                         uint8_t* out, const uint64_t* out_offset, const uint64_t* out_capacity,
                         int n_threads)
 {
-  build_arg a = {kind, keys16, seg_begin, bpk, src_page_id, out, out_offset, out_capacity};
+  return tkvo_build_segments_ex(kind, keys16, NULL, 16, seg_begin, n_segs, bpk, src_page_id, out,
+                                out_offset, out_capacity, n_threads);
+}
+
+int tkvo_build_segments_ex(int kind, const uint8_t* keys, const uint64_t* offsets, uint32_t stride,
+                           const uint64_t* seg_begin, uint32_t n_segs, uint32_t bpk,
+                           const uint64_t* src_page_id, uint8_t* out, const uint64_t* out_offset,
+                           const uint64_t* out_capacity, int n_threads)
+{
+  build_arg a = {kind, keys, offsets, stride, seg_begin, bpk, src_page_id, out, out_offset, out_capacity};
   return par_run(n_segs, n_threads, build_one, &a);
 }
 

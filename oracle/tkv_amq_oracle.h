@@ -60,7 +60,9 @@ int tkvo_bloom_build_payload(const uint8_t* keys, const uint64_t* offsets, uint3
                              uint8_t* out_payload, uint64_t out_capacity);
 int tkvo_bloom_query_payload(const uint8_t* payload, const uint8_t* key, size_t len);
 /* the blocks of sampled windows [blk0[i], blk1[i]) of the filter over tkvo_gen_keys16(seed,
- * first, n), keys generated and hashed on the fly (no key array, no whole filter) */
+ * first, n), keys generated and hashed on the fly (no key array); ascending, disjoint, at most
+ * TKVO_SAMPLE_MAX_WINDOWS; one window [0, block_count) is the whole filter */
+#define TKVO_SAMPLE_MAX_WINDOWS 65536
 int tkvo_bloom_sample_blocks_gen16(uint64_t seed, uint64_t first, uint64_t n, uint32_t bpk,
                                    const uint64_t* blk0, const uint64_t* blk1, uint32_t n_win,
                                    uint8_t* out, int n_threads);
@@ -99,6 +101,12 @@ int tkvo_build_segments(int kind, const uint8_t* keys16, const uint64_t* seg_beg
                         uint32_t n_segs, uint32_t bits_per_key, const uint64_t* src_page_id,
                         uint8_t* out, const uint64_t* out_offset, const uint64_t* out_capacity,
                         int n_threads);
+/* the same over keys of any fixed size (offsets NULL, `stride` bytes each) or variable-length
+ * keys (key i = keys[offsets[i], offsets[i+1]), offsets indexed by global key) */
+int tkvo_build_segments_ex(int kind, const uint8_t* keys, const uint64_t* offsets, uint32_t stride,
+                           const uint64_t* seg_begin, uint32_t n_segs, uint32_t bpk,
+                           const uint64_t* src_page_id, uint8_t* out, const uint64_t* out_offset,
+                           const uint64_t* out_capacity, int n_threads);
 
 /* batched probe: query i probes segment query_seg[i]; result[i] = 1 maybe-present, 0 absent */
 int tkvo_probe_segments(int kind, const uint8_t* filters, const uint64_t* out_offset,

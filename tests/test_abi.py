@@ -108,8 +108,9 @@ def test_batch_plan_layout(amq):
 def test_hash_shard_constants_match_library(amq):
     """turtle_kv_amd.dist's tile geometry is the library's (tkv_amq_bloom_tile_blocks and the
     range builds' tile caps), and the monolithic workspace the plan asks for covers the
-    routed-part form beyond one partition's tile table (16 bytes per key of routed items plus
-    the part's regions and overflow lists)."""
+    routed form beyond one partition's tile table (the one-pass route's 12-byte records in
+    their fixed-capacity regions, its overflow lists -- 16 bytes a key at worst -- and a part
+    build's regions and overflow lists)."""
     from turtle_kv_amd import dist as tdist
     L = amq.abi.lib()
     assert L.tkv_amq_bloom_tile_blocks() == tdist.BLOOM_TILE_BLOCKS == 2048
@@ -118,7 +119,7 @@ def test_hash_shard_constants_match_library(amq):
     direct = amq.plan_filters(amq.BLOOM, [100_000_000], 10)
     routed = amq.plan_filters(amq.BLOOM, [1_750_000_000], 12)
     assert direct.workspace_bytes >= 16 * 100_000_000
-    assert routed.workspace_bytes >= 16 * 1_750_000_000 * 2
+    assert routed.workspace_bytes >= (12 + 16) * 1_750_000_000
     # a range build past 6,400 tiles (the partition's LDS tile table) is refused
     assert L.tkv_amq_bloom_build_range_records_ws_bytes(1000, 0, 6400) > 0
     assert L.tkv_amq_bloom_build_range_records_ws_bytes(1000, 0, 6401) == 0

@@ -97,7 +97,7 @@ def test_hash_shard_tiles_cover_the_filter():
     accepted, and their range build writes the header only (GPU test
     test_gpu_hash_shard.py::test_empty_ranges_write_the_header)."""
     from turtle_kv_amd import abi
-    from turtle_kv_amd.dist import BLOOM_TILE_BLOCKS as TB, HashShardedBloom, hash_shard_tiles
+    from turtle_kv_amd.dist import BLOOM_TILE_BLOCKS as TB, ExactHashShardedBloom, hash_shard_tiles
     for nb, world in [(1, 1), (TB, 1), (TB + 1, 2), (93750, 8), (2_343_750, 8), (29297, 8),
                       (17 * TB, 8), (3000, 8)]:
         T, q = hash_shard_tiles(nb, world)
@@ -109,11 +109,11 @@ def test_hash_shard_tiles_cover_the_filter():
     assert (T, q) == (17, 3)
     empty = [r for r in range(8) if min(T, r * q) == min(T, (r + 1) * q)]
     assert empty == [6, 7]
-    hs = HashShardedBloom(100_000, 12, 8, 5, "cpu")   # 2 tiles over 8 ranks: rank 5 owns none
+    hs = ExactHashShardedBloom(100_000, 12, 8, 5, "cpu")   # 2 tiles over 8 ranks: rank 5 owns none
     assert hs.T == 2 and hs.tile_begin == hs.tile_end == 2
     with pytest.raises(abi.TkvAmqError, match="got shape"):
         hs.route(torch.zeros((10, 20), dtype=torch.uint8))   # 16- or 24-byte keys only
-    hk = HashShardedBloom(100_000, 16, 8, 0, "cpu")         # k = 11: keys travel, 16 bytes only
+    hk = ExactHashShardedBloom(100_000, 16, 8, 0, "cpu")    # k = 11: keys travel, 16 bytes only
     assert not hk.records
     with pytest.raises(abi.TkvAmqError, match="got shape"):
         hk.route(torch.zeros((10, 24), dtype=torch.uint8))
@@ -127,7 +127,7 @@ def test_hash_shard_parts_per_rank():
     range build's LDS tile table: BASELINE config 5 (1B keys at 12 bits/key, 11,445 tiles)
     builds 45 parts of 255 tiles on one rank, 23 of 249 on each of two, 6 of 239 on each of eight; the
     parts of all ranks tile the filter, and rank r's range is its parts' union."""
-    from turtle_kv_amd.dist import (ROUTED_KEY_PART_TILES, ROUTED_PART_TILES, HashShardedBloom,
+    from turtle_kv_amd.dist import (ROUTED_KEY_PART_TILES, ROUTED_PART_TILES, ExactHashShardedBloom,
                                     hash_shard_plan)
     nb_1b = -(-1_000_000_000 * 12 // 512)
     assert hash_shard_plan(nb_1b, 1) == (11445, 45, 255)
@@ -143,16 +143,49 @@ def test_hash_shard_parts_per_rank():
                 parts = [(min(T, p * q), min(T, (p + 1) * q)) for p in range(world * g)]
                 assert parts[0][0] == 0 and parts[-1][1] == T
                 assert all(a[1] == b[0] for a, b in zip(parts, parts[1:]))
-    hs = HashShardedBloom(1_000_000_000, 12, 2, 1, "meta")
+    hs = ExactHashShardedBloom(1_000_000_000, 12, 2, 1, "meta")
     assert (hs.g, hs.q, hs.tile_begin, hs.tile_end) == (23, 249, 5727, 11445)
     assert hs.part_tiles(0) == (5727, 5976) and hs.part_tiles(22) == (11205, 11445)
+
+
+@pytest.mark.parametrize("world,chunks", [(1, 1), (2, 1), (8, 4), (3, 2)])
+def test_pipelined_hash_shard_plan(world, chunks):
+    """The pipelined form (tkv_amq_bloom_route_plan, a host function): the same parts as the
+    exact form at config 5's size, owned round-robin (part p by rank p % world, so round j --
+    part j of every rank -- is one contiguous byte range of the bitmap, gathered in place);
+    every part is owned once; fixed-size blocks whose regions hold mean + 6 sigma + 16 records of
+    a uniform hash; a rank's recv buffer holds chunks x world blocks."""
+    from turtle_kv_amd.dist import HashShardedBloom, hash_shard_plan
+    nb_1b = -(-1_000_000_000 * 12 // 512)
+    owners = {}
+    for r in range(world):
+        hs = HashShardedBloom(1_000_000_000, 12, world, r, "meta", chunks=chunks)
+        assert (hs.T, hs.g, hs.q) == hash_shard_plan(nb_1b, world)
+        rp = hs.rp
+        assert rp.n_parts == world * hs.g and rp.world == world and rp.n_chunks == chunks
+        for p in hs.owned_parts():
+            assert p % world == r and p not in owners
+            owners[p] = r
+        assert hs.recv.numel() == chunks * world * rp.block_bytes
+        assert hs.out.numel() == 64 + rp.n_parts * rp.part_bytes >= hs.payload_bytes
+        e = -(-hs.chunk_keys // rp.route_wgs) * min(hs.q * 2048, nb_1b) / nb_1b   # its blocks' share
+        assert e + 6 * e ** 0.5 <= rp.region_cap <= e + 6 * e ** 0.5 + 32
+        assert rp.regions_off + 12 * hs.g * rp.route_wgs * rp.region_cap <= rp.ovf_off
+        assert rp.ovf_off + 16 * rp.ovf_cap <= rp.block_bytes and rp.block_bytes % 256 == 0
+    assert sorted(owners) == list(range(world * hs.g))
+    tiles = sorted(hs.part_tiles(p) for p in owners)
+    assert tiles[0][0] == 0 and tiles[-1][1] == hs.T
+    assert all(a[1] == b[0] for a, b in zip(tiles, tiles[1:]))
+    # k > 8: 16-byte keys travel through the exact form
+    hk = HashShardedBloom(100_000, 16, world, 0, "cpu")
+    assert not hk.records and hk._exact is not None
 
 
 def test_build_owned_regroups_parts():
     """With g > 1 parts per rank the all-to-all delivers, per sender, that sender's units for
     each of this rank's parts in order; build_owned hands part j all senders' pieces of it."""
-    from turtle_kv_amd.dist import HashShardedBloom
-    hs = HashShardedBloom.__new__(HashShardedBloom)
+    from turtle_kv_amd.dist import ExactHashShardedBloom
+    hs = ExactHashShardedBloom.__new__(ExactHashShardedBloom)
     got = []
     hs._build_part = lambda units, j: got.append((j, units.tolist()))
     W, g = 3, 2

@@ -104,9 +104,11 @@ def test_bench_hash_sharded_two_ranks_gloo():
     d = last_json(r)
     assert d["n_gpus"] == 2 and d["config"]["total_keys"] == 4_000_000
     assert d["verified"] is True
-    assert d["verify"]["equal_to_one_gpu_build"] and d["verify"]["equal_to_oracle"]
-    assert d["allgather_ms"] > 0
-    assert 0 < d["step_breakdown_rank0_ms"]["keys_owned"] < 4_000_000
+    assert d["verify"]["equal_to_oracle"] and d["verify"]["header_ok"]
+    assert d["config"]["chunks"] == 4 and d["config"]["allgather_in_step"] is True
+    assert d["route_plan"]["overflow_lost"] is False
+    b = d["step_breakdown_rank0_ms"]
+    assert b["route"] > 0 and b["all_to_all"] > 0 and b["part_builds"] > 0 and b["allgather"] > 0
 
 
 def test_bench_hash_sharded_one_rank():
@@ -279,4 +281,94 @@ def test_hash_sharded_world1_24_byte_keys(oracle, amq, torch, n_keys, bpk):
     filt = hs.build(torch.from_numpy(kn).cuda())
     torch.cuda.synchronize()
     st, ref = oracle.bloom_build(kn, n_keys, bpk, src_page_id=0, stride=24)
+    assert st == 0 and filt.cpu().numpy().tobytes() == ref.tobytes()
+
+
+def _pipelined_by_hand(amq, torch, keys_per_rank, bpk, chunks):
+    """The pipelined hash-range build of `len(keys_per_rank)` ranks played on one GPU: each rank
+    routes its chunks into its send blocks (tkv_amq_bloom_route_blocks), the all-to-all is done
+    by block copies (recv block (c, s) of rank d = send block d of rank s's chunk c), each rank
+    builds its round-robin parts (tkv_amq_bloom_build_part_blocks), and the filter is assembled
+    from the parts' owners as the in-place all-gather of every round would."""
+    from turtle_kv_amd.dist import HashShardedBloom
+    W = len(keys_per_rank)
+    n_total = sum(int(k.shape[0]) for k in keys_per_rank)
+    mx = max(int(k.shape[0]) for k in keys_per_rank)
+    hss = [HashShardedBloom(n_total, bpk, W, r, "cuda", chunks=chunks, max_keys_per_rank=mx) for r in range(W)]
+    for r, hs in enumerate(hss):
+        for c in range(chunks):
+            hs.route_chunk(keys_per_rank[r], c)
+    B = hss[0].block_bytes
+    if W > 1:
+        for d in range(W):
+            for c in range(chunks):
+                for s_ in range(W):
+                    i = c * W + s_
+                    hss[d].recv[i * B:(i + 1) * B].copy_(hss[s_].send[c][d * B:(d + 1) * B])
+    for hs in hss:
+        for j in range(hs.g):
+            hs.build_part(j)
+    torch.cuda.synchronize()
+    full = hss[0].out.clone()
+    pb = hss[0].part_bytes
+    for p in range(hss[0].n_parts):
+        o = 64 + p * pb
+        full[o:o + pb] = hss[p % W].out[o:o + pb]
+        assert torch.equal(hss[p % W].out[:64], full[:64]), "every rank writes the header"
+    return full[:hss[0].payload_bytes], hss
+
+
+@pytest.mark.parametrize("n_keys,bpk,world,chunks,dup", [
+    (3_000_000, 12, 1, 1, 0), (3_000_000, 12, 3, 2, 0), (1_500_001, 10, 8, 1, 0),
+    (2_000_000, 12, 4, 3, 5_000), (1_440_000, 12, 8, 2, 0), (900_000, 5, 2, 1, 0),
+    (40_000_000, 12, 2, 4, 0)])
+def test_pipelined_blocks_equal_oracle(oracle, amq, torch, n_keys, bpk, world, chunks, dup):
+    """The pipelined form against the oracle: k = 8, 7 and 3, ranks past the last tile (1.44M
+    keys: 17 tiles over 8 ranks), ragged chunks and ranks, duplicate keys (their regions
+    overflow: (record, part) entries through the blocks' overflow areas, within ovf_cap), and a
+    size with several parts per rank."""
+    keys = amq.gen_keys16(31, 0, n_keys)
+    if dup:
+        keys[n_keys - dup:] = keys[n_keys // 3]
+    per = -(-n_keys // world)
+    parts = [keys[r * per:min(n_keys, (r + 1) * per)] for r in range(world)]
+    filt, hss = _pipelined_by_hand(amq, torch, parts, bpk, chunks)
+    st, ref = oracle.bloom_build(keys.cpu().numpy(), n_keys, bpk, src_page_id=0)
+    assert st == 0
+    got = filt.cpu().numpy()
+    if got.tobytes() != ref.tobytes():
+        bad = np.nonzero(got != ref)[0]
+        pytest.fail(f"{bad.size} bytes differ, first tiles {sorted({(int(b) - 64) // (64 * 2048) for b in bad[:1000]})[:8]}")
+    # (5,000 copies of one key: ~3,300 records past their region, within a block's ovf_cap)
+    assert not any(h.lost() for h in hss)
+    if dup:
+        h = hss[0]
+        ovf = torch.stack([hs.recv.view(-1)[i * h.block_bytes + h.rp.ovf_n_off:
+                                            i * h.block_bytes + h.rp.ovf_n_off + 4].view(torch.int32)
+                           for hs in hss for i in range(h.chunks * h.world)]).sum()
+        assert int(ovf) > 0, "the duplicates must have taken the overflow path"
+
+
+def test_pipelined_blocks_24_byte_keys(oracle, amq, torch):
+    rng = np.random.default_rng(5)
+    n = 1_200_000
+    kn = rng.integers(0, 256, (n, 24), dtype=np.uint8)
+    keys = torch.from_numpy(kn).cuda()
+    filt, _ = _pipelined_by_hand(amq, torch, [keys[:700_000], keys[700_000:]], 12, 2)
+    st, ref = oracle.bloom_build(kn, n, 12, src_page_id=0, stride=24)
+    assert st == 0 and filt.cpu().numpy().tobytes() == ref.tobytes()
+
+
+def test_pipelined_blocks_report_lost_overflow(oracle, amq, torch):
+    """One key repeated far past a block's overflow area: the blocks report the loss, and
+    HashShardedBloom.build (one GPU, no process group) rebuilds through the exact exchange."""
+    from turtle_kv_amd.dist import HashShardedBloom
+    n = 30_000_000   # 344 tiles: two parts
+    keys = amq.gen_keys16(32, 0, n)
+    keys[n // 2:] = keys[7]
+    hs = HashShardedBloom(n, 12, 1, 0, "cuda")
+    hs.step(keys)
+    assert hs.lost()
+    filt = HashShardedBloom(n, 12, 1, 0, "cuda").build(keys)
+    st, ref = oracle.bloom_build(keys.cpu().numpy(), n, 12, src_page_id=0)
     assert st == 0 and filt.cpu().numpy().tobytes() == ref.tobytes()

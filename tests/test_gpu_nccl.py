@@ -3,9 +3,10 @@ box before any 8-GPU run: a child process creates a world-size-1 "nccl" group bo
 device 0 and runs
 
   - allgather_filters on device tensors (dist.all_gather_into_tensor, dist.py nccl branch),
-  - HashShardedBloom.route -> exchange (device all_to_all_single of the counts and the keys)
-    -> build_range -> allgather, via local_build/allgather (which take the collective path
-    whenever a process group exists),
+  - ExactHashShardedBloom.route -> exchange (device all_to_all_single of the counts and the
+    records) -> range builds -> allgather, and the pipelined HashShardedBloom step (route blocks
+    -> part builds -> in-place all_gather_into_tensor of every round), which take the
+    collective path whenever a process group exists,
   - the float64 MAX / int32 MIN all-reduces on device tensors that bench.py uses,
 
 and compares each result with the single-process build (and the oracle).  RCCL cannot put
@@ -56,12 +57,16 @@ def child():
     # 2. hash-range sharding through route -> all_to_all_single -> range build -> all-gather
     n = 1_500_000
     keys = amq.gen_keys16(7, 0, n)
-    hs = tdist.HashShardedBloom(n, 12, 1, 0, dev)
-    routed, sc = hs.route(keys)
-    owned, sub = hs.exchange(routed, sc)
+    ex = tdist.ExactHashShardedBloom(n, 12, 1, 0, dev)
+    routed, sc = ex.route(keys)
+    owned, sub = ex.exchange(routed, sc)
     # one rank: the all-to-all of the 12-byte bit records (k = 8 at 12 bits/key) is a copy
-    res["exchange_identity"] = bool(hs.records and owned.shape == (n, 12) and torch.equal(owned, routed)
-                                    and tuple(sub.shape) == (1, hs.g) and int(sub.sum()) == n)
+    res["exchange_identity"] = bool(ex.records and owned.shape == (n, 12) and torch.equal(owned, routed)
+                                    and tuple(sub.shape) == (1, ex.g) and int(sub.sum()) == n)
+    res["exact_equal_one_gpu"] = bool(torch.equal(ex.build(keys), amq.build_all_filters(
+        amq.plan_filters(0, [n], 12), amq.KeyBatch.fixed(keys))[:ex.payload_bytes]))
+    # the pipelined step: route blocks -> part builds -> in-place all_gather_into_tensor per round
+    hs = tdist.HashShardedBloom(n, 12, 1, 0, dev, chunks=2)
     filt = hs.build(keys)
     torch.cuda.synchronize()
     whole = amq.build_all_filters(amq.plan_filters(0, [n], 12), amq.KeyBatch.fixed(keys))

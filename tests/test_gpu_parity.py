@@ -594,22 +594,25 @@ def test_bloom_monolithic_duplicate_keys(oracle, amq, torch):
     assert_same(plan, out, ref)
 
 
-def sampled_tiles_equal_oracle(oracle, out, n, bpk, seed, n_random=6):
-    """The header and eight tiles of a GPU-built monolithic filter over gen_keys16(seed, 0, n)
-    (the first, the last, six seeded-random ones) against the oracle, which generates and
-    hashes every key for them (oracle.bloom_sample_blocks): the check for filters too large
-    for a whole oracle build in a test's time."""
+def sampled_tiles_equal_oracle(oracle, out, n, bpk, seed, n_random=6, extra_tiles=(), whole=False):
+    """The header and sampled tiles of a GPU-built monolithic filter over gen_keys16(seed, 0, n)
+    (the first, the last, six seeded-random ones and `extra_tiles`, e.g. both sides of every
+    routed part boundary) against the oracle, which generates and hashes every key for them
+    (oracle.bloom_sample_blocks); whole=True compares the whole bitmap (one window)."""
     from turtle_kv_amd.dist import BLOOM_TILE_BLOCKS as TB
     nb = int(oracle.lib().tkvo_bloom_block_count(n, bpk))
     T = -(-nb // TB)
     rng = np.random.default_rng(seed)
-    tiles = sorted({0, T - 1, *[int(t) for t in rng.choice(T, size=min(n_random, T), replace=False)]})
-    wins = [(t * TB, min(nb, (t + 1) * TB)) for t in tiles]
+    tiles = sorted({0, T - 1, *[int(t) for t in rng.choice(T, size=min(n_random, T), replace=False)],
+                    *[int(t) for t in extra_tiles if 0 <= t < T]})
+    wins = [(0, nb)] if whole else [(t * TB, min(nb, (t + 1) * TB)) for t in tiles]
     st, got = oracle.bloom_sample_blocks(seed, 0, n, bpk, wins, n_threads=min(16, os.cpu_count()))
     assert st == 0
     for (lo, hi), ref in got.items():
         mine = out[64 + 64 * lo:64 + 64 * hi].cpu().numpy()
-        assert mine.tobytes() == ref.tobytes(), f"blocks [{lo}, {hi}) of tile {lo // TB} / {T}"
+        if mine.tobytes() != ref.tobytes():
+            bad = sorted({(lo + int(i) // 64) // TB for i in np.nonzero(mine != ref)[0][:100000]})
+            pytest.fail(f"blocks [{lo}, {hi}) differ in tiles {bad[:16]} of {T}")
     k = int(oracle.lib().tkvo_bloom_hash_count(bpk))
     hdr = np.frombuffer(out[:64].cpu().numpy().tobytes(), dtype="<u8")
     assert [int(x) for x in hdr[:7]] == [0xCA6F49A0F3F8A4B0, 512 * nb, 0, 0, 8 * nb,
@@ -617,15 +620,17 @@ def sampled_tiles_equal_oracle(oracle, out, n, bpk, seed, n_random=6):
     return T
 
 
-@pytest.mark.parametrize("n,bpk,parts", [(108_000_000, 10, 1), (1_750_000_000, 12, 79),
-                                         (700_000_000, 64, 27)])
-def test_bloom_monolithic_large_sampled_oracle(oracle, amq, torch, n, bpk, parts):
-    """Full-size monolithic filters against the oracle on eight sampled tiles and the header:
-    108M keys at 10 bits/key (1,030 tiles: the partition reads the keys), 1.75B keys at 12
-    bits/key (20,028 tiles, beyond one partition's 6,400-tile table: routed as 12-byte records
-    into 79 parts of <= 256 tiles, each built from its records, its count read on the device)
-    and 700M keys at 64 bits/key (42,725 tiles, k = 44: the 16-byte keys themselves routed into
-    27 parts)."""
+@pytest.mark.parametrize("n,bpk,parts,whole", [(108_000_000, 10, 1, True), (1_750_000_000, 12, 79, False),
+                                               (700_000_000, 64, 27, False),
+                                               (600_000_000, 12, 27, True)])
+def test_bloom_monolithic_large_sampled_oracle(oracle, amq, torch, n, bpk, parts, whole):
+    """Full-size monolithic filters against the oracle: 108M keys at 10 bits/key (1,030 tiles:
+    the partition reads the keys) and 600M keys at 12 bits/key (6,867 tiles: routed as 12-byte
+    records into 27 parts) over the WHOLE bitmap; 1.75B keys at 12 bits/key (20,028 tiles,
+    beyond one partition's 6,400-tile table: routed into 79 parts of <= 256 tiles, each built
+    from its records, its count read on the device) and 700M keys at 64 bits/key (42,725 tiles,
+    k = 44: the 16-byte keys themselves routed into 27 parts) on the header, eight sampled
+    tiles and the tiles on both sides of every part boundary."""
     from turtle_kv_amd import abi
     L = abi.lib()
     seed = 16
@@ -636,11 +641,15 @@ def test_bloom_monolithic_large_sampled_oracle(oracle, amq, torch, n, bpk, parts
     if not direct:
         from turtle_kv_amd.dist import ROUTED_KEY_PART_TILES, ROUTED_PART_TILES
         assert -(-T // (ROUTED_PART_TILES if bpk <= 12 else ROUTED_KEY_PART_TILES)) == parts
+    edges = []
+    if not direct:
+        q = -(-T // parts)
+        edges = [t for j in range(1, parts) for t in (j * q - 1, j * q)]
     keys = amq.gen_keys16(seed, 0, n)
     out = amq.build_all_filters(plan, amq.KeyBatch.fixed(keys))
     del keys
     torch.cuda.synchronize()
-    assert sampled_tiles_equal_oracle(oracle, out, n, bpk, seed) == T
+    assert sampled_tiles_equal_oracle(oracle, out, n, bpk, seed, extra_tiles=edges, whole=whole) == T
     del out
     torch.cuda.empty_cache()
 

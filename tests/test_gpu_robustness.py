@@ -242,3 +242,46 @@ def test_probe_leaf_index_out_of_range(oracle, amq, torch, kind):
     # in range, the same misses are mostly rejected
     good = torch.zeros(1000, dtype=torch.int32, device="cuda")
     assert int(amq.probe_filters(plan, filt, miss, good).sum()) < 100
+
+
+@pytest.mark.parametrize("n_keys", [4_000_000, 1_300_000])
+def test_vqf_round_plans_on_one_poisoned_workspace(oracle, amq, torch, n_keys):
+    """PipelinedLeafGather builds differently sized round plans (41 / 40 leaves ... at fixed
+    stride) one after another on ONE workspace.  Built that way on a workspace first filled
+    with 0xFF, every round's leaves must equal a fresh whole-batch build of the same leaves on
+    a zeroed workspace (no kernel may read state an earlier build of another plan left), and
+    sampled leaves the oracle (an intermittent gathered-array mismatch)."""
+    from turtle_kv_amd import dist as tdist
+    cap = 32704
+    counts = [16384] * (n_keys // 16384) + ([n_keys % 16384] if n_keys % 16384 else [])
+    sb = np.concatenate([[0], np.cumsum(counts)]).astype(np.uint64)
+    keys = oracle.gen_keys16(42, 0, int(sb[-1]))
+    oracle.sort_segments(keys, sb, n_threads=8)
+    d = torch.from_numpy(keys).cuda()
+    stride = tdist.leaf_stride(1, 12, max(counts), cap)
+    W, per_rank = 2, -(-len(counts) // 2)
+    q = -(-per_rank // 3)
+    rounds = []
+    for r in range(W):
+        for b, e in tdist.cyclic_rounds(len(counts), W, r, q):
+            if b < e:
+                rounds.append((b, e, amq.plan_filters(1, np.asarray(counts[b:e], np.uint64), 12,
+                                                      payload_capacity=cap, out_stride=stride,
+                                                      src_page_ids=np.arange(b, e, dtype=np.uint64))))
+    ws = torch.full((max(p.workspace_bytes for *_, p in rounds),), 0xFF, dtype=torch.uint8, device="cuda")
+    got = torch.zeros(len(counts) * stride, dtype=torch.uint8, device="cuda")
+    for b, e, p in rounds:
+        amq.build_all_filters(p, amq.KeyBatch.fixed(d[int(sb[b]):int(sb[e])]),
+                              out=got[b * stride:e * stride], workspace=ws)
+    full_plan = amq.plan_filters(1, counts, 12, payload_capacity=cap, out_stride=stride)
+    fresh = torch.zeros(full_plan.total_out_bytes, dtype=torch.uint8, device="cuda")
+    amq.build_all_filters(full_plan, amq.KeyBatch.fixed(d), out=fresh,
+                          workspace=torch.zeros(full_plan.workspace_bytes, dtype=torch.uint8, device="cuda"))
+    if not torch.equal(got, fresh):
+        diff = torch.nonzero(got != fresh).flatten()
+        pytest.fail(f"{diff.numel()} bytes differ, leaves {sorted({int(x) // stride for x in diff[:4096].tolist()})[:16]}")
+    o = fresh.cpu().numpy()
+    for s in (0, q - 1, q, len(counts) - 1):
+        st, ref, pl = oracle.vqf_build(keys[int(sb[s]):], counts[s], 12, cap, src_page_id=s)
+        assert st == 0
+        assert o[s * stride:s * stride + pl.payload_used].tobytes() == ref[:pl.payload_used].tobytes()

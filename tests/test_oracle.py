@@ -195,3 +195,22 @@ def test_vqf_bmi2_baseline_overflow(oracle):
     st, ref, pl = oracle.vqf_build(keys[:48].copy(), 48, 12, 32704)
     sb, got = oracle.vqf_build_baseline(keys[:48].copy(), 48, 12, 32704)
     assert st == sb == 0 and got[:pl.payload_used].tobytes() == ref[:pl.payload_used].tobytes()
+
+
+def test_whole_filter_window_equals_build(oracle):
+    """bloom_sample_blocks with the one window [0, block_count) is the whole filter (the
+    multithreaded whole-filter check of BASELINE config 5), and many small windows -- every
+    part-boundary tile of a routed filter -- are found by their binary search."""
+    import numpy as np
+    n, bpk = 300_000, 12
+    keys = oracle.gen_keys16(16, 0, n)
+    st, ref = oracle.bloom_build(keys, n, bpk)
+    assert st == 0
+    nb = int(oracle.lib().tkvo_bloom_block_count(n, bpk))
+    st, got = oracle.bloom_sample_blocks(16, 0, n, bpk, [(0, nb)], n_threads=4)
+    assert st == 0 and got[(0, nb)].tobytes() == ref[64:].tobytes()
+    wins = [(b, min(nb, b + 3)) for b in range(0, nb, 37)]
+    st, got = oracle.bloom_sample_blocks(16, 0, n, bpk, wins, n_threads=4)
+    assert st == 0
+    for (a, b), v in got.items():
+        assert v.tobytes() == ref[64 + 64 * a:64 + 64 * b].tobytes()

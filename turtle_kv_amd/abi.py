@@ -89,7 +89,22 @@ EXPORTS = [
     "tkv_amq_bloom_build_range", "tkv_amq_bloom_route_records_ws_bytes", "tkv_amq_bloom_route_records",
     "tkv_amq_bloom_build_range_records_ws_bytes", "tkv_amq_bloom_build_range_records",
     "tkv_amq_bloom_route_records_ex", "tkv_amq_bloom_tile_blocks", "tkv_amq_bloom_range_max_tiles",
+    "tkv_amq_bloom_route_plan", "tkv_amq_bloom_route_blocks", "tkv_amq_bloom_build_part_blocks",
+    "tkv_amq_bloom_blocks_lost",
 ]
+
+
+class RoutePlan(ctypes.Structure):
+    """tkv_amq_route_plan: the pipelined hash-range build's parts, route workgroups and block
+    layout (include/tkv_amq.h)."""
+    _fields_ = [(n, ctypes.c_uint32) for n in (
+        "n_tiles", "n_parts", "parts_per_rank", "part_tiles", "world", "n_chunks", "route_wgs",
+        "region_cap", "ovf_cap", "hash_count")] + [(n, ctypes.c_uint64) for n in (
+        "chunk_keys", "block_bytes", "counts_off", "ovf_n_off", "regions_off", "ovf_off",
+        "route_ws_bytes", "part_ws_bytes", "part_bytes", "n_blocks")]
+
+
+assert ctypes.sizeof(RoutePlan) == 120
 
 # tkv_amq_key_view (libstdc++ std::string_view layout)
 KEY_VIEW_DTYPE = np.dtype([("size", "<u8"), ("data", "<u8")])
@@ -97,12 +112,25 @@ KEY_VIEW_DTYPE = np.dtype([("size", "<u8"), ("data", "<u8")])
 _lib = None
 
 
+def experiment_lib():
+    """TKV_AMQ_LIB names an experiment build of the library (kernel A/B timing).  It is taken
+    only together with TKV_AMQ_EXPERIMENT=1, so a stray variable cannot put an experiment
+    library behind the tests, smoke() or the bench."""
+    path = os.environ.get("TKV_AMQ_LIB")
+    if not path:
+        return None
+    if os.environ.get("TKV_AMQ_EXPERIMENT") != "1":
+        raise RuntimeError("TKV_AMQ_LIB is set but TKV_AMQ_EXPERIMENT is not 1: experiment "
+                           "libraries are loaded only on purpose")
+    return path
+
+
 def lib(build_if_missing: bool = True):
     """Load libtkv_amq.so (building it in-tree if absent and hipcc is available)."""
     global _lib
     if _lib is not None:
         return _lib
-    path = os.environ.get("TKV_AMQ_LIB") or _build.LIB  # override: kernel experiments
+    path = experiment_lib() or _build.LIB
     if not os.path.exists(path):
         if not build_if_missing:
             raise RuntimeError(f"libtkv_amq.so not built ({path}); run __graft_entry__.build()")
@@ -147,7 +175,7 @@ def lib(build_if_missing: bool = True):
     L.tkv_amq_gen_keys16.argtypes = [u64, u64, u64, vp, vp]
     L.tkv_amq_stage_keys.restype = i32
     L.tkv_amq_stage_keys.argtypes = [vp, u64, u64, u32, vp, u64, vp, i32]
-    if os.environ.get("TKV_AMQ_LIB") and not hasattr(L, "tkv_amq_probe_ex"):
+    if path != _build.LIB and not hasattr(L, "tkv_amq_probe_ex"):
         _lib = L  # an older experiment build (A/B timing): the round-1 entry points only
         return L
     L.tkv_amq_leaf_data_size.restype = u64
@@ -185,6 +213,16 @@ def lib(build_if_missing: bool = True):
         L.tkv_amq_bloom_build_range_records_ws_bytes.argtypes = [u64, u32, u32]
         L.tkv_amq_bloom_build_range_records.restype = i32
         L.tkv_amq_bloom_build_range_records.argtypes = [vp, u64, vp, u32, u32, u32, u32, vp, vp, u64, vp]
+    if hasattr(L, "tkv_amq_bloom_route_plan"):
+        prp = ctypes.POINTER(RoutePlan)
+        L.tkv_amq_bloom_route_plan.restype = i32
+        L.tkv_amq_bloom_route_plan.argtypes = [u64, u32, u32, u32, u32, prp]
+        L.tkv_amq_bloom_route_blocks.restype = i32
+        L.tkv_amq_bloom_route_blocks.argtypes = [vp, u32, u64, vp, prp, vp, vp, u64, vp]
+        L.tkv_amq_bloom_build_part_blocks.restype = i32
+        L.tkv_amq_bloom_build_part_blocks.argtypes = [vp, u32, vp, prp, u32, vp, vp, u64, vp]
+        L.tkv_amq_bloom_blocks_lost.restype = i32
+        L.tkv_amq_bloom_blocks_lost.argtypes = [vp, u32, prp, vp]
     if hasattr(L, "tkv_amq_bloom_tile_blocks"):
         L.tkv_amq_bloom_tile_blocks.restype = u32
         L.tkv_amq_bloom_tile_blocks.argtypes = []

@@ -41,6 +41,13 @@
 #include "tkv_amq.h"
 #include "tkv_amq_device.h"
 
+// The one diagnostic build option (TKV_DIAG_RING: per-step timestamps of vqf_ring_place's
+// decider, read by tools/ring_diag.py) is for experiment libraries only; the shipped library
+// refuses it, and no option changes what a kernel computes.
+#if defined(TKV_DIAG_RING) && !defined(TKV_AMQ_EXPERIMENT_BUILD)
+#error "TKV_DIAG_RING is a diagnostic: build it only as an experiment library (-DTKV_AMQ_EXPERIMENT_BUILD)"
+#endif
+
 namespace tkv {
 
 // ---------------------------------------------------------------------------------------
@@ -76,6 +83,9 @@ __constant__ BloomSeeds c_bloom = make_bloom_seeds();
 enum KeyMode : int { kKey16 = 0, kKeyFixed = 1, kKeyVar = 2, kKey24 = 3, kKeyLoc = 4 };
 
 typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+// the same vector at 4-byte alignment: 16-byte loads of 12-byte records at their 12-byte stride
+// (gfx950 global loads take any dword-aligned address; a u32x4_t* there would claim 16)
+typedef u32x4_t u32x4_a4_t __attribute__((aligned(4)));
 
 // streaming (non-temporal) loads/stores for data touched exactly once, so it does not
 // evict reused data (the probe's filter array) from L2 / the Infinity Cache
@@ -993,22 +1003,36 @@ constexpr uint32_t kPartPlaneBytes = 12 * kPartBatch;       // the batch's recor
 constexpr uint32_t kDirectMaxTiles = 6400;                  // LDS: 10 bytes per tile beside the planes
 constexpr uint32_t kRecPartMaxTiles = kDirectMaxTiles;      // (< 2^13: a record's tile field)
 constexpr uint32_t kRouteMaxParts = 2048;                   // tkv_amq_bloom_route(_records)
-#ifndef TKV_EXP_ROUTE_WGS
-#define TKV_EXP_ROUTE_WGS 1792
-#endif
-constexpr uint32_t kRouteMaxWgs = TKV_EXP_ROUTE_WGS;        // route count / scatter workgroups
+constexpr uint32_t kRouteMaxWgs = 1792;                     // route count / scatter workgroups
+static_assert(kRouteMaxWgs % 256 == 0, "route_scan_cols: kRouteMaxWgs / 256 rows per thread");
+// kSrcSeg12: the most route blocks one part build reads (chunks x senders)
+constexpr uint32_t kMaxSrcSegs = 256;
+// bloom_route_part (part_body bucketing by part): parts per route, and its LDS -- the three
+// record planes, a u16 plane of each record's part, the histograms / starts / cursors of the
+// parts, the wave sums and the overflow counter
+__host__ __device__ constexpr inline uint32_t route_lds_bytes(uint32_t n_parts)
+{
+  return kPartPlaneBytes + 2u * kPartBatch + 20u * ((n_parts + 1) / 2) + 4u * (kPartThreads / 64 + 1);
+}
+static_assert(route_lds_bytes(kRouteMaxParts) <= 160 * 1024, "one route workgroup per CU");
 
 __host__ __device__ constexpr inline uint32_t part_lds_bytes(uint32_t n_tiles)
 {
   // the planes; H0, H1, start: (T+1)/2 words each (u16 pairs); cursor: 2 * ((T+1)/2) words;
   // 16 wave sums and the overflow counter
-  return kPartPlaneBytes + 20u * ((n_tiles + 1) / 2) + 4u * (kPartThreads / 64 + 1);
+  return kPartPlaneBytes + 20u * ((n_tiles + 1) / 2) + 4u * (kPartThreads / 64 + 1) +
+         4u * (kMaxSrcSegs + 2);
 }
 static_assert(part_lds_bytes(kDirectMaxTiles) <= 160 * 1024, "one workgroup per CU");
 static_assert(kRecPartMaxTiles <= 8192, "a record's 13-bit tile field");
 static_assert(kPartBatch < 65536, "u16 ranks");
 
-enum PartSrc : int { kSrcKey16 = 0, kSrcKey24 = 1, kSrcRec12 = 2, kSrcRaw16 = 3 };
+enum PartSrc : int { kSrcKey16 = 0, kSrcKey24 = 1, kSrcRec12 = 2, kSrcRaw16 = 3, kSrcSeg12 = 4 };
+// what part_body buckets by: the filter's tiles (the partition, ahead of bloom_tile), or the
+// route's parts (bloom_route_part: the one-pass route of a filter past kDirectMaxTiles tiles,
+// and of a hash-range sharded filter's keys to their owners)
+enum PartDst : int { kDstTiles = 0, kDstParts = 1 };
+
 
 struct PartGeom {
   uint32_t P;        // partition workgroups
@@ -1327,8 +1351,32 @@ __global__ __launch_bounds__(NT) void route_recs(const uint8_t* __restrict__ key
 // ---------------------------------------------------------------------------------------
 // partition, tile build, overflow
 // ---------------------------------------------------------------------------------------
+// The route's output (bloom_route_part) and a part build's input (kSrcSeg12): fixed-size
+// blocks, one per (route chunk, sender, destination rank).  Block layout:
+//   counts_off   u32 [parts_per_dest][P]: records in region (jl, w) (<= cap)
+//   ovf_n_off    u32: overflow entries appended to the block (> ovf_cap: entries were lost)
+//   regions_off  region (jl, w) at regions_off + (jl * P + w) * cap * 12: route workgroup w's
+//                12-byte records of the destination's jl-th part, in its batches' order
+//   ovf_off      ovf_cap 16-byte entries (record, global part): records whose region was full
+// Part p belongs to rank p % world as its part jl = p / world (round-robin: round jl's parts of
+// all ranks are one contiguous byte range of the bitmap, all-gathered in place).  Every block
+// has the same size, so a chunk's exchange is one all-to-all of equal splits with no host
+// synchronisation to size it.
+struct RouteBlock {
+  uint64_t bytes;
+  uint64_t counts_off;
+  uint64_t ovf_n_off;
+  uint64_t regions_off;
+  uint64_t ovf_off;
+  uint32_t P;               // route workgroups (= the part builds' partition workgroups)
+  uint32_t cap;             // records per region
+  uint32_t ovf_cap;         // overflow entries per block
+  uint32_t parts_per_dest;  // g
+};
+
 struct PartArgs {
-  const uint8_t* src;  // keys (16 or 24 bytes), routed 12-byte records, or routed 16-byte keys
+  const uint8_t* src;  // keys (16 or 24 bytes), routed 12-byte records, or routed 16-byte keys;
+                       // kSrcSeg12: the first route block of the part's inputs
   uint32_t n;          // items [0, n) of src (from_seg: the segment's keys, n capped by it)
   uint32_t tile0;      // global tile of local tile 0
   uint32_t from_seg;
@@ -1339,7 +1387,23 @@ struct PartArgs {
   uint8_t* ws;
   PartGeom g;
   uint32_t src_kind;   // PartSrc of the partition (kSrcRec12: routed items), for bloom_overflow
+  // kDstParts: the route blocks (one per destination rank), tiles per part, ranks, and the
+  // multiply-high reciprocals of q and world (x / q = (x * q_magic) >> 32 for x < 2^21)
+  uint8_t* dst;
+  uint32_t q;
+  uint32_t world;
+  uint64_t q_magic;
+  uint64_t w_magic;
+  RouteBlock blk;
+  // kSrcSeg12: the blocks holding this part (n_src_segs of them, blk.bytes apart) and the
+  // part's index jl inside each
+  uint32_t n_src_segs;
+  uint32_t seg_part;
 };
+
+__host__ __device__ inline uint64_t div_magic(uint32_t d) { return (0x100000000ull / d) + 1; }
+static_assert(sizeof(tkv_amq_route_plan) == 120, "abi.RoutePlan");
+__device__ inline uint32_t div_by_magic(uint32_t x, uint64_t m) { return (uint32_t)(((uint64_t)x * m) >> 32); }
 
 __device__ inline uint4 load_rec12(const uint8_t* recs, uint32_t i)
 {
@@ -1412,52 +1476,105 @@ __device__ inline uint32_t lds_u16(const uint32_t* words, uint32_t t)
   return (words[t >> 1] >> ((t & 1u) << 4)) & 0xffffu;
 }
 
-// Per batch: hash U items per thread into records, each ranked in its tile's run by a
-// returning ds_add on the packed histogram (the next batch's items are then loaded, in flight
-// until its hash); LDS barrier; scan (two barriers); every record placed at its sorted position
-// in the LDS planes; LDS barrier; the planes written out in order, each tile's run to the end
-// of this workgroup's region of the tile, so a store instruction covers a few long runs (the L2
-// merges them into whole lines) instead of 64 scattered records.  Every lane issues the same
-// loads and stores per batch (clamped loads; lanes without a record store to a sink in the
-// workspace header).  Overflow entries are the records themselves (their tile is in the
-// record: T <= kDirectMaxTiles < 2^13) or, RAW, the 16-byte keys.
-template <int K, int SRC>
+// Per batch: hash U items per thread into records, each ranked in its bucket's run (its tile;
+// DST == kDstParts: its part) by a returning ds_add on the packed histogram (the next batch's
+// items are then loaded, in flight until its hash); LDS barrier; scan (two barriers); every
+// record placed at its sorted position in the LDS planes; LDS barrier; the planes written out
+// in order, each bucket's run to the end of this workgroup's region of that bucket, so a
+// store instruction covers a few long runs (the L2 merges them into whole lines) instead of
+// 64 scattered records.  Every lane issues the same loads and stores per batch (clamped loads;
+// lanes without a record store to a sink in the workspace header).  Overflow entries are the
+// records themselves (their tile is in the record: T <= kDirectMaxTiles < 2^13), RAW the
+// 16-byte keys, kDstParts the record and its part (16 bytes).
+template <int K, int SRC, int DST = kDstTiles>
 __device__ void part_body(const tkv_amq_segment& sg, const PartArgs& a, uint32_t* lds)
 {
   constexpr bool RAW = SRC == kSrcRaw16;
+  constexpr bool ROUTE = DST == kDstParts;
+  constexpr bool ROUTED = SRC == kSrcRec12 || SRC == kSrcSeg12;  // records with their tile in part
+  static_assert(!(ROUTE && (RAW || ROUTED)), "the route hashes keys");
   // 16-byte records: four key words and the tile per item in LDS, half the items per batch
   constexpr uint32_t RB = RAW ? 16 : 12, U = RAW ? kPartU / 2 : kPartU, NT = kPartThreads, B = U * NT;
-  constexpr uint32_t NPL = RAW ? 5 : 3;  // LDS planes
+  constexpr uint32_t NPL = RAW ? 5 : 3;  // LDS planes (ROUTE: + a u16 plane of parts)
   static_assert(NPL * B * 4 <= kPartPlaneBytes, "planes");
-  constexpr uint32_t IB = SRC == kSrcKey24 ? 24 : (SRC == kSrcRec12 ? 12 : 16);  // item bytes
+  constexpr uint32_t IB = SRC == kSrcKey24 ? 24 : (ROUTED ? 12 : 16);  // item bytes
   const uint32_t tid = threadIdx.x, w = blockIdx.x, P = a.g.P, T = a.g.n_tiles, cap = a.g.cap;
   const uint32_t nb = sg.n_blocks, k = sg.hash_count;
   const uint32_t HW = (T + 1) >> 1;
   uint32_t* pl = lds;  // plane j at pl + j * B
-  uint32_t* H0 = lds + kPartPlaneBytes / 4;
+  uint16_t* plp = reinterpret_cast<uint16_t*>(lds + kPartPlaneBytes / 4);  // ROUTE: parts
+  uint32_t* H0 = lds + (kPartPlaneBytes + (ROUTE ? 2 * B : 0)) / 4;
   uint32_t* H1 = H0 + HW;
   uint32_t* start = H1 + HW;
   uint32_t* cursor = start + HW;
   uint32_t* wsum = cursor + 2 * HW;  // 16 wave sums
   uint32_t* ovf_n = wsum + NT / 64;
+  uint32_t* pre = ovf_n + 1;         // kSrcSeg12: the item prefix over the source blocks
   for (uint32_t i = tid; i < 2 * HW; i += NT) {
     H0[i] = 0;  // (H0 and H1)
     cursor[i] = 0;
   }
   if (tid == 0) *ovf_n = 0;
-  __syncthreads();
+  if constexpr (ROUTE) {
+    // the destination blocks' overflow counters, appended to by bloom_route_ovf_pack after
+    // this kernel (a later launch on the same stream)
+    if (w == 0)
+      for (uint32_t d = tid; d < a.world; d += NT)
+        *reinterpret_cast<uint32_t*>(a.dst + (uint64_t)d * a.blk.bytes + a.blk.ovf_n_off) = 0;
+  }
   const uint8_t* src;
   uint32_t n;
-  part_items(sg, a, IB, src, n);
-  const uint32_t per = a.cnt ? (n + P - 1) / P : a.g.per;
-  const uint32_t kb = min(n, w * per), ke = min(n, kb + per);
-  const uint64_t ovf_base = a.g.ovf_off + (uint64_t)w * a.g.per * 16;
+  uint64_t seg_reg = 0;  // kSrcSeg12: this workgroup's region of the part inside a block
+  if constexpr (SRC == kSrcSeg12) {
+    const uint32_t S = a.n_src_segs;
+    seg_reg = a.blk.regions_off + ((uint64_t)a.seg_part * a.blk.P + w) * a.blk.cap * 12ull;
+    const uint64_t cnt_off = a.blk.counts_off + 4ull * ((uint64_t)a.seg_part * a.blk.P + w);
+    if (tid < 64) {  // one wave: the inclusive scan of the S counts, 64 at a time
+      uint32_t run = 0;
+      for (uint32_t s0 = 0; s0 < S; s0 += 64) {
+        const uint32_t sidx = s0 + tid;
+        uint32_t c = sidx < S ? *reinterpret_cast<const uint32_t*>(a.src + (uint64_t)sidx * a.blk.bytes + cnt_off) : 0u;
+        c = min(c, a.blk.cap);
+        uint32_t inc = c;
+#pragma unroll
+        for (uint32_t d = 1; d < 64; d <<= 1) {
+          const uint32_t v = __shfl_up(inc, d, 64);
+          if (tid >= d) inc += v;
+        }
+        if (sidx < S) pre[sidx + 1] = run + inc;
+        run += __shfl(inc, 63, 64);
+      }
+      if (tid == 0) pre[0] = 0;
+    }
+  }
+  __syncthreads();
+  uint32_t kb, ke;
+  if constexpr (SRC == kSrcSeg12) {
+    src = a.src;
+    n = pre[a.n_src_segs];
+    kb = 0;  // this workgroup's own regions, whole
+    ke = n;
+  } else {
+    part_items(sg, a, IB, src, n);
+    const uint32_t per = a.cnt ? (n + P - 1) / P : a.g.per;
+    kb = min(n, w * per);
+    ke = min(n, kb + per);
+  }
+  const uint64_t ovf_base = a.g.ovf_off + (uint64_t)w * a.g.per * 16;  // (lists 16 B per item apart)
   const uint32_t last_item = ke > 0 ? ke - 1 : 0;
+  uint32_t cs = 0;  // kSrcSeg12: the block of this thread's last item (items rise per thread)
   using In = typename std::conditional<SRC == kSrcKey24, Key24, uint4>::type;
   auto load_in = [&](uint32_t i) -> In {
-    if constexpr (SRC == kSrcRec12) return load_rec12(src, i);
-    else if constexpr (SRC == kSrcKey24) return load_key24(src, i);
-    else return load_nt16(src + 16ull * i);
+    if constexpr (SRC == kSrcSeg12) {
+      while (i >= pre[cs + 1]) ++cs;
+      return load_rec12(src + (uint64_t)cs * a.blk.bytes + seg_reg, i - pre[cs]);
+    } else if constexpr (SRC == kSrcRec12) {
+      return load_rec12(src, i);
+    } else if constexpr (SRC == kSrcKey24) {
+      return load_key24(src, i);
+    } else {
+      return load_nt16(src + 16ull * i);
+    }
   };
   In in[U];
   // the store phase: the previous batch's sorted records (LDS planes) to the regions
@@ -1473,28 +1590,45 @@ __device__ void part_body(const tkv_amq_segment& sg, const PartArgs& a, uint32_t
       if constexpr (RAW) {
         x3 = pl[3 * B + j];
         t = pl[4 * B + j];
+      } else if constexpr (ROUTE) {
+        t = plp[j];
       } else {
         t = rec_tile(x0, x1, x2);
       }
       t = v ? t : 0u;
       const uint32_t c = cursor[t] + (j - lds_u16(start, t));
-      uint64_t off = 0;  // the sink
+      uint8_t* d = a.ws;  // the sink
+      bool ovf = false;
       if (v) {
-        if (c < cap) off = a.g.regions_off + ((uint64_t)t * P + w) * cap * a.g.rb + (uint64_t)c * RB;
-        else off = ovf_base + (uint64_t)RB * atomicAdd(ovf_n, 1u);  // LDS atomic: this workgroup's list
+        if (c < cap) {
+          if constexpr (ROUTE) {
+            const uint32_t jl = div_by_magic(t, a.w_magic), dr = t - jl * a.world;
+            d = a.dst + (uint64_t)dr * a.blk.bytes + a.blk.regions_off +
+                (((uint64_t)jl * P + w) * cap + c) * 12ull;
+          } else {
+            d = a.ws + a.g.regions_off + ((uint64_t)t * P + w) * cap * a.g.rb + (uint64_t)c * RB;
+          }
+        } else {
+          ovf = true;  // LDS atomic: this workgroup's list
+          d = a.ws + ovf_base + (uint64_t)(ROUTE ? 16 : RB) * atomicAdd(ovf_n, 1u);
+        }
       }
-      uint32_t* d = reinterpret_cast<uint32_t*>(a.ws + off);
+      uint32_t* dw = reinterpret_cast<uint32_t*>(d);
       if constexpr (RAW) {
-        *reinterpret_cast<uint4*>(d) = make_uint4(x0, x1, x2, x3);
+        *reinterpret_cast<uint4*>(dw) = make_uint4(x0, x1, x2, x3);
       } else {
-        d[0] = x0;
-        d[1] = x1;
-        d[2] = x2;
+        dw[0] = x0;
+        dw[1] = x1;
+        dw[2] = x2;
+        if constexpr (ROUTE)
+          if (ovf) dw[3] = t;
       }
     }
   };
+  if (ke > kb) {  // (no items: src may be null)
 #pragma unroll
-  for (uint32_t u = 0; u < U; ++u) in[u] = load_in(min(kb + u * NT + tid, last_item));
+    for (uint32_t u = 0; u < U; ++u) in[u] = load_in(min(kb + u * NT + tid, last_item));
+  }
   uint32_t par = 0;
   // Per iteration: hash batch b; write out batch b - 1 (its stores then drain while this
   // batch is scanned and sorted: the compiler waits for every outstanding load and store
@@ -1503,7 +1637,7 @@ __device__ void part_body(const tkv_amq_segment& sg, const PartArgs& a, uint32_t
   for (uint32_t b0 = kb; b0 < ke; b0 += B, par ^= 1) {
     uint32_t* hist = par ? H1 : H0;
     uint32_t* prev = par ? H0 : H1;
-    // per item: its record and (tile << 16 | rank in the tile's run), ~0: no record
+    // per item: its record and (bucket << 16 | rank in the bucket's run), ~0: no record
     uint32_t r0[U], r1[U], r2[U], r3[RAW ? U : 1], tr[U];
 #pragma unroll
     for (uint32_t u = 0; u < U; ++u) {
@@ -1518,7 +1652,7 @@ __device__ void part_body(const tkv_amq_segment& sg, const PartArgs& a, uint32_t
           r1[u] = in[u].y;
           r2[u] = in[u].z;
           r3[u] = in[u].w;
-        } else if constexpr (SRC == kSrcRec12) {
+        } else if constexpr (ROUTED) {
           r0[u] = in[u].x;
           r1[u] = in[u].y;
           r2[u] = in[u].z;
@@ -1526,8 +1660,14 @@ __device__ void part_body(const tkv_amq_segment& sg, const PartArgs& a, uint32_t
         } else {
           uint32_t bits[8];
           const uint32_t blk = rec_hash_bits<K>(in[u], nb, k, bits);
-          t = (blk >> kTileShift) - a.tile0;
-          rec_pack(blk & (kTileBlocks - 1), t, bits, r0[u], r1[u], r2[u]);
+          const uint32_t tg = blk >> kTileShift;
+          if constexpr (ROUTE) {
+            t = div_by_magic(tg, a.q_magic);  // the key's part; its record's tile is in the part
+            rec_pack(blk & (kTileBlocks - 1), tg - t * a.q, bits, r0[u], r1[u], r2[u]);
+          } else {
+            t = tg - a.tile0;
+            rec_pack(blk & (kTileBlocks - 1), t, bits, r0[u], r1[u], r2[u]);
+          }
         }
       }
       if (t >= T) {
@@ -1556,6 +1696,7 @@ __device__ void part_body(const tkv_amq_segment& sg, const PartArgs& a, uint32_t
         pl[3 * B + pos] = r3[u];
         pl[4 * B + pos] = t;
       }
+      if constexpr (ROUTE) plp[pos] = (uint16_t)t;
     }
     lds_barrier();
   }
@@ -1563,9 +1704,17 @@ __device__ void part_body(const tkv_amq_segment& sg, const PartArgs& a, uint32_t
   __syncthreads();
   // the last batch's run lengths (its histogram is the one the loop's last batch counted into)
   const uint32_t* last = par ? H0 : H1;
-  uint32_t* counts = reinterpret_cast<uint32_t*>(a.ws + a.g.counts_off);
-  for (uint32_t t = tid; t < T; t += NT)
-    counts[(uint64_t)t * P + w] = min(cursor[t] + lds_u16(last, t), cap);
+  if constexpr (ROUTE) {
+    for (uint32_t t = tid; t < T; t += NT) {
+      const uint32_t jl = div_by_magic(t, a.w_magic), dr = t - jl * a.world;
+      *reinterpret_cast<uint32_t*>(a.dst + (uint64_t)dr * a.blk.bytes + a.blk.counts_off +
+                                   4ull * ((uint64_t)jl * P + w)) = min(cursor[t] + lds_u16(last, t), cap);
+    }
+  } else {
+    uint32_t* counts = reinterpret_cast<uint32_t*>(a.ws + a.g.counts_off);
+    for (uint32_t t = tid; t < T; t += NT)
+      counts[(uint64_t)t * P + w] = min(cursor[t] + lds_u16(last, t), cap);
+  }
   if (tid == 0) reinterpret_cast<uint32_t*>(a.ws + a.g.ovf_n_off)[w] = *ovf_n;
 }
 
@@ -1607,6 +1756,86 @@ __global__ __launch_bounds__(kPartThreads) void bloom_part_routed(const tkv_amq_
   if (k == 0) return;
   if (k <= 8) part_body<0, kSrcRec12>(sg, a, s_part);
   else part_body<0, kSrcRaw16>(sg, a, s_part);
+}
+
+// The one-pass route (k <= 8): every key hashed once into its 12-byte bit record, counting-
+// sorted by part in LDS and appended to this workgroup's region of the part in the part's
+// destination block (part p -> rank p % world), whole runs per store; records beyond a region's
+// capacity go to this workgroup's overflow list as (record, part).  No count pass: the regions
+// have a fixed capacity.
+__global__ __launch_bounds__(kPartThreads) void bloom_route_part(const tkv_amq_segment* __restrict__ segs,
+                                                                 PartArgs a)
+{
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_part[];
+  const tkv_amq_segment sg = segs[0];
+  const uint32_t k = sg.hash_count;
+  if (k == 0 || k > 8) return;  // (the host routes bit records for k <= 8 only)
+  if (a.kb == 24) {
+    if (k == 8) part_body<8, kSrcKey24, kDstParts>(sg, a, s_part);
+    else part_body<0, kSrcKey24, kDstParts>(sg, a, s_part);
+  } else {
+    if (k == 8) part_body<8, kSrcKey16, kDstParts>(sg, a, s_part);
+    else if (k == 7) part_body<7, kSrcKey16, kDstParts>(sg, a, s_part);
+    else part_body<0, kSrcKey16, kDstParts>(sg, a, s_part);
+  }
+}
+
+// a part's partition from the route blocks that hold it (kSrcSeg12): workgroup w reads region
+// (jl, w) of every block, back to back
+__global__ __launch_bounds__(kPartThreads) void bloom_part_segs(const tkv_amq_segment* __restrict__ segs,
+                                                                PartArgs a)
+{
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_part[];
+  const tkv_amq_segment sg = segs[0];
+  if (sg.hash_count == 0 || sg.hash_count > 8) return;
+  part_body<0, kSrcSeg12>(sg, a, s_part);
+}
+
+// Route overflow entries (record, part) of each route workgroup's list into the destination
+// blocks' fixed-capacity overflow areas; a block's counter past ovf_cap records the loss (the
+// caller then rebuilds through the exact exchange).  Empty lists: one count read per workgroup.
+__global__ __launch_bounds__(256) void bloom_route_ovf_pack(PartArgs a)
+{
+  const uint32_t w = blockIdx.x;
+  const uint32_t n = reinterpret_cast<const uint32_t*>(a.ws + a.g.ovf_n_off)[w];
+  const uint4* list = reinterpret_cast<const uint4*>(a.ws + a.g.ovf_off + (uint64_t)w * a.g.per * 16);
+  for (uint32_t e = threadIdx.x; e < n; e += 256) {
+    const uint4 x = list[e];
+    const uint32_t jl = div_by_magic(x.w, a.w_magic), dr = x.w - jl * a.world;
+    uint8_t* b = a.dst + (uint64_t)dr * a.blk.bytes;
+    const uint32_t slot = atomicAdd(reinterpret_cast<uint32_t*>(b + a.blk.ovf_n_off), 1u);
+    if (slot < a.blk.ovf_cap) reinterpret_cast<uint4*>(b + a.blk.ovf_off)[slot] = x;
+  }
+}
+
+// Overflow entries (record, part) into the finished filter with device-scope atomicOr, for the
+// parts [p0, p1) (after their bloom_tile): n_lists lists, list l's count at cnt + l * cnt_stride
+// (at most cap entries used), its entries at ent + l * ent_stride.  Per-workgroup route lists
+// (one GPU) and received blocks' overflow areas (hash-range shards) alike.
+__global__ __launch_bounds__(256) void bloom_route_ovf_apply(const tkv_amq_segment* __restrict__ segs,
+                                                             const uint8_t* cnt, uint64_t cnt_stride,
+                                                             const uint8_t* ent, uint64_t ent_stride,
+                                                             uint32_t cap, uint32_t q, uint32_t p0, uint32_t p1,
+                                                             uint8_t* __restrict__ out)
+{
+  const tkv_amq_segment sg = segs[0];
+  const uint32_t k = sg.hash_count, l = blockIdx.x;
+  if (k == 0) return;
+  const uint32_t n = min(*reinterpret_cast<const uint32_t*>(cnt + (uint64_t)l * cnt_stride), cap);
+  const uint4* list = reinterpret_cast<const uint4*>(ent + (uint64_t)l * ent_stride);
+  uint32_t* words = reinterpret_cast<uint32_t*>(out + sg.out_offset + kBloomHeader);
+  const uint32_t kk = k < 8 ? k : 8u;
+  for (uint32_t e = threadIdx.x; e < n; e += 256) {
+    const uint4 x = list[e];
+    if (x.w < p0 || x.w >= p1) continue;
+    const uint64_t blk = ((uint64_t)x.w * q + rec_tile(x.x, x.y, x.z)) * kTileBlocks + (x.x & (kTileBlocks - 1));
+    const uint32_t b[8] = {x.x >> 11, x.x >> 20, x.y, x.y >> 9, x.y >> 18, x.z, x.z >> 9, x.z >> 18};
+    uint32_t* bw = words + 16ull * blk;
+    for (uint32_t j = 0; j < kk; ++j) {
+      const uint32_t bj = b[j] & 511u;
+      atomicOr(bw + (bj >> 5), 1u << (bj & 31u));
+    }
+  }
 }
 
 // the tile and overflow kernels' records are 16-byte keys when the partition had them
@@ -1659,7 +1888,7 @@ __device__ void tile_body(const tkv_amq_segment& sg, const PartArgs& a, uint32_t
         // 16 bytes at the 12-byte stride (the next record's first word, or the workspace
         // after the last region, is ignored), nontemporal: the records are read once, and
         // plain loads ran 20% slower (0.351 vs 0.292 ms per 100M keys)
-        const u32x4_t e = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(p));
+        const u32x4_t e = __builtin_nontemporal_load(reinterpret_cast<const u32x4_a4_t*>(p));
         q.x[v][0] = e.x; q.x[v][1] = e.y; q.x[v][2] = e.z; q.x[v][3] = 0;
       }
     }
@@ -3042,11 +3271,6 @@ __device__ __attribute__((always_inline)) void vqf_ring_decide(const tkv_amq_seg
 #ifdef TKV_DIAG_RING
     const uint64_t d1 = __builtin_amdgcn_s_memtime();
 #endif
-#ifdef TKV_EXP_NODECIDE  // experiment: the producers' rate (the decider only frees slots)
-    lds_store_relaxed(freed, c + 1);
-    fetch((q + 1) % NS, next);
-    return;
-#endif
     const uint32_t cnt_p = lds_rd(S.pb4);
     const uint32_t cnt_a = lds_rd(S.ab4);
 #ifdef TKV_DIAG_RING
@@ -3071,11 +3295,7 @@ __device__ __attribute__((always_inline)) void vqf_ring_decide(const tkv_amq_seg
 #ifdef TKV_DIAG_RING
     uint64_t slow = 0;
 #endif
-#ifdef TKV_EXP_FASTONLY  // experiment: every step takes the fast path (wrong filters; timing only)
-    if (false) {
-#else
     if (bal(cp >= C::kThreshold) != 0) {
-#endif
 #ifdef TKV_DIAG_RING
       slow = 1;
 #endif
@@ -3708,14 +3928,8 @@ constexpr uint32_t kRingPlaceMaxSegs = 256;
 // vqf_locate_keys before vqf_ring_place up to this many leaves (variable-length keys, other
 // fixed sizes): measured crossovers, past which the chip is busy enough that hashing inside the
 // producers, overlapped with the decider, beats writing and re-reading 8-byte located records
-#ifndef TKV_EXP_LOC_VAR_SEGS
-#define TKV_EXP_LOC_VAR_SEGS 64
-#endif
-#ifndef TKV_EXP_LOC_FIXED_SEGS
-#define TKV_EXP_LOC_FIXED_SEGS 32
-#endif
-constexpr uint32_t kVqfLocMaxSegsVar = TKV_EXP_LOC_VAR_SEGS;
-constexpr uint32_t kVqfLocMaxSegsFixed = TKV_EXP_LOC_FIXED_SEGS;
+constexpr uint32_t kVqfLocMaxSegsVar = 64;
+constexpr uint32_t kVqfLocMaxSegsFixed = 32;
 __host__ __device__ inline uint32_t ring_place_cnt_words(uint32_t max_nb)
 {
   return (max_nb + 1 + 3) & ~3u;  // + the dummy block
@@ -4383,30 +4597,201 @@ inline void launch_route(const RouteGeom& g, hipStream_t s, const uint8_t* keys,
                        q, reinterpret_cast<uint4*>(out_keys), min_k);
 }
 
+// Tiles per routed part (a filter past kDirectMaxTiles): the fewer tiles a partition spreads
+// a batch over, the longer each tile's run per store (fewer partial-line writes), until the
+// route's output over that many parts pays more than the part builds save; and at most one
+// tile per CU, so a part's tile kernel runs in one round.  Bit records (k <= 8), 1B keys at 12
+// bits/key on one GPU, round 4's two-pass route: 1,431-tile parts 36.7 Gkeys/s, 800 39.2, 400
+// 40.4, 294 39.8, 255 42.6, 229 41.9, 198 41.5, 127 37.1, 100 33.6 (profiles/r04/part_tiles/).
+// 16-byte keys routed as themselves (k > 8) keep 1,600.  (turtle_kv_amd.dist.ROUTED_PART_TILES,
+// ROUTED_KEY_PART_TILES)
+constexpr uint32_t kRoutePartTiles = 256;
+constexpr uint32_t kRouteKeyPartTiles = 1600;
+static_assert(kRoutePartTiles <= kRecPartMaxTiles && kRouteKeyPartTiles <= kRecPartMaxTiles, "");
+static_assert(kRoutePartTiles < 2048, "div_by_magic: exact for q < 2048 and tiles < 2^21");
+
+// The route plan of tkv_amq_bloom_route_plan: parts, route workgroups, the block layout.  The
+// region capacity is mean + 6 sigma + 16 records of a uniform hash (as the partition's); an
+// overflow area of ovf_cap entries per block (0 for the one-GPU build, which applies its route
+// workgroups' own overflow lists instead).
+inline int route_plan(uint64_t chunk_keys, uint32_t n_chunks, uint64_t n_blocks, uint32_t k, uint32_t world,
+                      bool ovf_area, tkv_amq_route_plan& rp)
+{
+  if (world == 0 || n_chunks == 0 || n_blocks == 0 || n_blocks > 0xffffffffull || k == 0 || k > 8 ||
+      chunk_keys > 0xffffffffull || (uint64_t)n_chunks * world > kMaxSrcSegs)
+    return TKV_AMQ_INVALID_ARGUMENT;
+  memset(&rp, 0, sizeof(rp));
+  const uint32_t T = filter_tiles(n_blocks);
+  const uint32_t per_rank = (uint32_t)div_up(T, world);
+  const uint32_t g = (uint32_t)div_up(per_rank, kRoutePartTiles);
+  const uint32_t q = (uint32_t)div_up(T, (uint64_t)world * g);
+  if ((uint64_t)world * g > kRouteMaxParts) return TKV_AMQ_INVALID_ARGUMENT;
+  rp.n_tiles = T;
+  rp.n_blocks = n_blocks;
+  rp.parts_per_rank = g;
+  rp.n_parts = world * g;
+  rp.part_tiles = q;
+  rp.world = world;
+  rp.n_chunks = n_chunks;
+  rp.hash_count = k;
+  rp.chunk_keys = chunk_keys;
+  const uint64_t pw = div_up(chunk_keys, 32ull * kPartThreads);
+  const uint32_t P = (uint32_t)(pw < 1 ? 1 : (pw > kPartMaxWgs ? kPartMaxWgs : pw));
+  rp.route_wgs = P;
+  const uint64_t per = div_up(chunk_keys, P);  // keys per route workgroup
+  // a part's share of the keys is its blocks' share (q full tiles at most; the last tile may
+  // be short, and the last parts may hold fewer tiles, or none when world * g * q > T)
+  const double e = (double)per * std::min<uint64_t>((uint64_t)q * kTileBlocks, n_blocks) / n_blocks;
+  rp.region_cap = ((uint32_t)(e + 6.0 * sqrt(e) + 16.0) + 15) & ~15u;
+  // overflow entries per block: ~0.4% of a block's records (none expected from a uniform hash)
+  rp.ovf_cap = ovf_area ? (uint32_t)(4096 + chunk_keys / ((uint64_t)world * 256)) : 0u;
+  rp.counts_off = 0;
+  rp.ovf_n_off = align256(4ull * g * P);
+  rp.regions_off = rp.ovf_n_off + 256;
+  rp.ovf_off = align256(rp.regions_off + 12ull * g * P * rp.region_cap);
+  rp.block_bytes = align256(rp.ovf_off + 16ull * rp.ovf_cap);
+  // route workspace: [sink 256][u32 overflow count per workgroup][16-byte entries, per each]
+  rp.route_ws_bytes = align256(512 + 4ull * P) + 16ull * P * per;
+  // a part build: partition regions over the part's q tiles, overflow lists of what its
+  // workgroup may receive (every source block's region at capacity)
+  const uint64_t S = (uint64_t)n_chunks * world;
+  const double ep = (double)chunk_keys * S / P * std::min<uint64_t>(kTileBlocks, n_blocks) / n_blocks;  // per (full tile, workgroup)
+  const uint32_t capp = ((uint32_t)(ep + 6.0 * sqrt(ep) + 16.0) + 15) & ~15u;
+  const uint64_t regions = (uint64_t)q * P;
+  const uint64_t p_ovf_n = 256 + 4 * regions;
+  const uint64_t p_regions = align256(p_ovf_n + 4ull * P);
+  const uint64_t p_ovf = p_regions + 12ull * regions * capp;
+  rp.part_ws_bytes = p_ovf + 16ull * P * S * rp.region_cap;
+  rp.part_bytes = (uint64_t)q * kTileBlocks * 64;
+  return TKV_AMQ_OK;
+}
+
+// PartGeom of a part build of tn tiles from S route blocks (its workgroups: the route's)
+inline PartGeom route_part_geom(const tkv_amq_route_plan& rp, uint32_t tn, uint32_t S)
+{
+  PartGeom g{};
+  const uint32_t P = rp.route_wgs;
+  g.P = P;
+  g.n_tiles = tn ? tn : 1;
+  g.rb = 12;
+  g.per = S * rp.region_cap;
+  const double ep = (double)rp.chunk_keys * S / P * std::min<uint64_t>(kTileBlocks, rp.n_blocks) /
+                    rp.n_blocks;  // records per (full tile, workgroup)
+  g.cap = ((uint32_t)(ep + 6.0 * sqrt(ep) + 16.0) + 15) & ~15u;
+  const uint64_t regions = (uint64_t)g.n_tiles * P;
+  g.counts_off = 256;
+  g.ovf_n_off = g.counts_off + 4 * regions;
+  g.regions_off = (g.ovf_n_off + 4ull * P + 255) & ~255ull;
+  g.ovf_off = g.regions_off + 12ull * regions * g.cap;
+  g.bytes = g.ovf_off + 16ull * P * g.per;
+  return g;
+}
+
+inline RouteBlock route_block(const tkv_amq_route_plan& rp)
+{
+  RouteBlock b{};
+  b.bytes = rp.block_bytes;
+  b.counts_off = rp.counts_off;
+  b.ovf_n_off = rp.ovf_n_off;
+  b.regions_off = rp.regions_off;
+  b.ovf_off = rp.ovf_off;
+  b.P = rp.route_wgs;
+  b.cap = rp.region_cap;
+  b.ovf_cap = rp.ovf_cap;
+  b.parts_per_dest = rp.parts_per_rank;
+  return b;
+}
+
+inline void set_route_attributes()
+{
+  static std::once_flag attr[kMaxDevices];
+  once_per_device(attr, [] {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&bloom_route_part),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)route_lds_bytes(kRouteMaxParts));
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&bloom_part_segs),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)part_lds_bytes(kDirectMaxTiles));
+  });
+}
+
+// the route of n keys (kb 16 or 24) into the world blocks at d_send (from_seg: keys [0, n) of
+// the segment, n capped by its count -- tkv_amq_build's plan; else exactly n keys)
+inline PartArgs route_args(const tkv_amq_route_plan& rp, const uint8_t* keys, uint32_t kb, uint64_t n,
+                           uint32_t from_seg, uint8_t* d_send, uint8_t* ws)
+{
+  PartArgs a{};
+  a.src = keys;
+  a.n = (uint32_t)n;
+  a.from_seg = from_seg;
+  a.kb = kb;
+  a.ws = ws;
+  a.g.P = rp.route_wgs;
+  a.g.n_tiles = rp.n_parts;
+  a.g.per = (uint32_t)div_up(rp.chunk_keys, rp.route_wgs);
+  a.g.cap = rp.region_cap;
+  a.g.rb = 12;
+  a.g.ovf_n_off = 512;
+  a.g.ovf_off = align256(512 + 4ull * rp.route_wgs);
+  a.dst = d_send;
+  a.q = rp.part_tiles;
+  a.world = rp.world;
+  a.q_magic = div_magic(rp.part_tiles);
+  a.w_magic = div_magic(rp.world);
+  a.blk = route_block(rp);
+  return a;
+}
+
+inline void launch_route_blocks(const PartArgs& a, const tkv_amq_route_plan& rp, hipStream_t s,
+                                const tkv_amq_segment* d_seg, bool pack)
+{
+  set_route_attributes();
+  hipLaunchKernelGGL(bloom_route_part, dim3(rp.route_wgs), dim3(kPartThreads), route_lds_bytes(rp.n_parts), s,
+                     d_seg, a);
+  if (pack) hipLaunchKernelGGL(bloom_route_ovf_pack, dim3(rp.route_wgs), dim3(256), 0, s, a);
+}
+
+// part p's tiles from the n_recv blocks at d_recv (partition -> tiles -> the partition's own
+// overflow lists); the route overflow entries are applied by the caller
+inline void launch_part_from_blocks(const tkv_amq_route_plan& rp, hipStream_t s, const uint8_t* d_recv,
+                                    uint32_t n_recv, const tkv_amq_segment* d_seg, uint32_t p, uint8_t* d_out,
+                                    uint8_t* ws)
+{
+  const uint32_t t0 = p * rp.part_tiles;
+  if (t0 >= rp.n_tiles) return;
+  const uint32_t tn = std::min(rp.part_tiles, rp.n_tiles - t0);
+  set_mono_attributes();
+  set_route_attributes();
+  PartArgs a{};
+  a.src = d_recv;
+  a.tile0 = t0;
+  a.kb = 16;
+  a.ws = ws;
+  a.g = route_part_geom(rp, tn, n_recv);
+  a.src_kind = kSrcSeg12;
+  a.blk = route_block(rp);
+  a.n_src_segs = n_recv;
+  a.seg_part = p / rp.world;
+  hipLaunchKernelGGL(bloom_part_segs, dim3(a.g.P), dim3(kPartThreads), part_lds_bytes(tn), s, d_seg, a);
+  hipLaunchKernelGGL(bloom_tile, dim3(tn), dim3(kTileThreads), 64ull * kTileBlocks, s, d_seg, a, d_out, 1u);
+  hipLaunchKernelGGL(bloom_overflow, dim3(a.g.P), dim3(256), 0, s, d_seg, a, d_out);
+}
+
 // The monolithic build of one filter (a one-leaf tkv_amq_build batch beyond the window path):
-// up to kDirectMaxTiles tiles the partition reads the keys; beyond, the keys are first routed
-// into g parts of at most kRecPartMaxTiles tiles -- as 12-byte records (k <= 8) or as
-// themselves (16-byte keys, k > 8) -- and the parts are built one after another, each
-// partition reading its part's count on the device.  The host does not know k (the plan lives
-// on the device), so the workspace is sized for 16-byte region slots and routed items.
+// up to kDirectMaxTiles tiles the partition reads the keys.  Beyond, with k <= 8 (bits_per_key
+// <= 12): the one-pass route (bloom_route_part, one block) into parts of <= kRoutePartTiles
+// tiles, each part built from its regions (bloom_part_segs -> bloom_tile), then the route
+// workgroups' overflow lists applied (bloom_route_ovf_apply; empty for hashed keys).  k > 8
+// (or k not derivable from n_keys and n_blocks): the 16-byte keys routed as themselves by the
+// two-pass route (count, scan, scatter) into parts of <= kRouteKeyPartTiles tiles.
 struct MonoPlan {
   uint32_t T, g, q;  // tiles, parts, tiles per part
-  RouteGeom rg;
+  uint32_t k;        // hash count when known (the one-pass route needs 1..8)
+  bool blocks;       // the one-pass route
+  tkv_amq_route_plan rp;
+  RouteGeom rg;      // (the two-pass route)
   uint64_t items_off, part_off;
   PartGeom pg;       // a part of q tiles (every part's own geometry is no larger)
   uint64_t bytes;
 };
-
-// Tiles per routed part (a filter past kDirectMaxTiles): the fewer tiles a partition spreads
-// a batch over, the longer each tile's run per store (fewer partial-line writes), until the
-// route's scatter over that many parts pays more than the part builds save; and at most one
-// tile per CU, so a part's tile kernel runs in one round.  Bit records (k <= 8), 1B keys at 12
-// bits/key on one GPU: 1,431-tile parts 36.7 Gkeys/s, 800 39.2, 400 40.4, 294 39.8, 255 42.6,
-// 229 41.9, 198 41.5, 127 37.1, 100 33.6 (profiles/r04/part_tiles/).  16-byte keys routed as
-// themselves (k > 8) keep 1,600.  (turtle_kv_amd.dist.ROUTED_PART_TILES, ROUTED_KEY_PART_TILES)
-constexpr uint32_t kRoutePartTiles = 256;
-constexpr uint32_t kRouteKeyPartTiles = 1600;
-static_assert(kRoutePartTiles <= kRecPartMaxTiles && kRouteKeyPartTiles <= kRecPartMaxTiles, "");
 
 inline uint32_t bloom_k_of(uint64_t n_keys, uint64_t n_blocks);
 
@@ -4414,6 +4799,7 @@ inline MonoPlan mono_plan(uint64_t n_keys, uint64_t n_blocks)
 {
   MonoPlan m{};
   m.T = filter_tiles(n_blocks);
+  m.k = bloom_k_of(n_keys, n_blocks);  // (0: unknown)
   if (m.T <= kDirectMaxTiles) {
     m.g = 1;
     m.q = m.T;
@@ -4421,8 +4807,16 @@ inline MonoPlan mono_plan(uint64_t n_keys, uint64_t n_blocks)
     m.bytes = m.pg.bytes;
     return m;
   }
-  const uint32_t k = bloom_k_of(n_keys, n_blocks);  // (0: unknown -- any part size is exact)
-  m.g = (uint32_t)div_up(m.T, k >= 1 && k <= 8 ? kRoutePartTiles : kRouteKeyPartTiles);
+  if (m.k >= 1 && m.k <= 8 && route_plan(n_keys, 1, n_blocks, m.k, 1, false, m.rp) == TKV_AMQ_OK) {
+    m.blocks = true;
+    m.g = m.rp.n_parts;
+    m.q = m.rp.part_tiles;
+    m.items_off = align256(m.rp.route_ws_bytes);                  // the block
+    m.part_off = align256(m.items_off + m.rp.block_bytes);        // a part build's workspace
+    m.bytes = m.part_off + m.rp.part_ws_bytes;
+    return m;
+  }
+  m.g = (uint32_t)div_up(m.T, kRouteKeyPartTiles);
   m.q = (uint32_t)div_up(m.T, m.g);
   m.rg = route_geom(n_keys, m.g);
   m.items_off = align256(m.rg.bytes);
@@ -4443,13 +4837,25 @@ inline uint32_t bloom_k_of(uint64_t n_keys, uint64_t n_blocks)
   return 0;
 }
 
-// keys [0, n) of segment 0 (kb 16 or 24); with g > 1 and 24-byte keys k must be <= 8
+// keys [0, n) of segment 0 (kb 16 or 24; routed 24-byte keys need the one-pass route, k <= 8)
 inline void launch_mono(const MonoPlan& m, hipStream_t s, const uint8_t* keys, uint32_t kb, uint32_t n,
                         const tkv_amq_segment* d_segs, uint8_t* ws, uint8_t* d_out)
 {
   if (m.g == 1) {
     const PartArgs a{keys, n, 0u, 1u, kb, nullptr, 0u, ws, m.pg};
     launch_part_build(kb == 24 ? kSrcKey24 : kSrcKey16, a, s, d_segs, d_out, 0u);
+    return;
+  }
+  if (m.blocks) {
+    const tkv_amq_route_plan& rp = m.rp;
+    uint8_t* blk = ws + m.items_off;
+    const PartArgs ra = route_args(rp, keys, kb, n, 1u, blk, ws);
+    launch_route_blocks(ra, rp, s, d_segs, false);
+    for (uint32_t p = 0; p < rp.n_parts; ++p)
+      launch_part_from_blocks(rp, s, blk, 1, d_segs, p, d_out, ws + m.part_off);
+    // the route workgroups' overflow lists (entries: record, part), every part at once
+    hipLaunchKernelGGL(bloom_route_ovf_apply, dim3(rp.route_wgs), dim3(256), 0, s, d_segs, ws + ra.g.ovf_n_off,
+                       4ull, ws + ra.g.ovf_off, 16ull * ra.g.per, ra.g.per, rp.part_tiles, 0u, rp.n_parts, d_out);
     return;
   }
   uint32_t* rws = reinterpret_cast<uint32_t*>(ws);
@@ -4757,8 +5163,11 @@ int tkv_amq_build(int kind, const uint8_t* keys, const uint64_t* offs, uint32_t 
     const bool mono_part = bloom_partitioned(n_segs, max_blocks, n_keys) && d_ws;
     const MonoPlan mp = mono_plan(n_keys, max_blocks);
     const bool mono16 = mono_part && mode == kKey16 && ws_bytes >= mp.bytes;
+    // (routed 24-byte keys travel as bit records only: k must be known -- bloom_k_of 0 means
+    // the plan does not match n_keys -- and at most 8)
+    const uint32_t k_route = bloom_k_of(n_keys, max_blocks);
     const bool mono24 = mono_part && mono_mode == kKey24 && ws_bytes >= mp.bytes &&
-                        (mp.g == 1 || bloom_k_of(n_keys, max_blocks) <= 8);
+                        (mp.g == 1 || (mp.blocks && k_route >= 1 && k_route <= 8));
     if (bloom_window_path(n_segs, max_blocks, mono16 || mono24)) {
       // leaves beyond one CU's LDS: windows of the image, parts of the keys
       const uint32_t W = bloom_window_count(max_blocks), wblk = bloom_window_blocks(max_blocks);
@@ -5154,6 +5563,71 @@ int tkv_amq_bloom_build_range_records(const uint8_t* d_recs12, uint64_t n_recs, 
   const PartArgs a{d_recs12, (uint32_t)n_recs, tile_begin, 0u, 16u, nullptr, 0u, static_cast<uint8_t*>(d_ws), g};
   launch_part_build(kSrcRec12, a, as_stream(stream), d_seg, d_out, 1u);
   return hipGetLastError() == hipSuccess ? TKV_AMQ_OK : TKV_AMQ_INTERNAL;
+}
+
+int tkv_amq_bloom_route_plan(uint64_t chunk_keys, uint32_t n_chunks, uint32_t n_blocks,
+                             uint32_t hash_count, uint32_t world, tkv_amq_route_plan* plan)
+{
+  if (!plan) return TKV_AMQ_INVALID_ARGUMENT;
+  return route_plan(chunk_keys, n_chunks, n_blocks, hash_count, world, true, *plan);
+}
+
+int tkv_amq_bloom_route_blocks(const uint8_t* d_keys, uint32_t key_bytes, uint64_t n_keys,
+                               const tkv_amq_segment* d_seg, const tkv_amq_route_plan* plan,
+                               uint8_t* d_send, void* d_ws, uint64_t ws_bytes, void* stream)
+{
+  if (tkv_amq_device_count() == 0) return TKV_AMQ_UNAVAILABLE;
+  if (!plan || !d_seg || !d_send || (key_bytes != 16 && key_bytes != 24) || n_keys > plan->chunk_keys ||
+      plan->hash_count == 0 || plan->hash_count > 8 || plan->route_wgs == 0 || plan->world == 0)
+    return TKV_AMQ_INVALID_ARGUMENT;
+  const uintptr_t kalign = key_bytes == 16 ? 15 : 7;
+  if (n_keys && (!d_keys || (reinterpret_cast<uintptr_t>(d_keys) & kalign))) return TKV_AMQ_INVALID_ARGUMENT;
+  if (!d_ws || ws_bytes < plan->route_ws_bytes) return TKV_AMQ_INVALID_ARGUMENT;
+  const PartArgs a = route_args(*plan, d_keys, key_bytes, n_keys, 0u, d_send, static_cast<uint8_t*>(d_ws));
+  launch_route_blocks(a, *plan, as_stream(stream), d_seg, true);
+  return hipGetLastError() == hipSuccess ? TKV_AMQ_OK : TKV_AMQ_INTERNAL;
+}
+
+int tkv_amq_bloom_build_part_blocks(const uint8_t* d_recv, uint32_t n_recv, const tkv_amq_segment* d_seg,
+                                    const tkv_amq_route_plan* plan, uint32_t part, uint8_t* d_out,
+                                    void* d_ws, uint64_t ws_bytes, void* stream)
+{
+  if (tkv_amq_device_count() == 0) return TKV_AMQ_UNAVAILABLE;
+  if (!plan || !d_seg || !d_out || !d_recv || n_recv == 0 || n_recv > kMaxSrcSegs || part >= plan->n_parts ||
+      plan->hash_count == 0 || plan->hash_count > 8)
+    return TKV_AMQ_INVALID_ARGUMENT;
+  // the workspace sized for n_recv blocks (every source region full)
+  tkv_amq_route_plan rp = *plan;
+  const PartGeom g = route_part_geom(rp, rp.part_tiles, n_recv);
+  if (!d_ws || ws_bytes < g.bytes) return TKV_AMQ_INVALID_ARGUMENT;
+  const hipStream_t s = as_stream(stream);
+  if (part * rp.part_tiles >= rp.n_tiles) {  // a part past the last tile: the header only
+    hipLaunchKernelGGL(bloom_header_only, dim3(1), dim3(64), 0, s, d_seg, d_out);
+    return hipGetLastError() == hipSuccess ? TKV_AMQ_OK : TKV_AMQ_INTERNAL;
+  }
+  uint8_t* ws = static_cast<uint8_t*>(d_ws);
+  launch_part_from_blocks(rp, s, d_recv, n_recv, d_seg, part, d_out, ws);
+  // the part's overflow entries from every received block
+  hipLaunchKernelGGL(bloom_route_ovf_apply, dim3(n_recv), dim3(256), 0, s, d_seg, d_recv + rp.ovf_n_off,
+                     rp.block_bytes, d_recv + rp.ovf_off, rp.block_bytes, rp.ovf_cap, rp.part_tiles, part,
+                     part + 1, d_out);
+  return hipGetLastError() == hipSuccess ? TKV_AMQ_OK : TKV_AMQ_INTERNAL;
+}
+
+int tkv_amq_bloom_blocks_lost(const uint8_t* d_recv, uint32_t n_recv, const tkv_amq_route_plan* plan,
+                              void* stream)
+{
+  if (tkv_amq_device_count() == 0) return -TKV_AMQ_UNAVAILABLE;
+  if (!plan || (n_recv && !d_recv)) return -TKV_AMQ_INVALID_ARGUMENT;
+  const hipStream_t s = as_stream(stream);
+  std::vector<uint32_t> n(n_recv ? n_recv : 1);
+  if (n_recv && hipMemcpy2DAsync(n.data(), 4, d_recv + plan->ovf_n_off, plan->block_bytes, 4, n_recv,
+                                 hipMemcpyDeviceToHost, s) != hipSuccess)
+    return -TKV_AMQ_INTERNAL;
+  if (hipStreamSynchronize(s) != hipSuccess) return -TKV_AMQ_INTERNAL;
+  for (uint32_t i = 0; i < n_recv; ++i)
+    if (n[i] > plan->ovf_cap) return 1;
+  return 0;
 }
 
 uint64_t tkv_amq_bloom_build_range_ws_bytes(uint64_t n_keys, uint32_t tile_begin, uint32_t tile_end)

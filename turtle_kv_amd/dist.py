@@ -221,11 +221,14 @@ def hash_shard_tiles(n_blocks: int, world: int) -> tuple[int, int]:
     return T, -(-T // world)
 
 
-class HashShardedBloom:
+class ExactHashShardedBloom:
     """One rank's side of a hash-range sharded build of one Bloom filter over the keys of all
-    ranks (n_total_keys in all).  `build(keys)` returns the whole filter payload (header +
-    bitmap, byte-identical to a one-GPU tkv_amq_build of the concatenated keys) on every rank.
-    Buffers are allocated once and grown when a rank receives more keys than before."""
+    ranks (n_total_keys in all), with an exchange sized by exact counts (two host
+    synchronisations per build) and contiguous tile ranges per rank.  `build(keys)` returns the
+    whole filter payload (header + bitmap, byte-identical to a one-GPU tkv_amq_build of the
+    concatenated keys) on every rank.  HashShardedBloom uses it for k > 8 (16-byte keys travel)
+    and when a pipelined step lost overflow entries (keys far from uniform).  Buffers are
+    allocated once and grown when a rank receives more keys than before."""
 
     def __init__(self, n_total_keys: int, bits_per_key: int, world: int, rank: int, device,
                  src_page_id: int = 0, group=None):
@@ -437,3 +440,250 @@ class HashShardedBloom:
     def build(self, keys):
         self.local_build(keys)
         return self.allgather()
+
+
+class HashShardedBloom:
+    """One rank's side of the pipelined hash-range sharded build of one Bloom filter over the
+    keys of all ranks (n_total_keys in all; BASELINE config 5).  Per step (`step`):
+
+      route     the rank's keys in `chunks` chunks (tkv_amq_bloom_route_blocks): every key
+                hashed once into its 12-byte bit record, counting-sorted by part on chip and
+                appended to fixed-capacity regions of the part owner's block;
+      exchange  chunk c's blocks in one all-to-all of equal splits (RCCL over xGMI) on the
+                communication stream while chunk c + 1 routes -- no counts exchanged first, no
+                host synchronisation;
+      build     each owned part from the chunks x ranks blocks received, in place
+                (tkv_amq_bloom_build_part_blocks: no regrouping copy);
+      gather    round j (part j of every rank: one contiguous byte range, parts being owned
+                round-robin) all-gathered in place on the communication stream as soon as this
+                rank's part j is built, while part j + 1 builds.
+
+    `build(keys)` returns the whole filter payload (header + bitmap), byte-identical to a one-GPU
+    tkv_amq_build of the concatenated keys, on every rank.  Without a process group (one GPU)
+    the route's blocks are the part builds' input directly.  k > 8 (bits_per_key >= 13) and a
+    step whose blocks lost overflow entries (`lost()`; keys far from uniform, e.g. one key
+    repeated) go through ExactHashShardedBloom."""
+
+    def __init__(self, n_total_keys: int, bits_per_key: int, world: int, rank: int, device,
+                 src_page_id: int = 0, group=None, chunks: int = 1, max_keys_per_rank=None):
+        import ctypes
+
+        import torch
+        from . import abi
+        from .filters import plan_filters
+        self.world, self.rank, self.group, self.dev = world, rank, group, torch.device(device)
+        self.n_total_keys, self.bpk, self.src_page_id = n_total_keys, bits_per_key, src_page_id
+        self.plan = plan_filters(abi.BLOOM, [n_total_keys], bits_per_key, src_page_ids=[src_page_id])
+        seg = self.plan.segs[0]
+        self.n_blocks = int(seg["n_blocks"])
+        self.payload_bytes = int(seg["payload_bytes"])
+        self.hash_count = int(seg["hash_count"])
+        self.records = self.hash_count <= 8
+        self.unit = 12 if self.records else 16
+        self._exact = None
+        if not self.records:
+            self._exact = ExactHashShardedBloom(n_total_keys, bits_per_key, world, rank, device,
+                                                src_page_id, group)
+            self.T, self.g, self.q = self._exact.T, self._exact.g, self._exact.q
+            return
+        self.chunks = max(1, int(chunks))
+        per_rank = int(max_keys_per_rank) if max_keys_per_rank else -(-n_total_keys // world)
+        self.chunk_keys = max(1, -(-per_rank // self.chunks))
+        rp = abi.RoutePlan()
+        L = abi.lib()
+        abi.check(L.tkv_amq_bloom_route_plan(self.chunk_keys, self.chunks, self.n_blocks,
+                                             self.hash_count, world, ctypes.byref(rp)),
+                  "tkv_amq_bloom_route_plan")
+        self.rp = rp
+        self.T, self.g, self.q = int(rp.n_tiles), int(rp.parts_per_rank), int(rp.part_tiles)
+        self.n_parts = int(rp.n_parts)
+        self.block_bytes = int(rp.block_bytes)
+        self.part_bytes = int(rp.part_bytes)
+        self.round_bytes = world * self.part_bytes
+        # the filter payload, padded to whole rounds: part p's bitmap at 64 + p * part_bytes
+        self.out = torch.zeros(64 + self.n_parts * self.part_bytes, dtype=torch.uint8, device=self.dev)
+        S = self.chunks * world
+        self.recv = torch.empty(S * self.block_bytes, dtype=torch.uint8, device=self.dev)
+        # chunk c's send blocks (one per destination); one rank routes straight into recv
+        self.send = ([self.recv[c * self.block_bytes:(c + 1) * self.block_bytes] for c in range(self.chunks)]
+                     if world == 1 else
+                     [torch.empty(world * self.block_bytes, dtype=torch.uint8, device=self.dev)
+                      for _ in range(self.chunks)])
+        self.route_ws = torch.empty(int(rp.route_ws_bytes), dtype=torch.uint8, device=self.dev)
+        self.part_ws = torch.empty(int(rp.part_ws_bytes), dtype=torch.uint8, device=self.dev)
+        self.d_seg = self.plan.device_segs(self.dev)
+        self.comm = torch.cuda.Stream(device=self.dev) if self.dev.type == "cuda" else None
+        self.last_lost = None
+
+    # ---- ownership ------------------------------------------------------------------------
+    def owned_parts(self) -> list[int]:
+        """Global indices of this rank's parts (round-robin: part j * world + rank)."""
+        return [j * self.world + self.rank for j in range(self.g)]
+
+    def part_tiles(self, p: int) -> tuple[int, int]:
+        b = min(self.T, p * self.q)
+        return b, min(self.T, b + self.q)
+
+    @property
+    def _collective(self) -> bool:
+        import torch.distributed as dist
+        return self.world > 1 or (dist.is_available() and dist.is_initialized())
+
+    @property
+    def _gloo(self) -> bool:
+        import torch.distributed as dist
+        return dist.get_backend(self.group) != "nccl"
+
+    # ---- the stages -----------------------------------------------------------------------
+    def route_chunk(self, keys, c: int):
+        """Chunk c of this rank's keys ([n, 16] or [n, 24] uint8 on the device) into send[c]."""
+        import ctypes
+
+        from . import abi
+        from .filters import _ptr, _stream_handle
+        kb = keys.shape[1] if keys.dim() == 2 else 0
+        if kb not in (16, 24):
+            raise abi.TkvAmqError(abi.INVALID_ARGUMENT, "hash-range sharding takes [n, 16] or "
+                                  f"[n, 24] uint8 keys, got shape {tuple(keys.shape)}")
+        ck = self.chunk_keys
+        part = keys[c * ck:(c + 1) * ck]
+        n = part.shape[0]
+        L = abi.lib()
+        abi.check(L.tkv_amq_bloom_route_blocks(_ptr(part) if n else None, kb, n, _ptr(self.d_seg),
+                                               ctypes.byref(self.rp), _ptr(self.send[c]),
+                                               _ptr(self.route_ws), self.route_ws.numel(),
+                                               _stream_handle()), "tkv_amq_bloom_route_blocks")
+
+    def exchange_chunk(self, c: int):
+        """All-to-all of chunk c's blocks (equal splits of block_bytes), on the current stream."""
+        import torch
+        import torch.distributed as dist
+        if self.world == 1:
+            return  # routed straight into recv
+        B, W = self.block_bytes, self.world
+        dst = self.recv[c * W * B:(c + 1) * W * B]
+        if self._gloo:  # CPU rehearsal: stage through host memory
+            host = torch.empty(W * B, dtype=torch.uint8)
+            dist.all_to_all_single(host, self.send[c].cpu(), group=self.group)
+            dst.copy_(host)
+        else:
+            dist.all_to_all_single(dst, self.send[c], group=self.group)
+
+    def build_part(self, j: int):
+        """This rank's j-th part (global part j * world + rank) from every received block."""
+        import ctypes
+
+        from . import abi
+        from .filters import _ptr, _stream_handle
+        L = abi.lib()
+        S = self.chunks * self.world
+        abi.check(L.tkv_amq_bloom_build_part_blocks(_ptr(self.recv), S, _ptr(self.d_seg),
+                                                    ctypes.byref(self.rp), j * self.world + self.rank,
+                                                    _ptr(self.out), _ptr(self.part_ws),
+                                                    self.part_ws.numel(), _stream_handle()),
+                  "tkv_amq_bloom_build_part_blocks")
+
+    def gather_round(self, j: int):
+        """Round j (part j of every rank, contiguous) all-gathered in place."""
+        import torch
+        import torch.distributed as dist
+        R = self.round_bytes
+        rnd = self.out[64 + j * R:64 + (j + 1) * R]
+        mine = rnd[self.rank * self.part_bytes:(self.rank + 1) * self.part_bytes]
+        if self._gloo:
+            host = torch.empty(R, dtype=torch.uint8)
+            dist.all_gather_into_tensor(host, mine.cpu(), group=self.group)
+            rnd.copy_(host)
+        else:
+            dist.all_gather_into_tensor(rnd, mine, group=self.group)
+
+    # ---- the step -------------------------------------------------------------------------
+    def step(self, keys, gather: bool = True):
+        """route -> exchange -> part builds (-> gathers), pipelined over two streams; on return
+        the current stream is ordered after all of it (this rank's parts final, and with
+        gather every part on every rank)."""
+        import torch
+        if self._exact is not None:
+            self._exact.local_build(keys)
+            if gather:
+                self._exact_out = self._exact.allgather()
+            return
+        coll = self._collective and self.comm is not None
+        cur = torch.cuda.current_stream(self.dev)
+        if coll:
+            self.comm.wait_stream(cur)  # the previous step's readers are done
+        for c in range(self.chunks):
+            self.route_chunk(keys, c)
+            if coll and self.world > 1:
+                ev = torch.cuda.Event()
+                ev.record(cur)
+                with torch.cuda.stream(self.comm):
+                    self.comm.wait_event(ev)
+                    self.exchange_chunk(c)
+        if coll and self.world > 1:
+            cur.wait_stream(self.comm)
+        for j in range(self.g):
+            self.build_part(j)
+            if coll and gather:
+                ev = torch.cuda.Event()
+                ev.record(cur)
+                with torch.cuda.stream(self.comm):
+                    self.comm.wait_event(ev)
+                    self.gather_round(j)
+        if coll:
+            cur.wait_stream(self.comm)
+
+    def local_build(self, keys):
+        """route + exchange + part builds: this rank's parts of the bitmap are final."""
+        self.step(keys, gather=False)
+
+    def allgather(self):
+        """Every round all-gathered (after local_build) -> the whole payload on every rank."""
+        import torch
+        if self._exact is not None:
+            return self._exact.allgather()
+        if self._collective:
+            for j in range(self.g):
+                self.gather_round(j)
+        return self.filter()
+
+    def filter(self):
+        """The filter payload (header + bitmap) of the last step."""
+        if self._exact is not None:
+            return getattr(self, "_exact_out", None)
+        return self.out[:self.payload_bytes]
+
+    def lost(self) -> bool:
+        """Did any block of the last exchange lose overflow entries (synchronises)?"""
+        import ctypes
+
+        from . import abi
+        from .filters import _ptr, _stream_handle
+        if self._exact is not None:
+            return False
+        r = abi.lib().tkv_amq_bloom_blocks_lost(_ptr(self.recv), self.chunks * self.world,
+                                                ctypes.byref(self.rp), _stream_handle())
+        if r < 0:
+            raise abi.TkvAmqError(-r, "tkv_amq_bloom_blocks_lost")
+        self.last_lost = bool(r)
+        return self.last_lost
+
+    def build(self, keys):
+        """The whole filter on every rank; a step that lost overflow entries (decided together
+        by every rank) is rebuilt through the exact exchange."""
+        import torch
+        import torch.distributed as dist
+        self.step(keys, gather=True)
+        if self._exact is not None:
+            return self._exact_out
+        lost = self.lost()
+        if self._collective:
+            flag = torch.tensor([1 if lost else 0], dtype=torch.int32,
+                                device="cpu" if self._gloo else self.dev)
+            dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=self.group)
+            lost = bool(flag.item())
+        if lost:
+            ex = ExactHashShardedBloom(self.n_total_keys, self.bpk, self.world, self.rank, self.dev,
+                                       self.src_page_id, self.group)
+            return ex.build(keys)
+        return self.filter()
