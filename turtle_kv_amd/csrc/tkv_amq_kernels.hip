@@ -1012,7 +1012,8 @@ constexpr uint32_t kMaxSrcSegs = 256;
 // parts, the wave sums and the overflow counter
 __host__ __device__ constexpr inline uint32_t route_lds_bytes(uint32_t n_parts)
 {
-  return kPartPlaneBytes + 2u * kPartBatch + 20u * ((n_parts + 1) / 2) + 4u * (kPartThreads / 64 + 1);
+  return kPartPlaneBytes + 2u * kPartBatch + 20u * ((n_parts + 1) / 2) + 4u * (kPartThreads / 64 + 1) +
+         8u + 12u * n_parts;  // + the per-part store pointers and limits of the batch
 }
 static_assert(route_lds_bytes(kRouteMaxParts) <= 160 * 1024, "one route workgroup per CU");
 
@@ -1510,6 +1511,11 @@ __device__ void part_body(const tkv_amq_segment& sg, const PartArgs& a, uint32_t
   uint32_t* wsum = cursor + 2 * HW;  // 16 wave sums
   uint32_t* ovf_n = wsum + NT / 64;
   uint32_t* pre = ovf_n + 1;         // kSrcSeg12: the item prefix over the source blocks
+  // ROUTE: per part, for the batch in the planes: where its run's record j goes (a.dst + roff +
+  // 12 j) and the first j past its region (rlim), so a record's store address is one table read
+  // (index arithmetic on lds, not an integer round trip: the pointer must stay an LDS pointer)
+  uint64_t* roff = reinterpret_cast<uint64_t*>(lds + ((uint32_t)(ovf_n - lds) + 2u & ~1u));
+  int32_t* rlim = reinterpret_cast<int32_t*>(roff + T);
   for (uint32_t i = tid; i < 2 * HW; i += NT) {
     H0[i] = 0;  // (H0 and H1)
     cursor[i] = 0;
@@ -1596,17 +1602,24 @@ __device__ void part_body(const tkv_amq_segment& sg, const PartArgs& a, uint32_t
         t = rec_tile(x0, x1, x2);
       }
       t = v ? t : 0u;
-      const uint32_t c = cursor[t] + (j - lds_u16(start, t));
       uint8_t* d = a.ws;  // the sink
       bool ovf = false;
       if (v) {
-        if (c < cap) {
+        bool in_region;
+        if constexpr (ROUTE) {
+          in_region = (int32_t)j < rlim[t];
+        } else {
+          const uint32_t c = cursor[t] + (j - lds_u16(start, t));
+          in_region = c < cap;
+          d = a.ws + a.g.regions_off + ((uint64_t)t * P + w) * cap * a.g.rb + (uint64_t)c * RB;
+        }
+        if (in_region) {
+          // (relative to a.dst, so the store stays a global store, not a flat one; the asm
+          // keeps the compiler from hoisting a.dst + 12 j for every u into spilled registers)
           if constexpr (ROUTE) {
-            const uint32_t jl = div_by_magic(t, a.w_magic), dr = t - jl * a.world;
-            d = a.dst + (uint64_t)dr * a.blk.bytes + a.blk.regions_off +
-                (((uint64_t)jl * P + w) * cap + c) * 12ull;
-          } else {
-            d = a.ws + a.g.regions_off + ((uint64_t)t * P + w) * cap * a.g.rb + (uint64_t)c * RB;
+            uint32_t jj = j;
+            asm volatile("" : "+v"(jj));
+            d = a.dst + (roff[t] + 12u * jj);
           }
         } else {
           ovf = true;  // LDS atomic: this workgroup's list
@@ -1684,6 +1697,16 @@ __device__ void part_body(const tkv_amq_segment& sg, const PartArgs& a, uint32_t
       in[u] = load_in(min(b0 + B + u * NT + tid, last_item));
     lds_barrier();
     total = part_scan(hist, prev, start, cursor, HW, wsum);
+    if constexpr (ROUTE) {
+      // this batch's store table (read by its write-out, after the barrier below)
+      for (uint32_t t = tid; t < T; t += NT) {
+        const uint32_t st = lds_u16(start, t), cu = cursor[t];
+        const uint32_t jl = div_by_magic(t, a.w_magic), dr = t - jl * a.world;
+        const uint64_t base = (uint64_t)dr * a.blk.bytes + a.blk.regions_off + ((uint64_t)jl * P + w) * cap * 12ull;
+        roff[t] = base + 12ull * cu - 12ull * st;
+        rlim[t] = (int32_t)(cap + st) - (int32_t)cu;
+      }
+    }
 #pragma unroll
     for (uint32_t u = 0; u < U; ++u) {
       if (tr[u] == ~0u) continue;
@@ -1763,21 +1786,18 @@ __global__ __launch_bounds__(kPartThreads) void bloom_part_routed(const tkv_amq_
 // destination block (part p -> rank p % world), whole runs per store; records beyond a region's
 // capacity go to this workgroup's overflow list as (record, part).  No count pass: the regions
 // have a fixed capacity.
-__global__ __launch_bounds__(kPartThreads) void bloom_route_part(const tkv_amq_segment* __restrict__ segs,
-                                                                 PartArgs a)
+// (one 1024-thread workgroup per CU -- its LDS -- so four waves per SIMD: the compiler may take
+// 128 VGPRs instead of assuming two workgroups per CU and spilling at 64).  One kernel per
+// (k, key bytes) variant, chosen on the host, so each gets its own register allocation.
+template <int K, int KB>
+__global__ __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_eu(4, 4))) void bloom_route_part(
+    const tkv_amq_segment* __restrict__ segs, PartArgs a)
 {
   extern __shared__ __attribute__((aligned(16))) uint32_t s_part[];
   const tkv_amq_segment sg = segs[0];
   const uint32_t k = sg.hash_count;
-  if (k == 0 || k > 8) return;  // (the host routes bit records for k <= 8 only)
-  if (a.kb == 24) {
-    if (k == 8) part_body<8, kSrcKey24, kDstParts>(sg, a, s_part);
-    else part_body<0, kSrcKey24, kDstParts>(sg, a, s_part);
-  } else {
-    if (k == 8) part_body<8, kSrcKey16, kDstParts>(sg, a, s_part);
-    else if (k == 7) part_body<7, kSrcKey16, kDstParts>(sg, a, s_part);
-    else part_body<0, kSrcKey16, kDstParts>(sg, a, s_part);
-  }
+  if (k == 0 || k > 8 || (K != 0 && k != (uint32_t)K)) return;  // (the host passes the plan's k)
+  part_body<K, KB == 24 ? kSrcKey24 : kSrcKey16, kDstParts>(sg, a, s_part);
 }
 
 // a part's partition from the route blocks that hold it (kSrcSeg12): workgroup w reads region
@@ -4706,8 +4726,12 @@ inline void set_route_attributes()
 {
   static std::once_flag attr[kMaxDevices];
   once_per_device(attr, [] {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&bloom_route_part),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)route_lds_bytes(kRouteMaxParts));
+    for (const void* f : {reinterpret_cast<const void*>(&bloom_route_part<8, 16>),
+                          reinterpret_cast<const void*>(&bloom_route_part<7, 16>),
+                          reinterpret_cast<const void*>(&bloom_route_part<0, 16>),
+                          reinterpret_cast<const void*>(&bloom_route_part<8, 24>),
+                          reinterpret_cast<const void*>(&bloom_route_part<0, 24>)})
+      (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)route_lds_bytes(kRouteMaxParts));
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&bloom_part_segs),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)part_lds_bytes(kDirectMaxTiles));
   });
@@ -4744,8 +4768,13 @@ inline void launch_route_blocks(const PartArgs& a, const tkv_amq_route_plan& rp,
                                 const tkv_amq_segment* d_seg, bool pack)
 {
   set_route_attributes();
-  hipLaunchKernelGGL(bloom_route_part, dim3(rp.route_wgs), dim3(kPartThreads), route_lds_bytes(rp.n_parts), s,
-                     d_seg, a);
+  const dim3 g(rp.route_wgs), b(kPartThreads);
+  const size_t lds = route_lds_bytes(rp.n_parts);
+  if (a.kb == 24 && rp.hash_count == 8) hipLaunchKernelGGL((bloom_route_part<8, 24>), g, b, lds, s, d_seg, a);
+  else if (a.kb == 24) hipLaunchKernelGGL((bloom_route_part<0, 24>), g, b, lds, s, d_seg, a);
+  else if (rp.hash_count == 8) hipLaunchKernelGGL((bloom_route_part<8, 16>), g, b, lds, s, d_seg, a);
+  else if (rp.hash_count == 7) hipLaunchKernelGGL((bloom_route_part<7, 16>), g, b, lds, s, d_seg, a);
+  else hipLaunchKernelGGL((bloom_route_part<0, 16>), g, b, lds, s, d_seg, a);
   if (pack) hipLaunchKernelGGL(bloom_route_ovf_pack, dim3(rp.route_wgs), dim3(256), 0, s, a);
 }
 
