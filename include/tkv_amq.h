@@ -179,6 +179,18 @@ int tkv_amq_build(int kind, const uint8_t* keys, const uint64_t* key_offsets,
                   uint32_t n_segs, uint32_t max_seg_blocks, uint8_t* d_out,
                   void* d_workspace, uint64_t workspace_bytes, void* stream);
 
+/* tkv_amq_build with the host copy of the plan's segments (h_segs: the n_segs entries
+ * tkv_amq_plan filled; d_segs is their device copy).  With it a Bloom batch whose leaves include
+ * some of more than 16 LDS windows (images past 2.5 MB; tree/tree_options.hpp:177-215 sizes any
+ * leaf) builds the other leaves through the batch kernels and each oversize leaf through the
+ * tiled monolithic build of its own (16- and 24-byte keys; other key shapes set that leaf's bits
+ * with device atomics), instead of device atomics for the whole batch.  The workspace
+ * tkv_amq_plan sizes covers it.  h_segs == NULL, or any other batch: exactly tkv_amq_build. */
+int tkv_amq_build_ex(int kind, const uint8_t* keys, const uint64_t* key_offsets, uint32_t key_stride,
+                     uint64_t n_keys, const tkv_amq_segment* d_segs, const tkv_amq_segment* h_segs,
+                     uint32_t n_segs, uint32_t max_blocks, uint8_t* d_out, void* d_workspace,
+                     uint64_t workspace_bytes, void* stream);
+
 /* Synchronises `stream`; returns TKV_AMQ_OK, TKV_AMQ_INTERNAL (a VQF block overflowed) or
  * TKV_AMQ_INVALID_ARGUMENT (the workspace was smaller than the plan).  Bloom builds cannot
  * fail on the device. */

@@ -687,12 +687,39 @@ def test_bloom_big_leaves_in_lds(oracle, amq, torch, shape):
 def test_bloom_oversize_leaf_in_batch(oracle, amq, torch, big):
     """A multi-leaf batch holding a leaf beyond the LDS budget: a 175 KB image takes the
     window path (partial images in the workspace, merged); a 3.75 MB one (24 windows, more
-    than the window path's 16) the device-atomic path, with no workspace."""
+    than the window path's 16) the tiled monolithic build of its own (tkv_amq_build_ex), the
+    other leaves the batch kernels from a compacted leaf list."""
     counts = [big, 500, 16384]
     keys = oracle.gen_keys16(15, 0, sum(counts))
     ref = oracle_per_segment(oracle, 0, keys, counts, 10)
     plan, out = gpu_build(amq, torch, 0, torch.from_numpy(keys).cuda(), counts, 10)
-    assert (plan.workspace_bytes == 0) == (big > 1_000_000)
+    assert plan.workspace_bytes > 0
+    assert_same(plan, out, ref)
+
+
+@pytest.mark.parametrize("shape", ["k16", "k24", "var"])
+def test_bloom_oversize_leaves_among_many(oracle, amq, torch, shape):
+    """Several oversize leaves (past 16 windows) at the start, middle and end of a batch of
+    small and window-sized leaves, 16- and 24-byte keys (the monolithic build, one leaf at a
+    time) and variable-length keys (those leaves with device atomics, the rest batched)."""
+    rng = np.random.default_rng(3)
+    counts = [2_600_000] + [int(c) for c in rng.integers(0, 20000, 70)] + [3_100_000, 150_000] + \
+             [int(c) for c in rng.integers(0, 3000, 30)] + [2_300_001]
+    n = sum(counts)
+    offs = None
+    if shape == "k16":
+        keys, stride = oracle.gen_keys16(41, 0, n), 16
+    elif shape == "k24":
+        keys, stride = rng.integers(0, 256, (n, 24), dtype=np.uint8), 24
+    else:
+        lens = rng.integers(8, 32, n)
+        keys, stride = rng.integers(0, 256, int(lens.sum()), dtype=np.uint8), 0
+        offs = np.zeros(n + 1, np.int64)
+        offs[1:] = np.cumsum(lens)
+    ref = oracle_per_segment(oracle, 0, keys, counts, 10, stride=stride,
+                             offsets=None if offs is None else offs.astype(np.uint64))
+    plan, out = gpu_build(amq, torch, 0, torch.from_numpy(keys).cuda(), counts, 10,
+                          offsets_t=None if offs is None else torch.from_numpy(offs).cuda())
     assert_same(plan, out, ref)
 
 

@@ -90,7 +90,7 @@ EXPORTS = [
     "tkv_amq_bloom_build_range_records_ws_bytes", "tkv_amq_bloom_build_range_records",
     "tkv_amq_bloom_route_records_ex", "tkv_amq_bloom_tile_blocks", "tkv_amq_bloom_range_max_tiles",
     "tkv_amq_bloom_route_plan", "tkv_amq_bloom_route_blocks", "tkv_amq_bloom_build_part_blocks",
-    "tkv_amq_bloom_blocks_lost",
+    "tkv_amq_bloom_blocks_lost", "tkv_amq_build_ex",
 ]
 
 
@@ -157,6 +157,9 @@ def lib(build_if_missing: bool = True):
                                ctypes.POINTER(u64), ctypes.POINTER(u64), ctypes.POINTER(u32)]
     L.tkv_amq_build.restype = i32
     L.tkv_amq_build.argtypes = [i32, vp, vp, u32, u64, vp, u32, u32, vp, vp, u64, vp]
+    if hasattr(L, "tkv_amq_build_ex"):
+        L.tkv_amq_build_ex.restype = i32
+        L.tkv_amq_build_ex.argtypes = [i32, vp, vp, u32, u64, vp, vp, u32, u32, vp, vp, u64, vp]
     L.tkv_amq_build_check.restype = i32
     L.tkv_amq_build_check.argtypes = [i32, vp, u64, vp]
     L.tkv_amq_probe.restype = i32

@@ -924,13 +924,15 @@ __global__ __launch_bounds__(256) void bloom_global_set(const uint8_t* __restric
                                                         uint32_t stride,
                                                         const tkv_amq_segment* __restrict__ segs,
                                                         uint32_t n_segs, uint64_t n_keys,
-                                                        uint8_t* __restrict__ out)
+                                                        uint8_t* __restrict__ out, uint64_t first = 0)
 {
-  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n_keys;
+  for (uint64_t i = first + (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n_keys;
        i += (uint64_t)gridDim.x * 256) {
     const uint32_t s = find_segment(segs, n_segs, i);
     const tkv_amq_segment& sg = segs[s];
-    if (sg.hash_count == 0 || i >= sg.key_begin + sg.n_keys) continue;
+    // (a leaf list need not cover every key: tkv_amq_build_ex hands the batch kernels the
+    // leaves other than the oversize ones)
+    if (sg.hash_count == 0 || i < sg.key_begin || i >= sg.key_begin + sg.n_keys) continue;
     uint32_t* words = reinterpret_cast<uint32_t*>(out + sg.out_offset + kBloomHeader);
     uint64_t h0;
     if constexpr (MODE == kKey16) {
@@ -1025,6 +1027,15 @@ __host__ __device__ constexpr inline uint32_t part_lds_bytes(uint32_t n_tiles)
          4u * (kMaxSrcSegs + 2);
 }
 static_assert(part_lds_bytes(kDirectMaxTiles) <= 160 * 1024, "one workgroup per CU");
+// a partition with the store table (12 bytes per tile beside the rest) when it fits the CU's LDS
+__host__ __device__ constexpr inline uint32_t part_tbl_lds_bytes(uint32_t n_tiles)
+{
+  return part_lds_bytes(n_tiles) + 8u + 12u * n_tiles;
+}
+__host__ __device__ constexpr inline bool part_tbl_fits(uint32_t n_tiles)
+{
+  return part_tbl_lds_bytes(n_tiles) <= 160u * 1024u;
+}
 static_assert(kRecPartMaxTiles <= 8192, "a record's 13-bit tile field");
 static_assert(kPartBatch < 65536, "u16 ranks");
 
@@ -1400,6 +1411,9 @@ struct PartArgs {
   // part's index jl inside each
   uint32_t n_src_segs;
   uint32_t seg_part;
+  // a partition (kDstTiles) with the per-tile store table: part_tbl_fits(n_tiles), and the
+  // launch's LDS is part_tbl_lds_bytes
+  uint32_t tbl;
 };
 
 __host__ __device__ inline uint64_t div_magic(uint32_t d) { return (0x100000000ull / d) + 1; }
@@ -1487,11 +1501,12 @@ __device__ inline uint32_t lds_u16(const uint32_t* words, uint32_t t)
 // lanes without a record store to a sink in the workspace header).  Overflow entries are the
 // records themselves (their tile is in the record: T <= kDirectMaxTiles < 2^13), RAW the
 // 16-byte keys, kDstParts the record and its part (16 bytes).
-template <int K, int SRC, int DST = kDstTiles>
+template <int K, int SRC, int DST = kDstTiles, bool TBL = DST == kDstParts>
 __device__ void part_body(const tkv_amq_segment& sg, const PartArgs& a, uint32_t* lds)
 {
   constexpr bool RAW = SRC == kSrcRaw16;
   constexpr bool ROUTE = DST == kDstParts;
+  static_assert(TBL || !ROUTE, "the route stores through its table");
   constexpr bool ROUTED = SRC == kSrcRec12 || SRC == kSrcSeg12;  // records with their tile in part
   static_assert(!(ROUTE && (RAW || ROUTED)), "the route hashes keys");
   // 16-byte records: four key words and the tile per item in LDS, half the items per batch
@@ -1511,11 +1526,14 @@ __device__ void part_body(const tkv_amq_segment& sg, const PartArgs& a, uint32_t
   uint32_t* wsum = cursor + 2 * HW;  // 16 wave sums
   uint32_t* ovf_n = wsum + NT / 64;
   uint32_t* pre = ovf_n + 1;         // kSrcSeg12: the item prefix over the source blocks
-  // ROUTE: per part, for the batch in the planes: where its run's record j goes (a.dst + roff +
-  // 12 j) and the first j past its region (rlim), so a record's store address is one table read
+  // TBL: per bucket, for the batch in the planes: where its run's record j goes (the region
+  // base + roff + RB j) and the first j past its region (rlim), so a record's store address is
+  // one table read (the route always; a partition whose tiles leave room: part_tbl_fits).
   // (index arithmetic on lds, not an integer round trip: the pointer must stay an LDS pointer)
-  uint64_t* roff = reinterpret_cast<uint64_t*>(lds + ((uint32_t)(ovf_n - lds) + 2u & ~1u));
+  uint64_t* roff = reinterpret_cast<uint64_t*>(
+      lds + ((uint32_t)(ovf_n - lds) + (ROUTE ? 0u : kMaxSrcSegs + 2u) + 2u & ~1u));
   int32_t* rlim = reinterpret_cast<int32_t*>(roff + T);
+  uint8_t* const rbase = ROUTE ? a.dst : a.ws;  // what roff is relative to
   for (uint32_t i = tid; i < 2 * HW; i += NT) {
     H0[i] = 0;  // (H0 and H1)
     cursor[i] = 0;
@@ -1606,7 +1624,7 @@ __device__ void part_body(const tkv_amq_segment& sg, const PartArgs& a, uint32_t
       bool ovf = false;
       if (v) {
         bool in_region;
-        if constexpr (ROUTE) {
+        if constexpr (TBL) {
           in_region = (int32_t)j < rlim[t];
         } else {
           const uint32_t c = cursor[t] + (j - lds_u16(start, t));
@@ -1614,12 +1632,13 @@ __device__ void part_body(const tkv_amq_segment& sg, const PartArgs& a, uint32_t
           d = a.ws + a.g.regions_off + ((uint64_t)t * P + w) * cap * a.g.rb + (uint64_t)c * RB;
         }
         if (in_region) {
-          // (relative to a.dst, so the store stays a global store, not a flat one; the asm
-          // keeps the compiler from hoisting a.dst + 12 j for every u into spilled registers)
-          if constexpr (ROUTE) {
+          // (relative to a kernel-argument pointer, so the store stays a global store, not a
+          // flat one; the asm keeps the compiler from hoisting base + RB j for every u into
+          // spilled registers)
+          if constexpr (TBL) {
             uint32_t jj = j;
             asm volatile("" : "+v"(jj));
-            d = a.dst + (roff[t] + 12u * jj);
+            d = rbase + (roff[t] + RB * jj);
           }
         } else {
           ovf = true;  // LDS atomic: this workgroup's list
@@ -1697,13 +1716,18 @@ __device__ void part_body(const tkv_amq_segment& sg, const PartArgs& a, uint32_t
       in[u] = load_in(min(b0 + B + u * NT + tid, last_item));
     lds_barrier();
     total = part_scan(hist, prev, start, cursor, HW, wsum);
-    if constexpr (ROUTE) {
+    if constexpr (TBL) {
       // this batch's store table (read by its write-out, after the barrier below)
       for (uint32_t t = tid; t < T; t += NT) {
         const uint32_t st = lds_u16(start, t), cu = cursor[t];
-        const uint32_t jl = div_by_magic(t, a.w_magic), dr = t - jl * a.world;
-        const uint64_t base = (uint64_t)dr * a.blk.bytes + a.blk.regions_off + ((uint64_t)jl * P + w) * cap * 12ull;
-        roff[t] = base + 12ull * cu - 12ull * st;
+        uint64_t base;
+        if constexpr (ROUTE) {
+          const uint32_t jl = div_by_magic(t, a.w_magic), dr = t - jl * a.world;
+          base = (uint64_t)dr * a.blk.bytes + a.blk.regions_off + ((uint64_t)jl * P + w) * cap * 12ull;
+        } else {
+          base = a.g.regions_off + ((uint64_t)t * P + w) * cap * a.g.rb;
+        }
+        roff[t] = base + (uint64_t)RB * cu - (uint64_t)RB * st;
         rlim[t] = (int32_t)(cap + st) - (int32_t)cu;
       }
     }
@@ -1749,7 +1773,9 @@ __global__ __launch_bounds__(kPartThreads) void bloom_part_keys16(const tkv_amq_
   const tkv_amq_segment sg = segs[0];
   const uint32_t k = sg.hash_count;
   if (k == 0) return;
-  if (k == 7) part_body<7, kSrcKey16>(sg, a, s_part);
+  if (k == 7 && a.tbl) part_body<7, kSrcKey16, kDstTiles, true>(sg, a, s_part);
+  else if (k == 7) part_body<7, kSrcKey16>(sg, a, s_part);
+  else if (k == 8 && a.tbl) part_body<8, kSrcKey16, kDstTiles, true>(sg, a, s_part);
   else if (k == 8) part_body<8, kSrcKey16>(sg, a, s_part);
   else if (k < 8) part_body<0, kSrcKey16>(sg, a, s_part);
   else part_body<0, kSrcRaw16>(sg, a, s_part);
@@ -1764,7 +1790,7 @@ __global__ __launch_bounds__(kPartThreads) void bloom_part_keys24(const tkv_amq_
   const tkv_amq_segment sg = segs[0];
   const uint32_t k = sg.hash_count;
   if (k == 0) return;
-  if (k == 7) part_body<7, kSrcKey24>(sg, a, s_part);
+  if (k == 7) part_body<7, kSrcKey24>(sg, a, s_part);  // (the table variant spills here)
   else if (k == 8) part_body<8, kSrcKey24>(sg, a, s_part);
   else part_body<0, kSrcKey24>(sg, a, s_part);
 }
@@ -1808,7 +1834,8 @@ __global__ __launch_bounds__(kPartThreads) void bloom_part_segs(const tkv_amq_se
   extern __shared__ __attribute__((aligned(16))) uint32_t s_part[];
   const tkv_amq_segment sg = segs[0];
   if (sg.hash_count == 0 || sg.hash_count > 8) return;
-  part_body<0, kSrcSeg12>(sg, a, s_part);
+  if (a.tbl) part_body<0, kSrcSeg12, kDstTiles, true>(sg, a, s_part);
+  else part_body<0, kSrcSeg12>(sg, a, s_part);
 }
 
 // Route overflow entries (record, part) of each route workgroup's list into the destination
@@ -4382,6 +4409,33 @@ namespace {
 
 inline uint64_t div_up(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
 
+// The leaves of a Bloom batch other than the oversize ones (more than kWinMaxWindows windows),
+// in order, into `dst` (tkv_amq_build_ex): one workgroup scans the flags chunk by chunk.
+__global__ __launch_bounds__(1024) void bloom_compact_segs(const tkv_amq_segment* __restrict__ segs,
+                                                           uint32_t n_segs, uint32_t max_small_blocks,
+                                                           tkv_amq_segment* __restrict__ dst)
+{
+  __shared__ uint32_t s_w[16];
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  uint32_t base = 0;
+  for (uint32_t c0 = 0; c0 < n_segs; c0 += 1024) {
+    const uint32_t s = c0 + tid;
+    const bool keep = s < n_segs && segs[s].n_blocks <= max_small_blocks;
+    const uint64_t m = __ballot(keep);
+    const uint32_t before = (uint32_t)__popcll(m & lanemask_lt());
+    if (lane == 0) s_w[wave] = (uint32_t)__popcll(m);
+    __syncthreads();
+    uint32_t off = base, tot = 0;
+    for (uint32_t w = 0; w < 16; ++w) {
+      off += w < wave ? s_w[w] : 0u;
+      tot += s_w[w];
+    }
+    if (keep) dst[off + before] = segs[s];
+    base += tot;
+    __syncthreads();
+  }
+}
+
 constexpr uint32_t kBloomLdsBudget = 64 * 1024;  // dynamic LDS a launch gets without the attribute
 // Leaf images are built in LDS up to the whole CU's LDS (a 160 KB image: 1.3M bits, ~130K
 // keys at 10 bits/key; TurtleKV leaves of small items reach ~80K keys): one workgroup per
@@ -4560,7 +4614,7 @@ inline void set_mono_attributes()
                           reinterpret_cast<const void*>(&bloom_part_keys24),
                           reinterpret_cast<const void*>(&bloom_part_routed)})
       (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)part_lds_bytes(kDirectMaxTiles));
+                                (int)(160 * 1024));
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&bloom_tile),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)(64 * kTileBlocks));
   });
@@ -4577,7 +4631,8 @@ inline void launch_part_build(int src, PartArgs a, hipStream_t s, const tkv_amq_
 {
   set_mono_attributes();
   a.src_kind = (uint32_t)src;
-  const size_t lds = part_lds_bytes(a.g.n_tiles);
+  a.tbl = part_tbl_fits(a.g.n_tiles) ? 1u : 0u;
+  const size_t lds = a.tbl ? part_tbl_lds_bytes(a.g.n_tiles) : part_lds_bytes(a.g.n_tiles);
   const dim3 grid(a.g.P), block(kPartThreads);
   if (src == kSrcKey24) hipLaunchKernelGGL(bloom_part_keys24, grid, block, lds, s, d_segs, a);
   else if (src == kSrcKey16) hipLaunchKernelGGL(bloom_part_keys16, grid, block, lds, s, d_segs, a);
@@ -4733,7 +4788,7 @@ inline void set_route_attributes()
                           reinterpret_cast<const void*>(&bloom_route_part<0, 24>)})
       (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)route_lds_bytes(kRouteMaxParts));
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&bloom_part_segs),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)part_lds_bytes(kDirectMaxTiles));
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)(160 * 1024));
   });
 }
 
@@ -4799,7 +4854,9 @@ inline void launch_part_from_blocks(const tkv_amq_route_plan& rp, hipStream_t s,
   a.blk = route_block(rp);
   a.n_src_segs = n_recv;
   a.seg_part = p / rp.world;
-  hipLaunchKernelGGL(bloom_part_segs, dim3(a.g.P), dim3(kPartThreads), part_lds_bytes(tn), s, d_seg, a);
+  a.tbl = part_tbl_fits(tn) ? 1u : 0u;
+  hipLaunchKernelGGL(bloom_part_segs, dim3(a.g.P), dim3(kPartThreads),
+                     a.tbl ? part_tbl_lds_bytes(tn) : part_lds_bytes(tn), s, d_seg, a);
   hipLaunchKernelGGL(bloom_tile, dim3(tn), dim3(kTileThreads), 64ull * kTileBlocks, s, d_seg, a, d_out, 1u);
   hipLaunchKernelGGL(bloom_overflow, dim3(a.g.P), dim3(256), 0, s, d_seg, a, d_out);
 }
@@ -4868,8 +4925,10 @@ inline uint32_t bloom_k_of(uint64_t n_keys, uint64_t n_blocks)
 
 // keys [0, n) of segment 0 (kb 16 or 24; routed 24-byte keys need the one-pass route, k <= 8)
 inline void launch_mono(const MonoPlan& m, hipStream_t s, const uint8_t* keys, uint32_t kb, uint32_t n,
-                        const tkv_amq_segment* d_segs, uint8_t* ws, uint8_t* d_out)
+                        const tkv_amq_segment* d_segs, uint8_t* ws, uint8_t* d_out, uint64_t key0 = 0)
 {
+  // (key0: the segment's key_begin, for the two-pass route, which reads keys [0, n) of its
+  // pointer; the other paths add the segment's key_begin themselves)
   if (m.g == 1) {
     const PartArgs a{keys, n, 0u, 1u, kb, nullptr, 0u, ws, m.pg};
     launch_part_build(kb == 24 ? kSrcKey24 : kSrcKey16, a, s, d_segs, d_out, 0u);
@@ -4889,7 +4948,7 @@ inline void launch_mono(const MonoPlan& m, hipStream_t s, const uint8_t* keys, u
   }
   uint32_t* rws = reinterpret_cast<uint32_t*>(ws);
   uint8_t* items = ws + m.items_off;
-  launch_route(m.rg, s, keys, kb, n, d_segs, m.q, rws, kb == 16 ? items : nullptr, 9u, items);
+  launch_route(m.rg, s, keys + (uint64_t)kb * key0, kb, n, d_segs, m.q, rws, kb == 16 ? items : nullptr, 9u, items);
   const uint32_t* cnt = rws + (uint64_t)m.rg.P * m.g;  // the part totals
   for (uint32_t j = 0; j < m.g; ++j) {
     const uint32_t t0 = j * m.q, tn = m.T - t0 < m.q ? m.T - t0 : m.q;
@@ -4904,6 +4963,38 @@ inline void launch_mono(const MonoPlan& m, hipStream_t s, const uint8_t* keys, u
 inline bool bloom_partitioned(uint32_t n_segs, uint64_t max_blocks, uint64_t n_keys)
 {
   return n_segs == 1 && 64 * max_blocks > kBloomLeafLdsBudget && n_keys <= 0xffffffffull;
+}
+
+// A Bloom batch with leaves of more than kWinMaxWindows windows (images past 2.5 MB) among
+// others (tkv_amq_build_ex): the other leaves go through the batch kernels from a compacted
+// leaf list, each oversize leaf through the monolithic build of its own.  Workspace: the
+// compacted list, then the larger of the batch's and the biggest oversize leaf's needs.
+constexpr uint32_t kWinMaxBlocks = kWinMaxWindows * (kBloomLeafLdsBudget / 64);  // 16 windows
+inline bool bloom_oversize(uint64_t n_blocks) { return bloom_window_count(n_blocks) > kWinMaxWindows; }
+
+inline uint64_t bloom_batch_ws_bytes(uint32_t n_segs, uint64_t n_keys, uint64_t max_blocks)
+{
+  if (bloom_window_path(n_segs, max_blocks, false))
+    return bloom_split_ws_bytes(n_segs, bloom_window_parts(n_segs, n_keys, max_blocks), max_blocks);
+  return bloom_split_ws_bytes(n_segs, bloom_split_parts(n_segs, n_keys, max_blocks), max_blocks);
+}
+
+inline uint64_t bloom_oversize_ws_bytes(const tkv_amq_segment* segs, uint32_t n_segs)
+{
+  uint32_t n_small = 0;
+  uint64_t small_keys = 0, small_max = 0, big = 0;
+  for (uint32_t i = 0; i < n_segs; ++i) {
+    const tkv_amq_segment& g = segs[i];
+    if (bloom_oversize(g.n_blocks)) {
+      big = std::max(big, mono_plan(g.n_keys, g.n_blocks).bytes);
+    } else {
+      ++n_small;
+      small_keys += g.n_keys;
+      small_max = std::max<uint64_t>(small_max, g.n_blocks);
+    }
+  }
+  const uint64_t small = n_small ? bloom_batch_ws_bytes(n_small, small_keys, small_max) : 0;
+  return align256(64ull * n_segs) + std::max(small, big);
 }
 
 }  // namespace
@@ -5110,6 +5201,8 @@ int tkv_amq_plan(int kind, const uint64_t* counts, const uint64_t* src_ids, uint
     else if (kind == TKV_AMQ_BLOOM)
       *ws_bytes = bloom_split_ws_bytes(n_segs, bloom_split_parts(n_segs, key_begin, max_blocks),
                                        max_blocks);
+    if (kind == TKV_AMQ_BLOOM && bpk != 0 && n_segs > 1 && bloom_window_count(max_blocks) > kWinMaxWindows)
+      *ws_bytes = bloom_oversize_ws_bytes(segs, n_segs);
   }
   if (max_blocks_out) *max_blocks_out = max_blocks;
   return TKV_AMQ_OK;
@@ -5271,13 +5364,13 @@ int tkv_amq_build(int kind, const uint8_t* keys, const uint64_t* offs, uint32_t 
       if (g2) {
         if (mode == kKey16)
           hipLaunchKernelGGL(bloom_global_set<kKey16>, dim3(g2), b, 0, s, keys, offs, stride,
-                             d_segs, n_segs, n_keys, d_out);
+                             d_segs, n_segs, n_keys, d_out, 0ull);
         else if (mode == kKeyFixed)
           hipLaunchKernelGGL(bloom_global_set<kKeyFixed>, dim3(g2), b, 0, s, keys, offs, stride,
-                             d_segs, n_segs, n_keys, d_out);
+                             d_segs, n_segs, n_keys, d_out, 0ull);
         else
           hipLaunchKernelGGL(bloom_global_set<kKeyVar>, dim3(g2), b, 0, s, keys, offs, stride,
-                             d_segs, n_segs, n_keys, d_out);
+                             d_segs, n_segs, n_keys, d_out, 0ull);
       }
     }
     return hipGetLastError() == hipSuccess ? TKV_AMQ_OK : TKV_AMQ_INTERNAL;
@@ -5483,6 +5576,65 @@ int tkv_amq_build(int kind, const uint8_t* keys, const uint64_t* offs, uint32_t 
                                           ? div_up(max_blocks, 4 * kPlaceThreads) : 256);
     hipLaunchKernelGGL(vqf_place, dim3(n_segs * parts), dim3(kPlaceThreads), 0, s, d_segs, d_ws,
                        ws_bytes, n_segs, d_out, parts);
+  }
+  return hipGetLastError() == hipSuccess ? TKV_AMQ_OK : TKV_AMQ_INTERNAL;
+}
+
+int tkv_amq_build_ex(int kind, const uint8_t* keys, const uint64_t* offs, uint32_t stride, uint64_t n_keys,
+                     const tkv_amq_segment* d_segs, const tkv_amq_segment* h_segs, uint32_t n_segs,
+                     uint32_t max_blocks, uint8_t* d_out, void* d_ws, uint64_t ws_bytes, void* stream)
+{
+  if (kind != TKV_AMQ_BLOOM || !h_segs || n_segs < 2 || !bloom_oversize(max_blocks))
+    return tkv_amq_build(kind, keys, offs, stride, n_keys, d_segs, n_segs, max_blocks, d_out, d_ws, ws_bytes,
+                         stream);
+  if (tkv_amq_device_count() == 0) return TKV_AMQ_UNAVAILABLE;
+  if (!d_segs || !d_out || (n_keys && !keys) || (!offs && stride == 0)) return TKV_AMQ_INVALID_ARGUMENT;
+  const hipStream_t s = as_stream(stream);
+  const uint64_t list_bytes = align256(64ull * n_segs);
+  if (!d_ws || ws_bytes < list_bytes) return TKV_AMQ_INVALID_ARGUMENT;
+  uint8_t* ws = static_cast<uint8_t*>(d_ws);
+  uint8_t* rest = ws + list_bytes;
+  const uint64_t rest_bytes = ws_bytes - list_bytes;
+  uint32_t n_small = 0, small_max = 0;
+  for (uint32_t i = 0; i < n_segs; ++i)
+    if (!bloom_oversize(h_segs[i].n_blocks)) {
+      ++n_small;
+      small_max = std::max(small_max, h_segs[i].n_blocks);
+    }
+  if (n_small) {
+    tkv_amq_segment* list = reinterpret_cast<tkv_amq_segment*>(ws);
+    hipLaunchKernelGGL(bloom_compact_segs, dim3(1), dim3(1024), 0, s, d_segs, n_segs, kWinMaxBlocks, list);
+    const int st = tkv_amq_build(kind, keys, offs, stride, n_keys, list, n_small, small_max, d_out, rest,
+                                 rest_bytes, stream);
+    if (st != TKV_AMQ_OK) return st;
+  }
+  const int mode = key_mode(offs, stride), bmode = build_key_mode(keys, offs, stride);
+  for (uint32_t i = 0; i < n_segs; ++i) {
+    const tkv_amq_segment& g = h_segs[i];
+    if (!bloom_oversize(g.n_blocks) || g.bits_per_key == 0) continue;
+    const MonoPlan mp = mono_plan(g.n_keys, g.n_blocks);
+    const uint32_t k = bloom_k_of(g.n_keys, g.n_blocks);
+    const bool mono = rest_bytes >= mp.bytes &&
+                      (mode == kKey16 || (bmode == kKey24 && (mp.g == 1 || (mp.blocks && k >= 1 && k <= 8))));
+    if (mono) {
+      launch_mono(mp, s, keys, mode == kKey16 ? 16u : 24u, g.n_keys, d_segs + i, rest, d_out, g.key_begin);
+    } else {
+      // other key shapes (or no room): device atomics for this leaf alone
+      hipLaunchKernelGGL(bloom_global_init, dim3(1), dim3(256), 0, s, d_segs + i, d_out);
+      const uint32_t g2 = (uint32_t)std::min<uint64_t>(div_up(g.n_keys, 256), 8192);
+      if (g2) {
+        const uint64_t end = g.key_begin + g.n_keys;
+        if (mode == kKey16)
+          hipLaunchKernelGGL(bloom_global_set<kKey16>, dim3(g2), dim3(256), 0, s, keys, offs, stride, d_segs + i, 1u,
+                             end, d_out, g.key_begin);
+        else if (mode == kKeyFixed)
+          hipLaunchKernelGGL(bloom_global_set<kKeyFixed>, dim3(g2), dim3(256), 0, s, keys, offs, stride, d_segs + i,
+                             1u, end, d_out, g.key_begin);
+        else
+          hipLaunchKernelGGL(bloom_global_set<kKeyVar>, dim3(g2), dim3(256), 0, s, keys, offs, stride, d_segs + i,
+                             1u, end, d_out, g.key_begin);
+      }
+    }
   }
   return hipGetLastError() == hipSuccess ? TKV_AMQ_OK : TKV_AMQ_INTERNAL;
 }

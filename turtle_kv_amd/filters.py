@@ -539,10 +539,12 @@ def build_all_filters(plan: FilterPlan, keys: KeyBatch, out=None, workspace=None
                           f"workspace holds {ws_bytes} bytes, the plan needs {plan.workspace_bytes}")
     sh = _stream_handle(stream)
     t0 = time.perf_counter()
-    st = abi.lib().tkv_amq_build(plan.kind, _ptr(keys.data), _ptr(keys.offsets), keys.stride,
-                                 keys.n, _ptr(plan.device_segs(dev)), plan.n_segs,
-                                 plan.max_seg_blocks, _ptr(out), _ptr(workspace), ws_bytes, sh)
-    abi.check(st, "tkv_amq_build")
+    # (_ex with the host plan: a Bloom batch with leaves past 16 LDS windows builds those through
+    # the tiled monolithic build, one each, and the rest through the batch kernels)
+    st = abi.lib().tkv_amq_build_ex(plan.kind, _ptr(keys.data), _ptr(keys.offsets), keys.stride,
+                                    keys.n, _ptr(plan.device_segs(dev)), _ptr(plan.segs), plan.n_segs,
+                                    plan.max_seg_blocks, _ptr(out), _ptr(workspace), ws_bytes, sh)
+    abi.check(st, "tkv_amq_build_ex")
     if check:
         # synchronous: the batch is known good, record its metrics with the build latency
         abi.check(abi.lib().tkv_amq_build_check(plan.kind, _ptr(workspace), ws_bytes, sh),
