@@ -354,6 +354,40 @@ def test_vqf_decide_paths(oracle, amq, torch, n_leaves, shape):
             assert segment_bytes(plan, out, s) == ref[:p.payload_used].tobytes(), f"bpk {bpk} leaf {s}"
 
 
+@pytest.mark.parametrize("shape", ["k20", "var", "var_long"])
+def test_vqf_decide_odd_keys_all_leaves(oracle, amq, torch, shape):
+    """Past 4,096 leaves, keys other than 16 or 24 bytes take vqf_decide, hashing each key in
+    the leaf's chain.  EVERY leaf against the oracle (its batched build over the same key
+    shape): 8-bit tags with 4-byte records, leaves past 512 blocks with 8-byte records, and keys
+    of 32 bytes or more (var_long: XXH64's long path)."""
+    rng = np.random.default_rng(77)
+    n_leaves = 4200
+    counts = [int(c) for c in rng.integers(0, 4000, n_leaves)]
+    counts[0], counts[7], counts[100] = 0, 30000, 16384
+    n = sum(counts)
+    offs = None
+    if shape == "k20":
+        keys, stride = rng.integers(0, 256, (n, 20), dtype=np.uint8), 20
+    else:
+        lens = rng.integers(6, 40 if shape == "var" else 80, n)
+        keys, stride = rng.integers(0, 256, int(lens.sum()), dtype=np.uint8), 0
+        offs = np.zeros(n + 1, np.int64)
+        offs[1:] = np.cumsum(lens)
+    plan, out = gpu_build(amq, torch, 1, torch.from_numpy(keys).cuda(), counts, 12, cap=65472,
+                          offsets_t=None if offs is None else torch.from_numpy(offs).cuda())
+    assert plan.segs["n_blocks"][7] > 512
+    ref = np.zeros(len(out) + 65472, np.uint8)
+    st = oracle.build_segments_ex(1, keys.reshape(-1), None if offs is None else offs.astype(np.uint64),
+                                  stride, seg_bounds(counts), 12, plan.segs["out_offset"],
+                                  np.full(n_leaves, 65472, np.uint64), ref,
+                                  src_page_id=plan.segs["src_page_id"], n_threads=min(16, os.cpu_count()))
+    assert st == 0
+    for s_ in range(n_leaves):
+        o, b = int(plan.segs["out_offset"][s_]), int(plan.segs["payload_bytes"][s_])
+        if out[o:o + b].tobytes() != ref[o:o + b].tobytes():
+            pytest.fail(f"leaf {s_} ({counts[s_]} keys) differs from the oracle")
+
+
 @pytest.mark.parametrize("n_leaves", [1, 256, 257, 512])
 @pytest.mark.parametrize("edge", ["b402", "tbl", "ring512", "ring960", "plain961"])
 @pytest.mark.parametrize("bpk", [12, 22])

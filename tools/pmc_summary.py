@@ -45,13 +45,16 @@ def agg(d, kernel):
     GRBM_GUI_ACTIVE sums to the step's busy clock)."""
     rows = list(csv.DictReader(open(os.path.join(d, "run_counter_collection.csv"))))
     total = collections.defaultdict(float)
-    for name in kernel.split(","):
+    for spec in kernel.split(","):
+        # "name*n": the kernel runs n times per step (e.g. once per routed part)
+        name, _, times = spec.partition("*")
+        n = int(times) if times else 1
         out = collections.defaultdict(list)
         for r in rows:
             if name in r["Kernel_Name"]:
                 out[r["Counter_Name"]].append(float(r["Counter_Value"]))
         for k, v in out.items():
-            total[k] += sum(v) / len(v)
+            total[k] += n * sum(v) / len(v)
     return dict(total)
 
 
@@ -59,7 +62,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--workload", required=True)
     ap.add_argument("--kernel", required=True,
-                    help="kernel-name substring; several, comma-separated, for a multi-kernel step")
+                    help="kernel-name substring; several, comma-separated, for a multi-kernel step; "
+                         "name*n for a kernel launched n times per step")
     ap.add_argument("--fetch", required=True)
     ap.add_argument("--write", required=True)
     ap.add_argument("--sq", default=None)
