@@ -276,10 +276,12 @@ class FilterBatchBuilder
     if (!planned_) TKV_AMQ_REQUIRE_OK(plan());
     u64 n = 0;
     for (u64 c : counts_) n += c;
-    return Status::from(tkv_amq_build((int)kind_, d_keys, d_key_offsets, key_stride, n,
-                                      d_segs_.get<tkv_amq_segment>(), (u32)segs_.size(),
-                                      max_blocks_, d_out, d_ws_.get(), ws_bytes_, stream),
-                        "tkv_amq_build");
+    // (_ex with the host plan: leaves past 16 LDS windows in a Bloom batch take the tiled
+    // monolithic build, one each)
+    return Status::from(tkv_amq_build_ex((int)kind_, d_keys, d_key_offsets, key_stride, n,
+                                         d_segs_.get<tkv_amq_segment>(), segs_.data(), (u32)segs_.size(),
+                                         max_blocks_, d_out, d_ws_.get(), ws_bytes_, stream),
+                        "tkv_amq_build_ex");
   }
 
   Status check(hipStream_t stream = nullptr) const
@@ -837,10 +839,10 @@ class LeafBatcher
         (b.stride == 0 && hipMemcpyAsync(b.d_offs.get(), b.h_offs, 8 * (n + 1), hipMemcpyHostToDevice, s) != hipSuccess) ||
         hipMemcpyAsync(b.d_segs.get(), b.h_io, seg_bytes, hipMemcpyHostToDevice, s) != hipSuccess)
       return Status::from(TKV_AMQ_INTERNAL, "hipMemcpyAsync keys");
-    st = tkv_amq_build((int)b.kind, b.d_keys.get(), b.stride ? nullptr : b.d_offs.get<u64>(), b.stride, n,
-                       b.d_segs.get<tkv_amq_segment>(), (u32)n_segs, max_blocks, b.d_out.get(),
-                       b.d_ws.get(), ws_bytes, s);
-    if (st != TKV_AMQ_OK) return Status::from(st, "tkv_amq_build");
+    st = tkv_amq_build_ex((int)b.kind, b.d_keys.get(), b.stride ? nullptr : b.d_offs.get<u64>(), b.stride, n,
+                          b.d_segs.get<tkv_amq_segment>(), reinterpret_cast<const tkv_amq_segment*>(b.h_io),
+                          (u32)n_segs, max_blocks, b.d_out.get(), b.d_ws.get(), ws_bytes, s);
+    if (st != TKV_AMQ_OK) return Status::from(st, "tkv_amq_build_ex");
     if (hipMemcpyAsync(h_out, b.d_out.get(), total_out, hipMemcpyDeviceToHost, s) != hipSuccess ||
         (b.kind == FilterKind::kQuotient && ws_bytes >= TKV_AMQ_VQF_NELTS_OFFSET + 4 * n_segs &&
          hipMemcpyAsync(h_flags, b.d_ws.get<u8>() + TKV_AMQ_VQF_NELTS_OFFSET, 4 * n_segs,
