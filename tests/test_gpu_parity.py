@@ -757,6 +757,29 @@ def test_bloom_oversize_leaves_among_many(oracle, amq, torch, shape):
     assert_same(plan, out, ref)
 
 
+@pytest.mark.parametrize("shape,bpk,n_big", [("k16", 10, 35), ("k16", 16, 17), ("k24", 12, 17)])
+def test_bloom_many_oversize_leaves(oracle, amq, torch, shape, bpk, n_big):
+    """More oversize leaves than one multi-leaf launch holds (bloom_part_multi: 15 leaves), and
+    (16-byte keys @10, 35 leaves of 2.1-2.3M keys, ~2.7 GB of partition workspace in all) more
+    than its 2 GiB workspace budget: the launches split by count and by workspace; k > 8
+    (@16: the 16-byte keys as records), 24-byte keys; small leaves between them."""
+    rng = np.random.default_rng(bpk)
+    first = 40960 * 512 // bpk + 1  # keys past 16 windows (40,960 blocks)
+    counts = []
+    for _ in range(n_big):
+        counts += [int(first + rng.integers(0, 200_000)), int(rng.integers(0, 5000))]
+    n = sum(counts)
+    if shape == "k16":
+        keys, stride = oracle.gen_keys16(bpk, 0, n), 16
+    else:
+        keys, stride = rng.integers(0, 256, (n, 24), dtype=np.uint8), 24
+    ref = oracle_per_segment(oracle, 0, keys, counts, bpk, stride=stride)
+    plan, out = gpu_build(amq, torch, 0, torch.from_numpy(keys).cuda(), counts, bpk)
+    if n_big == 35:
+        assert plan.workspace_bytes < 2.3e9   # the budget, not every leaf's workspace at once
+    assert_same(plan, out, ref)
+
+
 def test_reference_api_mirror(oracle, amq, torch):
     keys = sorted_keys(oracle, 3, [4000])
     kb = amq.KeyBatch.fixed(torch.from_numpy(keys).cuda())

@@ -1059,24 +1059,33 @@ struct PartGeom {
   uint64_t bytes;
 };
 
-// n_max: items the build may receive (the overflow lists' capacity); n_exp: the expected
-// count (the regions' capacity; equal to n_max unless the count is only known on the device)
-inline PartGeom part_geom(uint64_t n_max, uint64_t n_exp, uint32_t n_tiles, uint32_t rb)
+// the workspace layout of a partition from its P, n_tiles, per, cap and rb (the multi-leaf
+// launch recomputes it on the device from the same five numbers)
+__host__ __device__ inline void part_layout(PartGeom& g)
 {
-  PartGeom g;
-  g.n_tiles = n_tiles ? n_tiles : 1;
-  g.rb = rb;
-  const uint64_t p = (n_exp + 32 * kPartThreads - 1) / (32 * kPartThreads);
-  g.P = (uint32_t)(p < 1 ? 1 : (p > kPartMaxWgs ? kPartMaxWgs : p));
-  g.per = (uint32_t)((n_max + g.P - 1) / g.P);
-  const double e = (double)((n_exp + g.P - 1) / g.P) / g.n_tiles;
-  g.cap = ((uint32_t)(e + 6.0 * sqrt(e) + 16.0) + 15) & ~15u;
   const uint64_t regions = (uint64_t)g.n_tiles * g.P;
   g.counts_off = 256;
   g.ovf_n_off = g.counts_off + 4 * regions;
   g.regions_off = (g.ovf_n_off + 4ull * g.P + 255) & ~255ull;
-  g.ovf_off = g.regions_off + (uint64_t)rb * regions * g.cap;
+  g.ovf_off = g.regions_off + (uint64_t)g.rb * regions * g.cap;
   g.bytes = g.ovf_off + 16ull * g.P * g.per;
+}
+
+// n_max: items the build may receive (the overflow lists' capacity); n_exp: the expected
+// count (the regions' capacity; equal to n_max unless the count is only known on the device);
+// wg_items: items per workgroup aimed at (the workgroups: at most one per CU)
+inline PartGeom part_geom(uint64_t n_max, uint64_t n_exp, uint32_t n_tiles, uint32_t rb,
+                          uint64_t wg_items = 32ull * kPartThreads)
+{
+  PartGeom g;
+  g.n_tiles = n_tiles ? n_tiles : 1;
+  g.rb = rb;
+  const uint64_t p = (n_exp + wg_items - 1) / wg_items;
+  g.P = (uint32_t)(p < 1 ? 1 : (p > kPartMaxWgs ? kPartMaxWgs : p));
+  g.per = (uint32_t)((n_max + g.P - 1) / g.P);
+  const double e = (double)((n_exp + g.P - 1) / g.P) / g.n_tiles;
+  g.cap = ((uint32_t)(e + 6.0 * sqrt(e) + 16.0) + 15) & ~15u;
+  part_layout(g);
   return g;
 }
 
@@ -1414,6 +1423,9 @@ struct PartArgs {
   // a partition (kDstTiles) with the per-tile store table: part_tbl_fits(n_tiles), and the
   // launch's LDS is part_tbl_lds_bytes
   uint32_t tbl;
+  // the build's first workgroup in its grid (0 but in a multi-leaf launch, whose grid holds the
+  // workgroups of several builds back to back)
+  uint32_t wg0;
 };
 
 __host__ __device__ inline uint64_t div_magic(uint32_t d) { return (0x100000000ull / d) + 1; }
@@ -1514,7 +1526,7 @@ __device__ void part_body(const tkv_amq_segment& sg, const PartArgs& a, uint32_t
   constexpr uint32_t NPL = RAW ? 5 : 3;  // LDS planes (ROUTE: + a u16 plane of parts)
   static_assert(NPL * B * 4 <= kPartPlaneBytes, "planes");
   constexpr uint32_t IB = SRC == kSrcKey24 ? 24 : (ROUTED ? 12 : 16);  // item bytes
-  const uint32_t tid = threadIdx.x, w = blockIdx.x, P = a.g.P, T = a.g.n_tiles, cap = a.g.cap;
+  const uint32_t tid = threadIdx.x, w = blockIdx.x - a.wg0, P = a.g.P, T = a.g.n_tiles, cap = a.g.cap;
   const uint32_t nb = sg.n_blocks, k = sg.hash_count;
   const uint32_t HW = (T + 1) >> 1;
   uint32_t* pl = lds;  // plane j at pl + j * B
@@ -1766,11 +1778,8 @@ __device__ void part_body(const tkv_amq_segment& sg, const PartArgs& a, uint32_t
 }
 
 // 16-byte keys: bit records for k <= 8, the keys themselves above
-__global__ __launch_bounds__(kPartThreads) void bloom_part_keys16(const tkv_amq_segment* __restrict__ segs,
-                                                                  PartArgs a)
+__device__ __attribute__((always_inline)) inline void part_keys16(const tkv_amq_segment& sg, const PartArgs& a, uint32_t* s_part)
 {
-  extern __shared__ __attribute__((aligned(16))) uint32_t s_part[];
-  const tkv_amq_segment sg = segs[0];
   const uint32_t k = sg.hash_count;
   if (k == 0) return;
   if (k == 7 && a.tbl) part_body<7, kSrcKey16, kDstTiles, true>(sg, a, s_part);
@@ -1781,18 +1790,31 @@ __global__ __launch_bounds__(kPartThreads) void bloom_part_keys16(const tkv_amq_
   else part_body<0, kSrcRaw16>(sg, a, s_part);
 }
 
-// 24-byte keys (a kernel of its own: their six key words per prefetched key would raise the
-// 16-byte kernel's register count): always bit records (k > 8: the first eight bits)
-__global__ __launch_bounds__(kPartThreads) void bloom_part_keys24(const tkv_amq_segment* __restrict__ segs,
+__global__ __launch_bounds__(kPartThreads) void bloom_part_keys16(const tkv_amq_segment* __restrict__ segs,
                                                                   PartArgs a)
 {
   extern __shared__ __attribute__((aligned(16))) uint32_t s_part[];
   const tkv_amq_segment sg = segs[0];
+  part_keys16(sg, a, s_part);
+}
+
+// 24-byte keys (a kernel of its own: their six key words per prefetched key would raise the
+// 16-byte kernel's register count): always bit records (k > 8: the first eight bits)
+__device__ __attribute__((always_inline)) inline void part_keys24(const tkv_amq_segment& sg, const PartArgs& a, uint32_t* s_part)
+{
   const uint32_t k = sg.hash_count;
   if (k == 0) return;
   if (k == 7) part_body<7, kSrcKey24>(sg, a, s_part);  // (the table variant spills here)
   else if (k == 8) part_body<8, kSrcKey24>(sg, a, s_part);
   else part_body<0, kSrcKey24>(sg, a, s_part);
+}
+
+__global__ __launch_bounds__(kPartThreads) void bloom_part_keys24(const tkv_amq_segment* __restrict__ segs,
+                                                                  PartArgs a)
+{
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_part[];
+  const tkv_amq_segment sg = segs[0];
+  part_keys24(sg, a, s_part);
 }
 
 // routed items: 12-byte bit records for k <= 8, 16-byte keys above (tkv_amq_bloom_route)
@@ -1908,7 +1930,7 @@ __device__ inline void rec_insert(uint32_t* img, uint32_t w0, uint32_t w1, uint3
 template <int K, bool RAW>
 __device__ void tile_body(const tkv_amq_segment& sg, const PartArgs& a, uint32_t* img, uint32_t t)
 {
-  constexpr uint32_t RB = RAW ? 16 : 12, NW = kTileThreads / 64, V = 4, PIECE = 64 * V;
+  constexpr uint32_t RB = RAW ? 16 : 12, NW = kTileThreads / 64, V = 8, PIECE = 64 * V;
   // wave-uniform in an SGPR: region counts are scalar loads (lgkmcnt), so waiting for one
   // never waits for the record loads in flight
   const uint32_t lane = threadIdx.x & 63u, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1975,13 +1997,10 @@ __device__ void tile_body(const tkv_amq_segment& sg, const PartArgs& a, uint32_t
   }
 }
 
-__global__ __launch_bounds__(kTileThreads) void bloom_tile(const tkv_amq_segment* __restrict__ segs,
-                                                           PartArgs a, uint8_t* __restrict__ out,
-                                                           uint32_t hdr_always)
+__device__ __attribute__((always_inline)) inline void tile_run(const tkv_amq_segment& sg, const PartArgs& a, uint8_t* __restrict__ out,
+                                uint32_t hdr_always, uint32_t* s_img)
 {
-  extern __shared__ __attribute__((aligned(16))) uint32_t s_img[];
-  const tkv_amq_segment sg = segs[0];
-  const uint32_t t = blockIdx.x, tid = threadIdx.x, k = sg.hash_count;
+  const uint32_t t = blockIdx.x - a.wg0, tid = threadIdx.x, k = sg.hash_count;
   if (k == 0) return;
   const bool raw = part_raw(sg, a);
   const uint32_t first = (a.tile0 + t) * kTileBlocks;
@@ -2002,6 +2021,15 @@ __global__ __launch_bounds__(kTileThreads) void bloom_tile(const tkv_amq_segment
   for (uint32_t q = tid; q < tb * 4; q += kTileThreads) dst[q] = src[q];
 }
 
+__global__ __launch_bounds__(kTileThreads) void bloom_tile(const tkv_amq_segment* __restrict__ segs,
+                                                           PartArgs a, uint8_t* __restrict__ out,
+                                                           uint32_t hdr_always)
+{
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_img[];
+  const tkv_amq_segment sg = segs[0];
+  tile_run(sg, a, out, hdr_always, s_img);
+}
+
 // the filter header alone (a hash-range shard that owns no tile still returns a whole header)
 __global__ __launch_bounds__(64) void bloom_header_only(const tkv_amq_segment* __restrict__ segs,
                                                         uint8_t* __restrict__ out)
@@ -2017,11 +2045,9 @@ __global__ __launch_bounds__(64) void bloom_header_only(const tkv_amq_segment* _
 // (runs after bloom_tile has stored every tile).  An entry is a record whose region was full
 // (the 16-byte key itself when the records were keys).  24-byte keys with k > 8 (bits_per_key
 // >= 13): the bits past the eighth of the workgroup's keys, also with atomics.
-__global__ __launch_bounds__(256) void bloom_overflow(const tkv_amq_segment* __restrict__ segs,
-                                                      PartArgs a, uint8_t* __restrict__ out)
+__device__ __attribute__((always_inline)) inline void overflow_run(const tkv_amq_segment& sg, const PartArgs& a, uint8_t* __restrict__ out)
 {
-  const tkv_amq_segment sg = segs[0];
-  const uint32_t k = sg.hash_count, w = blockIdx.x, nb = sg.n_blocks;
+  const uint32_t k = sg.hash_count, w = blockIdx.x - a.wg0, nb = sg.n_blocks;
   if (k == 0) return;
   const bool raw = part_raw(sg, a);
   const uint32_t n = reinterpret_cast<const uint32_t*>(a.ws + a.g.ovf_n_off)[w];
@@ -2070,6 +2096,80 @@ __global__ __launch_bounds__(256) void bloom_overflow(const tkv_amq_segment* __r
       atomicOr(bw + (bj >> 5), 1u << (bj & 31u));
     }
   }
+}
+
+__global__ __launch_bounds__(256) void bloom_overflow(const tkv_amq_segment* __restrict__ segs,
+                                                      PartArgs a, uint8_t* __restrict__ out)
+{
+  const tkv_amq_segment sg = segs[0];
+  overflow_run(sg, a, out);
+}
+
+// ---------------------------------------------------------------------------------------
+// Several monolithic builds in one launch each of partition, tile and overflow (the oversize
+// leaves of a tkv_amq_build_ex batch, each of at most kDirectMaxTiles tiles): one leaf alone
+// holds a few tiles -- a 3M-key leaf at 12 bits/key 35 -- so its tile kernel would leave most
+// CUs idle; back to back in one grid the leaves' workgroups fill the chip.  The leaves'
+// PartArgs are in the kernel argument (constant memory: the partition re-reads its fields
+// instead of holding them in registers), with the first tile workgroup and the segment of
+// each; a workgroup finds its leaf by a binary search over the first workgroups.
+// ---------------------------------------------------------------------------------------
+constexpr uint32_t kMultiMaxLeaves = 15;
+struct MultiParts {
+  uint32_t n;                      // leaves
+  uint32_t tg0[kMultiMaxLeaves];   // the leaf's first tile workgroup (a[i].wg0: partition)
+  uint32_t seg[kMultiMaxLeaves];   // its segment in the batch
+  PartArgs a[kMultiMaxLeaves];
+};
+static_assert(sizeof(MultiParts) <= 4096 - 32, "kernel argument");
+
+template <bool TILE>
+__device__ inline uint32_t multi_find(const MultiParts& m)
+{
+  uint32_t lo = 0, hi = m.n;  // the last leaf whose first workgroup is <= blockIdx.x
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if ((TILE ? m.tg0[mid] : m.a[mid].wg0) <= blockIdx.x) lo = mid;
+    else hi = mid;
+  }
+  return lo;
+}
+
+__global__ __launch_bounds__(kPartThreads) void bloom_part_multi16(const tkv_amq_segment* __restrict__ segs,
+                                                                   MultiParts m)
+{
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_part[];
+  const uint32_t l = multi_find<false>(m);
+  const tkv_amq_segment sg = segs[m.seg[l]];
+  part_keys16(sg, m.a[l], s_part);
+}
+
+__global__ __launch_bounds__(kPartThreads) void bloom_part_multi24(const tkv_amq_segment* __restrict__ segs,
+                                                                   MultiParts m)
+{
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_part[];
+  const uint32_t l = multi_find<false>(m);
+  const tkv_amq_segment sg = segs[m.seg[l]];
+  part_keys24(sg, m.a[l], s_part);
+}
+
+__global__ __launch_bounds__(kTileThreads) void bloom_tile_multi(const tkv_amq_segment* __restrict__ segs,
+                                                                 MultiParts m, uint8_t* __restrict__ out)
+{
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_img[];
+  const uint32_t l = multi_find<true>(m);
+  const tkv_amq_segment sg = segs[m.seg[l]];
+  PartArgs a = m.a[l];
+  a.wg0 = m.tg0[l];
+  tile_run(sg, a, out, 0u, s_img);
+}
+
+__global__ __launch_bounds__(256) void bloom_overflow_multi(const tkv_amq_segment* __restrict__ segs,
+                                                            MultiParts m, uint8_t* __restrict__ out)
+{
+  const uint32_t l = multi_find<false>(m);
+  const tkv_amq_segment sg = segs[m.seg[l]];
+  overflow_run(sg, m.a[l], out);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -4979,13 +5079,72 @@ inline uint64_t bloom_batch_ws_bytes(uint32_t n_segs, uint64_t n_keys, uint64_t 
   return bloom_split_ws_bytes(n_segs, bloom_split_parts(n_segs, n_keys, max_blocks), max_blocks);
 }
 
+// An oversize leaf of at most kDirectMaxTiles tiles joins a multi-leaf launch (bloom_part_multi).
+// Its partition workgroups take the batch's oversize keys / 256 each, between 2 and 8 batches:
+// few oversize keys still spread over every CU (a lone 3M-key leaf: 184 workgroups), many give
+// each workgroup a pipeline of 8 batches (64 x 3M keys: 46 per leaf), long enough to hide its
+// first load and last store.  The leaves of one launch share the workspace budget below (a
+// leaf larger than it runs alone).
+constexpr uint64_t kMultiWsBudget = 2ull << 30;
+
+inline uint64_t multi_wg_items(uint64_t multi_keys)
+{
+  return std::min<uint64_t>(8ull * kPartBatch, std::max<uint64_t>(2ull * kPartBatch, multi_keys / kPartMaxWgs));
+}
+
+inline bool multi_leaf(uint64_t n_keys, uint64_t n_blocks)
+{
+  return bloom_oversize(n_blocks) && filter_tiles(n_blocks) <= kDirectMaxTiles && n_keys <= 0xffffffffull;
+}
+
+inline PartGeom multi_geom(uint64_t n_keys, uint64_t n_blocks, uint64_t wg_items)
+{
+  return part_geom(n_keys, n_keys, filter_tiles(n_blocks), 16, wg_items);
+}
+
+// the keys of a batch's multi-leaf candidates
+inline uint64_t multi_keys_of(const tkv_amq_segment* segs, uint32_t n_segs)
+{
+  uint64_t n = 0;
+  for (uint32_t i = 0; i < n_segs; ++i)
+    if (segs[i].bits_per_key && multi_leaf(segs[i].n_keys, segs[i].n_blocks)) n += segs[i].n_keys;
+  return n;
+}
+
+inline size_t multi_lds_bytes(uint32_t n_tiles)
+{
+  return part_tbl_fits(n_tiles) ? part_tbl_lds_bytes(n_tiles) : part_lds_bytes(n_tiles);
+}
+
+inline void launch_multi(const MultiParts& m, uint32_t kb, uint32_t n_wgs, uint32_t n_tiles, size_t lds,
+                         hipStream_t s, const tkv_amq_segment* d_segs, uint8_t* d_out)
+{
+  static std::once_flag attr[kMaxDevices];
+  once_per_device(attr, [] {
+    for (const void* f : {reinterpret_cast<const void*>(&bloom_part_multi16),
+                          reinterpret_cast<const void*>(&bloom_part_multi24)})
+      (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(160 * 1024));
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&bloom_tile_multi),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)(64 * kTileBlocks));
+  });
+  if (kb == 24) hipLaunchKernelGGL(bloom_part_multi24, dim3(n_wgs), dim3(kPartThreads), lds, s, d_segs, m);
+  else hipLaunchKernelGGL(bloom_part_multi16, dim3(n_wgs), dim3(kPartThreads), lds, s, d_segs, m);
+  hipLaunchKernelGGL(bloom_tile_multi, dim3(n_tiles), dim3(kTileThreads), 64ull * kTileBlocks, s, d_segs, m, d_out);
+  hipLaunchKernelGGL(bloom_overflow_multi, dim3(n_wgs), dim3(256), 0, s, d_segs, m, d_out);
+}
+
 inline uint64_t bloom_oversize_ws_bytes(const tkv_amq_segment* segs, uint32_t n_segs)
 {
   uint32_t n_small = 0;
-  uint64_t small_keys = 0, small_max = 0, big = 0;
+  uint64_t small_keys = 0, small_max = 0, big = 0, multi_sum = 0, multi_max = 0;
+  const uint64_t wg_items = multi_wg_items(multi_keys_of(segs, n_segs));
   for (uint32_t i = 0; i < n_segs; ++i) {
     const tkv_amq_segment& g = segs[i];
-    if (bloom_oversize(g.n_blocks)) {
+    if (multi_leaf(g.n_keys, g.n_blocks)) {
+      const uint64_t b = align256(multi_geom(g.n_keys, g.n_blocks, wg_items).bytes);
+      multi_sum += b;
+      multi_max = std::max(multi_max, b);
+    } else if (bloom_oversize(g.n_blocks)) {
       big = std::max(big, mono_plan(g.n_keys, g.n_blocks).bytes);
     } else {
       ++n_small;
@@ -4994,7 +5153,8 @@ inline uint64_t bloom_oversize_ws_bytes(const tkv_amq_segment* segs, uint32_t n_
     }
   }
   const uint64_t small = n_small ? bloom_batch_ws_bytes(n_small, small_keys, small_max) : 0;
-  return align256(64ull * n_segs) + std::max(small, big);
+  const uint64_t multi = std::min(multi_sum, std::max(multi_max, kMultiWsBudget));
+  return align256(64ull * n_segs) + std::max(std::max(small, big), multi);
 }
 
 }  // namespace
@@ -5609,9 +5769,51 @@ int tkv_amq_build_ex(int kind, const uint8_t* keys, const uint64_t* offs, uint32
     if (st != TKV_AMQ_OK) return st;
   }
   const int mode = key_mode(offs, stride), bmode = build_key_mode(keys, offs, stride);
+  // the oversize leaves of at most kDirectMaxTiles tiles: multi-leaf launches, as many leaves
+  // per launch as the workspace holds
+  MultiParts m{};
+  const uint32_t mkb = mode == kKey16 ? 16u : 24u;
+  uint64_t used = 0;
+  uint32_t wgs = 0, tiles = 0;
+  size_t lds = 0;
+  auto flush = [&] {
+    if (m.n) launch_multi(m, mkb, wgs, tiles, lds, s, d_segs, d_out);
+    m.n = 0;
+    used = 0;
+    wgs = tiles = 0;
+    lds = 0;
+  };
+  const bool multi_keys = mode == kKey16 || bmode == kKey24;
+  const uint64_t wg_items = multi_wg_items(multi_keys_of(h_segs, n_segs));
   for (uint32_t i = 0; i < n_segs; ++i) {
     const tkv_amq_segment& g = h_segs[i];
     if (!bloom_oversize(g.n_blocks) || g.bits_per_key == 0) continue;
+    if (multi_keys && multi_leaf(g.n_keys, g.n_blocks)) {
+      const PartGeom pg = multi_geom(g.n_keys, g.n_blocks, wg_items);
+      const uint64_t b = align256(pg.bytes);
+      if (b <= rest_bytes) {
+        if (m.n == kMultiMaxLeaves || used + b > rest_bytes) flush();
+        PartArgs& a = m.a[m.n];
+        a = PartArgs{};
+        a.src = keys;
+        a.n = (uint32_t)g.n_keys;
+        a.from_seg = 1;
+        a.kb = mkb;
+        a.ws = rest + used;
+        a.g = pg;
+        a.src_kind = mkb == 24 ? (uint32_t)kSrcKey24 : (uint32_t)kSrcKey16;
+        a.tbl = part_tbl_fits(pg.n_tiles) ? 1u : 0u;
+        a.wg0 = wgs;
+        m.tg0[m.n] = tiles;
+        m.seg[m.n] = i;
+        ++m.n;
+        used += b;
+        wgs += pg.P;
+        tiles += pg.n_tiles;
+        lds = std::max(lds, multi_lds_bytes(pg.n_tiles));
+        continue;
+      }
+    }
     const MonoPlan mp = mono_plan(g.n_keys, g.n_blocks);
     const uint32_t k = bloom_k_of(g.n_keys, g.n_blocks);
     const bool mono = rest_bytes >= mp.bytes &&
@@ -5636,6 +5838,7 @@ int tkv_amq_build_ex(int kind, const uint8_t* keys, const uint64_t* offs, uint32
       }
     }
   }
+  flush();
   return hipGetLastError() == hipSuccess ? TKV_AMQ_OK : TKV_AMQ_INTERNAL;
 }
 
