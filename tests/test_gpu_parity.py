@@ -583,13 +583,15 @@ def test_vqf_hash_matches_xxhash(amq, torch):
 
 
 @pytest.mark.parametrize("n,bpk,seed", [(600000, 10, 8), (3000000, 10, 9), (1500000, 12, 10),
-                                         (1100000, 5, 11), (90000, 64, 12)])
+                                         (1100000, 5, 11), (90000, 64, 12), (8_000_000, 10, 13),
+                                         (14_000_000, 10, 14)])
 def test_bloom_monolithic_partitioned(oracle, amq, torch, n, bpk, seed):
     """One filter of 16-byte keys larger than four LDS windows (640 KB; smaller ones take the
     window path, tests/test_gpu_window.py): the hash-once record path (bloom_part_keys16 /
     bloom_tile), byte-identical to the oracle.  Covers a ragged last tile, k = 7 / 8 /
     generic <= 8 (12-byte bit records) and k = 44 (the keys themselves are partitioned and
-    hashed per tile), and 29 tiles over 92 partition workgroups."""
+    hashed per tile); below 128 tiles each tile's regions split over up to 16 tile workgroups
+    and their partial images merged (6 tiles x 16, 29 x 8, 77 x 3), 134 tiles unsplit."""
     keys = oracle.gen_keys16(seed, 0, n)
     ref = oracle_per_segment(oracle, 0, keys, [n], bpk)
     plan, out = gpu_build(amq, torch, 0, torch.from_numpy(keys).cuda(), [n], bpk)

@@ -1,9 +1,9 @@
 #!/bin/bash
 # tile-kernel variant: parity of the monolithic/oversize tests, oversize timings, bloom10mono line, kernel trace
 set -o pipefail
-O=gpurun_out/r05/multi2; mkdir -p $O
+O=gpurun_out/r05/${TAG:-multi2}; mkdir -p $O
 export PYTHONUNBUFFERED=1
-timeout -k 10 500 python -u -m pytest tests/test_gpu_parity.py -x -q -k "oversize or monolithic" --timeout 300 --timeout-method thread > $O/tests.log 2>&1 \
+timeout -k 10 500 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_window.py -x -q -k "oversize or monolithic or window" --timeout 300 --timeout-method thread > $O/tests.log 2>&1 \
   && tail -2 $O/tests.log \
   && timeout -k 10 300 python -u tools/oversize_batch.py > $O/timing.log 2>&1 \
   && grep -v amdgpu.ids $O/timing.log \

@@ -1,5 +1,6 @@
-"""Build rate of Bloom batches holding leaves past 16 LDS windows (tkv_amq_build_ex: those
-leaves through the tiled monolithic build, the others batched), HIP events, 20 reps."""
+"""Build rate of single Bloom filters past four LDS windows (the tiled monolithic build) and of
+batches holding leaves past 16 windows (tkv_amq_build_ex: those leaves built together through
+the tiled build, the others batched), @10 bits/key, HIP events, 20 reps."""
 import os
 import sys
 
@@ -13,7 +14,10 @@ def main():
     import torch
 
     import turtle_kv_amd as amq
-    for name, counts in [("test batch [3M, 500, 16384]", [3_000_000, 500, 16384]),
+    for name, counts in [("one filter of 1M", [1_000_000]),
+                         ("one filter of 3M", [3_000_000]),
+                         ("one filter of 12M", [12_000_000]),
+                         ("test batch [3M, 500, 16384]", [3_000_000, 500, 16384]),
                          ("8 x 3M + 200 x 16K", [3_000_000] * 8 + [16384] * 200),
                          ("64 x 3M", [3_000_000] * 64)]:
         n = sum(counts)

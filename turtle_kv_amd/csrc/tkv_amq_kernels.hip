@@ -1426,6 +1426,10 @@ struct PartArgs {
   // the build's first workgroup in its grid (0 but in a multi-leaf launch, whose grid holds the
   // workgroups of several builds back to back)
   uint32_t wg0;
+  // a filter of few tiles: each tile's regions split over `split` tile workgroups (> 1), each
+  // writing a partial image at part_img + (t * split + s) * 128 KiB, ORed by bloom_tile_merge
+  uint32_t split;
+  uint8_t* part_img;
 };
 
 __host__ __device__ inline uint64_t div_magic(uint32_t d) { return (0x100000000ull / d) + 1; }
@@ -1928,7 +1932,8 @@ __device__ inline void rec_insert(uint32_t* img, uint32_t w0, uint32_t w1, uint3
 // loads the next piece before it inserts the current one (two register sets, unrolled by two:
 // no copy of an in-flight load), so every wave has one piece in flight at all times.
 template <int K, bool RAW>
-__device__ void tile_body(const tkv_amq_segment& sg, const PartArgs& a, uint32_t* img, uint32_t t)
+__device__ void tile_body(const tkv_amq_segment& sg, const PartArgs& a, uint32_t* img, uint32_t t,
+                          uint32_t w_lo, uint32_t w_hi)
 {
   constexpr uint32_t RB = RAW ? 16 : 12, NW = kTileThreads / 64, V = 8, PIECE = 64 * V;
   // wave-uniform in an SGPR: region counts are scalar loads (lgkmcnt), so waiting for one
@@ -1943,9 +1948,9 @@ __device__ void tile_body(const tkv_amq_segment& sg, const PartArgs& a, uint32_t
     uint32_t w, i0, c;  // region, first record, records in the region
     uint32_t x[V][4];
   };
-  auto count = [&](uint32_t w) { return w < P ? counts[w] : 0u; };
+  auto count = [&](uint32_t w) { return w < w_hi ? counts[w] : 0u; };
   auto load = [&](Piece& q) {
-    const uint8_t* reg = q.w < P ? regions + (uint64_t)q.w * rstride : a.ws;
+    const uint8_t* reg = q.w < w_hi ? regions + (uint64_t)q.w * rstride : a.ws;
     const uint32_t lastr = q.c ? q.c - 1 : 0u;
 #pragma unroll
     for (uint32_t v = 0; v < V; ++v) {
@@ -1984,41 +1989,82 @@ __device__ void tile_body(const tkv_amq_segment& sg, const PartArgs& a, uint32_t
     }
   };
   Piece A, B;
-  A.w = wave;
+  A.w = w_lo + wave;
   A.i0 = 0;
   A.c = count(A.w);
   load(A);
-  while (A.w < P) {
+  while (A.w < w_hi) {
     advance(A, B);
     insert(A);
-    if (B.w >= P) break;
+    if (B.w >= w_hi) break;
     advance(B, A);
     insert(B);
   }
+  (void)P;
 }
 
 __device__ __attribute__((always_inline)) inline void tile_run(const tkv_amq_segment& sg, const PartArgs& a, uint8_t* __restrict__ out,
                                 uint32_t hdr_always, uint32_t* s_img)
 {
-  const uint32_t t = blockIdx.x - a.wg0, tid = threadIdx.x, k = sg.hash_count;
+  const uint32_t x = blockIdx.x - a.wg0, tid = threadIdx.x, k = sg.hash_count;
   if (k == 0) return;
+  const uint32_t S = a.split > 1 ? a.split : 1u;
+  const uint32_t t = x / S, sp = x - t * S;  // tile, and its share of the regions
+  const uint32_t w_lo = (uint32_t)((uint64_t)a.g.P * sp / S), w_hi = (uint32_t)((uint64_t)a.g.P * (sp + 1) / S);
   const bool raw = part_raw(sg, a);
   const uint32_t first = (a.tile0 + t) * kTileBlocks;
   const uint32_t tb = min(kTileBlocks, sg.n_blocks - first);
   for (uint32_t w = tid; w < tb * 16; w += kTileThreads) s_img[w] = 0;
   __syncthreads();
-  if (raw) tile_body<0, true>(sg, a, s_img, t);
-  else if (k == 7) tile_body<7, false>(sg, a, s_img, t);
-  else if (k == 8) tile_body<8, false>(sg, a, s_img, t);
-  else tile_body<0, false>(sg, a, s_img, t);  // (k > 8 with 24-byte keys: eight bits)
+  if (raw) tile_body<0, true>(sg, a, s_img, t, w_lo, w_hi);
+  else if (k == 7) tile_body<7, false>(sg, a, s_img, t, w_lo, w_hi);
+  else if (k == 8) tile_body<8, false>(sg, a, s_img, t, w_lo, w_hi);
+  else tile_body<0, false>(sg, a, s_img, t, w_lo, w_hi);  // (k > 8 with 24-byte keys: eight bits)
   __syncthreads();
   uint8_t* payload = out + sg.out_offset;
-  const bool hdr = t == 0 && (a.tile0 == 0 || hdr_always);
+  const bool hdr = t == 0 && sp == 0 && (a.tile0 == 0 || hdr_always);
   if (hdr && tid < 4) write_bloom_header(payload, sg, tid);
   else if (hdr && tid < 8) write_page_header(out, sg, kLayoutBloom, tid - 4);
-  uint4* dst = reinterpret_cast<uint4*>(payload + kBloomHeader + 64ull * first);
+  uint4* dst = reinterpret_cast<uint4*>(S > 1 ? a.part_img + ((uint64_t)(t * S + sp) << 17)
+                                              : payload + kBloomHeader + 64ull * first);
   const uint4* src = reinterpret_cast<const uint4*>(s_img);
   for (uint32_t q = tid; q < tb * 4; q += kTileThreads) dst[q] = src[q];
+}
+
+// a split tile's partial images ORed into the filter: workgroup (t, c) merges uint4s
+// [c * 256, (c + 1) * 256) of tile t, one per thread, its S partial loads issued together
+constexpr uint32_t kMergeChunks = kTileBlocks * 4 / 256;  // 32 per tile
+constexpr uint32_t kMaxSplit = 16;
+__device__ __attribute__((always_inline)) inline void tile_merge_run(const tkv_amq_segment& sg, const PartArgs& a,
+                                                                     uint8_t* __restrict__ out)
+{
+  const uint32_t x = blockIdx.x - a.wg0, t = x / kMergeChunks, c = x - t * kMergeChunks;
+  const uint32_t S = a.split, first = (a.tile0 + t) * kTileBlocks;
+  const uint32_t tb = min(kTileBlocks, sg.n_blocks - first);
+  const uint32_t q = c * 256 + threadIdx.x;
+  if (q >= tb * 4) return;
+  const uint4* src = reinterpret_cast<const uint4*>(a.part_img + ((uint64_t)t * S << 17)) + q;
+  uint4 w[kMaxSplit];
+#pragma unroll
+  for (uint32_t sp = 0; sp < kMaxSplit; ++sp)
+    w[sp] = sp < S ? load_nt16(src + ((uint64_t)sp << 13)) : make_uint4(0, 0, 0, 0);
+  uint4 v = w[0];
+#pragma unroll
+  for (uint32_t sp = 1; sp < kMaxSplit; ++sp) {
+    v.x |= w[sp].x;
+    v.y |= w[sp].y;
+    v.z |= w[sp].z;
+    v.w |= w[sp].w;
+  }
+  reinterpret_cast<uint4*>(out + sg.out_offset + kBloomHeader + 64ull * first)[q] = v;
+}
+
+__global__ __launch_bounds__(256) void bloom_tile_merge(const tkv_amq_segment* __restrict__ segs, PartArgs a,
+                                                         uint8_t* __restrict__ out)
+{
+  const tkv_amq_segment sg = segs[0];
+  if (sg.hash_count == 0) return;
+  tile_merge_run(sg, a, out);
 }
 
 __global__ __launch_bounds__(kTileThreads) void bloom_tile(const tkv_amq_segment* __restrict__ segs,
@@ -2114,22 +2160,24 @@ __global__ __launch_bounds__(256) void bloom_overflow(const tkv_amq_segment* __r
 // instead of holding them in registers), with the first tile workgroup and the segment of
 // each; a workgroup finds its leaf by a binary search over the first workgroups.
 // ---------------------------------------------------------------------------------------
-constexpr uint32_t kMultiMaxLeaves = 15;
+constexpr uint32_t kMultiMaxLeaves = 14;
 struct MultiParts {
   uint32_t n;                      // leaves
   uint32_t tg0[kMultiMaxLeaves];   // the leaf's first tile workgroup (a[i].wg0: partition)
+  uint32_t mg0[kMultiMaxLeaves];   // its first merge workgroup (split tiles)
   uint32_t seg[kMultiMaxLeaves];   // its segment in the batch
   PartArgs a[kMultiMaxLeaves];
 };
 static_assert(sizeof(MultiParts) <= 4096 - 32, "kernel argument");
 
-template <bool TILE>
+// GRID 0: partition / overflow, 1: tile, 2: merge
+template <int GRID>
 __device__ inline uint32_t multi_find(const MultiParts& m)
 {
   uint32_t lo = 0, hi = m.n;  // the last leaf whose first workgroup is <= blockIdx.x
   while (hi - lo > 1) {
     const uint32_t mid = (lo + hi) >> 1;
-    if ((TILE ? m.tg0[mid] : m.a[mid].wg0) <= blockIdx.x) lo = mid;
+    if ((GRID == 1 ? m.tg0[mid] : GRID == 2 ? m.mg0[mid] : m.a[mid].wg0) <= blockIdx.x) lo = mid;
     else hi = mid;
   }
   return lo;
@@ -2139,7 +2187,7 @@ __global__ __launch_bounds__(kPartThreads) void bloom_part_multi16(const tkv_amq
                                                                    MultiParts m)
 {
   extern __shared__ __attribute__((aligned(16))) uint32_t s_part[];
-  const uint32_t l = multi_find<false>(m);
+  const uint32_t l = multi_find<0>(m);
   const tkv_amq_segment sg = segs[m.seg[l]];
   part_keys16(sg, m.a[l], s_part);
 }
@@ -2148,7 +2196,7 @@ __global__ __launch_bounds__(kPartThreads) void bloom_part_multi24(const tkv_amq
                                                                    MultiParts m)
 {
   extern __shared__ __attribute__((aligned(16))) uint32_t s_part[];
-  const uint32_t l = multi_find<false>(m);
+  const uint32_t l = multi_find<0>(m);
   const tkv_amq_segment sg = segs[m.seg[l]];
   part_keys24(sg, m.a[l], s_part);
 }
@@ -2157,17 +2205,27 @@ __global__ __launch_bounds__(kTileThreads) void bloom_tile_multi(const tkv_amq_s
                                                                  MultiParts m, uint8_t* __restrict__ out)
 {
   extern __shared__ __attribute__((aligned(16))) uint32_t s_img[];
-  const uint32_t l = multi_find<true>(m);
+  const uint32_t l = multi_find<1>(m);
   const tkv_amq_segment sg = segs[m.seg[l]];
   PartArgs a = m.a[l];
   a.wg0 = m.tg0[l];
   tile_run(sg, a, out, 0u, s_img);
 }
 
+__global__ __launch_bounds__(256) void bloom_tile_merge_multi(const tkv_amq_segment* __restrict__ segs,
+                                                              MultiParts m, uint8_t* __restrict__ out)
+{
+  const uint32_t l = multi_find<2>(m);
+  const tkv_amq_segment sg = segs[m.seg[l]];
+  PartArgs a = m.a[l];
+  a.wg0 = m.mg0[l];
+  tile_merge_run(sg, a, out);
+}
+
 __global__ __launch_bounds__(256) void bloom_overflow_multi(const tkv_amq_segment* __restrict__ segs,
                                                             MultiParts m, uint8_t* __restrict__ out)
 {
-  const uint32_t l = multi_find<false>(m);
+  const uint32_t l = multi_find<0>(m);
   const tkv_amq_segment sg = segs[m.seg[l]];
   overflow_run(sg, m.a[l], out);
 }
@@ -4737,9 +4795,25 @@ inline void launch_part_build(int src, PartArgs a, hipStream_t s, const tkv_amq_
   if (src == kSrcKey24) hipLaunchKernelGGL(bloom_part_keys24, grid, block, lds, s, d_segs, a);
   else if (src == kSrcKey16) hipLaunchKernelGGL(bloom_part_keys16, grid, block, lds, s, d_segs, a);
   else hipLaunchKernelGGL(bloom_part_routed, grid, block, lds, s, d_segs, a);
-  hipLaunchKernelGGL(bloom_tile, dim3(a.g.n_tiles), dim3(kTileThreads), 64ull * kTileBlocks, s, d_segs, a,
+  const uint32_t S = a.split > 1 ? a.split : 1u;
+  hipLaunchKernelGGL(bloom_tile, dim3(a.g.n_tiles * S), dim3(kTileThreads), 64ull * kTileBlocks, s, d_segs, a,
                      d_out, hdr_always);
+  if (S > 1) hipLaunchKernelGGL(bloom_tile_merge, dim3(a.g.n_tiles * kMergeChunks), dim3(256), 0, s, d_segs, a, d_out);
   hipLaunchKernelGGL(bloom_overflow, dim3(a.g.P), dim3(256), 0, s, d_segs, a, d_out);
+}
+
+// Tile workgroups per tile for a filter of T tiles: one tile per CU leaves most of the chip
+// idle below 256 tiles (a tile's ~100K records take ~50 us of LDS ORs on one CU), so below 128
+// each tile's regions are split over S workgroups (T * S <= 256), their partial images ORed
+// by bloom_tile_merge; the partial images take T * S * 128 KiB <= kSplitImgBytes.
+constexpr uint64_t kSplitImgBytes = 256ull << 17;
+inline uint32_t tile_split(uint32_t T) { return T == 0 || T >= 128 ? 1u : std::min(kMaxSplit, 256u / T); }
+
+// partition workgroups of a monolithic build of n keys (several leaves: all of them): the keys
+// / 256 each, at least 1,024 and at most `most` -- every CU works, on fewer batches each
+inline uint64_t mono_wg_items(uint64_t n, uint64_t most)
+{
+  return std::min<uint64_t>(most, std::max<uint64_t>(1024, n / kPartMaxWgs));
 }
 
 // The route of n keys (16 or 24 bytes) into g.n_parts parts of q tiles: the count pass, the two
@@ -4976,6 +5050,8 @@ struct MonoPlan {
   RouteGeom rg;      // (the two-pass route)
   uint64_t items_off, part_off;
   PartGeom pg;       // a part of q tiles (every part's own geometry is no larger)
+  uint32_t split;    // g == 1: tile workgroups per tile (tile_split), partial images at img_off
+  uint64_t img_off;
   uint64_t bytes;
 };
 
@@ -4989,8 +5065,10 @@ inline MonoPlan mono_plan(uint64_t n_keys, uint64_t n_blocks)
   if (m.T <= kDirectMaxTiles) {
     m.g = 1;
     m.q = m.T;
-    m.pg = part_geom(n_keys, n_keys, m.T, 16);
-    m.bytes = m.pg.bytes;
+    m.pg = part_geom(n_keys, n_keys, m.T, 16, mono_wg_items(n_keys, 32ull * kPartThreads));
+    m.split = tile_split(m.T);
+    m.img_off = align256(m.pg.bytes);
+    m.bytes = m.split > 1 ? m.img_off + (uint64_t)m.T * m.split * (64ull * kTileBlocks) : m.pg.bytes;
     return m;
   }
   if (m.k >= 1 && m.k <= 8 && route_plan(n_keys, 1, n_blocks, m.k, 1, false, m.rp) == TKV_AMQ_OK) {
@@ -5030,7 +5108,9 @@ inline void launch_mono(const MonoPlan& m, hipStream_t s, const uint8_t* keys, u
   // (key0: the segment's key_begin, for the two-pass route, which reads keys [0, n) of its
   // pointer; the other paths add the segment's key_begin themselves)
   if (m.g == 1) {
-    const PartArgs a{keys, n, 0u, 1u, kb, nullptr, 0u, ws, m.pg};
+    PartArgs a{keys, n, 0u, 1u, kb, nullptr, 0u, ws, m.pg};
+    a.split = m.split;
+    a.part_img = ws + m.img_off;
     launch_part_build(kb == 24 ? kSrcKey24 : kSrcKey16, a, s, d_segs, d_out, 0u);
     return;
   }
@@ -5087,10 +5167,7 @@ inline uint64_t bloom_batch_ws_bytes(uint32_t n_segs, uint64_t n_keys, uint64_t 
 // leaf larger than it runs alone).
 constexpr uint64_t kMultiWsBudget = 2ull << 30;
 
-inline uint64_t multi_wg_items(uint64_t multi_keys)
-{
-  return std::min<uint64_t>(8ull * kPartBatch, std::max<uint64_t>(2ull * kPartBatch, multi_keys / kPartMaxWgs));
-}
+inline uint64_t multi_wg_items(uint64_t multi_keys) { return mono_wg_items(multi_keys, 8ull * kPartBatch); }
 
 inline bool multi_leaf(uint64_t n_keys, uint64_t n_blocks)
 {
@@ -5116,6 +5193,20 @@ inline size_t multi_lds_bytes(uint32_t n_tiles)
   return part_tbl_fits(n_tiles) ? part_tbl_lds_bytes(n_tiles) : part_lds_bytes(n_tiles);
 }
 
+// the leaves' tile grids (T_l * S each) and merge grids (T_l * kMergeChunks, split tiles only)
+// for the group's tile split S, and its partial images from split_img
+inline void multi_split(MultiParts& m, uint32_t n_tiles, uint8_t* split_img)
+{
+  const uint32_t S = tile_split(n_tiles);
+  for (uint32_t i = 0; i < m.n; ++i) {
+    const uint32_t t0 = m.tg0[i];
+    m.a[i].split = S;
+    m.a[i].part_img = split_img + ((uint64_t)t0 * S << 17);
+    m.tg0[i] = t0 * S;
+    m.mg0[i] = t0 * kMergeChunks;
+  }
+}
+
 inline void launch_multi(const MultiParts& m, uint32_t kb, uint32_t n_wgs, uint32_t n_tiles, size_t lds,
                          hipStream_t s, const tkv_amq_segment* d_segs, uint8_t* d_out)
 {
@@ -5129,7 +5220,11 @@ inline void launch_multi(const MultiParts& m, uint32_t kb, uint32_t n_wgs, uint3
   });
   if (kb == 24) hipLaunchKernelGGL(bloom_part_multi24, dim3(n_wgs), dim3(kPartThreads), lds, s, d_segs, m);
   else hipLaunchKernelGGL(bloom_part_multi16, dim3(n_wgs), dim3(kPartThreads), lds, s, d_segs, m);
-  hipLaunchKernelGGL(bloom_tile_multi, dim3(n_tiles), dim3(kTileThreads), 64ull * kTileBlocks, s, d_segs, m, d_out);
+  const uint32_t S = m.n ? (m.a[0].split > 1 ? m.a[0].split : 1u) : 1u;
+  hipLaunchKernelGGL(bloom_tile_multi, dim3(n_tiles * S), dim3(kTileThreads), 64ull * kTileBlocks, s, d_segs, m,
+                     d_out);
+  if (S > 1)
+    hipLaunchKernelGGL(bloom_tile_merge_multi, dim3(n_tiles * kMergeChunks), dim3(256), 0, s, d_segs, m, d_out);
   hipLaunchKernelGGL(bloom_overflow_multi, dim3(n_wgs), dim3(256), 0, s, d_segs, m, d_out);
 }
 
@@ -5153,7 +5248,7 @@ inline uint64_t bloom_oversize_ws_bytes(const tkv_amq_segment* segs, uint32_t n_
     }
   }
   const uint64_t small = n_small ? bloom_batch_ws_bytes(n_small, small_keys, small_max) : 0;
-  const uint64_t multi = std::min(multi_sum, std::max(multi_max, kMultiWsBudget));
+  const uint64_t multi = multi_sum ? std::min(multi_sum, std::max(multi_max, kMultiWsBudget)) + kSplitImgBytes : 0;
   return align256(64ull * n_segs) + std::max(std::max(small, big), multi);
 }
 
@@ -5776,8 +5871,14 @@ int tkv_amq_build_ex(int kind, const uint8_t* keys, const uint64_t* offs, uint32
   uint64_t used = 0;
   uint32_t wgs = 0, tiles = 0;
   size_t lds = 0;
+  // the group's partial tile images first, then the leaves' workspaces
+  uint8_t* const mrest = rest + kSplitImgBytes;
+  const uint64_t mbudget = rest_bytes > kSplitImgBytes ? rest_bytes - kSplitImgBytes : 0;
   auto flush = [&] {
-    if (m.n) launch_multi(m, mkb, wgs, tiles, lds, s, d_segs, d_out);
+    if (m.n) {
+      multi_split(m, tiles, rest);
+      launch_multi(m, mkb, wgs, tiles, lds, s, d_segs, d_out);
+    }
     m.n = 0;
     used = 0;
     wgs = tiles = 0;
@@ -5791,15 +5892,15 @@ int tkv_amq_build_ex(int kind, const uint8_t* keys, const uint64_t* offs, uint32
     if (multi_keys && multi_leaf(g.n_keys, g.n_blocks)) {
       const PartGeom pg = multi_geom(g.n_keys, g.n_blocks, wg_items);
       const uint64_t b = align256(pg.bytes);
-      if (b <= rest_bytes) {
-        if (m.n == kMultiMaxLeaves || used + b > rest_bytes) flush();
+      if (b <= mbudget) {
+        if (m.n == kMultiMaxLeaves || used + b > mbudget) flush();
         PartArgs& a = m.a[m.n];
         a = PartArgs{};
         a.src = keys;
         a.n = (uint32_t)g.n_keys;
         a.from_seg = 1;
         a.kb = mkb;
-        a.ws = rest + used;
+        a.ws = mrest + used;
         a.g = pg;
         a.src_kind = mkb == 24 ? (uint32_t)kSrcKey24 : (uint32_t)kSrcKey16;
         a.tbl = part_tbl_fits(pg.n_tiles) ? 1u : 0u;
