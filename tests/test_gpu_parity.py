@@ -586,8 +586,8 @@ def test_vqf_hash_matches_xxhash(amq, torch):
                                          (1100000, 5, 11), (90000, 64, 12), (8_000_000, 10, 13),
                                          (14_000_000, 10, 14)])
 def test_bloom_monolithic_partitioned(oracle, amq, torch, n, bpk, seed):
-    """One filter of 16-byte keys larger than four LDS windows (640 KB; smaller ones take the
-    window path, tests/test_gpu_window.py): the hash-once record path (bloom_part_keys16 /
+    """One filter of 16-byte keys larger than one LDS window (160 KB; tests/test_gpu_window.py
+    has 2-4-window ones too): the hash-once record path (bloom_part_keys16 /
     bloom_tile), byte-identical to the oracle.  Covers a ragged last tile, k = 7 / 8 /
     generic <= 8 (12-byte bit records) and k = 44 (the keys themselves are partitioned and
     hashed per tile); below 128 tiles each tile's regions split over up to 16 tile workgroups
@@ -604,7 +604,7 @@ def test_bloom_monolithic_partitioned(oracle, amq, torch, n, bpk, seed):
                                        (400000, 14, 0), (90000, 64, 0), (700000, 10, 200000),
                                        (450000, 14, 150000)])
 def test_bloom_monolithic_k24(oracle, amq, torch, n, bpk, dup):
-    """One filter of 24-byte keys (TurtleKV's default key size) beyond four windows: the record
+    """One filter of 24-byte keys (TurtleKV's default key size) beyond one window: the record
     path's own partition kernel (bloom_part_keys24) hashes each key once into a 12-byte bit
     record; k > 8 (14 and 64 bits/key) keeps the first eight bits in the records and
     bloom_overflow sets the others; duplicates overflow the regions of one tile.

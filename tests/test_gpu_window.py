@@ -3,7 +3,7 @@ window path (bloom_build_window + bloom_split_merge).  Round 2 sent these leaves
 atomics (~40x slower).  Every case is byte-compared with the CPU oracle, leaf by leaf:
 the verdict's 70 x 200K-key batch at 12 bits/key, 2..16 windows per leaf, leaves of one
 window mixed with leaves of several, every key shape (16-, 24-, 20-byte and variable-length
-keys), k = 3 / 7 / 8 / 11 / 32, one filter alone (the window path for <= 4 windows), and the
+keys), k = 3 / 7 / 8 / 11 / 32, one filter alone (the window path for variable-length keys; 16-byte keys take the tiled build), and the
 one-part fallback when the caller passes no workspace for partial images."""
 import numpy as np
 import pytest
@@ -73,14 +73,27 @@ def test_window_key_shapes(oracle, amq, torch, shape):
         assert_same(plan, out, ref)
 
 
+@pytest.mark.parametrize("shape", ["k16", "var"])
 @pytest.mark.parametrize("n,bpk", [(200_000, 10), (400_000, 5), (30_000, 64), (500_000, 10)])
-def test_window_one_filter(oracle, amq, torch, n, bpk):
-    """One filter of <= 4 windows (the per-leaf call site's big leaf) takes the window path,
-    split into parts over the chip; k = 7, 3 and 32."""
-    keys = oracle.gen_keys16(34, 0, n)
-    plan, out = gpu_build(amq, torch, 0, torch.from_numpy(keys).cuda(), [n], bpk)
+def test_window_one_filter(oracle, amq, torch, n, bpk, shape):
+    """One filter of 2-4 windows (the per-leaf call site's big leaf), k = 7, 3 and 32: 16-byte
+    keys take the tiled build (a few tiles, each split over the chip), variable-length keys
+    the window path, split into parts over the chip."""
+    if shape == "k16":
+        keys = oracle.gen_keys16(34, 0, n)
+        plan, out = gpu_build(amq, torch, 0, torch.from_numpy(keys).cuda(), [n], bpk)
+        ref = oracle_per_segment(oracle, 0, keys, [n], bpk)
+    else:
+        rng = np.random.default_rng(n + bpk)
+        lens = rng.integers(8, 32, n)
+        keys = rng.integers(0, 256, int(lens.sum()), dtype=np.uint8)
+        offs = np.zeros(n + 1, np.int64)
+        offs[1:] = np.cumsum(lens)
+        plan, out = gpu_build(amq, torch, 0, torch.from_numpy(keys).cuda(), [n], bpk,
+                              offsets_t=torch.from_numpy(offs).cuda())
+        ref = oracle_per_segment(oracle, 0, keys, [n], bpk, stride=0, offsets=offs.astype(np.uint64))
     assert 2 <= windows(plan) <= 4
-    assert_same(plan, out, oracle_per_segment(oracle, 0, keys, [n], bpk))
+    assert_same(plan, out, ref)
 
 
 def test_window_without_workspace_one_part(oracle, amq, torch):

@@ -4636,9 +4636,11 @@ inline uint64_t bloom_split_ws_bytes(uint32_t n_segs, uint32_t parts, uint64_t m
 }
 
 // The window path (bloom_build_window): leaves whose image exceeds kBloomLeafLdsBudget, cut
-// into W windows.  A single 16-byte-key filter of more than kWinMonoMax windows takes the tiled
-// monolithic build instead (it hashes each key once, whatever the tile count).
-constexpr uint32_t kWinMonoMax = 4;
+// into W windows.  A single 16- or 24-byte-key filter of more than kWinMonoMax windows takes
+// the tiled monolithic build instead (it hashes each key once, whatever the tile count; since
+// round 5 its few tiles are split over the chip, so it wins from two windows on: one 200K-key
+// filter 53.3 vs 28.7 us, 500K 95.3 vs 34.3 us, profiles/r05/winmono/).
+constexpr uint32_t kWinMonoMax = 1;
 constexpr uint32_t kChipCUs = 256;  // MI355X; plans are made without a device
 
 inline uint32_t bloom_window_count(uint64_t max_blocks)
