@@ -2003,10 +2003,11 @@ __device__ void tile_body(const tkv_amq_segment& sg, const PartArgs& a, uint32_t
   (void)P;
 }
 
+// (wg0: the build's first tile workgroup in the grid)
 __device__ __attribute__((always_inline)) inline void tile_run(const tkv_amq_segment& sg, const PartArgs& a, uint8_t* __restrict__ out,
-                                uint32_t hdr_always, uint32_t* s_img)
+                                uint32_t hdr_always, uint32_t* s_img, uint32_t wg0)
 {
-  const uint32_t x = blockIdx.x - a.wg0, tid = threadIdx.x, k = sg.hash_count;
+  const uint32_t x = blockIdx.x - wg0, tid = threadIdx.x, k = sg.hash_count;
   if (k == 0) return;
   const uint32_t S = a.split > 1 ? a.split : 1u;
   const uint32_t t = x / S, sp = x - t * S;  // tile, and its share of the regions
@@ -2036,9 +2037,9 @@ __device__ __attribute__((always_inline)) inline void tile_run(const tkv_amq_seg
 constexpr uint32_t kMergeChunks = kTileBlocks * 4 / 256;  // 32 per tile
 constexpr uint32_t kMaxSplit = 16;
 __device__ __attribute__((always_inline)) inline void tile_merge_run(const tkv_amq_segment& sg, const PartArgs& a,
-                                                                     uint8_t* __restrict__ out)
+                                                                     uint8_t* __restrict__ out, uint32_t wg0)
 {
-  const uint32_t x = blockIdx.x - a.wg0, t = x / kMergeChunks, c = x - t * kMergeChunks;
+  const uint32_t x = blockIdx.x - wg0, t = x / kMergeChunks, c = x - t * kMergeChunks;
   const uint32_t S = a.split, first = (a.tile0 + t) * kTileBlocks;
   const uint32_t tb = min(kTileBlocks, sg.n_blocks - first);
   const uint32_t q = c * 256 + threadIdx.x;
@@ -2064,7 +2065,7 @@ __global__ __launch_bounds__(256) void bloom_tile_merge(const tkv_amq_segment* _
 {
   const tkv_amq_segment sg = segs[0];
   if (sg.hash_count == 0) return;
-  tile_merge_run(sg, a, out);
+  tile_merge_run(sg, a, out, 0u);
 }
 
 __global__ __launch_bounds__(kTileThreads) void bloom_tile(const tkv_amq_segment* __restrict__ segs,
@@ -2073,7 +2074,7 @@ __global__ __launch_bounds__(kTileThreads) void bloom_tile(const tkv_amq_segment
 {
   extern __shared__ __attribute__((aligned(16))) uint32_t s_img[];
   const tkv_amq_segment sg = segs[0];
-  tile_run(sg, a, out, hdr_always, s_img);
+  tile_run(sg, a, out, hdr_always, s_img, 0u);
 }
 
 // the filter header alone (a hash-range shard that owns no tile still returns a whole header)
@@ -2160,15 +2161,49 @@ __global__ __launch_bounds__(256) void bloom_overflow(const tkv_amq_segment* __r
 // instead of holding them in registers), with the first tile workgroup and the segment of
 // each; a workgroup finds its leaf by a binary search over the first workgroups.
 // ---------------------------------------------------------------------------------------
-constexpr uint32_t kMultiMaxLeaves = 14;
+// Per leaf, what its PartArgs need beyond the launch's shared fields, all precomputed on the
+// host: the kernels copy them from the kernel argument (constant memory, re-read rather than
+// held in registers), never compute them
+struct MultiLeaf {
+  uint8_t* ws;
+  uint8_t* part_img;
+  uint64_t counts_off, ovf_n_off, regions_off, ovf_off;
+  uint32_t n, P, n_tiles, per, cap, tbl, split;
+  uint32_t wg0, tg0, mg0;  // the leaf's first partition / tile / merge workgroup
+  uint32_t seg;            // its segment in the batch
+};
+constexpr uint32_t kMultiMaxLeaves = 40;
 struct MultiParts {
-  uint32_t n;                      // leaves
-  uint32_t tg0[kMultiMaxLeaves];   // the leaf's first tile workgroup (a[i].wg0: partition)
-  uint32_t mg0[kMultiMaxLeaves];   // its first merge workgroup (split tiles)
-  uint32_t seg[kMultiMaxLeaves];   // its segment in the batch
-  PartArgs a[kMultiMaxLeaves];
+  const uint8_t* keys;
+  uint32_t kb, n;
+  MultiLeaf l[kMultiMaxLeaves];
 };
 static_assert(sizeof(MultiParts) <= 4096 - 32, "kernel argument");
+
+__device__ __attribute__((always_inline)) inline PartArgs multi_args(const MultiParts& m, const MultiLeaf& l)
+{
+  PartArgs a{};
+  a.src = m.keys;
+  a.n = l.n;
+  a.from_seg = 1;
+  a.kb = m.kb;
+  a.ws = l.ws;
+  a.g.P = l.P;
+  a.g.n_tiles = l.n_tiles;
+  a.g.per = l.per;
+  a.g.cap = l.cap;
+  a.g.rb = 16;
+  a.g.counts_off = l.counts_off;
+  a.g.ovf_n_off = l.ovf_n_off;
+  a.g.regions_off = l.regions_off;
+  a.g.ovf_off = l.ovf_off;
+  a.src_kind = m.kb == 24 ? kSrcKey24 : kSrcKey16;
+  a.tbl = l.tbl;
+  a.wg0 = l.wg0;
+  a.split = l.split;
+  a.part_img = l.part_img;
+  return a;
+}
 
 // GRID 0: partition / overflow, 1: tile, 2: merge
 template <int GRID>
@@ -2177,7 +2212,8 @@ __device__ inline uint32_t multi_find(const MultiParts& m)
   uint32_t lo = 0, hi = m.n;  // the last leaf whose first workgroup is <= blockIdx.x
   while (hi - lo > 1) {
     const uint32_t mid = (lo + hi) >> 1;
-    if ((GRID == 1 ? m.tg0[mid] : GRID == 2 ? m.mg0[mid] : m.a[mid].wg0) <= blockIdx.x) lo = mid;
+    const MultiLeaf& x = m.l[mid];
+    if ((GRID == 1 ? x.tg0 : GRID == 2 ? x.mg0 : x.wg0) <= blockIdx.x) lo = mid;
     else hi = mid;
   }
   return lo;
@@ -2187,47 +2223,43 @@ __global__ __launch_bounds__(kPartThreads) void bloom_part_multi16(const tkv_amq
                                                                    MultiParts m)
 {
   extern __shared__ __attribute__((aligned(16))) uint32_t s_part[];
-  const uint32_t l = multi_find<0>(m);
-  const tkv_amq_segment sg = segs[m.seg[l]];
-  part_keys16(sg, m.a[l], s_part);
+  const MultiLeaf& l = m.l[multi_find<0>(m)];
+  const tkv_amq_segment sg = segs[l.seg];
+  part_keys16(sg, multi_args(m, l), s_part);
 }
 
 __global__ __launch_bounds__(kPartThreads) void bloom_part_multi24(const tkv_amq_segment* __restrict__ segs,
                                                                    MultiParts m)
 {
   extern __shared__ __attribute__((aligned(16))) uint32_t s_part[];
-  const uint32_t l = multi_find<0>(m);
-  const tkv_amq_segment sg = segs[m.seg[l]];
-  part_keys24(sg, m.a[l], s_part);
+  const MultiLeaf& l = m.l[multi_find<0>(m)];
+  const tkv_amq_segment sg = segs[l.seg];
+  part_keys24(sg, multi_args(m, l), s_part);
 }
 
 __global__ __launch_bounds__(kTileThreads) void bloom_tile_multi(const tkv_amq_segment* __restrict__ segs,
                                                                  MultiParts m, uint8_t* __restrict__ out)
 {
   extern __shared__ __attribute__((aligned(16))) uint32_t s_img[];
-  const uint32_t l = multi_find<1>(m);
-  const tkv_amq_segment sg = segs[m.seg[l]];
-  PartArgs a = m.a[l];
-  a.wg0 = m.tg0[l];
-  tile_run(sg, a, out, 0u, s_img);
+  const MultiLeaf& l = m.l[multi_find<1>(m)];
+  const tkv_amq_segment sg = segs[l.seg];
+  tile_run(sg, multi_args(m, l), out, 0u, s_img, l.tg0);
 }
 
 __global__ __launch_bounds__(256) void bloom_tile_merge_multi(const tkv_amq_segment* __restrict__ segs,
                                                               MultiParts m, uint8_t* __restrict__ out)
 {
-  const uint32_t l = multi_find<2>(m);
-  const tkv_amq_segment sg = segs[m.seg[l]];
-  PartArgs a = m.a[l];
-  a.wg0 = m.mg0[l];
-  tile_merge_run(sg, a, out);
+  const MultiLeaf& l = m.l[multi_find<2>(m)];
+  const tkv_amq_segment sg = segs[l.seg];
+  tile_merge_run(sg, multi_args(m, l), out, l.mg0);
 }
 
 __global__ __launch_bounds__(256) void bloom_overflow_multi(const tkv_amq_segment* __restrict__ segs,
                                                             MultiParts m, uint8_t* __restrict__ out)
 {
-  const uint32_t l = multi_find<0>(m);
-  const tkv_amq_segment sg = segs[m.seg[l]];
-  overflow_run(sg, m.a[l], out);
+  const MultiLeaf& l = m.l[multi_find<0>(m)];
+  const tkv_amq_segment sg = segs[l.seg];
+  overflow_run(sg, multi_args(m, l), out);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -5201,16 +5233,17 @@ inline void multi_split(MultiParts& m, uint32_t n_tiles, uint8_t* split_img)
 {
   const uint32_t S = tile_split(n_tiles);
   for (uint32_t i = 0; i < m.n; ++i) {
-    const uint32_t t0 = m.tg0[i];
-    m.a[i].split = S;
-    m.a[i].part_img = split_img + ((uint64_t)t0 * S << 17);
-    m.tg0[i] = t0 * S;
-    m.mg0[i] = t0 * kMergeChunks;
+    MultiLeaf& l = m.l[i];
+    const uint32_t t0 = l.tg0;
+    l.split = S;
+    l.part_img = split_img + ((uint64_t)t0 * S << 17);
+    l.tg0 = t0 * S;
+    l.mg0 = t0 * kMergeChunks;
   }
 }
 
-inline void launch_multi(const MultiParts& m, uint32_t kb, uint32_t n_wgs, uint32_t n_tiles, size_t lds,
-                         hipStream_t s, const tkv_amq_segment* d_segs, uint8_t* d_out)
+inline void launch_multi(const MultiParts& m, uint32_t kb, uint32_t n_wgs, uint32_t n_tiles, size_t lds, hipStream_t s,
+                         const tkv_amq_segment* d_segs, uint8_t* d_out)
 {
   static std::once_flag attr[kMaxDevices];
   once_per_device(attr, [] {
@@ -5222,7 +5255,7 @@ inline void launch_multi(const MultiParts& m, uint32_t kb, uint32_t n_wgs, uint3
   });
   if (kb == 24) hipLaunchKernelGGL(bloom_part_multi24, dim3(n_wgs), dim3(kPartThreads), lds, s, d_segs, m);
   else hipLaunchKernelGGL(bloom_part_multi16, dim3(n_wgs), dim3(kPartThreads), lds, s, d_segs, m);
-  const uint32_t S = m.n ? (m.a[0].split > 1 ? m.a[0].split : 1u) : 1u;
+  const uint32_t S = m.n ? (m.l[0].split > 1 ? m.l[0].split : 1u) : 1u;
   hipLaunchKernelGGL(bloom_tile_multi, dim3(n_tiles * S), dim3(kTileThreads), 64ull * kTileBlocks, s, d_segs, m,
                      d_out);
   if (S > 1)
@@ -5870,6 +5903,8 @@ int tkv_amq_build_ex(int kind, const uint8_t* keys, const uint64_t* offs, uint32
   // per launch as the workspace holds
   MultiParts m{};
   const uint32_t mkb = mode == kKey16 ? 16u : 24u;
+  m.keys = keys;
+  m.kb = mkb;
   uint64_t used = 0;
   uint32_t wgs = 0, tiles = 0;
   size_t lds = 0;
@@ -5896,19 +5931,22 @@ int tkv_amq_build_ex(int kind, const uint8_t* keys, const uint64_t* offs, uint32
       const uint64_t b = align256(pg.bytes);
       if (b <= mbudget) {
         if (m.n == kMultiMaxLeaves || used + b > mbudget) flush();
-        PartArgs& a = m.a[m.n];
-        a = PartArgs{};
-        a.src = keys;
-        a.n = (uint32_t)g.n_keys;
-        a.from_seg = 1;
-        a.kb = mkb;
-        a.ws = mrest + used;
-        a.g = pg;
-        a.src_kind = mkb == 24 ? (uint32_t)kSrcKey24 : (uint32_t)kSrcKey16;
-        a.tbl = part_tbl_fits(pg.n_tiles) ? 1u : 0u;
-        a.wg0 = wgs;
-        m.tg0[m.n] = tiles;
-        m.seg[m.n] = i;
+        MultiLeaf& l = m.l[m.n];
+        l = MultiLeaf{};
+        l.ws = mrest + used;
+        l.counts_off = pg.counts_off;
+        l.ovf_n_off = pg.ovf_n_off;
+        l.regions_off = pg.regions_off;
+        l.ovf_off = pg.ovf_off;
+        l.n = (uint32_t)g.n_keys;
+        l.P = pg.P;
+        l.n_tiles = pg.n_tiles;
+        l.per = pg.per;
+        l.cap = pg.cap;
+        l.tbl = part_tbl_fits(pg.n_tiles) ? 1u : 0u;
+        l.wg0 = wgs;
+        l.tg0 = tiles;
+        l.seg = i;
         ++m.n;
         used += b;
         wgs += pg.P;
