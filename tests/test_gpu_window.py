@@ -37,7 +37,8 @@ def test_verdict_batch_70_leaves_200k_keys_12bpk(oracle, amq, torch):
                                      (2_000_000, 10), (350_000, 5), (60_000, 32), (100_000, 16)])
 def test_window_counts_and_hash_counts(oracle, amq, torch, big, bpk):
     """2, 4, 10 and 16 windows (2M keys at 10 bits/key: 2.5 MB), k = 3 / 7 / 8 / 11 / 22, a
-    ragged mix of big, small, one-key and empty leaves in one batch."""
+    ragged mix of big, small, one-key and empty leaves in one batch (16-byte keys: the leaves
+    past 4 windows take the tiled build, the others the window path)."""
     rng = np.random.default_rng(big + bpk)
     counts = [int(c) for c in rng.integers(0, 3000, 12)]
     counts[0], counts[3], counts[7], counts[-1] = big, 1, 0, big // 3
@@ -45,6 +46,24 @@ def test_window_counts_and_hash_counts(oracle, amq, torch, big, bpk):
     plan, out = gpu_build(amq, torch, 0, torch.from_numpy(keys).cuda(), counts, bpk)
     assert 2 <= windows(plan) <= 16
     ref = oracle_per_segment(oracle, 0, keys, counts, bpk)
+    assert_same(plan, out, ref)
+
+
+@pytest.mark.parametrize("big", [1_000_000, 2_000_000])
+def test_window_many_windows_variable_keys(oracle, amq, torch, big):
+    """Variable-length keys keep the window path up to 16 windows in a batch (8 and 16 windows
+    at 10 bits/key), beside small leaves."""
+    rng = np.random.default_rng(big)
+    counts = [big, 3000, 0, big // 2, 17]
+    n = sum(counts)
+    lens = rng.integers(8, 32, n)
+    keys = rng.integers(0, 256, int(lens.sum()), dtype=np.uint8)
+    offs = np.zeros(n + 1, np.int64)
+    offs[1:] = np.cumsum(lens)
+    plan, out = gpu_build(amq, torch, 0, torch.from_numpy(keys).cuda(), counts, 10,
+                          offsets_t=torch.from_numpy(offs).cuda())
+    assert 8 <= windows(plan) <= 16
+    ref = oracle_per_segment(oracle, 0, keys, counts, 10, stride=0, offsets=offs.astype(np.uint64))
     assert_same(plan, out, ref)
 
 

@@ -9,5 +9,6 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout
   && tail -1 $O/smoke.log \
   && timeout -k 10 300 python -u tools/single_filter.py > $O/single.log 2>&1 \
   && timeout -k 10 300 python -u tools/oversize_batch.py > $O/oversize.log 2>&1 \
-  && grep -hv amdgpu.ids $O/single.log $O/oversize.log
+  && timeout -k 10 300 python -u tools/window_batch.py > $O/window_batch.log 2>&1 \
+  && grep -hv amdgpu.ids $O/single.log $O/oversize.log $O/window_batch.log
 rc=$?; echo "rc=$rc"; tail -5 $O/gpu_tests.log | grep -E "passed|failed|error" ; exit $rc

@@ -5183,8 +5183,17 @@ inline bool bloom_partitioned(uint32_t n_segs, uint64_t max_blocks, uint64_t n_k
 // others (tkv_amq_build_ex): the other leaves go through the batch kernels from a compacted
 // leaf list, each oversize leaf through the monolithic build of its own.  Workspace: the
 // compacted list, then the larger of the batch's and the biggest oversize leaf's needs.
-constexpr uint32_t kWinMaxBlocks = kWinMaxWindows * (kBloomLeafLdsBudget / 64);  // 16 windows
 inline bool bloom_oversize(uint64_t n_blocks) { return bloom_window_count(n_blocks) > kWinMaxWindows; }
+
+// In a batch of 16- or 24-byte keys the tiled build takes over from the window path earlier:
+// past kBatchMonoWindows windows (each window re-reads its part's keys and repeats their first
+// hash, the tiled build hashes every key once).  Measured (tools/window_batch.py, 10 bits/key,
+// Gkeys/s, window path vs tiled): 128 x 650K keys (5 windows) 44.4 vs 42.0, 64 x 1M (8) 31.5 vs
+// 68.6, 48 x 1.5M (12) 25.3 vs 68.0, 32 x 2M (16) 18.4 vs 67.8.  Other key shapes keep the
+// window path up to kWinMaxWindows.  (fixed: the batch's keys are 16 or 24 bytes)
+constexpr uint32_t kBatchMonoWindows = 5;
+inline uint32_t batch_window_max(bool fixed) { return fixed ? kBatchMonoWindows : kWinMaxWindows; }
+inline bool batch_tiled(uint64_t n_blocks, bool fixed) { return bloom_window_count(n_blocks) > batch_window_max(fixed); }
 
 inline uint64_t bloom_batch_ws_bytes(uint32_t n_segs, uint64_t n_keys, uint64_t max_blocks)
 {
@@ -5193,19 +5202,23 @@ inline uint64_t bloom_batch_ws_bytes(uint32_t n_segs, uint64_t n_keys, uint64_t 
   return bloom_split_ws_bytes(n_segs, bloom_split_parts(n_segs, n_keys, max_blocks), max_blocks);
 }
 
-// An oversize leaf of at most kDirectMaxTiles tiles joins a multi-leaf launch (bloom_part_multi).
-// Its partition workgroups take the batch's oversize keys / 256 each, between 2 and 8 batches:
-// few oversize keys still spread over every CU (a lone 3M-key leaf: 184 workgroups), many give
-// each workgroup a pipeline of 8 batches (64 x 3M keys: 46 per leaf), long enough to hide its
-// first load and last store.  The leaves of one launch share the workspace budget below (a
-// leaf larger than it runs alone).
+// A tiled leaf of at most kDirectMaxTiles tiles joins a multi-leaf launch (bloom_part_multi).
+// Its partition workgroups take the batch's tiled keys / 256 each, between 1,024 keys and 4
+// batches: few keys still spread over every CU (a lone 3M-key leaf: 256 workgroups), many give
+// each workgroup a pipeline of 4 batches and the chip several rounds of workgroups per launch,
+// so a short last round idles little of it.  Measured against 8 batches (Gkeys/s): 64 x 1M
+// keys 68.6 vs 64.2, 32 x 2M 67.8 vs 64.4, 8 x 3M + 200 x 16K 71.9 vs 63.4, 64 x 3M 70.6 vs
+// 72.2; a workgroup size chosen per launch from its keys (launch keys / 768) measured no
+// steadier (60.4 / 64.2 / 72.8 / 72.9).  The leaves of one launch share the workspace budget
+// below (a leaf larger than it runs alone).
 constexpr uint64_t kMultiWsBudget = 2ull << 30;
 
-inline uint64_t multi_wg_items(uint64_t multi_keys) { return mono_wg_items(multi_keys, 8ull * kPartBatch); }
+inline uint64_t multi_wg_items(uint64_t multi_keys) { return mono_wg_items(multi_keys, 4ull * kPartBatch); }
 
+// (a batch of 16- or 24-byte keys)
 inline bool multi_leaf(uint64_t n_keys, uint64_t n_blocks)
 {
-  return bloom_oversize(n_blocks) && filter_tiles(n_blocks) <= kDirectMaxTiles && n_keys <= 0xffffffffull;
+  return batch_tiled(n_blocks, true) && filter_tiles(n_blocks) <= kDirectMaxTiles && n_keys <= 0xffffffffull;
 }
 
 inline PartGeom multi_geom(uint64_t n_keys, uint64_t n_blocks, uint64_t wg_items)
@@ -5213,12 +5226,17 @@ inline PartGeom multi_geom(uint64_t n_keys, uint64_t n_blocks, uint64_t wg_items
   return part_geom(n_keys, n_keys, filter_tiles(n_blocks), 16, wg_items);
 }
 
-// the keys of a batch's multi-leaf candidates
-inline uint64_t multi_keys_of(const tkv_amq_segment* segs, uint32_t n_segs)
+// the keys (and, in `count`, the number) of a batch's multi-leaf candidates
+inline uint64_t multi_keys_of(const tkv_amq_segment* segs, uint32_t n_segs, uint32_t* count = nullptr)
 {
   uint64_t n = 0;
+  uint32_t c = 0;
   for (uint32_t i = 0; i < n_segs; ++i)
-    if (segs[i].bits_per_key && multi_leaf(segs[i].n_keys, segs[i].n_blocks)) n += segs[i].n_keys;
+    if (segs[i].bits_per_key && multi_leaf(segs[i].n_keys, segs[i].n_blocks)) {
+      n += segs[i].n_keys;
+      ++c;
+    }
+  if (count) *count = c;
   return n;
 }
 
@@ -5263,28 +5281,37 @@ inline void launch_multi(const MultiParts& m, uint32_t kb, uint32_t n_wgs, uint3
   hipLaunchKernelGGL(bloom_overflow_multi, dim3(n_wgs), dim3(256), 0, s, d_segs, m, d_out);
 }
 
+// The workspace of a tkv_amq_build_ex batch, for either key shape (the plan does not know
+// it): 16- or 24-byte keys -- the leaves past kBatchMonoWindows windows tiled (multi-leaf
+// launches, or alone past kDirectMaxTiles tiles), the others batched; other key shapes -- the
+// leaves up to kWinMaxWindows windows batched (the window path), the larger ones with device
+// atomics.  After the compacted leaf list.
 inline uint64_t bloom_oversize_ws_bytes(const tkv_amq_segment* segs, uint32_t n_segs)
 {
-  uint32_t n_small = 0;
-  uint64_t small_keys = 0, small_max = 0, big = 0, multi_sum = 0, multi_max = 0;
-  const uint64_t wg_items = multi_wg_items(multi_keys_of(segs, n_segs));
-  for (uint32_t i = 0; i < n_segs; ++i) {
-    const tkv_amq_segment& g = segs[i];
-    if (multi_leaf(g.n_keys, g.n_blocks)) {
-      const uint64_t b = align256(multi_geom(g.n_keys, g.n_blocks, wg_items).bytes);
-      multi_sum += b;
-      multi_max = std::max(multi_max, b);
-    } else if (bloom_oversize(g.n_blocks)) {
-      big = std::max(big, mono_plan(g.n_keys, g.n_blocks).bytes);
-    } else {
-      ++n_small;
-      small_keys += g.n_keys;
-      small_max = std::max<uint64_t>(small_max, g.n_blocks);
+  uint64_t need = 0;
+  for (const bool fixed : {true, false}) {
+    uint32_t n_small = 0;
+    uint64_t small_keys = 0, small_max = 0, big = 0, multi_sum = 0, multi_max = 0;
+    const uint64_t wg_items = multi_wg_items(multi_keys_of(segs, n_segs));
+    for (uint32_t i = 0; i < n_segs; ++i) {
+      const tkv_amq_segment& g = segs[i];
+      if (!batch_tiled(g.n_blocks, fixed)) {
+        ++n_small;
+        small_keys += g.n_keys;
+        small_max = std::max<uint64_t>(small_max, g.n_blocks);
+      } else if (fixed && multi_leaf(g.n_keys, g.n_blocks)) {
+        const uint64_t b = align256(multi_geom(g.n_keys, g.n_blocks, wg_items).bytes);
+        multi_sum += b;
+        multi_max = std::max(multi_max, b);
+      } else if (fixed) {
+        big = std::max(big, mono_plan(g.n_keys, g.n_blocks).bytes);
+      }
     }
+    const uint64_t small = n_small ? bloom_batch_ws_bytes(n_small, small_keys, small_max) : 0;
+    const uint64_t multi = multi_sum ? std::min(multi_sum, std::max(multi_max, kMultiWsBudget)) + kSplitImgBytes : 0;
+    need = std::max(need, std::max(std::max(small, big), multi));
   }
-  const uint64_t small = n_small ? bloom_batch_ws_bytes(n_small, small_keys, small_max) : 0;
-  const uint64_t multi = multi_sum ? std::min(multi_sum, std::max(multi_max, kMultiWsBudget)) + kSplitImgBytes : 0;
-  return align256(64ull * n_segs) + std::max(std::max(small, big), multi);
+  return align256(64ull * n_segs) + need;
 }
 
 }  // namespace
@@ -5491,7 +5518,7 @@ int tkv_amq_plan(int kind, const uint64_t* counts, const uint64_t* src_ids, uint
     else if (kind == TKV_AMQ_BLOOM)
       *ws_bytes = bloom_split_ws_bytes(n_segs, bloom_split_parts(n_segs, key_begin, max_blocks),
                                        max_blocks);
-    if (kind == TKV_AMQ_BLOOM && bpk != 0 && n_segs > 1 && bloom_window_count(max_blocks) > kWinMaxWindows)
+    if (kind == TKV_AMQ_BLOOM && bpk != 0 && n_segs > 1 && batch_tiled(max_blocks, true))
       *ws_bytes = bloom_oversize_ws_bytes(segs, n_segs);
   }
   if (max_blocks_out) *max_blocks_out = max_blocks;
@@ -5874,7 +5901,9 @@ int tkv_amq_build_ex(int kind, const uint8_t* keys, const uint64_t* offs, uint32
                      const tkv_amq_segment* d_segs, const tkv_amq_segment* h_segs, uint32_t n_segs,
                      uint32_t max_blocks, uint8_t* d_out, void* d_ws, uint64_t ws_bytes, void* stream)
 {
-  if (kind != TKV_AMQ_BLOOM || !h_segs || n_segs < 2 || !bloom_oversize(max_blocks))
+  const int mode = key_mode(offs, stride), bmode = build_key_mode(keys, offs, stride);
+  const bool fixed = mode == kKey16 || bmode == kKey24;  // the tiled build takes these keys
+  if (kind != TKV_AMQ_BLOOM || !h_segs || n_segs < 2 || !batch_tiled(max_blocks, fixed))
     return tkv_amq_build(kind, keys, offs, stride, n_keys, d_segs, n_segs, max_blocks, d_out, d_ws, ws_bytes,
                          stream);
   if (tkv_amq_device_count() == 0) return TKV_AMQ_UNAVAILABLE;
@@ -5887,19 +5916,19 @@ int tkv_amq_build_ex(int kind, const uint8_t* keys, const uint64_t* offs, uint32
   const uint64_t rest_bytes = ws_bytes - list_bytes;
   uint32_t n_small = 0, small_max = 0;
   for (uint32_t i = 0; i < n_segs; ++i)
-    if (!bloom_oversize(h_segs[i].n_blocks)) {
+    if (!batch_tiled(h_segs[i].n_blocks, fixed)) {
       ++n_small;
       small_max = std::max(small_max, h_segs[i].n_blocks);
     }
   if (n_small) {
     tkv_amq_segment* list = reinterpret_cast<tkv_amq_segment*>(ws);
-    hipLaunchKernelGGL(bloom_compact_segs, dim3(1), dim3(1024), 0, s, d_segs, n_segs, kWinMaxBlocks, list);
+    const uint32_t small_blocks = batch_window_max(fixed) * (kBloomLeafLdsBudget / 64);
+    hipLaunchKernelGGL(bloom_compact_segs, dim3(1), dim3(1024), 0, s, d_segs, n_segs, small_blocks, list);
     const int st = tkv_amq_build(kind, keys, offs, stride, n_keys, list, n_small, small_max, d_out, rest,
                                  rest_bytes, stream);
     if (st != TKV_AMQ_OK) return st;
   }
-  const int mode = key_mode(offs, stride), bmode = build_key_mode(keys, offs, stride);
-  // the oversize leaves of at most kDirectMaxTiles tiles: multi-leaf launches, as many leaves
+  // the tiled leaves of at most kDirectMaxTiles tiles: multi-leaf launches, as many leaves
   // per launch as the workspace holds
   MultiParts m{};
   const uint32_t mkb = mode == kKey16 ? 16u : 24u;
@@ -5921,16 +5950,20 @@ int tkv_amq_build_ex(int kind, const uint8_t* keys, const uint64_t* offs, uint32
     wgs = tiles = 0;
     lds = 0;
   };
-  const bool multi_keys = mode == kKey16 || bmode == kKey24;
-  const uint64_t wg_items = multi_wg_items(multi_keys_of(h_segs, n_segs));
+  const bool multi_keys = fixed;
+  uint32_t n_multi = 0;
+  const uint64_t tiled_keys = multi_keys_of(h_segs, n_segs, &n_multi);
+  const uint64_t wg_items = multi_wg_items(tiled_keys);
+  // leaves per launch: as even as the launches allow (no short last launch)
+  const uint32_t per_launch = n_multi ? (uint32_t)div_up(n_multi, div_up(n_multi, kMultiMaxLeaves)) : 1u;
   for (uint32_t i = 0; i < n_segs; ++i) {
     const tkv_amq_segment& g = h_segs[i];
-    if (!bloom_oversize(g.n_blocks) || g.bits_per_key == 0) continue;
+    if (!batch_tiled(g.n_blocks, fixed) || g.bits_per_key == 0) continue;
     if (multi_keys && multi_leaf(g.n_keys, g.n_blocks)) {
       const PartGeom pg = multi_geom(g.n_keys, g.n_blocks, wg_items);
       const uint64_t b = align256(pg.bytes);
       if (b <= mbudget) {
-        if (m.n == kMultiMaxLeaves || used + b > mbudget) flush();
+        if (m.n == per_launch || used + b > mbudget) flush();
         MultiLeaf& l = m.l[m.n];
         l = MultiLeaf{};
         l.ws = mrest + used;
