@@ -49,6 +49,26 @@ def test_window_counts_and_hash_counts(oracle, amq, torch, big, bpk):
     assert_same(plan, out, ref)
 
 
+@pytest.mark.parametrize("shape,bpk", [("k16", 16), ("k24", 10), ("k24", 14)])
+def test_batch_tiled_past_five_windows(oracle, amq, torch, shape, bpk):
+    """In a batch of 16- or 24-byte keys the leaves past 5 windows take the multi-leaf tiled
+    build, the others the window / LDS paths: k = 11 (16-byte keys as records), 24-byte keys
+    at k = 7 and at k = 10 (the bits past the eighth set by the overflow pass), ragged sizes
+    around the threshold, small and empty leaves between."""
+    rng = np.random.default_rng(bpk + len(shape))
+    first = 5 * 2560 * 512 // bpk + 1   # keys past 5 windows of 2,560 blocks
+    counts = [first + 50_000, 4000, 0, first - 1, 900_000, 17, first * 2, 2500]
+    n = sum(counts)
+    if shape == "k16":
+        keys, stride = oracle.gen_keys16(bpk, 0, n), 16
+    else:
+        keys, stride = rng.integers(0, 256, (n, 24), dtype=np.uint8), 24
+    plan, out = gpu_build(amq, torch, 0, torch.from_numpy(keys).cuda(), counts, bpk)
+    assert windows(plan) > 5
+    ref = oracle_per_segment(oracle, 0, keys, counts, bpk, stride=stride)
+    assert_same(plan, out, ref)
+
+
 @pytest.mark.parametrize("big", [1_000_000, 2_000_000])
 def test_window_many_windows_variable_keys(oracle, amq, torch, big):
     """Variable-length keys keep the window path up to 16 windows in a batch (8 and 16 windows
