@@ -3,7 +3,7 @@ set -o pipefail
 R=$GRAFT_REPO_ROOT; cd $R
 O=$R/gpurun_out/r05/${TAG:-vqfvar}; mkdir -p $O
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -k "vqf" -x -q --timeout 300 --timeout-method thread > $O/tests.log 2>&1; rc=$?; echo "tests rc=$rc"; tail -3 $O/tests.log
+timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -k "vqf" -x -q --timeout 300 --timeout-method thread > $O/tests.log 2>&1 || { echo "tests failed"; tail -30 $O/tests.log; exit 3; }; tail -3 $O/tests.log
 [ $rc -eq 0 ] || exit 2
 cd /tmp
 for W in vqf12var vqf12; do
