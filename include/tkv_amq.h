@@ -180,12 +180,13 @@ int tkv_amq_build(int kind, const uint8_t* keys, const uint64_t* key_offsets,
                   void* d_workspace, uint64_t workspace_bytes, void* stream);
 
 /* tkv_amq_build with the host copy of the plan's segments (h_segs: the n_segs entries
- * tkv_amq_plan filled; d_segs is their device copy).  With it a Bloom batch whose leaves include
- * some of more than 16 LDS windows (images past 2.5 MB; tree/tree_options.hpp:177-215 sizes any
- * leaf) builds the other leaves through the batch kernels and each oversize leaf through the
- * tiled monolithic build of its own (16- and 24-byte keys; other key shapes set that leaf's bits
- * with device atomics), instead of device atomics for the whole batch.  The workspace
- * tkv_amq_plan sizes covers it.  h_segs == NULL, or any other batch: exactly tkv_amq_build. */
+ * tkv_amq_plan filled; d_segs is their device copy).  With it a Bloom batch of 16- or 24-byte
+ * keys builds its leaves of more than 5 LDS windows (images past 800 KB; tree/tree_options.hpp:
+ * 177-215 sizes any leaf) through the tiled build, up to 40 of them per launch, and the other
+ * leaves through the batch kernels; with other key shapes only the leaves past 16 windows (2.5
+ * MB) leave the batch kernels, each setting its bits with device atomics (tkv_amq_build: device
+ * atomics for the whole batch).  The workspace tkv_amq_plan sizes covers either key shape.
+ * h_segs == NULL, a single leaf, or a batch without such leaves: exactly tkv_amq_build. */
 int tkv_amq_build_ex(int kind, const uint8_t* keys, const uint64_t* key_offsets, uint32_t key_stride,
                      uint64_t n_keys, const tkv_amq_segment* d_segs, const tkv_amq_segment* h_segs,
                      uint32_t n_segs, uint32_t max_blocks, uint8_t* d_out, void* d_workspace,
