@@ -1,0 +1,17 @@
+#!/bin/bash
+# part_scan on the active waves only: parity of the partitioned paths, then A/B bench lines vs the previous library
+set -o pipefail
+O=gpurun_out/r05/scan; mkdir -p $O
+export PYTHONUNBUFFERED=1
+X="TKV_AMQ_EXPERIMENT=1 TKV_AMQ_LIB=$PWD/turtle_kv_amd/exp_head.so"
+timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_hash_shard.py tests/test_gpu_window.py -x -q -k "monolithic or oversize or pipelined or hash or window" --timeout 300 --timeout-method thread > $O/tests.log 2>&1 \
+  && tail -2 $O/tests.log \
+  && timeout -k 10 300 python -u bench.py --workload bloom10mono --no-e2e --no-cpu-baseline > $O/mono_new.log 2>&1 \
+  && env $X timeout -k 10 300 python -u bench.py --experiment-lib --workload bloom10mono --no-e2e --no-cpu-baseline > $O/mono_head.log 2>&1 \
+  && timeout -k 10 300 python -u bench.py --workload bloom10monok24 --no-e2e --no-cpu-baseline > $O/k24_new.log 2>&1 \
+  && env $X timeout -k 10 300 python -u bench.py --experiment-lib --workload bloom10monok24 --no-e2e --no-cpu-baseline > $O/k24_head.log 2>&1 \
+  && timeout -k 10 400 python -u bench.py --workload bloom12hash --total-keys 1000000000 --steps 10 --no-e2e --no-cpu-baseline > $O/c5_new.log 2>&1 \
+  && env $X timeout -k 10 400 python -u bench.py --experiment-lib --workload bloom12hash --total-keys 1000000000 --steps 10 --no-e2e --no-cpu-baseline > $O/c5_head.log 2>&1
+rc=$?; echo "rc=$rc"
+for f in $O/*_new.log $O/*_head.log; do grep '^{' $f | tail -1 | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('$(basename $f)', d['value'], d['ms_per_step'], d.get('verified'), d.get('step_breakdown_rank0_ms'))"; done
+exit $rc

@@ -1466,37 +1466,43 @@ __device__ inline uint32_t part_scan(const uint32_t* cur, uint32_t* prev, uint32
 {
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
   const uint32_t c = (HW + kPartThreads - 1) / kPartThreads;
+  // only the waves holding counter words scan (one for the route's parts, eight for a
+  // 954-tile partition); the others skip to the barriers
+  const uint32_t nwa = ((HW + c - 1) / c + 63) / 64;
   const uint32_t j0 = min(HW, tid * c), j1 = min(HW, j0 + c);
-  uint32_t s = 0;
-  for (uint32_t j = j0; j < j1; ++j) {
-    const uint32_t x = cur[j], y = prev[j];
-    if (y) {
-      cursor[2 * j] += y & 0xffffu;
-      cursor[2 * j + 1] += y >> 16;
-      prev[j] = 0;
+  uint32_t s = 0, inc = 0;
+  if (wave < nwa) {
+    for (uint32_t j = j0; j < j1; ++j) {
+      const uint32_t x = cur[j], y = prev[j];
+      if (y) {
+        cursor[2 * j] += y & 0xffffu;
+        cursor[2 * j + 1] += y >> 16;
+        prev[j] = 0;
+      }
+      s += (x & 0xffffu) + (x >> 16);
     }
-    s += (x & 0xffffu) + (x >> 16);
-  }
-  uint32_t inc = s;  // inclusive scan over the wave
+    inc = s;  // inclusive scan over the wave
 #pragma unroll
-  for (uint32_t d = 1; d < 64; d <<= 1) {
-    const uint32_t v = __shfl_up(inc, d, 64);
-    if (lane >= d) inc += v;
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+      const uint32_t v = __shfl_up(inc, d, 64);
+      if (lane >= d) inc += v;
+    }
+    if (lane == 63) wsum[wave] = inc;
   }
-  if (lane == 63) wsum[wave] = inc;
   lds_barrier();
   uint32_t before = 0, total = 0;
-#pragma unroll
-  for (uint32_t q = 0; q < kPartThreads / 64; ++q) {
+  for (uint32_t q = 0; q < nwa; ++q) {
     const uint32_t t = wsum[q];
     before += q < wave ? t : 0u;
     total += t;
   }
-  uint32_t run = before + inc - s;
-  for (uint32_t j = j0; j < j1; ++j) {
-    const uint32_t x = cur[j], lo = x & 0xffffu;
-    start[j] = run | (run + lo) << 16;
-    run += lo + (x >> 16);
+  if (wave < nwa) {
+    uint32_t run = before + inc - s;
+    for (uint32_t j = j0; j < j1; ++j) {
+      const uint32_t x = cur[j], lo = x & 0xffffu;
+      start[j] = run | (run + lo) << 16;
+      run += lo + (x >> 16);
+    }
   }
   lds_barrier();  // start / cursor complete; wsum is reused by the next call
   return total;
