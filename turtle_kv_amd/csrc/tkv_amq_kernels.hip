@@ -4398,8 +4398,9 @@ __device__ inline bool vqf_present(const uint8_t* payload, uint32_t n_blocks, ui
 }
 
 // One VQF (hash, leaf) test: result bit | class << 1.
+// (always inlined: out of line it was a real call in every probe kernel, with a stack frame)
 template <bool kOpts>
-__device__ inline uint32_t vqf_probe_one(const uint8_t* filters, const tkv_amq_segment* segs,
+__device__ __attribute__((always_inline)) inline uint32_t vqf_probe_one(const uint8_t* filters, const tkv_amq_segment* segs,
                                          uint32_t n_segs, uint32_t s, uint64_t h,
                                          const uint64_t* page_ids = nullptr, uint64_t i = 0)
 {
