@@ -125,3 +125,41 @@ def test_random_big_leaf_batches_match_oracle(oracle, amq, torch, case):
         got = o[int(seg["out_offset"]):int(seg["out_offset"]) + int(seg["payload_bytes"])].tobytes()
         assert got == ref, (f"case {case}: kind {kind} bpk {bpk} cap {cap} shape {shape} leaf {s} "
                             f"of {n_leaves} ({c} keys, {int(seg['n_blocks'])} blocks)")
+
+
+@pytest.mark.parametrize("case", range(8))
+def test_random_tiled_leaf_batches_match_oracle(oracle, amq, torch, case):
+    """Bloom batches whose leaves cross the tiled-build thresholds at random (a single filter
+    past one LDS window; in a batch, 16/24-byte keys past 5 windows, other shapes past 16):
+    2-12 leaves of 0-2.6M keys among small ones, random bits per key (k from 3 to 16), every
+    key shape; every large leaf is checked, and a sample of the others."""
+    rng = np.random.default_rng(9300 + case)
+    shape = [16, 24, 0, 16][case % 4]
+    bpk = int(rng.choice([5, 8, 10, 12, 14, 20]))
+    n_big = int(rng.integers(1, 6)) if case != 0 else 1
+    big = [int(rng.integers(200_000, 2_600_000)) for _ in range(n_big)]
+    n_small = 0 if case == 0 else int(rng.integers(0, 40))
+    counts = [int(c) for c in rng.integers(0, 20000, n_small)] + big
+    rng.shuffle(counts)
+    n = sum(counts)
+    keys, offs, stride = make_keys(rng, shape, n)
+    plan = amq.plan_filters(0, counts, bpk)
+    kt = torch.from_numpy(keys).cuda()
+    kb = amq.KeyBatch.fixed(kt) if offs is None else amq.KeyBatch.variable(kt, torch.from_numpy(offs).cuda())
+    out = amq.build_all_filters(plan, kb)
+    torch.cuda.synchronize()
+    o = out.cpu().numpy()
+    sb = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
+    large = [i for i, c in enumerate(counts) if c >= 200_000]
+    sample = sorted({*large, *rng.choice(len(counts), size=min(len(counts), 6), replace=False).tolist()})
+    for s in sample:
+        b, c = int(sb[s]), counts[s]
+        if offs is None:
+            kp, o_s = keys[b:], None
+        else:
+            kp, o_s = keys[int(offs[b]):], (offs[b:b + c + 1] - offs[b]).astype(np.uint64)
+        st, ref = oracle.bloom_build(kp, c, bpk, src_page_id=s, offsets=o_s, stride=stride)
+        assert st == 0
+        seg = plan.segs[s]
+        got = o[int(seg["out_offset"]):int(seg["out_offset"]) + int(seg["payload_bytes"])].tobytes()
+        assert got == ref.tobytes(), f"case {case}: bpk {bpk} shape {shape} leaf {s} ({c} keys) of {len(counts)}"
