@@ -556,7 +556,9 @@ class LeafBatcher
     usize arena_bytes;  // pinned key bytes per batch (and as many bytes of offsets)
   };
 
-  LeafBatcher() : LeafBatcher(Options{8, std::chrono::microseconds{20}, usize{8} << 20}) {}
+  // (a batch collects callers for up to 60 us: 16 VQF callers 786-860 Mkeys/s at 60, 658-785 at
+  // 20-40, 634-757 at 80-120; profiles/r05/leaf_bench_sweep*.txt)
+  LeafBatcher() : LeafBatcher(Options{8, std::chrono::microseconds{60}, usize{8} << 20}) {}
   explicit LeafBatcher(Options o) : opt_{o}
   {
     if (opt_.max_batch == 0) opt_.max_batch = 1;

@@ -2,7 +2,7 @@
 // worker threads, as TreeSerializeContext::build_all_pages does (tree/tree_serialize_context.cpp
 // :71-75, tree/filter_builder.hpp:307-331).  Host keys in, host filter pages out (PCIe
 // included); the batched host pipeline's rate is bench.py's e2e_pcie_inclusive.
-//   leaf_bench <threads> <leaves> [keys_per_leaf=16384] [kind: 0 bloom | 1 vqf] [batched: 0 | 1] [max_batch=8] [linger_us=20]
+//   leaf_bench <threads> <leaves> [keys_per_leaf=16384] [kind: 0 bloom | 1 vqf] [batched: 0 | 1] [max_batch=8] [linger_us=60]
 #include <turtle_kv_amd/filter_builder.hpp>
 
 #include <algorithm>
@@ -32,7 +32,7 @@ int main(int argc, char** argv)
   const FilterKind kind = (argc > 4 && std::atoi(argv[4]) == 1) ? FilterKind::kQuotient : FilterKind::kBloom;
   const bool batched = argc > 5 && std::atoi(argv[5]) == 1;
   LeafBatcher batcher{LeafBatcher::Options{(usize)(argc > 6 ? std::atoi(argv[6]) : 8),
-                                           std::chrono::microseconds{argc > 7 ? std::atoi(argv[7]) : 20}, usize{8} << 20}};
+                                           std::chrono::microseconds{argc > 7 ? std::atoi(argv[7]) : 60}, usize{8} << 20}};
   const usize bpk = kind == FilterKind::kBloom ? 10 : 12;
   const u64 page = 32768 - kPackedPageHeaderSize;
   if (tkv_amq_device_count() == 0) {
@@ -86,7 +86,7 @@ int main(int argc, char** argv)
     std::printf("per-leaf %s: %2d threads  %d leaves x %llu keys  %.2f ms  %.0f leaves/s  %.1f Mkeys/s%s\n",
                 batched ? "batched " : "drop-in", t, leaves, (unsigned long long)per, dt * 1e3, leaves / dt, leaves * per / dt / 1e6,
                 failed ? "  FAILED" : "");
-    if (batched) std::printf("  (max_batch %s, linger %s us)\n", argc > 6 ? argv[6] : "8", argc > 7 ? argv[7] : "20");
+    if (batched) std::printf("  (max_batch %s, linger %s us)\n", argc > 6 ? argv[6] : "8", argc > 7 ? argv[7] : "60");
   }
   return 0;
 }
