@@ -697,12 +697,12 @@ class LeafBatcher
     usize bpk = 0;
     u64 cap = 0;
     u32 stride = 0;
-    u8* h_keys = nullptr;   // [arena_bytes]
+    u8* h_keys = nullptr;   // [arena_bytes + seg_area()]: the keys, then the segments (one copy in)
     u64* h_offs = nullptr;  // [arena_bytes / 8]
     u8* h_io = nullptr;     // [segments][status 64 B][pages]
     usize h_io_cap = 0;
     hipStream_t stream = nullptr;
-    DeviceBuffer d_keys, d_offs, d_segs, d_ws, d_out;
+    DeviceBuffer d_keys, d_offs, d_out;  // d_keys: keys then segments; d_out: pages then workspace
     u64 n = 0, bytes = 0;
     usize staged = 0, users = 0;
     bool closed = false;
@@ -723,15 +723,17 @@ class LeafBatcher
     cv_.notify_all();
   }
 
+  // the segments after the batch's keys in the same buffers (256-byte aligned)
+  usize seg_area() const { return 256 + opt_.max_batch * sizeof(tkv_amq_segment); }
+  static u64 align256(u64 x) { return (x + 255) & ~u64{255}; }
+
   Batch* create()
   {
     Batch* b = new Batch;
-    const usize seg_bytes = opt_.max_batch * sizeof(tkv_amq_segment);
-    if (hipHostMalloc(reinterpret_cast<void**>(&b->h_keys), opt_.arena_bytes ? opt_.arena_bytes : 1) != hipSuccess ||
+    if (hipHostMalloc(reinterpret_cast<void**>(&b->h_keys), opt_.arena_bytes + seg_area()) != hipSuccess ||
         hipHostMalloc(reinterpret_cast<void**>(&b->h_offs), 8 * key_cap() + 8) != hipSuccess ||
         hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking) != hipSuccess ||
-        !b->d_keys.resize(opt_.arena_bytes ? opt_.arena_bytes : 1) || !b->d_offs.resize(8 * key_cap() + 8) ||
-        !b->d_segs.resize(seg_bytes)) {
+        !b->d_keys.resize(opt_.arena_bytes + seg_area()) || !b->d_offs.resize(8 * key_cap() + 8)) {
       destroy(b);
       return nullptr;
     }
@@ -823,36 +825,40 @@ class LeafBatcher
                           segs.data(), &total_out, &ws_bytes, &max_blocks);
     if (st != TKV_AMQ_OK) return Status::from(st, "tkv_amq_plan");
     const usize seg_bytes = n_segs * sizeof(tkv_amq_segment);
-    const usize flag_bytes = (4 * n_segs + 63) / 64 * 64;  // the leaves' nelts words (VQF)
-    const usize io_bytes = seg_bytes + flag_bytes + total_out;
+    // one copy out: the pages, then (VQF) the workspace header up to the leaves' nelts words,
+    // the workspace placed after the pages in one device buffer
+    const u64 ws_off = align256(total_out);
+    const bool flags_out = b.kind == FilterKind::kQuotient && ws_bytes >= TKV_AMQ_VQF_NELTS_OFFSET + 4 * n_segs;
+    const u64 out_bytes = flags_out ? ws_off + TKV_AMQ_VQF_NELTS_OFFSET + 4 * n_segs : total_out;
+    const usize io_bytes = seg_bytes + out_bytes;
     if (!detail::LeafScratch::grow_pinned(b.h_io, b.h_io_cap, io_bytes <= b.h_io_cap ? io_bytes : io_bytes + io_bytes / 2))
       return Status::from(TKV_AMQ_RESOURCE_EXHAUSTED, "hipHostMalloc");
     const u64 n = b.n, bytes = b.bytes;
-    if (!reserve_device(b.d_segs, seg_bytes) || !reserve_device(b.d_ws, ws_bytes) ||
-        !reserve_device(b.d_out, total_out))
-      return Status::from(TKV_AMQ_RESOURCE_EXHAUSTED, "hipMalloc");
-    std::memcpy(b.h_io, segs.data(), seg_bytes);
-    u32* h_flags = reinterpret_cast<u32*>(b.h_io + seg_bytes);
-    std::memset(h_flags, 0, 4 * n_segs);
-    u8* h_out = b.h_io + seg_bytes + flag_bytes;
+    if (!reserve_device(b.d_out, ws_off + ws_bytes)) return Status::from(TKV_AMQ_RESOURCE_EXHAUSTED, "hipMalloc");
+    std::memcpy(b.h_io, segs.data(), seg_bytes);  // the host plan (tkv_amq_build_ex's h_segs)
+    u8* h_out = b.h_io + seg_bytes;
+    // one copy in: the keys, then the segments at the next 256-byte boundary
+    const u64 seg_off = align256(bytes);
+    std::memcpy(b.h_keys + seg_off, segs.data(), seg_bytes);
     if (b.stride == 0) b.h_offs[n] = bytes;
     hipStream_t s = b.stream;
-    if ((bytes && hipMemcpyAsync(b.d_keys.get(), b.h_keys, bytes, hipMemcpyHostToDevice, s) != hipSuccess) ||
-        (b.stride == 0 && hipMemcpyAsync(b.d_offs.get(), b.h_offs, 8 * (n + 1), hipMemcpyHostToDevice, s) != hipSuccess) ||
-        hipMemcpyAsync(b.d_segs.get(), b.h_io, seg_bytes, hipMemcpyHostToDevice, s) != hipSuccess)
+    if (hipMemcpyAsync(b.d_keys.get(), b.h_keys, seg_off + seg_bytes, hipMemcpyHostToDevice, s) != hipSuccess ||
+        (b.stride == 0 && hipMemcpyAsync(b.d_offs.get(), b.h_offs, 8 * (n + 1), hipMemcpyHostToDevice, s) != hipSuccess))
       return Status::from(TKV_AMQ_INTERNAL, "hipMemcpyAsync keys");
+    u8* d_ws = b.d_out.get<u8>() + ws_off;
     st = tkv_amq_build_ex((int)b.kind, b.d_keys.get(), b.stride ? nullptr : b.d_offs.get<u64>(), b.stride, n,
-                          b.d_segs.get<tkv_amq_segment>(), reinterpret_cast<const tkv_amq_segment*>(b.h_io),
-                          (u32)n_segs, max_blocks, b.d_out.get(), b.d_ws.get(), ws_bytes, s);
+                          reinterpret_cast<const tkv_amq_segment*>(b.d_keys.get<u8>() + seg_off),
+                          reinterpret_cast<const tkv_amq_segment*>(b.h_io), (u32)n_segs, max_blocks, b.d_out.get(),
+                          ws_bytes ? d_ws : nullptr, ws_bytes, s);
     if (st != TKV_AMQ_OK) return Status::from(st, "tkv_amq_build_ex");
-    if (hipMemcpyAsync(h_out, b.d_out.get(), total_out, hipMemcpyDeviceToHost, s) != hipSuccess ||
-        (b.kind == FilterKind::kQuotient && ws_bytes >= TKV_AMQ_VQF_NELTS_OFFSET + 4 * n_segs &&
-         hipMemcpyAsync(h_flags, b.d_ws.get<u8>() + TKV_AMQ_VQF_NELTS_OFFSET, 4 * n_segs,
-                        hipMemcpyDeviceToHost, s) != hipSuccess) ||
+    if (hipMemcpyAsync(h_out, b.d_out.get(), out_bytes, hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipStreamSynchronize(s) != hipSuccess)
       return Status::from(TKV_AMQ_INTERNAL, "hipMemcpyAsync pages");
     u32 flags = 0;
-    for (usize i = 0; i < n_segs; ++i) flags |= h_flags[i];
+    if (flags_out) {
+      const u32* h_flags = reinterpret_cast<const u32*>(h_out + ws_off + TKV_AMQ_VQF_NELTS_OFFSET);
+      for (usize i = 0; i < n_segs; ++i) flags |= h_flags[i];
+    }
     if (flags & TKV_AMQ_VQF_FLAG_WORKSPACE) return Status::from(TKV_AMQ_INVALID_ARGUMENT, "workspace");
     if (flags & TKV_AMQ_VQF_FLAG_OVERFLOW)
       return Status::from(TKV_AMQ_INTERNAL, "vqf_insert (filter_builder.hpp:211)");
