@@ -862,6 +862,15 @@ def bench_hash_sharded(args, torch, dist, amq, world, rank, dev, bpk, label, pg=
     ev[4].record()
     torch.cuda.synchronize()
     route_ms, a2a_ms, build_ms, gather_ms = (ev[i].elapsed_time(ev[i + 1]) for i in range(4))
+    # one more pipelined step with an event at every stage boundary: when each chunk's route,
+    # each round's exchange, each part build and each round's gather ended on its stream
+    timeline = None
+    if hs.records:
+        if pg:
+            dist.barrier()
+        hs.step(keys, gather=gather_in_step, timeline=True)
+        torch.cuda.synchronize()
+        timeline = hs.timeline_ms()
 
     allgather_ms = None
     if pg and not gather_in_step:
@@ -936,12 +945,15 @@ def bench_hash_sharded(args, torch, dist, amq, world, rank, dev, bpk, label, pg=
                                     "part_builds": round(build_ms, 4),
                                     "allgather": round(gather_ms, 4),
                                     "note": "the stages run one after another (untimed by value)"},
+        "step_timeline_rank0_ms": timeline,
         "verified": check["ok"] if check else None, "verify": check,
     }
     if rp is not None:
-        line["route_plan"] = {"route_wgs": rp.route_wgs, "region_cap": rp.region_cap,
+        line["route_plan"] = {"route_wgs": rp.route_wgs, "block_cap": rp.block_cap,
                               "block_bytes": rp.block_bytes, "ovf_cap": rp.ovf_cap,
-                              "exchanged_bytes_per_rank": (world - 1) * chunks * rp.block_bytes,
+                              "parts_per_rank": hs.g,
+                              "exchanged_bytes_per_rank": (world - 1) * chunks * hs.g * rp.block_bytes,
+                              "record_bytes_per_rank": 12 * n_local * (world - 1) // world,
                               "overflow_lost": lost}
     if comm is not None:
         line["comm"] = comm

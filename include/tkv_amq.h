@@ -266,25 +266,27 @@ int tkv_amq_bloom_build_range_records(const uint8_t* d_recs12, uint64_t n_recs,
                                       uint8_t* d_out, void* d_workspace, uint64_t workspace_bytes,
                                       void* stream);
 
-/* The pipelined hash-range build (hash_count <= 8): the route writes fixed-capacity blocks, so
- * the exchange needs no counts first.  Parts of q tiles are owned round-robin: part p belongs
- * to rank p % world as its part p / world, so round j (parts [j*world, (j+1)*world)) is one
- * contiguous byte range of the bitmap and can be all-gathered in place as soon as every rank has
- * built its part of it.  Per step, each rank:
+/* The pipelined hash-range build (hash_count <= 8): the route writes fixed-capacity part
+ * blocks, so the exchange needs no counts first.  Parts of q tiles are owned round-robin: part p
+ * belongs to rank p % world as its part j = p / world, so round j (parts [j*world, (j+1)*world))
+ * is one contiguous byte range of the bitmap and can be all-gathered in place as soon as every
+ * rank has built its part of it.  Per step, each rank:
  *   1. routes its keys in n_chunks chunks (tkv_amq_bloom_route_blocks): every key hashed once
- *      into its 12-byte bit record, counting-sorted by part on chip, appended to its route
- *      workgroup's region of that part in the part owner's block.  Chunk c's send buffer is
- *      world blocks of block_bytes (destination d at d * block_bytes);
- *   2. exchanges chunk c's blocks with one all-to-all of equal splits (block_bytes per peer),
- *      which can run while chunk c + 1 routes;
- *   3. builds each of its parts from the n_chunks * world blocks it received
- *      (tkv_amq_bloom_build_part_blocks: recv block (c, s) at (c * world + s) * block_bytes),
- *      writing the part's tiles where tkv_amq_build puts them (and the header);
- *   4. all-gathers round j as soon as its part of round j is built.
- * Records beyond a region's capacity travel as (record, part) entries in the block's overflow
- * area, at most ovf_cap per block; tkv_amq_bloom_blocks_lost reports a block that needed more
- * (keys far from uniform, e.g. one key repeated), after which the caller must build through the
- * exact exchange (tkv_amq_bloom_route_records + tkv_amq_bloom_build_range_records) instead. */
+ *      into its 12-byte bit record, counting-sorted by part on chip, and appended to that
+ *      part's block (a run per batch and part, reserved with one atomic on the block's count).
+ *      Chunk c's send buffer holds n_parts blocks in global part order (part p at
+ *      p * block_bytes), so round j's blocks -- one per destination -- are one slice;
+ *   2. exchanges round j of chunk c with one all-to-all of equal splits (block_bytes per peer):
+ *      the chunks' rounds as their routes finish, the last chunk round by round;
+ *   3. builds its part j from the n_chunks * world blocks of round j it received, laid out
+ *      contiguously (tkv_amq_bloom_build_part_blocks), as soon as they have landed, writing the
+ *      part's tiles where tkv_amq_build puts them (and the header);
+ *   4. all-gathers round j as soon as its part of round j is built, while the next rounds
+ *      are exchanged and built.
+ * Records beyond a block's capacity travel as (record, part) entries in its overflow area, at
+ * most ovf_cap per block; tkv_amq_bloom_blocks_lost reports a block that needed more (keys far
+ * from uniform, e.g. one key repeated), after which the caller must build through the exact
+ * exchange (tkv_amq_bloom_route_records + tkv_amq_bloom_build_range_records) instead. */
 typedef struct tkv_amq_route_plan {
   uint32_t n_tiles;          /* T = ceil(n_blocks / tile_blocks) */
   uint32_t n_parts;          /* world * parts_per_rank */
@@ -293,12 +295,12 @@ typedef struct tkv_amq_route_plan {
   uint32_t world;
   uint32_t n_chunks;
   uint32_t route_wgs;        /* P: route workgroups per chunk (= a part build's workgroups) */
-  uint32_t region_cap;       /* records per (part, route workgroup) region */
-  uint32_t ovf_cap;          /* overflow entries per block */
+  uint32_t block_cap;        /* records per part block (mean + 6 sigma + 16 of a uniform hash) */
+  uint32_t ovf_cap;          /* overflow entries per part block */
   uint32_t hash_count;
   uint64_t chunk_keys;       /* keys per chunk the capacities are sized for (fewer is fine) */
-  uint64_t block_bytes;      /* one (chunk, sender, destination) block */
-  uint64_t counts_off, ovf_n_off, regions_off, ovf_off;  /* block layout */
+  uint64_t block_bytes;      /* one (chunk, sender, part) block */
+  uint64_t count_off, ovf_n_off, recs_off, ovf_off;  /* block layout */
   uint64_t route_ws_bytes;   /* workspace of one tkv_amq_bloom_route_blocks call */
   uint64_t part_ws_bytes;    /* workspace of one tkv_amq_bloom_build_part_blocks call */
   uint64_t part_bytes;       /* bitmap bytes per part (q tiles; parts past the last tile pad) */
@@ -309,14 +311,18 @@ typedef struct tkv_amq_route_plan {
 int tkv_amq_bloom_route_plan(uint64_t chunk_keys, uint32_t n_chunks, uint32_t n_blocks,
                              uint32_t hash_count, uint32_t world, tkv_amq_route_plan* plan);
 /* d_keys: n_keys keys of key_bytes 16 (16-byte aligned) or 24 (8-byte aligned), n_keys <=
- * plan->chunk_keys; d_send: world * block_bytes bytes */
+ * plan->chunk_keys.  Part p's block goes to d_dst + (p / world) * round_stride + (p % world) *
+ * block_bytes; round_stride 0 means world * block_bytes (a send buffer: n_parts * block_bytes,
+ * part p at p * block_bytes).  A rank that exchanges nothing (world 1) routes chunk c straight
+ * into its receive layout with d_dst = recv + c * block_bytes, round_stride = n_chunks *
+ * block_bytes. */
 int tkv_amq_bloom_route_blocks(const uint8_t* d_keys, uint32_t key_bytes, uint64_t n_keys,
                                const tkv_amq_segment* d_seg, const tkv_amq_route_plan* plan,
-                               uint8_t* d_send, void* d_workspace, uint64_t workspace_bytes,
-                               void* stream);
-/* part: the global part index (this rank's part j is j * world + rank); d_recv: n_recv blocks
- * (n_chunks * world after the exchange); d_out: the whole filter payload (header + bitmap,
- * padded to 64 + n_parts * part_bytes) */
+                               uint8_t* d_dst, uint64_t round_stride, void* d_workspace,
+                               uint64_t workspace_bytes, void* stream);
+/* part: the global part index (this rank's part j is j * world + rank); d_recv: the part's
+ * n_recv blocks, block_bytes apart (n_chunks * world after the exchange of its round); d_out:
+ * the whole filter payload (header + bitmap, padded to 64 + n_parts * part_bytes) */
 int tkv_amq_bloom_build_part_blocks(const uint8_t* d_recv, uint32_t n_recv,
                                     const tkv_amq_segment* d_seg, const tkv_amq_route_plan* plan,
                                     uint32_t part, uint8_t* d_out, void* d_workspace,

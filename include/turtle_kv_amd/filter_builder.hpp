@@ -276,8 +276,8 @@ class FilterBatchBuilder
     if (!planned_) TKV_AMQ_REQUIRE_OK(plan());
     u64 n = 0;
     for (u64 c : counts_) n += c;
-    // (_ex with the host plan: leaves past 16 LDS windows in a Bloom batch take the tiled
-    // monolithic build, one each)
+    // (_ex with the host plan: in a Bloom batch, leaves of 16- or 24-byte keys past 5 LDS
+    // windows -- other key shapes past 16 -- take the tiled build, up to 40 per launch)
     return Status::from(tkv_amq_build_ex((int)kind_, d_keys, d_key_offsets, key_stride, n,
                                          d_segs_.get<tkv_amq_segment>(), segs_.data(), (u32)segs_.size(),
                                          max_blocks_, d_out, d_ws_.get(), ws_bytes_, stream),

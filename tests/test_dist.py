@@ -166,12 +166,19 @@ def test_pipelined_hash_shard_plan(world, chunks):
         for p in hs.owned_parts():
             assert p % world == r and p not in owners
             owners[p] = r
-        assert hs.recv.numel() == chunks * world * rp.block_bytes
+        # round j's blocks at [j][chunk][sender]; a chunk's send buffer: every part's block
+        assert hs.recv.numel() == hs.g * chunks * world * rp.block_bytes
+        assert hs.recv_round(1).data_ptr() - hs.recv_round(0).data_ptr() == chunks * world * rp.block_bytes
+        if world > 1:
+            assert all(b.numel() == rp.n_parts * rp.block_bytes for b in hs.send)
         assert hs.out.numel() == 64 + rp.n_parts * rp.part_bytes >= hs.payload_bytes
-        e = -(-hs.chunk_keys // rp.route_wgs) * min(hs.q * 2048, nb_1b) / nb_1b   # its blocks' share
-        assert e + 6 * e ** 0.5 <= rp.region_cap <= e + 6 * e ** 0.5 + 32
-        assert rp.regions_off + 12 * hs.g * rp.route_wgs * rp.region_cap <= rp.ovf_off
+        e = hs.chunk_keys * min(hs.q * 2048, nb_1b) / nb_1b   # the part's share of a chunk
+        assert e + 6 * e ** 0.5 <= rp.block_cap <= e + 6 * e ** 0.5 + 32
+        assert rp.recs_off + 12 * rp.block_cap <= rp.ovf_off
         assert rp.ovf_off + 16 * rp.ovf_cap <= rp.block_bytes and rp.block_bytes % 256 == 0
+        # what crosses xGMI beyond the records themselves: the 6-sigma slack of one count per
+        # block, the overflow area and the header (round 5's per-(part, workgroup) regions: 14%)
+        assert rp.block_bytes <= 1.03 * 12 * e + 4096, (rp.block_bytes, 12 * e)
     assert sorted(owners) == list(range(world * hs.g))
     tiles = sorted(hs.part_tiles(p) for p in owners)
     assert tiles[0][0] == 0 and tiles[-1][1] == hs.T
@@ -264,3 +271,36 @@ def test_cyclic_round_allgather(kind, world, q):
         p.join(120)
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     assert rq.get(timeout=5) is True
+
+
+def test_hash_shard_build_falls_back_past_capacity():
+    """a rank holding more keys than its plan's chunks take (an uneven split
+    with the default max_keys_per_rank) must not lose keys: build() decides over every rank and
+    takes the exact exchange; step() refuses such keys rather than routing a prefix of them."""
+    from turtle_kv_amd import abi
+    from turtle_kv_amd.dist import HashShardedBloom
+    hs = HashShardedBloom(1_000_000, 12, 2, 0, "meta", chunks=2)
+    assert hs.capacity == 2 * hs.chunk_keys == 500_000   # the even share of 2 ranks
+    keys = torch.empty((600_000, 16), dtype=torch.uint8, device="meta")
+    hs._any_rank = lambda flag: flag   # (no process group here: this rank's flag decides)
+    calls = []
+
+    class Exact:
+        def build(self, k):
+            calls.append(k.shape[0])
+            return torch.zeros(8, dtype=torch.uint8)
+    hs._exact_builder = lambda: Exact()
+
+    def no_step(*a, **kw):
+        raise AssertionError("the pipelined step must not run past the plan's capacity")
+    hs.step = no_step
+    out = hs.build(keys)
+    assert hs.last_fallback == "keys_over_capacity" and calls == [600_000] and out.numel() == 8
+    # another rank over capacity decides for this one too
+    hs._any_rank = lambda flag: True
+    hs.build(torch.empty((10, 16), dtype=torch.uint8, device="meta"))
+    assert hs.last_fallback == "keys_over_capacity"
+    # step() itself refuses (route_chunk) instead of dropping keys
+    hs2 = HashShardedBloom(1_000_000, 12, 2, 0, "meta", chunks=2)
+    with pytest.raises(abi.TkvAmqError):
+        hs2.route_chunk(keys, 0)

@@ -299,12 +299,14 @@ def _pipelined_by_hand(amq, torch, keys_per_rank, bpk, chunks):
         for c in range(chunks):
             hs.route_chunk(keys_per_rank[r], c)
     B = hss[0].block_bytes
-    if W > 1:
+    if W > 1:  # recv block [j][c][s] of rank d = rank s's chunk-c block of part j * W + d
         for d in range(W):
-            for c in range(chunks):
-                for s_ in range(W):
-                    i = c * W + s_
-                    hss[d].recv[i * B:(i + 1) * B].copy_(hss[s_].send[c][d * B:(d + 1) * B])
+            for j in range(hss[0].g):
+                for c in range(chunks):
+                    for s_ in range(W):
+                        i = (j * chunks + c) * W + s_
+                        p = j * W + d
+                        hss[d].recv[i * B:(i + 1) * B].copy_(hss[s_].send[c][p * B:(p + 1) * B])
     for hs in hss:
         for j in range(hs.g):
             hs.build_part(j)
@@ -345,7 +347,7 @@ def test_pipelined_blocks_equal_oracle(oracle, amq, torch, n_keys, bpk, world, c
         h = hss[0]
         ovf = torch.stack([hs.recv.view(-1)[i * h.block_bytes + h.rp.ovf_n_off:
                                             i * h.block_bytes + h.rp.ovf_n_off + 4].view(torch.int32)
-                           for hs in hss for i in range(h.chunks * h.world)]).sum()
+                           for hs in hss for i in range(h.g * h.chunks * h.world)]).sum()
         assert int(ovf) > 0, "the duplicates must have taken the overflow path"
 
 
@@ -372,3 +374,85 @@ def test_pipelined_blocks_report_lost_overflow(oracle, amq, torch):
     filt = HashShardedBloom(n, 12, 1, 0, "cuda").build(keys)
     st, ref = oracle.bloom_build(keys.cpu().numpy(), n, 12, src_page_id=0)
     assert st == 0 and filt.cpu().numpy().tobytes() == ref.tobytes()
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _sharded_worker(rank, world, port, n_total, bpk, chunks, split, q):
+    """One gloo rank on the box's one GPU: HashShardedBloom.build over this rank's keys (the
+    real step: route chunks, the rounds' all-to-alls, part builds, round all-gathers on the
+    communication stream); rank 0 checks the filter against the oracle."""
+    import os
+    import sys
+
+    import torch
+    import torch.distributed as dist
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import turtle_kv_amd as amq
+    from turtle_kv_amd.dist import HashShardedBloom
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    bounds = [0] + [int(n_total * f) for f in split] + [n_total]
+    k0, k1 = bounds[rank], bounds[rank + 1]
+    keys = amq.gen_keys16(77, k0, k1 - k0)
+    hs = HashShardedBloom(n_total, bpk, world, rank, "cuda", chunks=chunks)
+    filt = hs.build(keys)
+    hs2 = None
+    if hs.last_fallback is None:  # the same step again, its stages timed
+        hs.step(keys, timeline=True)
+        torch.cuda.synchronize()
+        hs2 = hs.timeline_ms()
+        again = torch.equal(hs.filter(), filt)
+    else:
+        again = True
+    res = None
+    if rank == 0:
+        from oracle import oracle as O
+        O.build_oracle()
+        allk = amq.gen_keys16(77, 0, n_total).cpu().numpy()
+        st, ref = O.bloom_build(allk, n_total, bpk, src_page_id=0)
+        res = (st == 0 and filt.cpu().numpy().tobytes() == ref.tobytes(), again, hs.last_fallback, hs2)
+    dist.barrier()
+    dist.destroy_process_group()
+    if rank == 0:
+        q.put(res)
+
+
+@pytest.mark.parametrize("world,n_total,bpk,chunks,split,fallback", [
+    (2, 3_000_000, 12, 2, (0.5,), None),               # even: the pipelined step
+    (3, 2_500_001, 10, 3, (0.3, 0.62), None),          # ragged, k = 7
+    (2, 2_000_000, 12, 2, (0.6,), "keys_over_capacity"),  # rank 0 over its even share
+])
+def test_hash_sharded_step_gloo_ranks(world, n_total, bpk, chunks, split, fallback):
+    """HashShardedBloom.build with `world` gloo ranks on the one GPU: the round-major exchange
+    (chunks' rounds as routed, the last chunk round by round, part j built once its round has
+    landed, round j gathered behind the exchange of round j + 2) gives the oracle's filter, and
+    a rank holding more keys than the plan's chunks take sends every rank through the exact
+    exchange.  (Parts per rank g = 1 at these sizes; config 5's g = 6 runs in the
+    bench's 8-rank rehearsal.)"""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_sharded_worker, args=(r, world, port, n_total, bpk, chunks, split, q))
+          for r in range(world)]
+    for p in ps:
+        p.start()
+    for p in ps:
+        p.join(300)
+    assert all(p.exitcode == 0 for p in ps), [p.exitcode for p in ps]
+    ok, again, fb, tl = q.get(timeout=5)
+    assert ok, "filter differs from the oracle"
+    assert again and fb == fallback
+    if fallback is None:  # every stage of the timed step was recorded, in stream order
+        assert tl["route_0"] <= tl["build_0_start"] <= tl["build_0"] <= tl["end"], tl
+        assert tl["exchange_0"] <= tl["build_0_start"] and tl["gather_0"] <= tl["end"], tl

@@ -99,8 +99,8 @@ class RoutePlan(ctypes.Structure):
     layout (include/tkv_amq.h)."""
     _fields_ = [(n, ctypes.c_uint32) for n in (
         "n_tiles", "n_parts", "parts_per_rank", "part_tiles", "world", "n_chunks", "route_wgs",
-        "region_cap", "ovf_cap", "hash_count")] + [(n, ctypes.c_uint64) for n in (
-        "chunk_keys", "block_bytes", "counts_off", "ovf_n_off", "regions_off", "ovf_off",
+        "block_cap", "ovf_cap", "hash_count")] + [(n, ctypes.c_uint64) for n in (
+        "chunk_keys", "block_bytes", "count_off", "ovf_n_off", "recs_off", "ovf_off",
         "route_ws_bytes", "part_ws_bytes", "part_bytes", "n_blocks")]
 
 
@@ -221,7 +221,7 @@ def lib(build_if_missing: bool = True):
         L.tkv_amq_bloom_route_plan.restype = i32
         L.tkv_amq_bloom_route_plan.argtypes = [u64, u32, u32, u32, u32, prp]
         L.tkv_amq_bloom_route_blocks.restype = i32
-        L.tkv_amq_bloom_route_blocks.argtypes = [vp, u32, u64, vp, prp, vp, vp, u64, vp]
+        L.tkv_amq_bloom_route_blocks.argtypes = [vp, u32, u64, vp, prp, vp, u64, vp, u64, vp]
         L.tkv_amq_bloom_build_part_blocks.restype = i32
         L.tkv_amq_bloom_build_part_blocks.argtypes = [vp, u32, vp, prp, u32, vp, vp, u64, vp]
         L.tkv_amq_bloom_blocks_lost.restype = i32

@@ -1373,26 +1373,30 @@ __global__ __launch_bounds__(NT) void route_recs(const uint8_t* __restrict__ key
 // partition, tile build, overflow
 // ---------------------------------------------------------------------------------------
 // The route's output (bloom_route_part) and a part build's input (kSrcSeg12): fixed-size
-// blocks, one per (route chunk, sender, destination rank).  Block layout:
-//   counts_off   u32 [parts_per_dest][P]: records in region (jl, w) (<= cap)
+// PART blocks, one per (route chunk, sender, part).  Block layout:
+//   count_off    u32: records appended to the block (> cap: the rest went to overflow)
 //   ovf_n_off    u32: overflow entries appended to the block (> ovf_cap: entries were lost)
-//   regions_off  region (jl, w) at regions_off + (jl * P + w) * cap * 12: route workgroup w's
-//                12-byte records of the destination's jl-th part, in its batches' order
-//   ovf_off      ovf_cap 16-byte entries (record, global part): records whose region was full
+//   recs_off     cap 12-byte records of the part, appended by the route workgroups in runs of
+//                one (batch, part) each: a workgroup reserves its run with one device-scope
+//                atomicAdd on the count per batch, so the block holds no per-workgroup slack
+//   ovf_off      ovf_cap 16-byte entries (record, global part): records past the block's cap
 // Part p belongs to rank p % world as its part jl = p / world (round-robin: round jl's parts of
-// all ranks are one contiguous byte range of the bitmap, all-gathered in place).  Every block
-// has the same size, so a chunk's exchange is one all-to-all of equal splits with no host
-// synchronisation to size it.
+// all ranks are one contiguous byte range of the bitmap, all-gathered in place).  The route
+// writes part p's block at dst + jl * jstride + (p % world) * bytes: with jstride = world *
+// bytes a chunk's send buffer holds the parts in global order, so round jl's blocks (one per
+// destination) are one contiguous slice -- one all-to-all of equal splits per (chunk, round),
+// no host synchronisation to size it, and a part can be built as soon as its round has landed.
 struct RouteBlock {
   uint64_t bytes;
-  uint64_t counts_off;
+  uint64_t jstride;         // the route's destination: bytes from round jl to jl + 1
+  uint64_t count_off;
   uint64_t ovf_n_off;
-  uint64_t regions_off;
+  uint64_t recs_off;
   uint64_t ovf_off;
   uint32_t P;               // route workgroups (= the part builds' partition workgroups)
-  uint32_t cap;             // records per region
+  uint32_t cap;             // records per block
   uint32_t ovf_cap;         // overflow entries per block
-  uint32_t parts_per_dest;  // g
+  uint32_t pad;
 };
 
 struct PartArgs {
@@ -1416,10 +1420,9 @@ struct PartArgs {
   uint64_t q_magic;
   uint64_t w_magic;
   RouteBlock blk;
-  // kSrcSeg12: the blocks holding this part (n_src_segs of them, blk.bytes apart) and the
-  // part's index jl inside each
+  // kSrcSeg12: the part blocks holding this part (n_src_segs of them, blk.bytes apart)
   uint32_t n_src_segs;
-  uint32_t seg_part;
+  uint32_t seg_part;  // (unused)
   // a partition (kDstTiles) with the per-tile store table: part_tbl_fits(n_tiles), and the
   // launch's LDS is part_tbl_lds_bytes
   uint32_t tbl;
@@ -1561,20 +1564,14 @@ __device__ void part_body(const tkv_amq_segment& sg, const PartArgs& a, uint32_t
     cursor[i] = 0;
   }
   if (tid == 0) *ovf_n = 0;
-  if constexpr (ROUTE) {
-    // the destination blocks' overflow counters, appended to by bloom_route_ovf_pack after
-    // this kernel (a later launch on the same stream)
-    if (w == 0)
-      for (uint32_t d = tid; d < a.world; d += NT)
-        *reinterpret_cast<uint32_t*>(a.dst + (uint64_t)d * a.blk.bytes + a.blk.ovf_n_off) = 0;
-  }
+  // (ROUTE: the part blocks' counters were zeroed by bloom_route_reset, an earlier launch)
   const uint8_t* src;
   uint32_t n;
-  uint64_t seg_reg = 0;  // kSrcSeg12: this workgroup's region of the part inside a block
+  uint64_t seg_reg = 0;  // kSrcSeg12: the records inside a part block
   if constexpr (SRC == kSrcSeg12) {
     const uint32_t S = a.n_src_segs;
-    seg_reg = a.blk.regions_off + ((uint64_t)a.seg_part * a.blk.P + w) * a.blk.cap * 12ull;
-    const uint64_t cnt_off = a.blk.counts_off + 4ull * ((uint64_t)a.seg_part * a.blk.P + w);
+    seg_reg = a.blk.recs_off;
+    const uint64_t cnt_off = a.blk.count_off;
     if (tid < 64) {  // one wave: the inclusive scan of the S counts, 64 at a time
       uint32_t run = 0;
       for (uint32_t s0 = 0; s0 < S; s0 += 64) {
@@ -1596,10 +1593,12 @@ __device__ void part_body(const tkv_amq_segment& sg, const PartArgs& a, uint32_t
   __syncthreads();
   uint32_t kb, ke;
   if constexpr (SRC == kSrcSeg12) {
+    // the part's records, block after block: this workgroup's share of them
     src = a.src;
     n = pre[a.n_src_segs];
-    kb = 0;  // this workgroup's own regions, whole
-    ke = n;
+    const uint32_t per = (n + P - 1) / P;
+    kb = min(n, w * per);
+    ke = min(n, kb + per);
   } else {
     part_items(sg, a, IB, src, n);
     const uint32_t per = a.cnt ? (n + P - 1) / P : a.g.per;
@@ -1733,24 +1732,54 @@ __device__ void part_body(const tkv_amq_segment& sg, const PartArgs& a, uint32_t
       }
     }
     write_out();  // batch b - 1 (total = 0 before the first batch: sink stores only)
+    // ROUTE: each part's run of this batch reserved in the part's block with one device-scope
+    // atomicAdd on its count, issued before the next batch's loads (the returns share vmcnt
+    // with them, in order: the table below waits for the reservations, not for the loads)
+    uint32_t resv[ROUTE ? 2 : 1];
+    if constexpr (ROUTE) {
+      static_assert(kRouteMaxParts <= 2 * NT, "two parts per thread at most");
+      lds_barrier();  // the batch's histogram is complete
+#pragma unroll
+      for (uint32_t r = 0; r < 2; ++r) {
+        const uint32_t t = tid + r * NT;
+        resv[r] = 0;
+        if (t < T) {
+          const uint32_t len = lds_u16(hist, t);
+          if (len) {
+            const uint32_t jl = div_by_magic(t, a.w_magic), dr = t - jl * a.world;
+            resv[r] = atomicAdd(reinterpret_cast<uint32_t*>(a.dst + (uint64_t)jl * a.blk.jstride +
+                                                            (uint64_t)dr * a.blk.bytes + a.blk.count_off),
+                                len);
+          }
+        }
+      }
+    }
 #pragma unroll
     for (uint32_t u = 0; u < U; ++u)  // the next batch's items
       in[u] = load_in(min(b0 + B + u * NT + tid, last_item));
-    lds_barrier();
+    if constexpr (!ROUTE) lds_barrier();
     total = part_scan(hist, prev, start, cursor, HW, wsum);
     if constexpr (TBL) {
       // this batch's store table (read by its write-out, after the barrier below)
-      for (uint32_t t = tid; t < T; t += NT) {
-        const uint32_t st = lds_u16(start, t), cu = cursor[t];
-        uint64_t base;
-        if constexpr (ROUTE) {
-          const uint32_t jl = div_by_magic(t, a.w_magic), dr = t - jl * a.world;
-          base = (uint64_t)dr * a.blk.bytes + a.blk.regions_off + ((uint64_t)jl * P + w) * cap * 12ull;
-        } else {
-          base = a.g.regions_off + ((uint64_t)t * P + w) * cap * a.g.rb;
+      if constexpr (ROUTE) {
+#pragma unroll
+        for (uint32_t r = 0; r < 2; ++r) {
+          const uint32_t t = tid + r * NT;
+          if (t < T) {
+            const uint32_t st = lds_u16(start, t), o = min(resv[r], cap);  // (o = cap: all overflow)
+            const uint32_t jl = div_by_magic(t, a.w_magic), dr = t - jl * a.world;
+            const uint64_t base = (uint64_t)jl * a.blk.jstride + (uint64_t)dr * a.blk.bytes + a.blk.recs_off;
+            roff[t] = base + (uint64_t)RB * o - (uint64_t)RB * st;
+            rlim[t] = (int32_t)(cap + st) - (int32_t)o;
+          }
         }
-        roff[t] = base + (uint64_t)RB * cu - (uint64_t)RB * st;
-        rlim[t] = (int32_t)(cap + st) - (int32_t)cu;
+      } else {
+        for (uint32_t t = tid; t < T; t += NT) {
+          const uint32_t st = lds_u16(start, t), cu = cursor[t];
+          const uint64_t base = a.g.regions_off + ((uint64_t)t * P + w) * cap * a.g.rb;
+          roff[t] = base + (uint64_t)RB * cu - (uint64_t)RB * st;
+          rlim[t] = (int32_t)(cap + st) - (int32_t)cu;
+        }
       }
     }
 #pragma unroll
@@ -1773,13 +1802,7 @@ __device__ void part_body(const tkv_amq_segment& sg, const PartArgs& a, uint32_t
   __syncthreads();
   // the last batch's run lengths (its histogram is the one the loop's last batch counted into)
   const uint32_t* last = par ? H0 : H1;
-  if constexpr (ROUTE) {
-    for (uint32_t t = tid; t < T; t += NT) {
-      const uint32_t jl = div_by_magic(t, a.w_magic), dr = t - jl * a.world;
-      *reinterpret_cast<uint32_t*>(a.dst + (uint64_t)dr * a.blk.bytes + a.blk.counts_off +
-                                   4ull * ((uint64_t)jl * P + w)) = min(cursor[t] + lds_u16(last, t), cap);
-    }
-  } else {
+  if constexpr (!ROUTE) {  // (ROUTE: the blocks' counts are the reservations)
     uint32_t* counts = reinterpret_cast<uint32_t*>(a.ws + a.g.counts_off);
     for (uint32_t t = tid; t < T; t += NT)
       counts[(uint64_t)t * P + w] = min(cursor[t] + lds_u16(last, t), cap);
@@ -1882,9 +1905,21 @@ __global__ __launch_bounds__(256) void bloom_route_ovf_pack(PartArgs a)
   for (uint32_t e = threadIdx.x; e < n; e += 256) {
     const uint4 x = list[e];
     const uint32_t jl = div_by_magic(x.w, a.w_magic), dr = x.w - jl * a.world;
-    uint8_t* b = a.dst + (uint64_t)dr * a.blk.bytes;
+    uint8_t* b = a.dst + (uint64_t)jl * a.blk.jstride + (uint64_t)dr * a.blk.bytes;
     const uint32_t slot = atomicAdd(reinterpret_cast<uint32_t*>(b + a.blk.ovf_n_off), 1u);
     if (slot < a.blk.ovf_cap) reinterpret_cast<uint4*>(b + a.blk.ovf_off)[slot] = x;
+  }
+}
+
+// The route's part blocks' record and overflow counters to zero (ahead of bloom_route_part,
+// whose workgroups reserve their runs with atomics on them)
+__global__ __launch_bounds__(256) void bloom_route_reset(PartArgs a, uint32_t n_parts)
+{
+  for (uint32_t p = threadIdx.x; p < n_parts; p += 256) {
+    const uint32_t jl = p / a.world, dr = p - jl * a.world;
+    uint8_t* b = a.dst + (uint64_t)jl * a.blk.jstride + (uint64_t)dr * a.blk.bytes;
+    *reinterpret_cast<uint32_t*>(b + a.blk.count_off) = 0;
+    *reinterpret_cast<uint32_t*>(b + a.blk.ovf_n_off) = 0;
   }
 }
 
@@ -4901,10 +4936,11 @@ constexpr uint32_t kRouteKeyPartTiles = 1600;
 static_assert(kRoutePartTiles <= kRecPartMaxTiles && kRouteKeyPartTiles <= kRecPartMaxTiles, "");
 static_assert(kRoutePartTiles < 2048, "div_by_magic: exact for q < 2048 and tiles < 2^21");
 
-// The route plan of tkv_amq_bloom_route_plan: parts, route workgroups, the block layout.  The
-// region capacity is mean + 6 sigma + 16 records of a uniform hash (as the partition's); an
-// overflow area of ovf_cap entries per block (0 for the one-GPU build, which applies its route
-// workgroups' own overflow lists instead).
+// The route plan of tkv_amq_bloom_route_plan: parts, route workgroups, the part block layout.
+// A block holds mean + 6 sigma + 16 records of a uniform hash (the part's share of a chunk: one
+// count over the whole block, so 6 sigma is ~1% of it at config 5's size, where round 5's
+// per-(part, workgroup) regions carried 14%); an overflow area of ovf_cap entries per block (0
+// for the one-GPU build, which applies its route workgroups' own overflow lists instead).
 inline int route_plan(uint64_t chunk_keys, uint32_t n_chunks, uint64_t n_blocks, uint32_t k, uint32_t world,
                       bool ovf_area, tkv_amq_route_plan& rp)
 {
@@ -4932,19 +4968,21 @@ inline int route_plan(uint64_t chunk_keys, uint32_t n_chunks, uint64_t n_blocks,
   const uint64_t per = div_up(chunk_keys, P);  // keys per route workgroup
   // a part's share of the keys is its blocks' share (q full tiles at most; the last tile may
   // be short, and the last parts may hold fewer tiles, or none when world * g * q > T)
-  const double e = (double)per * std::min<uint64_t>((uint64_t)q * kTileBlocks, n_blocks) / n_blocks;
-  rp.region_cap = ((uint32_t)(e + 6.0 * sqrt(e) + 16.0) + 15) & ~15u;
-  // overflow entries per block: ~0.4% of a block's records (none expected from a uniform hash)
-  rp.ovf_cap = ovf_area ? (uint32_t)(4096 + chunk_keys / ((uint64_t)world * 256)) : 0u;
-  rp.counts_off = 0;
-  rp.ovf_n_off = align256(4ull * g * P);
-  rp.regions_off = rp.ovf_n_off + 256;
-  rp.ovf_off = align256(rp.regions_off + 12ull * g * P * rp.region_cap);
+  const double e = (double)chunk_keys * std::min<uint64_t>((uint64_t)q * kTileBlocks, n_blocks) / n_blocks;
+  const double capd = e + 6.0 * sqrt(e) + 16.0;
+  if (capd > 4.0e9) return TKV_AMQ_INVALID_ARGUMENT;
+  rp.block_cap = ((uint32_t)capd + 15) & ~15u;
+  // overflow entries per block (none expected from a uniform hash; duplicated keys land here)
+  rp.ovf_cap = ovf_area ? (uint32_t)(4096 + chunk_keys / ((uint64_t)world * g * 256)) : 0u;
+  rp.count_off = 0;
+  rp.ovf_n_off = 4;
+  rp.recs_off = 256;
+  rp.ovf_off = align256(rp.recs_off + 12ull * rp.block_cap);
   rp.block_bytes = align256(rp.ovf_off + 16ull * rp.ovf_cap);
   // route workspace: [sink 256][u32 overflow count per workgroup][16-byte entries, per each]
   rp.route_ws_bytes = align256(512 + 4ull * P) + 16ull * P * per;
   // a part build: partition regions over the part's q tiles, overflow lists of what its
-  // workgroup may receive (every source block's region at capacity)
+  // workgroup may receive (its share of every source block at capacity)
   const uint64_t S = (uint64_t)n_chunks * world;
   const double ep = (double)chunk_keys * S / P * std::min<uint64_t>(kTileBlocks, n_blocks) / n_blocks;  // per (full tile, workgroup)
   const uint32_t capp = ((uint32_t)(ep + 6.0 * sqrt(ep) + 16.0) + 15) & ~15u;
@@ -4952,12 +4990,12 @@ inline int route_plan(uint64_t chunk_keys, uint32_t n_chunks, uint64_t n_blocks,
   const uint64_t p_ovf_n = 256 + 4 * regions;
   const uint64_t p_regions = align256(p_ovf_n + 4ull * P);
   const uint64_t p_ovf = p_regions + 12ull * regions * capp;
-  rp.part_ws_bytes = p_ovf + 16ull * P * S * rp.region_cap;
+  rp.part_ws_bytes = p_ovf + 16ull * P * div_up(S * rp.block_cap, P);
   rp.part_bytes = (uint64_t)q * kTileBlocks * 64;
   return TKV_AMQ_OK;
 }
 
-// PartGeom of a part build of tn tiles from S route blocks (its workgroups: the route's)
+// PartGeom of a part build of tn tiles from S part blocks (its workgroups: the route's)
 inline PartGeom route_part_geom(const tkv_amq_route_plan& rp, uint32_t tn, uint32_t S)
 {
   PartGeom g{};
@@ -4965,7 +5003,7 @@ inline PartGeom route_part_geom(const tkv_amq_route_plan& rp, uint32_t tn, uint3
   g.P = P;
   g.n_tiles = tn ? tn : 1;
   g.rb = 12;
-  g.per = S * rp.region_cap;
+  g.per = (uint32_t)div_up((uint64_t)S * rp.block_cap, P);  // a workgroup's share at most
   const double ep = (double)rp.chunk_keys * S / P * std::min<uint64_t>(kTileBlocks, rp.n_blocks) /
                     rp.n_blocks;  // records per (full tile, workgroup)
   g.cap = ((uint32_t)(ep + 6.0 * sqrt(ep) + 16.0) + 15) & ~15u;
@@ -4978,18 +5016,19 @@ inline PartGeom route_part_geom(const tkv_amq_route_plan& rp, uint32_t tn, uint3
   return g;
 }
 
-inline RouteBlock route_block(const tkv_amq_route_plan& rp)
+// jstride 0: the send-buffer layout, part p at p * block_bytes
+inline RouteBlock route_block(const tkv_amq_route_plan& rp, uint64_t jstride = 0)
 {
   RouteBlock b{};
   b.bytes = rp.block_bytes;
-  b.counts_off = rp.counts_off;
+  b.jstride = jstride ? jstride : (uint64_t)rp.world * rp.block_bytes;
+  b.count_off = rp.count_off;
   b.ovf_n_off = rp.ovf_n_off;
-  b.regions_off = rp.regions_off;
+  b.recs_off = rp.recs_off;
   b.ovf_off = rp.ovf_off;
   b.P = rp.route_wgs;
-  b.cap = rp.region_cap;
+  b.cap = rp.block_cap;
   b.ovf_cap = rp.ovf_cap;
-  b.parts_per_dest = rp.parts_per_rank;
   return b;
 }
 
@@ -5008,10 +5047,11 @@ inline void set_route_attributes()
   });
 }
 
-// the route of n keys (kb 16 or 24) into the world blocks at d_send (from_seg: keys [0, n) of
+// the route of n keys (kb 16 or 24) into the part blocks at d_dst (part p at (p / world) *
+// jstride + (p % world) * block_bytes; jstride 0: world * block_bytes) (from_seg: keys [0, n) of
 // the segment, n capped by its count -- tkv_amq_build's plan; else exactly n keys)
 inline PartArgs route_args(const tkv_amq_route_plan& rp, const uint8_t* keys, uint32_t kb, uint64_t n,
-                           uint32_t from_seg, uint8_t* d_send, uint8_t* ws)
+                           uint32_t from_seg, uint8_t* d_dst, uint8_t* ws, uint64_t jstride = 0)
 {
   PartArgs a{};
   a.src = keys;
@@ -5022,16 +5062,16 @@ inline PartArgs route_args(const tkv_amq_route_plan& rp, const uint8_t* keys, ui
   a.g.P = rp.route_wgs;
   a.g.n_tiles = rp.n_parts;
   a.g.per = (uint32_t)div_up(rp.chunk_keys, rp.route_wgs);
-  a.g.cap = rp.region_cap;
+  a.g.cap = rp.block_cap;
   a.g.rb = 12;
   a.g.ovf_n_off = 512;
   a.g.ovf_off = align256(512 + 4ull * rp.route_wgs);
-  a.dst = d_send;
+  a.dst = d_dst;
   a.q = rp.part_tiles;
   a.world = rp.world;
   a.q_magic = div_magic(rp.part_tiles);
   a.w_magic = div_magic(rp.world);
-  a.blk = route_block(rp);
+  a.blk = route_block(rp, jstride);
   return a;
 }
 
@@ -5041,6 +5081,7 @@ inline void launch_route_blocks(const PartArgs& a, const tkv_amq_route_plan& rp,
   set_route_attributes();
   const dim3 g(rp.route_wgs), b(kPartThreads);
   const size_t lds = route_lds_bytes(rp.n_parts);
+  hipLaunchKernelGGL(bloom_route_reset, dim3(1), dim3(256), 0, s, a, rp.n_parts);
   if (a.kb == 24 && rp.hash_count == 8) hipLaunchKernelGGL((bloom_route_part<8, 24>), g, b, lds, s, d_seg, a);
   else if (a.kb == 24) hipLaunchKernelGGL((bloom_route_part<0, 24>), g, b, lds, s, d_seg, a);
   else if (rp.hash_count == 8) hipLaunchKernelGGL((bloom_route_part<8, 16>), g, b, lds, s, d_seg, a);
@@ -5049,8 +5090,8 @@ inline void launch_route_blocks(const PartArgs& a, const tkv_amq_route_plan& rp,
   if (pack) hipLaunchKernelGGL(bloom_route_ovf_pack, dim3(rp.route_wgs), dim3(256), 0, s, a);
 }
 
-// part p's tiles from the n_recv blocks at d_recv (partition -> tiles -> the partition's own
-// overflow lists); the route overflow entries are applied by the caller
+// part p's tiles from its n_recv part blocks at d_recv, block_bytes apart (partition -> tiles
+// -> the partition's own overflow lists); the route overflow entries are applied by the caller
 inline void launch_part_from_blocks(const tkv_amq_route_plan& rp, hipStream_t s, const uint8_t* d_recv,
                                     uint32_t n_recv, const tkv_amq_segment* d_seg, uint32_t p, uint8_t* d_out,
                                     uint8_t* ws)
@@ -5069,7 +5110,7 @@ inline void launch_part_from_blocks(const tkv_amq_route_plan& rp, hipStream_t s,
   a.src_kind = kSrcSeg12;
   a.blk = route_block(rp);
   a.n_src_segs = n_recv;
-  a.seg_part = p / rp.world;
+  a.seg_part = 0;
   a.tbl = part_tbl_fits(tn) ? 1u : 0u;
   hipLaunchKernelGGL(bloom_part_segs, dim3(a.g.P), dim3(kPartThreads),
                      a.tbl ? part_tbl_lds_bytes(tn) : part_lds_bytes(tn), s, d_seg, a);
@@ -5117,8 +5158,8 @@ inline MonoPlan mono_plan(uint64_t n_keys, uint64_t n_blocks)
     m.blocks = true;
     m.g = m.rp.n_parts;
     m.q = m.rp.part_tiles;
-    m.items_off = align256(m.rp.route_ws_bytes);                  // the block
-    m.part_off = align256(m.items_off + m.rp.block_bytes);        // a part build's workspace
+    m.items_off = align256(m.rp.route_ws_bytes);                  // the part blocks
+    m.part_off = align256(m.items_off + (uint64_t)m.rp.n_parts * m.rp.block_bytes);  // a part build's workspace
     m.bytes = m.part_off + m.rp.part_ws_bytes;
     return m;
   }
@@ -5162,7 +5203,7 @@ inline void launch_mono(const MonoPlan& m, hipStream_t s, const uint8_t* keys, u
     const PartArgs ra = route_args(rp, keys, kb, n, 1u, blk, ws);
     launch_route_blocks(ra, rp, s, d_segs, false);
     for (uint32_t p = 0; p < rp.n_parts; ++p)
-      launch_part_from_blocks(rp, s, blk, 1, d_segs, p, d_out, ws + m.part_off);
+      launch_part_from_blocks(rp, s, blk + (uint64_t)p * rp.block_bytes, 1, d_segs, p, d_out, ws + m.part_off);
     // the route workgroups' overflow lists (entries: record, part), every part at once
     hipLaunchKernelGGL(bloom_route_ovf_apply, dim3(rp.route_wgs), dim3(256), 0, s, d_segs, ws + ra.g.ovf_n_off,
                        4ull, ws + ra.g.ovf_off, 16ull * ra.g.per, ra.g.per, rp.part_tiles, 0u, rp.n_parts, d_out);
@@ -5551,9 +5592,26 @@ int tkv_amq_plan_pages(int kind, const uint64_t* counts, const uint64_t* src_ids
   return TKV_AMQ_OK;
 }
 
+// tkv_amq_build with the keys its leaves hold (sizing_keys: the Bloom launch heuristics and the
+// monolithic plan) apart from the key array's count (n_keys: what the device-atomics fallback
+// and VQF scan): tkv_amq_build_ex's compacted small leaves are a subset of the array's keys
+static int build_batch(int kind, const uint8_t* keys, const uint64_t* offs, uint32_t stride,
+                       uint64_t n_keys, const tkv_amq_segment* d_segs, uint32_t n_segs,
+                       uint32_t max_blocks, uint8_t* d_out, void* d_ws, uint64_t ws_bytes, void* stream,
+                       uint64_t sizing_keys);
+
 int tkv_amq_build(int kind, const uint8_t* keys, const uint64_t* offs, uint32_t stride,
                   uint64_t n_keys, const tkv_amq_segment* d_segs, uint32_t n_segs,
                   uint32_t max_blocks, uint8_t* d_out, void* d_ws, uint64_t ws_bytes, void* stream)
+{
+  return build_batch(kind, keys, offs, stride, n_keys, d_segs, n_segs, max_blocks, d_out, d_ws, ws_bytes,
+                     stream, n_keys);
+}
+
+static int build_batch(int kind, const uint8_t* keys, const uint64_t* offs, uint32_t stride,
+                       uint64_t n_keys, const tkv_amq_segment* d_segs, uint32_t n_segs,
+                       uint32_t max_blocks, uint8_t* d_out, void* d_ws, uint64_t ws_bytes, void* stream,
+                       uint64_t sizing_keys)
 {
   if (tkv_amq_device_count() == 0) return TKV_AMQ_UNAVAILABLE;
   if (n_segs == 0) return TKV_AMQ_OK;
@@ -5566,7 +5624,7 @@ int tkv_amq_build(int kind, const uint8_t* keys, const uint64_t* offs, uint32_t 
   if (kind == TKV_AMQ_BLOOM) {
     const uint64_t lds = 64ull * max_blocks;
     if (max_blocks == 0) return TKV_AMQ_OK;
-    const uint32_t parts = bloom_split_parts(n_segs, n_keys, max_blocks);
+    const uint32_t parts = bloom_split_parts(n_segs, sizing_keys, max_blocks);
     const uint64_t split_ws = bloom_split_ws_bytes(n_segs, parts, max_blocks);
     if (parts > 1 && d_ws && ws_bytes >= split_ws) {
       // a small batch: each leaf's keys over `parts` workgroups, then their images ORed
@@ -5607,18 +5665,18 @@ int tkv_amq_build(int kind, const uint8_t* keys, const uint64_t* offs, uint32_t 
     // key hashed once); 24-byte keys with k > 8 only up to kDirectMaxTiles tiles (their records
     // hold eight bits, and the others are set from the keys, which the route does not carry)
     const int mono_mode = build_key_mode(keys, offs, stride);
-    const bool mono_part = bloom_partitioned(n_segs, max_blocks, n_keys) && d_ws;
-    const MonoPlan mp = mono_plan(n_keys, max_blocks);
+    const bool mono_part = bloom_partitioned(n_segs, max_blocks, sizing_keys) && d_ws;
+    const MonoPlan mp = mono_plan(sizing_keys, max_blocks);
     const bool mono16 = mono_part && mode == kKey16 && ws_bytes >= mp.bytes;
     // (routed 24-byte keys travel as bit records only: k must be known -- bloom_k_of 0 means
     // the plan does not match n_keys -- and at most 8)
-    const uint32_t k_route = bloom_k_of(n_keys, max_blocks);
+    const uint32_t k_route = bloom_k_of(sizing_keys, max_blocks);
     const bool mono24 = mono_part && mono_mode == kKey24 && ws_bytes >= mp.bytes &&
                         (mp.g == 1 || (mp.blocks && k_route >= 1 && k_route <= 8));
     if (bloom_window_path(n_segs, max_blocks, mono16 || mono24)) {
       // leaves beyond one CU's LDS: windows of the image, parts of the keys
       const uint32_t W = bloom_window_count(max_blocks), wblk = bloom_window_blocks(max_blocks);
-      uint32_t wparts = bloom_window_parts(n_segs, n_keys, max_blocks);
+      uint32_t wparts = bloom_window_parts(n_segs, sizing_keys, max_blocks);
       if (wparts > 1 && (!d_ws || ws_bytes < bloom_split_ws_bytes(n_segs, wparts, max_blocks)))
         wparts = 1;  // no workspace for partial images: one part per leaf, no merge
       static std::once_flag win_attr[kMaxDevices];
@@ -5677,7 +5735,7 @@ int tkv_amq_build(int kind, const uint8_t* keys, const uint64_t* offs, uint32_t 
     if (mono16 || mono24) {
       // one monolithic filter: every key hashed once into its bit record, records partitioned
       // by tile (routed into parts first beyond kDirectMaxTiles tiles), tiles built in LDS
-      launch_mono(mp, s, keys, mono24 ? 24u : 16u, (uint32_t)n_keys, d_segs, static_cast<uint8_t*>(d_ws),
+      launch_mono(mp, s, keys, mono24 ? 24u : 16u, (uint32_t)sizing_keys, d_segs, static_cast<uint8_t*>(d_ws),
                   d_out);
     } else {
       // fewer than kBloomSpreadSegs leaves, leaves beyond the LDS budget in a multi-leaf batch,
@@ -5923,17 +5981,19 @@ int tkv_amq_build_ex(int kind, const uint8_t* keys, const uint64_t* offs, uint32
   uint8_t* rest = ws + list_bytes;
   const uint64_t rest_bytes = ws_bytes - list_bytes;
   uint32_t n_small = 0, small_max = 0;
+  uint64_t small_keys = 0;  // (the inner build's launch heuristics size from these)
   for (uint32_t i = 0; i < n_segs; ++i)
     if (!batch_tiled(h_segs[i].n_blocks, fixed)) {
       ++n_small;
       small_max = std::max(small_max, h_segs[i].n_blocks);
+      small_keys += h_segs[i].n_keys;
     }
   if (n_small) {
     tkv_amq_segment* list = reinterpret_cast<tkv_amq_segment*>(ws);
     const uint32_t small_blocks = batch_window_max(fixed) * (kBloomLeafLdsBudget / 64);
     hipLaunchKernelGGL(bloom_compact_segs, dim3(1), dim3(1024), 0, s, d_segs, n_segs, small_blocks, list);
-    const int st = tkv_amq_build(kind, keys, offs, stride, n_keys, list, n_small, small_max, d_out, rest,
-                                 rest_bytes, stream);
+    const int st = build_batch(kind, keys, offs, stride, n_keys, list, n_small, small_max, d_out, rest,
+                               rest_bytes, stream, small_keys);
     if (st != TKV_AMQ_OK) return st;
   }
   // the tiled leaves of at most kDirectMaxTiles tiles: multi-leaf launches, as many leaves
@@ -6140,16 +6200,20 @@ int tkv_amq_bloom_route_plan(uint64_t chunk_keys, uint32_t n_chunks, uint32_t n_
 
 int tkv_amq_bloom_route_blocks(const uint8_t* d_keys, uint32_t key_bytes, uint64_t n_keys,
                                const tkv_amq_segment* d_seg, const tkv_amq_route_plan* plan,
-                               uint8_t* d_send, void* d_ws, uint64_t ws_bytes, void* stream)
+                               uint8_t* d_dst, uint64_t round_stride, void* d_ws, uint64_t ws_bytes,
+                               void* stream)
 {
   if (tkv_amq_device_count() == 0) return TKV_AMQ_UNAVAILABLE;
-  if (!plan || !d_seg || !d_send || (key_bytes != 16 && key_bytes != 24) || n_keys > plan->chunk_keys ||
+  if (!plan || !d_seg || !d_dst || (key_bytes != 16 && key_bytes != 24) || n_keys > plan->chunk_keys ||
       plan->hash_count == 0 || plan->hash_count > 8 || plan->route_wgs == 0 || plan->world == 0)
     return TKV_AMQ_INVALID_ARGUMENT;
+  // a round's world blocks must not overlap the next round's
+  if (round_stride && round_stride < (uint64_t)plan->world * plan->block_bytes) return TKV_AMQ_INVALID_ARGUMENT;
   const uintptr_t kalign = key_bytes == 16 ? 15 : 7;
   if (n_keys && (!d_keys || (reinterpret_cast<uintptr_t>(d_keys) & kalign))) return TKV_AMQ_INVALID_ARGUMENT;
   if (!d_ws || ws_bytes < plan->route_ws_bytes) return TKV_AMQ_INVALID_ARGUMENT;
-  const PartArgs a = route_args(*plan, d_keys, key_bytes, n_keys, 0u, d_send, static_cast<uint8_t*>(d_ws));
+  const PartArgs a = route_args(*plan, d_keys, key_bytes, n_keys, 0u, d_dst, static_cast<uint8_t*>(d_ws),
+                                round_stride);
   launch_route_blocks(a, *plan, as_stream(stream), d_seg, true);
   return hipGetLastError() == hipSuccess ? TKV_AMQ_OK : TKV_AMQ_INTERNAL;
 }

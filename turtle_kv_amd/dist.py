@@ -448,21 +448,24 @@ class HashShardedBloom:
 
       route     the rank's keys in `chunks` chunks (tkv_amq_bloom_route_blocks): every key
                 hashed once into its 12-byte bit record, counting-sorted by part on chip and
-                appended to fixed-capacity regions of the part owner's block;
-      exchange  chunk c's blocks in one all-to-all of equal splits (RCCL over xGMI) on the
-                communication stream while chunk c + 1 routes -- no counts exchanged first, no
-                host synchronisation;
-      build     each owned part from the chunks x ranks blocks received, in place
-                (tkv_amq_bloom_build_part_blocks: no regrouping copy);
+                appended to the part's fixed-capacity block (one block per part and chunk, in
+                global part order, so round j -- part j of every rank -- is one slice);
+      exchange  round j of chunk c in one all-to-all of equal splits (RCCL over xGMI) on the
+                communication stream: every round of a chunk as soon as its route is done, the
+                last chunk round by round -- no counts exchanged first, no host synchronisation;
+      build     part j from the chunks x ranks blocks of its round, in place
+                (tkv_amq_bloom_build_part_blocks: no regrouping copy), as soon as the last
+                chunk's round j has landed -- while rounds j + 1, j + 2 are exchanged;
       gather    round j (part j of every rank: one contiguous byte range, parts being owned
-                round-robin) all-gathered in place on the communication stream as soon as this
-                rank's part j is built, while part j + 1 builds.
+                round-robin) all-gathered in place on the communication stream once this
+                rank's part j is built, behind the exchange of round j + 2.
 
     `build(keys)` returns the whole filter payload (header + bitmap), byte-identical to a one-GPU
     tkv_amq_build of the concatenated keys, on every rank.  Without a process group (one GPU)
-    the route's blocks are the part builds' input directly.  k > 8 (bits_per_key >= 13) and a
-    step whose blocks lost overflow entries (`lost()`; keys far from uniform, e.g. one key
-    repeated) go through ExactHashShardedBloom."""
+    the route writes the part builds' input directly.  k > 8 (bits_per_key >= 13), a rank holding
+    more keys than the plan's chunks take, and a step whose blocks lost overflow entries (`lost()`;
+    keys far from uniform, e.g. one key repeated) go through ExactHashShardedBloom.  The receive
+    buffer holds round j's blocks at [j][chunk][sender]."""
 
     def __init__(self, n_total_keys: int, bits_per_key: int, world: int, rank: int, device,
                  src_page_id: int = 0, group=None, chunks: int = 1, max_keys_per_rank=None):
@@ -481,6 +484,9 @@ class HashShardedBloom:
         self.records = self.hash_count <= 8
         self.unit = 12 if self.records else 16
         self._exact = None
+        self._exact_out = None
+        self._fallback_out = None
+        self.last_fallback = None
         if not self.records:
             self._exact = ExactHashShardedBloom(n_total_keys, bits_per_key, world, rank, device,
                                                 src_page_id, group)
@@ -502,18 +508,25 @@ class HashShardedBloom:
         self.round_bytes = world * self.part_bytes
         # the filter payload, padded to whole rounds: part p's bitmap at 64 + p * part_bytes
         self.out = torch.zeros(64 + self.n_parts * self.part_bytes, dtype=torch.uint8, device=self.dev)
-        S = self.chunks * world
-        self.recv = torch.empty(S * self.block_bytes, dtype=torch.uint8, device=self.dev)
-        # chunk c's send blocks (one per destination); one rank routes straight into recv
-        self.send = ([self.recv[c * self.block_bytes:(c + 1) * self.block_bytes] for c in range(self.chunks)]
-                     if world == 1 else
-                     [torch.empty(world * self.block_bytes, dtype=torch.uint8, device=self.dev)
-                      for _ in range(self.chunks)])
+        C, W, B = self.chunks, world, self.block_bytes
+        # round j's blocks at [j][chunk][sender]: part j's inputs are C * W consecutive blocks
+        self.recv = torch.empty(self.g * C * W * B, dtype=torch.uint8, device=self.dev)
+        # chunk c's send buffer: every part's block in global part order (round j's W blocks =
+        # one slice); one rank routes straight into recv
+        self.send = (None if world == 1 else
+                     [torch.empty(self.n_parts * B, dtype=torch.uint8, device=self.dev)
+                      for _ in range(C)])
         self.route_ws = torch.empty(int(rp.route_ws_bytes), dtype=torch.uint8, device=self.dev)
         self.part_ws = torch.empty(int(rp.part_ws_bytes), dtype=torch.uint8, device=self.dev)
         self.d_seg = self.plan.device_segs(self.dev)
         self.comm = torch.cuda.Stream(device=self.dev) if self.dev.type == "cuda" else None
         self.last_lost = None
+        self.timeline = None
+
+    @property
+    def capacity(self) -> int:
+        """The most keys one rank's step routes (chunks x chunk_keys)."""
+        return self.chunks * self.chunk_keys if self._exact is None else 1 << 62
 
     # ---- ownership ------------------------------------------------------------------------
     def owned_parts(self) -> list[int]:
@@ -534,9 +547,22 @@ class HashShardedBloom:
         import torch.distributed as dist
         return dist.get_backend(self.group) != "nccl"
 
+    def _exact_builder(self):
+        """The exact exchange (built once, on first use: its buffers are reused)."""
+        if self._exact is None:
+            self._exact = ExactHashShardedBloom(self.n_total_keys, self.bpk, self.world, self.rank,
+                                                self.dev, self.src_page_id, self.group)
+        return self._exact
+
     # ---- the stages -----------------------------------------------------------------------
+    def recv_round(self, j: int):
+        """Round j's received blocks ([chunk][sender], C * W blocks)."""
+        n = self.chunks * self.world * self.block_bytes
+        return self.recv[j * n:(j + 1) * n]
+
     def route_chunk(self, keys, c: int):
-        """Chunk c of this rank's keys ([n, 16] or [n, 24] uint8 on the device) into send[c]."""
+        """Chunk c of this rank's keys ([n, 16] or [n, 24] uint8 on the device) into send[c]
+        (world 1: into recv at [j][c])."""
         import ctypes
 
         from . import abi
@@ -545,39 +571,53 @@ class HashShardedBloom:
         if kb not in (16, 24):
             raise abi.TkvAmqError(abi.INVALID_ARGUMENT, "hash-range sharding takes [n, 16] or "
                                   f"[n, 24] uint8 keys, got shape {tuple(keys.shape)}")
+        if keys.shape[0] > self.capacity:
+            raise abi.TkvAmqError(abi.INVALID_ARGUMENT, f"{keys.shape[0]} keys on rank {self.rank}: "
+                                  f"the plan routes at most {self.capacity} (max_keys_per_rank)")
         ck = self.chunk_keys
         part = keys[c * ck:(c + 1) * ck]
         n = part.shape[0]
-        L = abi.lib()
-        abi.check(L.tkv_amq_bloom_route_blocks(_ptr(part) if n else None, kb, n, _ptr(self.d_seg),
-                                               ctypes.byref(self.rp), _ptr(self.send[c]),
-                                               _ptr(self.route_ws), self.route_ws.numel(),
-                                               _stream_handle()), "tkv_amq_bloom_route_blocks")
+        B = self.block_bytes
+        if self.world == 1:
+            dst, stride = self.recv[c * B:], self.chunks * B
+        else:
+            dst, stride = self.send[c], 0
+        abi.check(abi.lib().tkv_amq_bloom_route_blocks(_ptr(part) if n else None, kb, n, _ptr(self.d_seg),
+                                                       ctypes.byref(self.rp), _ptr(dst), stride,
+                                                       _ptr(self.route_ws), self.route_ws.numel(),
+                                                       _stream_handle()), "tkv_amq_bloom_route_blocks")
 
-    def exchange_chunk(self, c: int):
-        """All-to-all of chunk c's blocks (equal splits of block_bytes), on the current stream."""
+    def exchange(self, c: int, j: int):
+        """All-to-all of round j of chunk c (one block of block_bytes per peer), on the current
+        stream, into recv at [j][c][sender]."""
         import torch
         import torch.distributed as dist
         if self.world == 1:
             return  # routed straight into recv
-        B, W = self.block_bytes, self.world
-        dst = self.recv[c * W * B:(c + 1) * W * B]
+        B, W, C = self.block_bytes, self.world, self.chunks
+        dst = self.recv[(j * C + c) * W * B:(j * C + c + 1) * W * B]
+        src = self.send[c][j * W * B:(j + 1) * W * B]
         if self._gloo:  # CPU rehearsal: stage through host memory
             host = torch.empty(W * B, dtype=torch.uint8)
-            dist.all_to_all_single(host, self.send[c].cpu(), group=self.group)
+            dist.all_to_all_single(host, src.cpu(), group=self.group)
             dst.copy_(host)
         else:
-            dist.all_to_all_single(dst, self.send[c], group=self.group)
+            dist.all_to_all_single(dst, src, group=self.group)
+
+    def exchange_chunk(self, c: int):
+        """Every round of chunk c."""
+        for j in range(self.g):
+            self.exchange(c, j)
 
     def build_part(self, j: int):
-        """This rank's j-th part (global part j * world + rank) from every received block."""
+        """This rank's j-th part (global part j * world + rank) from its round's blocks."""
         import ctypes
 
         from . import abi
         from .filters import _ptr, _stream_handle
         L = abi.lib()
         S = self.chunks * self.world
-        abi.check(L.tkv_amq_bloom_build_part_blocks(_ptr(self.recv), S, _ptr(self.d_seg),
+        abi.check(L.tkv_amq_bloom_build_part_blocks(_ptr(self.recv_round(j)), S, _ptr(self.d_seg),
                                                     ctypes.byref(self.rp), j * self.world + self.rank,
                                                     _ptr(self.out), _ptr(self.part_ws),
                                                     self.part_ws.numel(), _stream_handle()),
@@ -598,40 +638,95 @@ class HashShardedBloom:
             dist.all_gather_into_tensor(rnd, mine, group=self.group)
 
     # ---- the step -------------------------------------------------------------------------
-    def step(self, keys, gather: bool = True):
+    def step(self, keys, gather: bool = True, timeline: bool = False):
         """route -> exchange -> part builds (-> gathers), pipelined over two streams; on return
         the current stream is ordered after all of it (this rank's parts final, and with
-        gather every part on every rank)."""
+        gather every part on every rank).  timeline=True records timing events at every stage
+        boundary (`timeline_ms()` reads them after a synchronisation).
+
+        Communication-stream order (the same on every rank): the rounds of chunks 0..C-2 as
+        their routes finish, then X(0) X(1) X(2) G(0) X(3) G(1) ... X(g-1) G(g-3) G(g-2) G(g-1),
+        X(j) the last chunk's round j and G(j) the gather of round j; the compute stream builds
+        part j as soon as X(j) has landed."""
         import torch
         if self._exact is not None:
             self._exact.local_build(keys)
             if gather:
                 self._exact_out = self._exact.allgather()
             return
+        self.last_fallback = None
         coll = self._collective and self.comm is not None
+        xch = coll and self.world > 1
         cur = torch.cuda.current_stream(self.dev)
+        tl = {} if timeline else None
+
+        def mark(name, stream):
+            if tl is not None:
+                e = torch.cuda.Event(enable_timing=True)
+                e.record(stream)
+                tl[name] = e
+
+        mark("start", cur)
         if coll:
             self.comm.wait_stream(cur)  # the previous step's readers are done
-        for c in range(self.chunks):
+        C, g = self.chunks, self.g
+        for c in range(C):
             self.route_chunk(keys, c)
-            if coll and self.world > 1:
+            mark(f"route_{c}", cur)
+            if xch:
                 ev = torch.cuda.Event()
                 ev.record(cur)
                 with torch.cuda.stream(self.comm):
                     self.comm.wait_event(ev)
-                    self.exchange_chunk(c)
-        if coll and self.world > 1:
-            cur.wait_stream(self.comm)
-        for j in range(self.g):
+                    if c < C - 1:  # every round of an early chunk as soon as it is routed
+                        self.exchange_chunk(c)
+                        mark(f"exchange_chunk_{c}", self.comm)
+        x_ev = [None] * g
+        b_ev = [None] * g
+
+        def exchange_last(j):  # the last chunk's round j, on the communication stream
+            with torch.cuda.stream(self.comm):
+                self.exchange(C - 1, j)
+                mark(f"exchange_{j}", self.comm)
+                x_ev[j] = torch.cuda.Event()
+                x_ev[j].record(self.comm)
+
+        def gather_after_build(j):
+            with torch.cuda.stream(self.comm):
+                self.comm.wait_event(b_ev[j])
+                self.gather_round(j)
+                mark(f"gather_{j}", self.comm)
+
+        if xch:
+            for j in range(min(2, g)):
+                exchange_last(j)
+        for j in range(g):
+            if xch:
+                cur.wait_event(x_ev[j])
+            mark(f"build_{j}_start", cur)
             self.build_part(j)
+            mark(f"build_{j}", cur)
             if coll and gather:
-                ev = torch.cuda.Event()
-                ev.record(cur)
-                with torch.cuda.stream(self.comm):
-                    self.comm.wait_event(ev)
-                    self.gather_round(j)
+                b_ev[j] = torch.cuda.Event()
+                b_ev[j].record(cur)
+            if xch and j + 2 < g:
+                exchange_last(j + 2)
+            if coll and gather and j >= 1:
+                gather_after_build(j - 1)
+        if coll and gather and g:
+            gather_after_build(g - 1)
         if coll:
             cur.wait_stream(self.comm)
+        mark("end", cur)
+        self.timeline = tl
+
+    def timeline_ms(self) -> dict:
+        """Milliseconds from the step's start to each recorded stage end (after a step with
+        timeline=True and a synchronisation)."""
+        if not self.timeline:
+            return {}
+        t0 = self.timeline["start"]
+        return {k: round(t0.elapsed_time(e), 4) for k, e in self.timeline.items() if k != "start"}
 
     def local_build(self, keys):
         """route + exchange + part builds: this rank's parts of the bitmap are final."""
@@ -639,8 +734,7 @@ class HashShardedBloom:
 
     def allgather(self):
         """Every round all-gathered (after local_build) -> the whole payload on every rank."""
-        import torch
-        if self._exact is not None:
+        if not self.records:
             return self._exact.allgather()
         if self._collective:
             for j in range(self.g):
@@ -648,9 +742,12 @@ class HashShardedBloom:
         return self.filter()
 
     def filter(self):
-        """The filter payload (header + bitmap) of the last step."""
-        if self._exact is not None:
-            return getattr(self, "_exact_out", None)
+        """The filter payload (header + bitmap) of the last step: a view of this builder's
+        buffer, overwritten by its next step (build() returns a copy)."""
+        if not self.records:
+            return self._exact_out
+        if self.last_fallback is not None:
+            return self._fallback_out
         return self.out[:self.payload_bytes]
 
     def lost(self) -> bool:
@@ -659,31 +756,40 @@ class HashShardedBloom:
 
         from . import abi
         from .filters import _ptr, _stream_handle
-        if self._exact is not None:
+        if not self.records:
             return False
-        r = abi.lib().tkv_amq_bloom_blocks_lost(_ptr(self.recv), self.chunks * self.world,
+        r = abi.lib().tkv_amq_bloom_blocks_lost(_ptr(self.recv), self.g * self.chunks * self.world,
                                                 ctypes.byref(self.rp), _stream_handle())
         if r < 0:
             raise abi.TkvAmqError(-r, "tkv_amq_bloom_blocks_lost")
         self.last_lost = bool(r)
         return self.last_lost
 
-    def build(self, keys):
-        """The whole filter on every rank; a step that lost overflow entries (decided together
-        by every rank) is rebuilt through the exact exchange."""
+    def _any_rank(self, flag: bool) -> bool:
+        """MAX of a flag over the ranks (every rank takes the same path)."""
         import torch
         import torch.distributed as dist
-        self.step(keys, gather=True)
-        if self._exact is not None:
-            return self._exact_out
-        lost = self.lost()
-        if self._collective:
-            flag = torch.tensor([1 if lost else 0], dtype=torch.int32,
-                                device="cpu" if self._gloo else self.dev)
-            dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=self.group)
-            lost = bool(flag.item())
-        if lost:
-            ex = ExactHashShardedBloom(self.n_total_keys, self.bpk, self.world, self.rank, self.dev,
-                                       self.src_page_id, self.group)
-            return ex.build(keys)
-        return self.filter()
+        if not self._collective:
+            return flag
+        t = torch.tensor([1 if flag else 0], dtype=torch.int32,
+                         device="cpu" if self._gloo else self.dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        return bool(t.item())
+
+    def build(self, keys):
+        """The whole filter on every rank, as a new tensor.  A rank holding more keys than the
+        plan's chunks take, or a step that lost overflow entries (each decided together by
+        every rank), is built through the exact exchange instead."""
+        if not self.records:
+            self.step(keys, gather=True)
+            return self._exact_out.clone()
+        self.last_fallback = None
+        if self._any_rank(keys.shape[0] > self.capacity):
+            self.last_fallback = "keys_over_capacity"
+        else:
+            self.step(keys, gather=True)
+            if self._any_rank(self.lost()):
+                self.last_fallback = "overflow_lost"
+        if self.last_fallback is not None:
+            self._fallback_out = self._exact_builder().build(keys)
+        return self.filter().clone()

@@ -539,12 +539,20 @@ def build_all_filters(plan: FilterPlan, keys: KeyBatch, out=None, workspace=None
                           f"workspace holds {ws_bytes} bytes, the plan needs {plan.workspace_bytes}")
     sh = _stream_handle(stream)
     t0 = time.perf_counter()
-    # (_ex with the host plan: a Bloom batch with leaves past 16 LDS windows builds those through
-    # the tiled monolithic build, one each, and the rest through the batch kernels)
-    st = abi.lib().tkv_amq_build_ex(plan.kind, _ptr(keys.data), _ptr(keys.offsets), keys.stride,
-                                    keys.n, _ptr(plan.device_segs(dev)), _ptr(plan.segs), plan.n_segs,
-                                    plan.max_seg_blocks, _ptr(out), _ptr(workspace), ws_bytes, sh)
-    abi.check(st, "tkv_amq_build_ex")
+    # (_ex with the host plan: in a Bloom batch, leaves of 16- or 24-byte keys past 5 LDS windows
+    # -- other key shapes past 16 -- take the tiled build, up to 40 such leaves per launch, and
+    # the rest the batch kernels)
+    L = abi.lib()
+    if hasattr(L, "tkv_amq_build_ex"):
+        st = L.tkv_amq_build_ex(plan.kind, _ptr(keys.data), _ptr(keys.offsets), keys.stride,
+                                keys.n, _ptr(plan.device_segs(dev)), _ptr(plan.segs), plan.n_segs,
+                                plan.max_seg_blocks, _ptr(out), _ptr(workspace), ws_bytes, sh)
+        abi.check(st, "tkv_amq_build_ex")
+    else:  # (an older library loaded through TKV_AMQ_LIB: the batch entry without the host plan)
+        st = L.tkv_amq_build(plan.kind, _ptr(keys.data), _ptr(keys.offsets), keys.stride, keys.n,
+                             _ptr(plan.device_segs(dev)), plan.n_segs, plan.max_seg_blocks,
+                             _ptr(out), _ptr(workspace), ws_bytes, sh)
+        abi.check(st, "tkv_amq_build")
     if check:
         # synchronous: the batch is known good, record its metrics with the build latency
         abi.check(abi.lib().tkv_amq_build_check(plan.kind, _ptr(workspace), ws_bytes, sh),
