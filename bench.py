@@ -732,7 +732,7 @@ def bench_pipelined_gather(args, torch, dist, amq, world, rank, dev, kind, bpk, 
     gather_ok = None
     if rank == 0 and not args.no_verify:
         gather_ok = verify_gather(torch, amq, kind, bpk, cap, all_counts, stride, pl.filters(), 16,
-                                  dev)
+                                  dev, layout=(world, q), batches=batches)
     flag = torch.tensor([0 if gather_ok is False else 1], dtype=torch.int32, device=coll_dev)
     dist.all_reduce(flag, op=dist.ReduceOp.MIN)
     if not bool(flag.item()):
@@ -1084,9 +1084,14 @@ def verify_all_leaves(torch, kind, bpk, cap, plan, keys, offsets, out, key_bytes
     return res
 
 
-def verify_gather(torch, amq, kind, bpk, cap, all_counts, stride, gathered, key_bytes, dev):
+def verify_gather(torch, amq, kind, bpk, cap, all_counts, stride, gathered, key_bytes, dev,
+                  layout=None, batches=None):
     """Rank 0: the all-gathered array equals a single-process build of every leaf at the same
-    stride (16-byte keys; other key shapes are generated per rank and are not regenerable)."""
+    stride (16-byte keys; other key shapes are generated per rank and are not regenerable).
+    layout = (world, chunk_leaves) for the block-cyclic pipelined array (None: contiguous leaf
+    ranges of ceil(n_leaves / world) leaves; world then from the process group).  On a mismatch
+    `diagnose_gather` names every differing leaf with its owning rank and round, decides from
+    the oracle which side is wrong, and keeps the bytes (gpurun_out/verify_gather_fail/)."""
     if key_bytes != 16 or sum(all_counts) > 1_200_000_000:
         return None
     full_plan = amq.plan_filters(kind, all_counts, bpk, payload_capacity=cap, out_stride=stride)
@@ -1099,11 +1104,79 @@ def verify_gather(torch, amq, kind, bpk, cap, all_counts, stride, gathered, key_
     ok = bool(torch.equal(full[:gathered.numel()], gathered))
     if not ok and stride:
         bad = torch.nonzero(full[:gathered.numel()] != gathered).flatten()
-        leaves = sorted({int(x) // stride for x in bad[:4096].tolist()})
-        print(f"verify_gather: {bad.numel()} bytes differ, in leaves {leaves[:16]} "
+        leaves = sorted({int(x) // stride for x in bad.tolist()})
+        print(f"verify_gather: {bad.numel()} bytes differ, in {len(leaves)} leaves {leaves[:16]} "
               f"(first byte {int(bad[0])})", file=sys.stderr, flush=True)
+        try:
+            diagnose_gather(torch, amq, kind, bpk, cap, all_counts, stride, gathered, full, allk,
+                            leaves, layout, batches)
+        except Exception as e:  # (the diagnosis must not hide the failure itself)
+            print(f"verify_gather: diagnosis failed: {e!r}", file=sys.stderr, flush=True)
     del full, allk
     return ok
+
+
+def diagnose_gather(torch, amq, kind, bpk, cap, all_counts, stride, gathered, full, allk, leaves,
+                    layout, batches, max_leaves=32):
+    """For each differing leaf (up to max_leaves): its owner rank and round, whether the keys
+    each side built from are the oracle's (for VQF: sorted as the oracle sorts them), which
+    side's bytes equal the oracle's filter, and whether a rebuild of the leaf alone on this GPU
+    reproduces either side.  Writes summary.json plus the leaves' bytes from both sides and the
+    oracle under gpurun_out/verify_gather_fail/ and prints the summary on stderr."""
+    import torch.distributed as dist
+    from oracle import oracle as O
+    O.build_oracle()
+    world = layout[0] if layout else dist.get_world_size()
+    n = len(all_counts)
+    begin = np.concatenate([[0], np.cumsum(np.asarray(all_counts, dtype=np.int64))])
+    out_dir = os.path.join(ROOT, "gpurun_out", "verify_gather_fail")
+    os.makedirs(out_dir, exist_ok=True)
+    rows, keep = [], {}
+    for s_ in leaves[:max_leaves]:
+        if layout:
+            q = layout[1]
+            rnd, rank = s_ // (world * q), (s_ // q) % world
+        else:
+            per = -(-n // world)
+            rnd, rank = 0, s_ // per
+        k0, k1 = int(begin[s_]), int(begin[s_ + 1])
+        kh = O.gen_keys16(42, k0, k1 - k0)
+        if kind == 1:
+            O.sort_segments(kh, np.array([0, k1 - k0], dtype=np.uint64))
+            st, ref, pl = O.vqf_build(kh, k1 - k0, bpk, cap, src_page_id=s_)
+            ref = ref[:pl.payload_used]
+        else:
+            st, ref = O.bloom_build(kh, k1 - k0, bpk, src_page_id=s_)
+        ref = ref.tobytes()
+        g = gathered[s_ * stride:s_ * stride + len(ref)].cpu().numpy().tobytes()
+        f = full[s_ * stride:s_ * stride + len(ref)].cpu().numpy().tobytes()
+        row = {"leaf": int(s_), "rank": int(rank), "round": int(rnd), "keys": k1 - k0,
+               "gathered_equals_oracle": g == ref, "single_build_equals_oracle": f == ref,
+               "single_build_keys_equal_oracle": bool(np.array_equal(allk[k0:k1].cpu().numpy(), kh)),
+               "bytes_differing": int(sum(a != b for a, b in zip(g, f)))}
+        if batches is not None and layout and rank == 0 and rnd < len(batches) and batches[rnd] is not None:
+            # this rank's own round batch: the keys its build actually read
+            rb = rnd * world * q  # the round's first leaf; rank 0's leaves come first in it
+            off = int(begin[s_] - begin[rb])
+            row["round_batch_keys_equal_oracle"] = bool(np.array_equal(
+                batches[rnd].data[off:off + k1 - k0].cpu().numpy(), kh))
+        # the leaf alone, twice, on this GPU
+        sp = amq.plan_filters(kind, [k1 - k0], bpk, payload_capacity=cap, src_page_ids=[s_])
+        again = []
+        for _ in range(2):
+            o = amq.build_all_filters(sp, amq.KeyBatch.fixed(torch.from_numpy(kh).to(allk.device)))
+            again.append(o[:len(ref)].cpu().numpy().tobytes() == ref)
+        row["alone_equals_oracle"] = again
+        rows.append(row)
+        keep[f"leaf{s_}_gathered"] = np.frombuffer(g, np.uint8)
+        keep[f"leaf{s_}_single"] = np.frombuffer(f, np.uint8)
+        keep[f"leaf{s_}_oracle"] = np.frombuffer(ref, np.uint8)
+    summary = {"kind": kind, "bpk": bpk, "world": world, "layout": layout, "n_leaves": n,
+               "differing_leaves": len(leaves), "leaves": rows}
+    with open(os.path.join(out_dir, "summary.json"), "w") as fh:
+        json.dump(summary, fh, indent=1)
+    np.savez(os.path.join(out_dir, "leaves.npz"), **keep)
+    print("verify_gather diagnosis: " + json.dumps(summary), file=sys.stderr, flush=True)
 
 
 def verify_probe(torch, kind, plan, filters, q, qseg, is_hit, res, baseline):

@@ -639,7 +639,15 @@ class LeafBatcher
     if (b->reqs.size() >= opt_.max_batch) close(b);
     lk.unlock();
 
-    const Status staged = stage(r, *b);
+    Status staged = stage(r, *b);
+    // this leaf's keys (and offsets) to the device now, on the batch's stream: the copies of
+    // the members overlap the collection window and each other's staging, so the leader's
+    // build waits only for the last of them (round 6; they were one copy after the batch closed)
+    // (a leaf whose staging failed copies too: its zero-length offsets keep the batch valid)
+    if (n) {
+      const Status c = copy_in(r, *b);
+      if (staged.ok()) staged = c;
+    }
 
     lk.lock();
     ++b->staged;
@@ -796,6 +804,17 @@ class LeafBatcher
     return OkStatus();
   }
 
+  // a member's staged keys (and its offsets) to the batch's device buffers, on its stream
+  static Status copy_in(const Req& r, Batch& b)
+  {
+    if (hipMemcpyAsync(b.d_keys.get<u8>() + r.byte_off, b.h_keys + r.byte_off, r.bytes, hipMemcpyHostToDevice,
+                       b.stream) != hipSuccess ||
+        (b.stride == 0 && hipMemcpyAsync(b.d_offs.get<u8>() + 8 * r.key_off, b.h_offs + r.key_off, 8 * r.n,
+                                         hipMemcpyHostToDevice, b.stream) != hipSuccess))
+      return Status::from(TKV_AMQ_INTERNAL, "hipMemcpyAsync keys");
+    return OkStatus();
+  }
+
   // on the leader's thread: every member staged, nothing else touches the batch
   void run(Batch& b)
   {
@@ -837,14 +856,17 @@ class LeafBatcher
     if (!reserve_device(b.d_out, ws_off + ws_bytes)) return Status::from(TKV_AMQ_RESOURCE_EXHAUSTED, "hipMalloc");
     std::memcpy(b.h_io, segs.data(), seg_bytes);  // the host plan (tkv_amq_build_ex's h_segs)
     u8* h_out = b.h_io + seg_bytes;
-    // one copy in: the keys, then the segments at the next 256-byte boundary
+    // the members copied their keys in (copy_in); the segments follow at the next 256-byte
+    // boundary, and the offsets' closing entry
     const u64 seg_off = align256(bytes);
     std::memcpy(b.h_keys + seg_off, segs.data(), seg_bytes);
     if (b.stride == 0) b.h_offs[n] = bytes;
     hipStream_t s = b.stream;
-    if (hipMemcpyAsync(b.d_keys.get(), b.h_keys, seg_off + seg_bytes, hipMemcpyHostToDevice, s) != hipSuccess ||
-        (b.stride == 0 && hipMemcpyAsync(b.d_offs.get(), b.h_offs, 8 * (n + 1), hipMemcpyHostToDevice, s) != hipSuccess))
-      return Status::from(TKV_AMQ_INTERNAL, "hipMemcpyAsync keys");
+    if (hipMemcpyAsync(b.d_keys.get<u8>() + seg_off, b.h_keys + seg_off, seg_bytes, hipMemcpyHostToDevice, s) !=
+            hipSuccess ||
+        (b.stride == 0 && hipMemcpyAsync(b.d_offs.get<u8>() + 8 * n, b.h_offs + n, 8, hipMemcpyHostToDevice, s) !=
+                              hipSuccess))
+      return Status::from(TKV_AMQ_INTERNAL, "hipMemcpyAsync segments");
     u8* d_ws = b.d_out.get<u8>() + ws_off;
     st = tkv_amq_build_ex((int)b.kind, b.d_keys.get(), b.stride ? nullptr : b.d_offs.get<u64>(), b.stride, n,
                           reinterpret_cast<const tkv_amq_segment*>(b.d_keys.get<u8>() + seg_off),

@@ -429,7 +429,7 @@ def _sharded_worker(rank, world, port, n_total, bpk, chunks, split, q):
 
 @pytest.mark.parametrize("world,n_total,bpk,chunks,split,fallback", [
     (2, 3_000_000, 12, 2, (0.5,), None),               # even: the pipelined step
-    (3, 2_500_001, 10, 3, (0.3, 0.62), None),          # ragged, k = 7
+    (3, 2_500_001, 10, 3, (1 / 3, 2 / 3), None),        # ragged chunks, k = 7
     (2, 2_000_000, 12, 2, (0.6,), "keys_over_capacity"),  # rank 0 over its even share
 ])
 def test_hash_sharded_step_gloo_ranks(world, n_total, bpk, chunks, split, fallback):

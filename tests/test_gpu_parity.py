@@ -759,6 +759,39 @@ def test_bloom_oversize_leaves_among_many(oracle, amq, torch, shape):
     assert_same(plan, out, ref)
 
 
+@pytest.mark.parametrize("shape,bpk,counts", [
+    ("var", 10, [3_000_000, 500, 16384]),          # one 3M-key variable-length leaf
+    ("var", 12, [16384, 2_700_000, 0, 1, 2_900_000, 77]),
+    ("k20", 10, [3_000_000, 500, 16384]),          # a fixed stride other than 16 and 24
+    ("k40", 8, [5_200_000, 3]),                    # keys of 32 bytes and more: hashed per seed
+    ("var", 16, [3_000_000, 500]),                 # k > 8: device atomics (records hold 8 bits)
+    ("var", 10, [2_700_000]),                      # one filter past the window path
+    ("k20", 12, [2_200_000]),
+])
+def test_bloom_oversize_other_key_shapes(oracle, amq, torch, shape, bpk, counts):
+    """Leaves past 16 LDS windows of variable-length or other fixed-size keys, in a batch and
+    alone: the tiled build with the partition hashing each key into its bit record
+    (bloom_part_any; round 5: device atomics at 3.6 Gkeys/s), byte-equal to the oracle."""
+    rng = np.random.default_rng(len(counts) * bpk)
+    n = sum(counts)
+    offs = None
+    if shape == "var":
+        lens = rng.integers(8, 32, n)
+        lens[::97] = rng.integers(32, 48, lens[::97].size)   # some past XxhShort's 31 bytes
+        keys, stride = rng.integers(0, 256, int(lens.sum()), dtype=np.uint8), 0
+        offs = np.zeros(n + 1, np.int64)
+        offs[1:] = np.cumsum(lens)
+    else:
+        stride = int(shape[1:])
+        keys = rng.integers(0, 256, (n, stride), dtype=np.uint8)
+    ref = oracle_per_segment(oracle, 0, keys, counts, bpk, stride=stride,
+                             offsets=None if offs is None else offs.astype(np.uint64))
+    plan, out = gpu_build(amq, torch, 0, torch.from_numpy(keys).cuda(), counts, bpk,
+                          offsets_t=None if offs is None else torch.from_numpy(offs).cuda())
+    assert plan.max_seg_blocks > 16 * 160 * 1024 // 64
+    assert_same(plan, out, ref)
+
+
 @pytest.mark.parametrize("shape,bpk,n_big", [("k16", 10, 35), ("k16", 16, 17), ("k24", 12, 17)])
 def test_bloom_many_oversize_leaves(oracle, amq, torch, shape, bpk, n_big):
     """More oversize leaves than one multi-leaf launch holds (bloom_part_multi: 15 leaves), and

@@ -285,3 +285,42 @@ def test_vqf_round_plans_on_one_poisoned_workspace(oracle, amq, torch, n_keys):
         st, ref, pl = oracle.vqf_build(keys[int(sb[s]):], counts[s], 12, cap, src_page_id=s)
         assert st == 0
         assert o[s * stride:s * stride + pl.payload_used].tobytes() == ref[:pl.payload_used].tobytes()
+
+
+@pytest.mark.parametrize("kind", [0, 1])
+def test_verify_gather_names_the_wrong_leaf(oracle, amq, torch, kind, capsys):
+    """VERDICT r05 (wrong gathered VQF array, round 4): a gathered array that differs from the
+    single-process build is reported leaf by leaf -- its owning rank and round in the
+    block-cyclic layout, which side equals the oracle, whether the keys each side built from are
+    the oracle's, whether a lone rebuild reproduces the oracle -- and its bytes are kept.  Here
+    one byte of leaf 5's gathered payload is flipped: the diagnosis must blame the gathered side
+    (leaf 5 = round 1, rank 0 with 2 ranks and 2-leaf chunks) and clear the single build."""
+    import json
+    import os
+
+    import bench
+    counts = [4096] * 9 + [1000]
+    bpk, cap = (10, 0) if kind == 0 else (12, 16320)
+    from turtle_kv_amd import dist as tdist
+    stride = tdist.leaf_stride(kind, bpk, max(counts), cap)
+    plan = amq.plan_filters(kind, counts, bpk, payload_capacity=cap, out_stride=stride)
+    keys = amq.gen_keys16(42, 0, sum(counts))
+    if kind == 1:
+        keys = bench.sort_segments_device(torch, keys, counts)
+    good = torch.zeros(plan.total_out_bytes, dtype=torch.uint8, device="cuda")
+    amq.build_all_filters(plan, amq.KeyBatch.fixed(keys), out=good)
+    assert bench.verify_gather(torch, amq, kind, bpk, cap, counts, stride, good, 16,
+                               torch.device("cuda"), layout=(2, 2)) is True
+    bad = good.clone()
+    bad[5 * stride + 100] ^= 0x40
+    assert bench.verify_gather(torch, amq, kind, bpk, cap, counts, stride, bad, 16,
+                               torch.device("cuda"), layout=(2, 2)) is False
+    d = os.path.join(bench.ROOT, "gpurun_out", "verify_gather_fail")
+    summary = json.load(open(os.path.join(d, "summary.json")))
+    (row,) = summary["leaves"]
+    assert (row["leaf"], row["rank"], row["round"]) == (5, 0, 1)
+    assert row["gathered_equals_oracle"] is False and row["single_build_equals_oracle"] is True
+    assert row["single_build_keys_equal_oracle"] is True and row["alone_equals_oracle"] == [True, True]
+    z = np.load(os.path.join(d, "leaves.npz"))
+    assert (z["leaf5_gathered"] != z["leaf5_oracle"]).sum() == 1
+    assert "verify_gather diagnosis" in capsys.readouterr().err

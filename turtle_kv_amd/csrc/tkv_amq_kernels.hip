@@ -1039,7 +1039,10 @@ __host__ __device__ constexpr inline bool part_tbl_fits(uint32_t n_tiles)
 static_assert(kRecPartMaxTiles <= 8192, "a record's 13-bit tile field");
 static_assert(kPartBatch < 65536, "u16 ranks");
 
-enum PartSrc : int { kSrcKey16 = 0, kSrcKey24 = 1, kSrcRec12 = 2, kSrcRaw16 = 3, kSrcSeg12 = 4 };
+// kSrcKeyVar / kSrcKeyFixed: keys of any other shape (the reference's KeyView ranges: bytes +
+// offsets, or a fixed stride), hashed by the partition (k <= 8: bit records)
+enum PartSrc : int { kSrcKey16 = 0, kSrcKey24 = 1, kSrcRec12 = 2, kSrcRaw16 = 3, kSrcSeg12 = 4,
+                     kSrcKeyVar = 5, kSrcKeyFixed = 6 };
 // what part_body buckets by: the filter's tiles (the partition, ahead of bloom_tile), or the
 // route's parts (bloom_route_part: the one-pass route of a filter past kDirectMaxTiles tiles,
 // and of a hash-range sharded filter's keys to their owners)
@@ -1165,6 +1168,31 @@ __device__ inline uint32_t rec_hash_bits(const Key24& kv, uint32_t nb, uint32_t 
   for (uint32_t j = 1; j < 8; ++j) {
     if (K != 0 ? j < (uint32_t)K : j < k) b[j] = x.finish_lo9(xxh_fixed_rc<24>(c_bloom.seed[j])) & 511u;
     else b[j] = b[0];
+  }
+  return (uint32_t)__umul64hi(h0, (uint64_t)nb);
+}
+
+// a key of any other shape (kSrcKeyVar / kSrcKeyFixed): its bytes and length
+struct KeyRef {
+  const uint8_t* p;
+  uint32_t len;
+};
+
+// its block and bit indices (k <= 8): under 32 bytes the seed-independent lane rounds are
+// shared by the k hashes (XxhShort), longer keys hash from scratch per seed
+__device__ inline uint32_t rec_hash_bits_any(const KeyRef& kr, uint32_t nb, uint32_t k, uint32_t (&b)[8])
+{
+  uint64_t h0;
+  if (kr.len < 32) {
+    const XxhShort x(kr.p, kr.len);
+    h0 = x.finish(c_bloom.seed_p5[0]);
+    b[0] = (uint32_t)h0 & 511u;
+#pragma unroll
+    for (uint32_t j = 1; j < 8; ++j) b[j] = j < k ? x.finish_lo9(c_bloom.seed_p5[j]) & 511u : b[0];
+  } else {
+    h0 = xxh64_bytes(kr.p, kr.len, c_bloom.seed[0]);
+    b[0] = (uint32_t)h0 & 511u;
+    for (uint32_t j = 1; j < 8; ++j) b[j] = j < k ? (uint32_t)xxh64_bytes(kr.p, kr.len, c_bloom.seed[j]) & 511u : b[0];
   }
   return (uint32_t)__umul64hi(h0, (uint64_t)nb);
 }
@@ -1433,6 +1461,9 @@ struct PartArgs {
   // writing a partial image at part_img + (t * split + s) * 128 KiB, ORed by bloom_tile_merge
   uint32_t split;
   uint8_t* part_img;
+  // kSrcKeyVar: the key offsets; kSrcKeyFixed: the key stride
+  const uint64_t* offs;
+  uint32_t stride;
 };
 
 __host__ __device__ inline uint64_t div_magic(uint32_t d) { return (0x100000000ull / d) + 1; }
@@ -1533,7 +1564,8 @@ __device__ void part_body(const tkv_amq_segment& sg, const PartArgs& a, uint32_t
   constexpr bool ROUTE = DST == kDstParts;
   static_assert(TBL || !ROUTE, "the route stores through its table");
   constexpr bool ROUTED = SRC == kSrcRec12 || SRC == kSrcSeg12;  // records with their tile in part
-  static_assert(!(ROUTE && (RAW || ROUTED)), "the route hashes keys");
+  constexpr bool ANY = SRC == kSrcKeyVar || SRC == kSrcKeyFixed;  // keys through KeyRef
+  static_assert(!(ROUTE && (RAW || ROUTED || ANY)), "the route hashes 16- or 24-byte keys");
   // 16-byte records: four key words and the tile per item in LDS, half the items per batch
   constexpr uint32_t RB = RAW ? 16 : 12, U = RAW ? kPartU / 2 : kPartU, NT = kPartThreads, B = U * NT;
   constexpr uint32_t NPL = RAW ? 5 : 3;  // LDS planes (ROUTE: + a u16 plane of parts)
@@ -1599,18 +1631,31 @@ __device__ void part_body(const tkv_amq_segment& sg, const PartArgs& a, uint32_t
     const uint32_t per = (n + P - 1) / P;
     kb = min(n, w * per);
     ke = min(n, kb + per);
+  } else if constexpr (ANY) {
+    // (the key array itself: items index from the segment's first key when from_seg)
+    src = a.src;
+    n = a.from_seg ? min(a.n, sg.n_keys) : a.n;
+    kb = min(n, w * a.g.per);
+    ke = min(n, kb + a.g.per);
   } else {
     part_items(sg, a, IB, src, n);
     const uint32_t per = a.cnt ? (n + P - 1) / P : a.g.per;
     kb = min(n, w * per);
     ke = min(n, kb + per);
   }
+  const uint64_t key0 = ANY && a.from_seg ? sg.key_begin : 0;  // kSrcKeyVar / kSrcKeyFixed
   const uint64_t ovf_base = a.g.ovf_off + (uint64_t)w * a.g.per * 16;  // (lists 16 B per item apart)
   const uint32_t last_item = ke > 0 ? ke - 1 : 0;
   uint32_t cs = 0;  // kSrcSeg12: the block of this thread's last item (items rise per thread)
-  using In = typename std::conditional<SRC == kSrcKey24, Key24, uint4>::type;
+  using In = typename std::conditional<SRC == kSrcKey24, Key24,
+                                      typename std::conditional<ANY, KeyRef, uint4>::type>::type;
   auto load_in = [&](uint32_t i) -> In {
-    if constexpr (SRC == kSrcSeg12) {
+    if constexpr (SRC == kSrcKeyVar) {
+      const uint64_t o0 = a.offs[key0 + i], o1 = a.offs[key0 + i + 1];
+      return KeyRef{src + o0, (uint32_t)(o1 - o0)};
+    } else if constexpr (SRC == kSrcKeyFixed) {
+      return KeyRef{src + (key0 + i) * a.stride, a.stride};
+    } else if constexpr (SRC == kSrcSeg12) {
       while (i >= pre[cs + 1]) ++cs;
       return load_rec12(src + (uint64_t)cs * a.blk.bytes + seg_reg, i - pre[cs]);
     } else if constexpr (SRC == kSrcRec12) {
@@ -1682,6 +1727,25 @@ __device__ void part_body(const tkv_amq_segment& sg, const PartArgs& a, uint32_t
 #pragma unroll
     for (uint32_t u = 0; u < U; ++u) in[u] = load_in(min(kb + u * NT + tid, last_item));
   }
+  // ROUTE: the previous batch's run reservations (thread t: parts t and t + NT) and its store
+  // table from them and the run starts its scan left in `start`
+  uint32_t resv[ROUTE ? 2 : 1] = {};
+  auto route_table = [&]() {
+    if constexpr (ROUTE) {
+      static_assert(kRouteMaxParts <= 2 * NT, "two parts per thread at most");
+#pragma unroll
+      for (uint32_t r = 0; r < 2; ++r) {
+        const uint32_t t = tid + r * NT;
+        if (t < T) {
+          const uint32_t st = lds_u16(start, t), o = min(resv[r], cap);  // (o = cap: all overflow)
+          const uint32_t jl = div_by_magic(t, a.w_magic), dr = t - jl * a.world;
+          const uint64_t base = (uint64_t)jl * a.blk.jstride + (uint64_t)dr * a.blk.bytes + a.blk.recs_off;
+          roff[t] = base + (uint64_t)RB * o - (uint64_t)RB * st;
+          rlim[t] = (int32_t)(cap + st) - (int32_t)o;
+        }
+      }
+    }
+  };
   uint32_t par = 0;
   // Per iteration: hash batch b; write out batch b - 1 (its stores then drain while this
   // batch is scanned and sorted: the compiler waits for every outstanding load and store
@@ -1712,7 +1776,9 @@ __device__ void part_body(const tkv_amq_segment& sg, const PartArgs& a, uint32_t
           t = rec_tile(r0[u], r1[u], r2[u]);
         } else {
           uint32_t bits[8];
-          const uint32_t blk = rec_hash_bits<K>(in[u], nb, k, bits);
+          uint32_t blk;
+          if constexpr (ANY) blk = rec_hash_bits_any(in[u], nb, k, bits);
+          else blk = rec_hash_bits<K>(in[u], nb, k, bits);
           const uint32_t tg = blk >> kTileShift;
           if constexpr (ROUTE) {
             t = div_by_magic(tg, a.q_magic);  // the key's part; its record's tile is in the part
@@ -1731,14 +1797,14 @@ __device__ void part_body(const tkv_amq_segment& sg, const PartArgs& a, uint32_t
         tr[u] = t << 16 | rank;
       }
     }
-    write_out();  // batch b - 1 (total = 0 before the first batch: sink stores only)
-    // ROUTE: each part's run of this batch reserved in the part's block with one device-scope
-    // atomicAdd on its count, issued before the next batch's loads (the returns share vmcnt
-    // with them, in order: the table below waits for the reservations, not for the loads)
-    uint32_t resv[ROUTE ? 2 : 1];
     if constexpr (ROUTE) {
-      static_assert(kRouteMaxParts <= 2 * NT, "two parts per thread at most");
-      lds_barrier();  // the batch's histogram is complete
+      // batch b - 1's store table from its reservations (their returns came back with the
+      // loads of this batch's items, which this batch's hash waited for), then batch b's runs
+      // reserved -- one device-scope atomicAdd per part on its block's count, issued ahead of
+      // the write-out's stores and the next batch's loads and read one batch later, so no
+      // wait of the loop is on them
+      route_table();
+      lds_barrier();  // the table is complete; so is batch b's histogram
 #pragma unroll
       for (uint32_t r = 0; r < 2; ++r) {
         const uint32_t t = tid + r * NT;
@@ -1754,26 +1820,15 @@ __device__ void part_body(const tkv_amq_segment& sg, const PartArgs& a, uint32_t
         }
       }
     }
+    write_out();  // batch b - 1 (total = 0 before the first batch: sink stores only)
 #pragma unroll
     for (uint32_t u = 0; u < U; ++u)  // the next batch's items
       in[u] = load_in(min(b0 + B + u * NT + tid, last_item));
-    if constexpr (!ROUTE) lds_barrier();
+    lds_barrier();
     total = part_scan(hist, prev, start, cursor, HW, wsum);
-    if constexpr (TBL) {
+    if constexpr (TBL && !ROUTE) {
       // this batch's store table (read by its write-out, after the barrier below)
-      if constexpr (ROUTE) {
-#pragma unroll
-        for (uint32_t r = 0; r < 2; ++r) {
-          const uint32_t t = tid + r * NT;
-          if (t < T) {
-            const uint32_t st = lds_u16(start, t), o = min(resv[r], cap);  // (o = cap: all overflow)
-            const uint32_t jl = div_by_magic(t, a.w_magic), dr = t - jl * a.world;
-            const uint64_t base = (uint64_t)jl * a.blk.jstride + (uint64_t)dr * a.blk.bytes + a.blk.recs_off;
-            roff[t] = base + (uint64_t)RB * o - (uint64_t)RB * st;
-            rlim[t] = (int32_t)(cap + st) - (int32_t)o;
-          }
-        }
-      } else {
+      {
         for (uint32_t t = tid; t < T; t += NT) {
           const uint32_t st = lds_u16(start, t), cu = cursor[t];
           const uint64_t base = a.g.regions_off + ((uint64_t)t * P + w) * cap * a.g.rb;
@@ -1796,6 +1851,10 @@ __device__ void part_body(const tkv_amq_segment& sg, const PartArgs& a, uint32_t
       }
       if constexpr (ROUTE) plp[pos] = (uint16_t)t;
     }
+    lds_barrier();
+  }
+  if constexpr (ROUTE) {
+    route_table();
     lds_barrier();
   }
   write_out();  // the last batch
@@ -1861,6 +1920,20 @@ __global__ __launch_bounds__(kPartThreads) void bloom_part_routed(const tkv_amq_
   if (k == 0) return;
   if (k <= 8) part_body<0, kSrcRec12>(sg, a, s_part);
   else part_body<0, kSrcRaw16>(sg, a, s_part);
+}
+
+// keys of any other shape (variable-length through offsets, or a fixed stride; k <= 8): each
+// key hashed once into its bit record by the partition, as 16- and 24-byte keys are (round 6:
+// such a leaf past the window path set its bits with device atomics, 3.6 Gkeys/s)
+template <int SRC>
+__global__ __launch_bounds__(kPartThreads) void bloom_part_any(const tkv_amq_segment* __restrict__ segs,
+                                                               PartArgs a)
+{
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_part[];
+  const tkv_amq_segment sg = segs[0];
+  if (sg.hash_count == 0 || sg.hash_count > 8) return;
+  if (a.tbl) part_body<0, SRC, kDstTiles, true>(sg, a, s_part);
+  else part_body<0, SRC>(sg, a, s_part);
 }
 
 // The one-pass route (k <= 8): every key hashed once into its 12-byte bit record, counting-
@@ -4847,7 +4920,9 @@ inline void set_mono_attributes()
   once_per_device(lds_attr, [] {
     for (const void* f : {reinterpret_cast<const void*>(&bloom_part_keys16),
                           reinterpret_cast<const void*>(&bloom_part_keys24),
-                          reinterpret_cast<const void*>(&bloom_part_routed)})
+                          reinterpret_cast<const void*>(&bloom_part_routed),
+                          reinterpret_cast<const void*>(&bloom_part_any<kSrcKeyVar>),
+                          reinterpret_cast<const void*>(&bloom_part_any<kSrcKeyFixed>)})
       (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)(160 * 1024));
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&bloom_tile),
@@ -4871,6 +4946,8 @@ inline void launch_part_build(int src, PartArgs a, hipStream_t s, const tkv_amq_
   const dim3 grid(a.g.P), block(kPartThreads);
   if (src == kSrcKey24) hipLaunchKernelGGL(bloom_part_keys24, grid, block, lds, s, d_segs, a);
   else if (src == kSrcKey16) hipLaunchKernelGGL(bloom_part_keys16, grid, block, lds, s, d_segs, a);
+  else if (src == kSrcKeyVar) hipLaunchKernelGGL(bloom_part_any<kSrcKeyVar>, grid, block, lds, s, d_segs, a);
+  else if (src == kSrcKeyFixed) hipLaunchKernelGGL(bloom_part_any<kSrcKeyFixed>, grid, block, lds, s, d_segs, a);
   else hipLaunchKernelGGL(bloom_part_routed, grid, block, lds, s, d_segs, a);
   const uint32_t S = a.split > 1 ? a.split : 1u;
   hipLaunchKernelGGL(bloom_tile, dim3(a.g.n_tiles * S), dim3(kTileThreads), 64ull * kTileBlocks, s, d_segs, a,
@@ -5184,6 +5261,43 @@ inline uint32_t bloom_k_of(uint64_t n_keys, uint64_t n_blocks)
   return 0;
 }
 
+// One filter of keys of any other shape (variable-length, or a fixed stride other than 16 and
+// 24) with k <= 8 and at most kDirectMaxTiles tiles: the tiled build with the partition hashing
+// each key into its bit record (bloom_part_any), tiles split over the chip below 128 of them.
+struct AnyPlan {
+  PartGeom pg;
+  uint32_t split;
+  uint64_t img_off, bytes;
+};
+
+inline bool any_tiled_ok(uint32_t k, uint64_t n_keys, uint64_t n_blocks)
+{
+  return k >= 1 && k <= 8 && filter_tiles(n_blocks) <= kDirectMaxTiles && n_keys <= 0xffffffffull;
+}
+
+inline AnyPlan any_plan(uint64_t n_keys, uint64_t n_blocks)
+{
+  AnyPlan p{};
+  const uint32_t T = filter_tiles(n_blocks);
+  p.pg = part_geom(n_keys, n_keys, T, 12, mono_wg_items(n_keys, 32ull * kPartThreads));
+  p.split = tile_split(T);
+  p.img_off = align256(p.pg.bytes);
+  p.bytes = p.split > 1 ? p.img_off + (uint64_t)T * p.split * (64ull * kTileBlocks) : p.pg.bytes;
+  return p;
+}
+
+// keys [0, n) of segment 0 (from its key_begin), offs != nullptr: variable-length
+inline void launch_any(const AnyPlan& p, hipStream_t s, const uint8_t* keys, const uint64_t* offs, uint32_t stride,
+                       uint32_t n, const tkv_amq_segment* d_seg, uint8_t* ws, uint8_t* d_out)
+{
+  PartArgs a{keys, n, 0u, 1u, 16u, nullptr, 0u, ws, p.pg};
+  a.split = p.split;
+  a.part_img = ws + p.img_off;
+  a.offs = offs;
+  a.stride = stride;
+  launch_part_build(offs ? kSrcKeyVar : kSrcKeyFixed, a, s, d_seg, d_out, 0u);
+}
+
 // keys [0, n) of segment 0 (kb 16 or 24; routed 24-byte keys need the one-pass route, k <= 8)
 inline void launch_mono(const MonoPlan& m, hipStream_t s, const uint8_t* keys, uint32_t kb, uint32_t n,
                         const tkv_amq_segment* d_segs, uint8_t* ws, uint8_t* d_out, uint64_t key0 = 0)
@@ -5354,6 +5468,8 @@ inline uint64_t bloom_oversize_ws_bytes(const tkv_amq_segment* segs, uint32_t n_
         multi_max = std::max(multi_max, b);
       } else if (fixed) {
         big = std::max(big, mono_plan(g.n_keys, g.n_blocks).bytes);
+      } else if (any_tiled_ok(g.hash_count, g.n_keys, g.n_blocks)) {
+        big = std::max(big, any_plan(g.n_keys, g.n_blocks).bytes);  // (bloom_part_any)
       }
     }
     const uint64_t small = n_small ? bloom_batch_ws_bytes(n_small, small_keys, small_max) : 0;
@@ -5732,11 +5848,19 @@ static int build_batch(int kind, const uint8_t* keys, const uint64_t* offs, uint
         launch_bloom_lds<256>(bmode, mode, n_segs, lds, s, keys, offs, stride, d_segs, d_out);
       return hipGetLastError() == hipSuccess ? TKV_AMQ_OK : TKV_AMQ_INTERNAL;
     }
+    const bool mono_any = mono_part && !mono16 && !mono24 && mode != kKey16 && mono_mode != kKey24 &&
+                          any_tiled_ok(k_route, sizing_keys, max_blocks) &&
+                          ws_bytes >= any_plan(sizing_keys, max_blocks).bytes;
     if (mono16 || mono24) {
       // one monolithic filter: every key hashed once into its bit record, records partitioned
       // by tile (routed into parts first beyond kDirectMaxTiles tiles), tiles built in LDS
       launch_mono(mp, s, keys, mono24 ? 24u : 16u, (uint32_t)sizing_keys, d_segs, static_cast<uint8_t*>(d_ws),
                   d_out);
+    } else if (mono_any) {
+      // one filter of variable-length or other fixed-size keys: the same, the partition
+      // hashing them (bloom_part_any)
+      launch_any(any_plan(sizing_keys, max_blocks), s, keys, mode == kKeyVar ? offs : nullptr, stride,
+                 (uint32_t)sizing_keys, d_segs, static_cast<uint8_t*>(d_ws), d_out);
     } else {
       // fewer than kBloomSpreadSegs leaves, leaves beyond the LDS budget in a multi-leaf batch,
       // or a monolithic filter whose keys are neither 16 nor 24 bytes (or 24-byte keys with
@@ -6060,8 +6184,14 @@ int tkv_amq_build_ex(int kind, const uint8_t* keys, const uint64_t* offs, uint32
     const uint32_t k = bloom_k_of(g.n_keys, g.n_blocks);
     const bool mono = rest_bytes >= mp.bytes &&
                       (mode == kKey16 || (bmode == kKey24 && (mp.g == 1 || (mp.blocks && k >= 1 && k <= 8))));
+    const bool any = !mono && mode != kKey16 && bmode != kKey24 && any_tiled_ok(g.hash_count, g.n_keys, g.n_blocks) &&
+                     rest_bytes >= any_plan(g.n_keys, g.n_blocks).bytes;
     if (mono) {
       launch_mono(mp, s, keys, mode == kKey16 ? 16u : 24u, g.n_keys, d_segs + i, rest, d_out, g.key_begin);
+    } else if (any) {
+      // variable-length or other fixed-size keys: the partition hashes them (bloom_part_any)
+      launch_any(any_plan(g.n_keys, g.n_blocks), s, keys, mode == kKeyVar ? offs : nullptr, stride,
+                 (uint32_t)g.n_keys, d_segs + i, rest, d_out);
     } else {
       // other key shapes (or no room): device atomics for this leaf alone
       hipLaunchKernelGGL(bloom_global_init, dim3(1), dim3(256), 0, s, d_segs + i, d_out);
