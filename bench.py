@@ -949,7 +949,7 @@ def bench_hash_sharded(args, torch, dist, amq, world, rank, dev, bpk, label, pg=
         "verified": check["ok"] if check else None, "verify": check,
     }
     if rp is not None:
-        line["route_plan"] = {"route_wgs": rp.route_wgs, "block_cap": rp.block_cap,
+        line["route_plan"] = {"route_wgs": rp.route_wgs, "region_cap": rp.region_cap,
                               "block_bytes": rp.block_bytes, "ovf_cap": rp.ovf_cap,
                               "parts_per_rank": hs.g,
                               "exchanged_bytes_per_rank": (world - 1) * chunks * hs.g * rp.block_bytes,

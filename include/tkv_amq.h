@@ -272,10 +272,10 @@ int tkv_amq_bloom_build_range_records(const uint8_t* d_recs12, uint64_t n_recs,
  * is one contiguous byte range of the bitmap and can be all-gathered in place as soon as every
  * rank has built its part of it.  Per step, each rank:
  *   1. routes its keys in n_chunks chunks (tkv_amq_bloom_route_blocks): every key hashed once
- *      into its 12-byte bit record, counting-sorted by part on chip, and appended to that
- *      part's block (a run per batch and part, reserved with one atomic on the block's count).
- *      Chunk c's send buffer holds n_parts blocks in global part order (part p at
- *      p * block_bytes), so round j's blocks -- one per destination -- are one slice;
+ *      into its 12-byte bit record, counting-sorted by part on chip, and appended to its route
+ *      workgroup's region of that part's block.  Chunk c's send buffer holds n_parts blocks in
+ *      global part order (part p at p * block_bytes), so round j's blocks -- one per
+ *      destination -- are one slice;
  *   2. exchanges round j of chunk c with one all-to-all of equal splits (block_bytes per peer):
  *      the chunks' rounds as their routes finish, the last chunk round by round;
  *   3. builds its part j from the n_chunks * world blocks of round j it received, laid out
@@ -283,7 +283,7 @@ int tkv_amq_bloom_build_range_records(const uint8_t* d_recs12, uint64_t n_recs,
  *      part's tiles where tkv_amq_build puts them (and the header);
  *   4. all-gathers round j as soon as its part of round j is built, while the next rounds
  *      are exchanged and built.
- * Records beyond a block's capacity travel as (record, part) entries in its overflow area, at
+ * Records beyond a region's capacity travel as (record, part) entries in its block's overflow area, at
  * most ovf_cap per block; tkv_amq_bloom_blocks_lost reports a block that needed more (keys far
  * from uniform, e.g. one key repeated), after which the caller must build through the exact
  * exchange (tkv_amq_bloom_route_records + tkv_amq_bloom_build_range_records) instead. */
@@ -295,12 +295,12 @@ typedef struct tkv_amq_route_plan {
   uint32_t world;
   uint32_t n_chunks;
   uint32_t route_wgs;        /* P: route workgroups per chunk (= a part build's workgroups) */
-  uint32_t block_cap;        /* records per part block (mean + 6 sigma + 16 of a uniform hash) */
+  uint32_t region_cap;       /* records per (part block, route workgroup) region */
   uint32_t ovf_cap;          /* overflow entries per part block */
   uint32_t hash_count;
   uint64_t chunk_keys;       /* keys per chunk the capacities are sized for (fewer is fine) */
   uint64_t block_bytes;      /* one (chunk, sender, part) block */
-  uint64_t count_off, ovf_n_off, recs_off, ovf_off;  /* block layout */
+  uint64_t counts_off, ovf_n_off, regions_off, ovf_off;  /* block layout */
   uint64_t route_ws_bytes;   /* workspace of one tkv_amq_bloom_route_blocks call */
   uint64_t part_ws_bytes;    /* workspace of one tkv_amq_bloom_build_part_blocks call */
   uint64_t part_bytes;       /* bitmap bytes per part (q tiles; parts past the last tile pad) */

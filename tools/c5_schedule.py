@@ -20,11 +20,12 @@ def plan(n_total, bpk, world, chunks):
     g = -(-per_rank // 256)
     q = -(-T // (world * g))
     ck = -(-(-(-n_total // world)) // chunks)
-    e = ck * min(q * 2048, n_blocks) / n_blocks
-    cap = (int(e + 6 * math.sqrt(e) + 16) + 15) & ~15
-    ovf_cap = 4096 + ck // (world * g * 256)
+    P = min(256, max(1, -(-ck // (32 * 1024))))
+    e = -(-ck // P) * min(q * 2048, n_blocks) / n_blocks  # records per region
+    cap = (int(e + 2 * math.sqrt(e) + 16) + 15) & ~15
+    ovf_cap = 4096 + 4 * P + ck // (world * g * 256)
     a256 = lambda x: (x + 255) & ~255
-    block = a256(a256(256 + 12 * cap) + 16 * ovf_cap)
+    block = a256(a256(a256(4 * P) + 256 + 12 * P * cap) + 16 * ovf_cap)
     part_bytes = q * 2048 * 64
     return dict(T=T, g=g, q=q, chunk_keys=ck, block_bytes=block, part_bytes=part_bytes,
                 records_per_part=n_total / (world * g))

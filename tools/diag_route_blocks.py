@@ -27,7 +27,7 @@ def main():
         st, ref = O.bloom_build(keys.cpu().numpy(), n, bpk, src_page_id=0)
         got = filt.cpu().numpy()
         h = hss[0]
-        msg = f"n={n} bpk={bpk} W={world} K={chunks} T={h.T} q={h.q} parts={h.n_parts} P={h.rp.route_wgs} cap={h.rp.block_cap}"
+        msg = f"n={n} bpk={bpk} W={world} K={chunks} T={h.T} q={h.q} parts={h.n_parts} P={h.rp.route_wgs} cap={h.rp.region_cap}"
         if got.tobytes() == ref.tobytes():
             print(msg, "OK", flush=True)
             continue
@@ -40,16 +40,16 @@ def main():
             if miss or extra:
                 tiles[t] = (miss, extra, int(np.unpackbits(b).sum()))
         print(msg, "header", got[:64].tobytes() == ref[:64].tobytes(), "tiles (missing, extra, ref bits):", tiles, flush=True)
-        # each received part block's record count and overflow counter ([round][chunk][sender])
+        # each received part block's region counts and overflow counter ([round][chunk][sender])
         for r, hs in enumerate(hss):
             rp = hs.rp
             blk = hs.recv.cpu().numpy()
             for i in range(hs.g * hs.chunks * hs.world):
                 b = blk[i * rp.block_bytes:(i + 1) * rp.block_bytes]
-                cnt = int(b[rp.count_off:rp.count_off + 4].view(np.uint32)[0])
+                cnt = b[rp.counts_off:rp.counts_off + 4 * rp.route_wgs].view(np.uint32)
                 ovf = int(b[rp.ovf_n_off:rp.ovf_n_off + 4].view(np.uint32)[0])
-                print(f"  rank {r} block {i}: count {cnt} (cap {rp.block_cap}) ovf {ovf}")
-
+                print(f"  rank {r} block {i}: records {int(cnt.sum())} max region {int(cnt.max())} "
+                      f"(cap {rp.region_cap}) ovf {ovf}")
 
 if __name__ == "__main__":
     main()

@@ -36,6 +36,7 @@ def main():
     import turtle_kv_amd as amq
     ap = argparse.ArgumentParser()
     ap.add_argument("--shape", default="k16", help="k16, var, or kN (N-byte keys)")
+    ap.add_argument("--only", default=None, help="run the cases whose name contains this")
     args = ap.parse_args()
     cases = [("one filter of 1M", [1_000_000]),
              ("one filter of 3M", [3_000_000]),
@@ -45,6 +46,8 @@ def main():
              ("64 x 3M", [3_000_000] * 64)]
     if args.shape != "k16":  # (single filters of 1M keys take the window path, not the tiled build)
         cases = [c for c in cases if c[1] != [1_000_000]]
+    if args.only:
+        cases = [c for c in cases if args.only in c[0]]
     for name, counts in cases:
         n = sum(counts)
         kb = make_keys(torch, amq, args.shape, n)

@@ -99,8 +99,8 @@ class RoutePlan(ctypes.Structure):
     layout (include/tkv_amq.h)."""
     _fields_ = [(n, ctypes.c_uint32) for n in (
         "n_tiles", "n_parts", "parts_per_rank", "part_tiles", "world", "n_chunks", "route_wgs",
-        "block_cap", "ovf_cap", "hash_count")] + [(n, ctypes.c_uint64) for n in (
-        "chunk_keys", "block_bytes", "count_off", "ovf_n_off", "recs_off", "ovf_off",
+        "region_cap", "ovf_cap", "hash_count")] + [(n, ctypes.c_uint64) for n in (
+        "chunk_keys", "block_bytes", "counts_off", "ovf_n_off", "regions_off", "ovf_off",
         "route_ws_bytes", "part_ws_bytes", "part_bytes", "n_blocks")]
 
 

@@ -1039,10 +1039,7 @@ __host__ __device__ constexpr inline bool part_tbl_fits(uint32_t n_tiles)
 static_assert(kRecPartMaxTiles <= 8192, "a record's 13-bit tile field");
 static_assert(kPartBatch < 65536, "u16 ranks");
 
-// kSrcKeyVar / kSrcKeyFixed: keys of any other shape (the reference's KeyView ranges: bytes +
-// offsets, or a fixed stride), hashed by the partition (k <= 8: bit records)
-enum PartSrc : int { kSrcKey16 = 0, kSrcKey24 = 1, kSrcRec12 = 2, kSrcRaw16 = 3, kSrcSeg12 = 4,
-                     kSrcKeyVar = 5, kSrcKeyFixed = 6 };
+enum PartSrc : int { kSrcKey16 = 0, kSrcKey24 = 1, kSrcRec12 = 2, kSrcRaw16 = 3, kSrcSeg12 = 4 };
 // what part_body buckets by: the filter's tiles (the partition, ahead of bloom_tile), or the
 // route's parts (bloom_route_part: the one-pass route of a filter past kDirectMaxTiles tiles,
 // and of a hash-range sharded filter's keys to their owners)
@@ -1172,7 +1169,7 @@ __device__ inline uint32_t rec_hash_bits(const Key24& kv, uint32_t nb, uint32_t 
   return (uint32_t)__umul64hi(h0, (uint64_t)nb);
 }
 
-// a key of any other shape (kSrcKeyVar / kSrcKeyFixed): its bytes and length
+// a key of any other shape (bloom_any_records): its bytes and length
 struct KeyRef {
   const uint8_t* p;
   uint32_t len;
@@ -1402,12 +1399,11 @@ __global__ __launch_bounds__(NT) void route_recs(const uint8_t* __restrict__ key
 // ---------------------------------------------------------------------------------------
 // The route's output (bloom_route_part) and a part build's input (kSrcSeg12): fixed-size
 // PART blocks, one per (route chunk, sender, part).  Block layout:
-//   count_off    u32: records appended to the block (> cap: the rest went to overflow)
+//   counts_off   u32 [P]: records in region w (<= cap)
 //   ovf_n_off    u32: overflow entries appended to the block (> ovf_cap: entries were lost)
-//   recs_off     cap 12-byte records of the part, appended by the route workgroups in runs of
-//                one (batch, part) each: a workgroup reserves its run with one device-scope
-//                atomicAdd on the count per batch, so the block holds no per-workgroup slack
-//   ovf_off      ovf_cap 16-byte entries (record, global part): records past the block's cap
+//   regions_off  region w at regions_off + w * cap * 12: route workgroup w's 12-byte records of
+//                the part, in its batches' order (no atomics: each workgroup owns its region)
+//   ovf_off      ovf_cap 16-byte entries (record, global part): records whose region was full
 // Part p belongs to rank p % world as its part jl = p / world (round-robin: round jl's parts of
 // all ranks are one contiguous byte range of the bitmap, all-gathered in place).  The route
 // writes part p's block at dst + jl * jstride + (p % world) * bytes: with jstride = world *
@@ -1417,12 +1413,12 @@ __global__ __launch_bounds__(NT) void route_recs(const uint8_t* __restrict__ key
 struct RouteBlock {
   uint64_t bytes;
   uint64_t jstride;         // the route's destination: bytes from round jl to jl + 1
-  uint64_t count_off;
+  uint64_t counts_off;
   uint64_t ovf_n_off;
-  uint64_t recs_off;
+  uint64_t regions_off;
   uint64_t ovf_off;
   uint32_t P;               // route workgroups (= the part builds' partition workgroups)
-  uint32_t cap;             // records per block
+  uint32_t cap;             // records per region
   uint32_t ovf_cap;         // overflow entries per block
   uint32_t pad;
 };
@@ -1461,9 +1457,6 @@ struct PartArgs {
   // writing a partial image at part_img + (t * split + s) * 128 KiB, ORed by bloom_tile_merge
   uint32_t split;
   uint8_t* part_img;
-  // kSrcKeyVar: the key offsets; kSrcKeyFixed: the key stride
-  const uint64_t* offs;
-  uint32_t stride;
 };
 
 __host__ __device__ inline uint64_t div_magic(uint32_t d) { return (0x100000000ull / d) + 1; }
@@ -1564,8 +1557,7 @@ __device__ void part_body(const tkv_amq_segment& sg, const PartArgs& a, uint32_t
   constexpr bool ROUTE = DST == kDstParts;
   static_assert(TBL || !ROUTE, "the route stores through its table");
   constexpr bool ROUTED = SRC == kSrcRec12 || SRC == kSrcSeg12;  // records with their tile in part
-  constexpr bool ANY = SRC == kSrcKeyVar || SRC == kSrcKeyFixed;  // keys through KeyRef
-  static_assert(!(ROUTE && (RAW || ROUTED || ANY)), "the route hashes 16- or 24-byte keys");
+  static_assert(!(ROUTE && (RAW || ROUTED)), "the route hashes keys");
   // 16-byte records: four key words and the tile per item in LDS, half the items per batch
   constexpr uint32_t RB = RAW ? 16 : 12, U = RAW ? kPartU / 2 : kPartU, NT = kPartThreads, B = U * NT;
   constexpr uint32_t NPL = RAW ? 5 : 3;  // LDS planes (ROUTE: + a u16 plane of parts)
@@ -1596,14 +1588,23 @@ __device__ void part_body(const tkv_amq_segment& sg, const PartArgs& a, uint32_t
     cursor[i] = 0;
   }
   if (tid == 0) *ovf_n = 0;
-  // (ROUTE: the part blocks' counters were zeroed by bloom_route_reset, an earlier launch)
+  if constexpr (ROUTE) {
+    // the part blocks' overflow counters, appended to by bloom_route_ovf_pack after this
+    // kernel (a later launch on the same stream)
+    if (w == 0)
+      for (uint32_t t = tid; t < T; t += NT) {
+        const uint32_t jl = div_by_magic(t, a.w_magic), dr = t - jl * a.world;
+        *reinterpret_cast<uint32_t*>(a.dst + (uint64_t)jl * a.blk.jstride + (uint64_t)dr * a.blk.bytes +
+                                     a.blk.ovf_n_off) = 0;
+      }
+  }
   const uint8_t* src;
   uint32_t n;
-  uint64_t seg_reg = 0;  // kSrcSeg12: the records inside a part block
+  uint64_t seg_reg = 0;  // kSrcSeg12: this workgroup's region inside a part block
   if constexpr (SRC == kSrcSeg12) {
     const uint32_t S = a.n_src_segs;
-    seg_reg = a.blk.recs_off;
-    const uint64_t cnt_off = a.blk.count_off;
+    seg_reg = a.blk.regions_off + (uint64_t)w * a.blk.cap * 12ull;
+    const uint64_t cnt_off = a.blk.counts_off + 4ull * w;
     if (tid < 64) {  // one wave: the inclusive scan of the S counts, 64 at a time
       uint32_t run = 0;
       for (uint32_t s0 = 0; s0 < S; s0 += 64) {
@@ -1625,37 +1626,22 @@ __device__ void part_body(const tkv_amq_segment& sg, const PartArgs& a, uint32_t
   __syncthreads();
   uint32_t kb, ke;
   if constexpr (SRC == kSrcSeg12) {
-    // the part's records, block after block: this workgroup's share of them
     src = a.src;
     n = pre[a.n_src_segs];
-    const uint32_t per = (n + P - 1) / P;
-    kb = min(n, w * per);
-    ke = min(n, kb + per);
-  } else if constexpr (ANY) {
-    // (the key array itself: items index from the segment's first key when from_seg)
-    src = a.src;
-    n = a.from_seg ? min(a.n, sg.n_keys) : a.n;
-    kb = min(n, w * a.g.per);
-    ke = min(n, kb + a.g.per);
+    kb = 0;  // this workgroup's own regions, whole
+    ke = n;
   } else {
     part_items(sg, a, IB, src, n);
     const uint32_t per = a.cnt ? (n + P - 1) / P : a.g.per;
     kb = min(n, w * per);
     ke = min(n, kb + per);
   }
-  const uint64_t key0 = ANY && a.from_seg ? sg.key_begin : 0;  // kSrcKeyVar / kSrcKeyFixed
   const uint64_t ovf_base = a.g.ovf_off + (uint64_t)w * a.g.per * 16;  // (lists 16 B per item apart)
   const uint32_t last_item = ke > 0 ? ke - 1 : 0;
   uint32_t cs = 0;  // kSrcSeg12: the block of this thread's last item (items rise per thread)
-  using In = typename std::conditional<SRC == kSrcKey24, Key24,
-                                      typename std::conditional<ANY, KeyRef, uint4>::type>::type;
+  using In = typename std::conditional<SRC == kSrcKey24, Key24, uint4>::type;
   auto load_in = [&](uint32_t i) -> In {
-    if constexpr (SRC == kSrcKeyVar) {
-      const uint64_t o0 = a.offs[key0 + i], o1 = a.offs[key0 + i + 1];
-      return KeyRef{src + o0, (uint32_t)(o1 - o0)};
-    } else if constexpr (SRC == kSrcKeyFixed) {
-      return KeyRef{src + (key0 + i) * a.stride, a.stride};
-    } else if constexpr (SRC == kSrcSeg12) {
+    if constexpr (SRC == kSrcSeg12) {
       while (i >= pre[cs + 1]) ++cs;
       return load_rec12(src + (uint64_t)cs * a.blk.bytes + seg_reg, i - pre[cs]);
     } else if constexpr (SRC == kSrcRec12) {
@@ -1727,25 +1713,6 @@ __device__ void part_body(const tkv_amq_segment& sg, const PartArgs& a, uint32_t
 #pragma unroll
     for (uint32_t u = 0; u < U; ++u) in[u] = load_in(min(kb + u * NT + tid, last_item));
   }
-  // ROUTE: the previous batch's run reservations (thread t: parts t and t + NT) and its store
-  // table from them and the run starts its scan left in `start`
-  uint32_t resv[ROUTE ? 2 : 1] = {};
-  auto route_table = [&]() {
-    if constexpr (ROUTE) {
-      static_assert(kRouteMaxParts <= 2 * NT, "two parts per thread at most");
-#pragma unroll
-      for (uint32_t r = 0; r < 2; ++r) {
-        const uint32_t t = tid + r * NT;
-        if (t < T) {
-          const uint32_t st = lds_u16(start, t), o = min(resv[r], cap);  // (o = cap: all overflow)
-          const uint32_t jl = div_by_magic(t, a.w_magic), dr = t - jl * a.world;
-          const uint64_t base = (uint64_t)jl * a.blk.jstride + (uint64_t)dr * a.blk.bytes + a.blk.recs_off;
-          roff[t] = base + (uint64_t)RB * o - (uint64_t)RB * st;
-          rlim[t] = (int32_t)(cap + st) - (int32_t)o;
-        }
-      }
-    }
-  };
   uint32_t par = 0;
   // Per iteration: hash batch b; write out batch b - 1 (its stores then drain while this
   // batch is scanned and sorted: the compiler waits for every outstanding load and store
@@ -1776,9 +1743,7 @@ __device__ void part_body(const tkv_amq_segment& sg, const PartArgs& a, uint32_t
           t = rec_tile(r0[u], r1[u], r2[u]);
         } else {
           uint32_t bits[8];
-          uint32_t blk;
-          if constexpr (ANY) blk = rec_hash_bits_any(in[u], nb, k, bits);
-          else blk = rec_hash_bits<K>(in[u], nb, k, bits);
+          const uint32_t blk = rec_hash_bits<K>(in[u], nb, k, bits);
           const uint32_t tg = blk >> kTileShift;
           if constexpr (ROUTE) {
             t = div_by_magic(tg, a.q_magic);  // the key's part; its record's tile is in the part
@@ -1797,44 +1762,26 @@ __device__ void part_body(const tkv_amq_segment& sg, const PartArgs& a, uint32_t
         tr[u] = t << 16 | rank;
       }
     }
-    if constexpr (ROUTE) {
-      // batch b - 1's store table from its reservations (their returns came back with the
-      // loads of this batch's items, which this batch's hash waited for), then batch b's runs
-      // reserved -- one device-scope atomicAdd per part on its block's count, issued ahead of
-      // the write-out's stores and the next batch's loads and read one batch later, so no
-      // wait of the loop is on them
-      route_table();
-      lds_barrier();  // the table is complete; so is batch b's histogram
-#pragma unroll
-      for (uint32_t r = 0; r < 2; ++r) {
-        const uint32_t t = tid + r * NT;
-        resv[r] = 0;
-        if (t < T) {
-          const uint32_t len = lds_u16(hist, t);
-          if (len) {
-            const uint32_t jl = div_by_magic(t, a.w_magic), dr = t - jl * a.world;
-            resv[r] = atomicAdd(reinterpret_cast<uint32_t*>(a.dst + (uint64_t)jl * a.blk.jstride +
-                                                            (uint64_t)dr * a.blk.bytes + a.blk.count_off),
-                                len);
-          }
-        }
-      }
-    }
     write_out();  // batch b - 1 (total = 0 before the first batch: sink stores only)
 #pragma unroll
     for (uint32_t u = 0; u < U; ++u)  // the next batch's items
       in[u] = load_in(min(b0 + B + u * NT + tid, last_item));
     lds_barrier();
     total = part_scan(hist, prev, start, cursor, HW, wsum);
-    if constexpr (TBL && !ROUTE) {
+    if constexpr (TBL) {
       // this batch's store table (read by its write-out, after the barrier below)
-      {
-        for (uint32_t t = tid; t < T; t += NT) {
-          const uint32_t st = lds_u16(start, t), cu = cursor[t];
-          const uint64_t base = a.g.regions_off + ((uint64_t)t * P + w) * cap * a.g.rb;
-          roff[t] = base + (uint64_t)RB * cu - (uint64_t)RB * st;
-          rlim[t] = (int32_t)(cap + st) - (int32_t)cu;
+      for (uint32_t t = tid; t < T; t += NT) {
+        const uint32_t st = lds_u16(start, t), cu = cursor[t];
+        uint64_t base;
+        if constexpr (ROUTE) {
+          const uint32_t jl = div_by_magic(t, a.w_magic), dr = t - jl * a.world;
+          base = (uint64_t)jl * a.blk.jstride + (uint64_t)dr * a.blk.bytes + a.blk.regions_off +
+                 (uint64_t)w * cap * 12ull;
+        } else {
+          base = a.g.regions_off + ((uint64_t)t * P + w) * cap * a.g.rb;
         }
+        roff[t] = base + (uint64_t)RB * cu - (uint64_t)RB * st;
+        rlim[t] = (int32_t)(cap + st) - (int32_t)cu;
       }
     }
 #pragma unroll
@@ -1853,15 +1800,17 @@ __device__ void part_body(const tkv_amq_segment& sg, const PartArgs& a, uint32_t
     }
     lds_barrier();
   }
-  if constexpr (ROUTE) {
-    route_table();
-    lds_barrier();
-  }
   write_out();  // the last batch
   __syncthreads();
   // the last batch's run lengths (its histogram is the one the loop's last batch counted into)
   const uint32_t* last = par ? H0 : H1;
-  if constexpr (!ROUTE) {  // (ROUTE: the blocks' counts are the reservations)
+  if constexpr (ROUTE) {
+    for (uint32_t t = tid; t < T; t += NT) {
+      const uint32_t jl = div_by_magic(t, a.w_magic), dr = t - jl * a.world;
+      *reinterpret_cast<uint32_t*>(a.dst + (uint64_t)jl * a.blk.jstride + (uint64_t)dr * a.blk.bytes +
+                                   a.blk.counts_off + 4ull * w) = min(cursor[t] + lds_u16(last, t), cap);
+    }
+  } else {
     uint32_t* counts = reinterpret_cast<uint32_t*>(a.ws + a.g.counts_off);
     for (uint32_t t = tid; t < T; t += NT)
       counts[(uint64_t)t * P + w] = min(cursor[t] + lds_u16(last, t), cap);
@@ -1922,18 +1871,32 @@ __global__ __launch_bounds__(kPartThreads) void bloom_part_routed(const tkv_amq_
   else part_body<0, kSrcRaw16>(sg, a, s_part);
 }
 
-// keys of any other shape (variable-length through offsets, or a fixed stride; k <= 8): each
-// key hashed once into its bit record by the partition, as 16- and 24-byte keys are (round 6:
-// such a leaf past the window path set its bits with device atomics, 3.6 Gkeys/s)
-template <int SRC>
-__global__ __launch_bounds__(kPartThreads) void bloom_part_any(const tkv_amq_segment* __restrict__ segs,
-                                                               PartArgs a)
+// Keys of any other shape (variable-length through offsets, or a fixed stride; k <= 8) for the
+// tiled build: one thread per key hashes it into its 12-byte bit record, the tile in the
+// record's tile field (the filter has <= kDirectMaxTiles tiles), and the partition then sorts
+// the records (kSrcRec12) as it sorts routed ones.  A pass of its own, at full occupancy, hides
+// the latency of the keys' scattered byte loads, which the partition's batch loop could not
+// (round 6: hashing them inside the partition ran at 97.5 us for 3M variable-length keys).
+// (Round 5: such a leaf past the window path set its bits with device atomics, 3.6 Gkeys/s.)
+template <int MODE>
+__global__ __launch_bounds__(256) void bloom_any_records(const uint8_t* __restrict__ keys,
+                                                         const uint64_t* __restrict__ offs, uint32_t stride,
+                                                         const tkv_amq_segment* __restrict__ segs, uint32_t n,
+                                                         uint32_t* __restrict__ recs)
 {
-  extern __shared__ __attribute__((aligned(16))) uint32_t s_part[];
   const tkv_amq_segment sg = segs[0];
-  if (sg.hash_count == 0 || sg.hash_count > 8) return;
-  if (a.tbl) part_body<0, SRC, kDstTiles, true>(sg, a, s_part);
-  else part_body<0, SRC>(sg, a, s_part);
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n || i >= sg.n_keys || sg.hash_count == 0 || sg.hash_count > 8) return;
+  uint32_t len;
+  const uint8_t* p = key_at<MODE>(keys, offs, stride, sg.key_begin + i, len);
+  uint32_t bits[8], r0, r1, r2;
+  const uint32_t blk = rec_hash_bits_any(KeyRef{p, len}, sg.n_blocks, sg.hash_count, bits);
+  rec_pack(blk & (kTileBlocks - 1), blk >> kTileShift, bits, r0, r1, r2);
+  uint3 v;
+  v.x = r0;
+  v.y = r1;
+  v.z = r2;
+  reinterpret_cast<uint3*>(recs)[i] = v;
 }
 
 // The one-pass route (k <= 8): every key hashed once into its 12-byte bit record, counting-
@@ -1981,18 +1944,6 @@ __global__ __launch_bounds__(256) void bloom_route_ovf_pack(PartArgs a)
     uint8_t* b = a.dst + (uint64_t)jl * a.blk.jstride + (uint64_t)dr * a.blk.bytes;
     const uint32_t slot = atomicAdd(reinterpret_cast<uint32_t*>(b + a.blk.ovf_n_off), 1u);
     if (slot < a.blk.ovf_cap) reinterpret_cast<uint4*>(b + a.blk.ovf_off)[slot] = x;
-  }
-}
-
-// The route's part blocks' record and overflow counters to zero (ahead of bloom_route_part,
-// whose workgroups reserve their runs with atomics on them)
-__global__ __launch_bounds__(256) void bloom_route_reset(PartArgs a, uint32_t n_parts)
-{
-  for (uint32_t p = threadIdx.x; p < n_parts; p += 256) {
-    const uint32_t jl = p / a.world, dr = p - jl * a.world;
-    uint8_t* b = a.dst + (uint64_t)jl * a.blk.jstride + (uint64_t)dr * a.blk.bytes;
-    *reinterpret_cast<uint32_t*>(b + a.blk.count_off) = 0;
-    *reinterpret_cast<uint32_t*>(b + a.blk.ovf_n_off) = 0;
   }
 }
 
@@ -4920,9 +4871,7 @@ inline void set_mono_attributes()
   once_per_device(lds_attr, [] {
     for (const void* f : {reinterpret_cast<const void*>(&bloom_part_keys16),
                           reinterpret_cast<const void*>(&bloom_part_keys24),
-                          reinterpret_cast<const void*>(&bloom_part_routed),
-                          reinterpret_cast<const void*>(&bloom_part_any<kSrcKeyVar>),
-                          reinterpret_cast<const void*>(&bloom_part_any<kSrcKeyFixed>)})
+                          reinterpret_cast<const void*>(&bloom_part_routed)})
       (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)(160 * 1024));
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&bloom_tile),
@@ -4946,8 +4895,6 @@ inline void launch_part_build(int src, PartArgs a, hipStream_t s, const tkv_amq_
   const dim3 grid(a.g.P), block(kPartThreads);
   if (src == kSrcKey24) hipLaunchKernelGGL(bloom_part_keys24, grid, block, lds, s, d_segs, a);
   else if (src == kSrcKey16) hipLaunchKernelGGL(bloom_part_keys16, grid, block, lds, s, d_segs, a);
-  else if (src == kSrcKeyVar) hipLaunchKernelGGL(bloom_part_any<kSrcKeyVar>, grid, block, lds, s, d_segs, a);
-  else if (src == kSrcKeyFixed) hipLaunchKernelGGL(bloom_part_any<kSrcKeyFixed>, grid, block, lds, s, d_segs, a);
   else hipLaunchKernelGGL(bloom_part_routed, grid, block, lds, s, d_segs, a);
   const uint32_t S = a.split > 1 ? a.split : 1u;
   hipLaunchKernelGGL(bloom_tile, dim3(a.g.n_tiles * S), dim3(kTileThreads), 64ull * kTileBlocks, s, d_segs, a,
@@ -5014,10 +4961,12 @@ static_assert(kRoutePartTiles <= kRecPartMaxTiles && kRouteKeyPartTiles <= kRecP
 static_assert(kRoutePartTiles < 2048, "div_by_magic: exact for q < 2048 and tiles < 2^21");
 
 // The route plan of tkv_amq_bloom_route_plan: parts, route workgroups, the part block layout.
-// A block holds mean + 6 sigma + 16 records of a uniform hash (the part's share of a chunk: one
-// count over the whole block, so 6 sigma is ~1% of it at config 5's size, where round 5's
-// per-(part, workgroup) regions carried 14%); an overflow area of ovf_cap entries per block (0
-// for the one-GPU build, which applies its route workgroups' own overflow lists instead).
+// A region holds mean + 6 sigma + 16 records of a uniform hash when its overflow has nowhere to
+// go but the route workgroup's own list (the one-GPU build), and mean + 2 sigma + 16 when the
+// block carries an overflow area of ovf_cap entries (the exchange): the regions' slack is what
+// crosses xGMI beside the records (round 5: 6 sigma, 14% at config 5's size on eight ranks; 2
+// sigma: ~5%), and the ~2% of regions that fill send their few extra records as overflow
+// entries (~0.4 per region of a uniform hash; the part build sets them with atomics).
 inline int route_plan(uint64_t chunk_keys, uint32_t n_chunks, uint64_t n_blocks, uint32_t k, uint32_t world,
                       bool ovf_area, tkv_amq_route_plan& rp)
 {
@@ -5045,21 +4994,22 @@ inline int route_plan(uint64_t chunk_keys, uint32_t n_chunks, uint64_t n_blocks,
   const uint64_t per = div_up(chunk_keys, P);  // keys per route workgroup
   // a part's share of the keys is its blocks' share (q full tiles at most; the last tile may
   // be short, and the last parts may hold fewer tiles, or none when world * g * q > T)
-  const double e = (double)chunk_keys * std::min<uint64_t>((uint64_t)q * kTileBlocks, n_blocks) / n_blocks;
-  const double capd = e + 6.0 * sqrt(e) + 16.0;
-  if (capd > 4.0e9) return TKV_AMQ_INVALID_ARGUMENT;
-  rp.block_cap = ((uint32_t)capd + 15) & ~15u;
-  // overflow entries per block (none expected from a uniform hash; duplicated keys land here)
-  rp.ovf_cap = ovf_area ? (uint32_t)(4096 + chunk_keys / ((uint64_t)world * g * 256)) : 0u;
-  rp.count_off = 0;
-  rp.ovf_n_off = 4;
-  rp.recs_off = 256;
-  rp.ovf_off = align256(rp.recs_off + 12ull * rp.block_cap);
+  const double e = (double)per * std::min<uint64_t>((uint64_t)q * kTileBlocks, n_blocks) / n_blocks;
+  // (2 sigma only where the blocks cross xGMI: one rank keeps 6 and sends nothing to the
+  // overflow path)
+  rp.region_cap = ((uint32_t)(e + (ovf_area && world > 1 ? 2.0 : 6.0) * sqrt(e) + 16.0) + 15) & ~15u;
+  // overflow entries per block: the expected spill of 2-sigma regions (~0.4 per region) many
+  // times over, plus room for keys that are not spread by the hash (duplicates)
+  rp.ovf_cap = ovf_area ? (uint32_t)(4096 + 4 * P + chunk_keys / ((uint64_t)world * g * 256)) : 0u;
+  rp.counts_off = 0;
+  rp.ovf_n_off = align256(4ull * P);
+  rp.regions_off = rp.ovf_n_off + 256;
+  rp.ovf_off = align256(rp.regions_off + 12ull * P * rp.region_cap);
   rp.block_bytes = align256(rp.ovf_off + 16ull * rp.ovf_cap);
   // route workspace: [sink 256][u32 overflow count per workgroup][16-byte entries, per each]
   rp.route_ws_bytes = align256(512 + 4ull * P) + 16ull * P * per;
   // a part build: partition regions over the part's q tiles, overflow lists of what its
-  // workgroup may receive (its share of every source block at capacity)
+  // workgroup may receive (every source block's region at capacity)
   const uint64_t S = (uint64_t)n_chunks * world;
   const double ep = (double)chunk_keys * S / P * std::min<uint64_t>(kTileBlocks, n_blocks) / n_blocks;  // per (full tile, workgroup)
   const uint32_t capp = ((uint32_t)(ep + 6.0 * sqrt(ep) + 16.0) + 15) & ~15u;
@@ -5067,7 +5017,7 @@ inline int route_plan(uint64_t chunk_keys, uint32_t n_chunks, uint64_t n_blocks,
   const uint64_t p_ovf_n = 256 + 4 * regions;
   const uint64_t p_regions = align256(p_ovf_n + 4ull * P);
   const uint64_t p_ovf = p_regions + 12ull * regions * capp;
-  rp.part_ws_bytes = p_ovf + 16ull * P * div_up(S * rp.block_cap, P);
+  rp.part_ws_bytes = p_ovf + 16ull * P * S * rp.region_cap;
   rp.part_bytes = (uint64_t)q * kTileBlocks * 64;
   return TKV_AMQ_OK;
 }
@@ -5080,7 +5030,7 @@ inline PartGeom route_part_geom(const tkv_amq_route_plan& rp, uint32_t tn, uint3
   g.P = P;
   g.n_tiles = tn ? tn : 1;
   g.rb = 12;
-  g.per = (uint32_t)div_up((uint64_t)S * rp.block_cap, P);  // a workgroup's share at most
+  g.per = S * rp.region_cap;
   const double ep = (double)rp.chunk_keys * S / P * std::min<uint64_t>(kTileBlocks, rp.n_blocks) /
                     rp.n_blocks;  // records per (full tile, workgroup)
   g.cap = ((uint32_t)(ep + 6.0 * sqrt(ep) + 16.0) + 15) & ~15u;
@@ -5099,12 +5049,12 @@ inline RouteBlock route_block(const tkv_amq_route_plan& rp, uint64_t jstride = 0
   RouteBlock b{};
   b.bytes = rp.block_bytes;
   b.jstride = jstride ? jstride : (uint64_t)rp.world * rp.block_bytes;
-  b.count_off = rp.count_off;
+  b.counts_off = rp.counts_off;
   b.ovf_n_off = rp.ovf_n_off;
-  b.recs_off = rp.recs_off;
+  b.regions_off = rp.regions_off;
   b.ovf_off = rp.ovf_off;
   b.P = rp.route_wgs;
-  b.cap = rp.block_cap;
+  b.cap = rp.region_cap;
   b.ovf_cap = rp.ovf_cap;
   return b;
 }
@@ -5139,7 +5089,7 @@ inline PartArgs route_args(const tkv_amq_route_plan& rp, const uint8_t* keys, ui
   a.g.P = rp.route_wgs;
   a.g.n_tiles = rp.n_parts;
   a.g.per = (uint32_t)div_up(rp.chunk_keys, rp.route_wgs);
-  a.g.cap = rp.block_cap;
+  a.g.cap = rp.region_cap;
   a.g.rb = 12;
   a.g.ovf_n_off = 512;
   a.g.ovf_off = align256(512 + 4ull * rp.route_wgs);
@@ -5158,7 +5108,6 @@ inline void launch_route_blocks(const PartArgs& a, const tkv_amq_route_plan& rp,
   set_route_attributes();
   const dim3 g(rp.route_wgs), b(kPartThreads);
   const size_t lds = route_lds_bytes(rp.n_parts);
-  hipLaunchKernelGGL(bloom_route_reset, dim3(1), dim3(256), 0, s, a, rp.n_parts);
   if (a.kb == 24 && rp.hash_count == 8) hipLaunchKernelGGL((bloom_route_part<8, 24>), g, b, lds, s, d_seg, a);
   else if (a.kb == 24) hipLaunchKernelGGL((bloom_route_part<0, 24>), g, b, lds, s, d_seg, a);
   else if (rp.hash_count == 8) hipLaunchKernelGGL((bloom_route_part<8, 16>), g, b, lds, s, d_seg, a);
@@ -5262,12 +5211,13 @@ inline uint32_t bloom_k_of(uint64_t n_keys, uint64_t n_blocks)
 }
 
 // One filter of keys of any other shape (variable-length, or a fixed stride other than 16 and
-// 24) with k <= 8 and at most kDirectMaxTiles tiles: the tiled build with the partition hashing
-// each key into its bit record (bloom_part_any), tiles split over the chip below 128 of them.
+// 24) with k <= 8 and at most kDirectMaxTiles tiles: the tiled build from bit records that
+// bloom_any_records hashes, tiles split over the chip below 128 of them.  Workspace: the
+// records, the partition's, the partial tile images.
 struct AnyPlan {
   PartGeom pg;
   uint32_t split;
-  uint64_t img_off, bytes;
+  uint64_t part_off, img_off, bytes;
 };
 
 inline bool any_tiled_ok(uint32_t k, uint64_t n_keys, uint64_t n_blocks)
@@ -5281,8 +5231,9 @@ inline AnyPlan any_plan(uint64_t n_keys, uint64_t n_blocks)
   const uint32_t T = filter_tiles(n_blocks);
   p.pg = part_geom(n_keys, n_keys, T, 12, mono_wg_items(n_keys, 32ull * kPartThreads));
   p.split = tile_split(T);
-  p.img_off = align256(p.pg.bytes);
-  p.bytes = p.split > 1 ? p.img_off + (uint64_t)T * p.split * (64ull * kTileBlocks) : p.pg.bytes;
+  p.part_off = align256(12ull * n_keys);
+  p.img_off = align256(p.part_off + p.pg.bytes);
+  p.bytes = p.split > 1 ? p.img_off + (uint64_t)T * p.split * (64ull * kTileBlocks) : p.img_off;
   return p;
 }
 
@@ -5290,12 +5241,16 @@ inline AnyPlan any_plan(uint64_t n_keys, uint64_t n_blocks)
 inline void launch_any(const AnyPlan& p, hipStream_t s, const uint8_t* keys, const uint64_t* offs, uint32_t stride,
                        uint32_t n, const tkv_amq_segment* d_seg, uint8_t* ws, uint8_t* d_out)
 {
-  PartArgs a{keys, n, 0u, 1u, 16u, nullptr, 0u, ws, p.pg};
+  uint32_t* recs = reinterpret_cast<uint32_t*>(ws);
+  const uint32_t g = (uint32_t)div_up(n, 256);
+  if (g) {
+    if (offs) hipLaunchKernelGGL(bloom_any_records<kKeyVar>, dim3(g), dim3(256), 0, s, keys, offs, 0u, d_seg, n, recs);
+    else hipLaunchKernelGGL(bloom_any_records<kKeyFixed>, dim3(g), dim3(256), 0, s, keys, offs, stride, d_seg, n, recs);
+  }
+  PartArgs a{reinterpret_cast<const uint8_t*>(recs), n, 0u, 0u, 16u, nullptr, 0u, ws + p.part_off, p.pg};
   a.split = p.split;
   a.part_img = ws + p.img_off;
-  a.offs = offs;
-  a.stride = stride;
-  launch_part_build(offs ? kSrcKeyVar : kSrcKeyFixed, a, s, d_seg, d_out, 0u);
+  launch_part_build(kSrcRec12, a, s, d_seg, d_out, 0u);
 }
 
 // keys [0, n) of segment 0 (kb 16 or 24; routed 24-byte keys need the one-pass route, k <= 8)
@@ -5679,7 +5634,11 @@ int tkv_amq_plan(int kind, const uint64_t* counts, const uint64_t* src_ids, uint
     if (kind == TKV_AMQ_BLOOM && bpk != 0 && bloom_window_path(n_segs, max_blocks, true))
       *ws_bytes = win_ws;
     else if (kind == TKV_AMQ_BLOOM && bloom_partitioned(n_segs, max_blocks, key_begin))
-      *ws_bytes = std::max(mono_plan(key_begin, max_blocks).bytes, win_ws);
+      // (the plan does not know the key shape: other shapes take bloom_any_records' records)
+      *ws_bytes = std::max<uint64_t>({mono_plan(key_begin, max_blocks).bytes, win_ws,
+                                      any_tiled_ok(segs[0].hash_count, key_begin, max_blocks)
+                                          ? any_plan(key_begin, max_blocks).bytes
+                                          : uint64_t{0}});
     else if (kind == TKV_AMQ_BLOOM)
       *ws_bytes = bloom_split_ws_bytes(n_segs, bloom_split_parts(n_segs, key_begin, max_blocks),
                                        max_blocks);

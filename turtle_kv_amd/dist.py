@@ -448,8 +448,9 @@ class HashShardedBloom:
 
       route     the rank's keys in `chunks` chunks (tkv_amq_bloom_route_blocks): every key
                 hashed once into its 12-byte bit record, counting-sorted by part on chip and
-                appended to the part's fixed-capacity block (one block per part and chunk, in
-                global part order, so round j -- part j of every rank -- is one slice);
+                appended to its route workgroup's fixed-capacity region of the part's block
+                (one block per part and chunk, in global part order, so round j -- part j of
+                every rank -- is one slice);
       exchange  round j of chunk c in one all-to-all of equal splits (RCCL over xGMI) on the
                 communication stream: every round of a chunk as soon as its route is done, the
                 last chunk round by round -- no counts exchanged first, no host synchronisation;
