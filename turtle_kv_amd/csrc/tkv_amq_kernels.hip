@@ -1886,11 +1886,34 @@ __global__ __launch_bounds__(256) void bloom_any_records(const uint8_t* __restri
 {
   const tkv_amq_segment sg = segs[0];
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= n || i >= sg.n_keys || sg.hash_count == 0 || sg.hash_count > 8) return;
+  const uint32_t k = sg.hash_count;
+  if (i >= n || i >= sg.n_keys || k == 0 || k > 8) return;
+  // the leaf's bytes through a buffer resource: a key under 32 bytes as one 32-byte window
+  // (two 16-byte loads; KeyWin, as the VQF producers read them) instead of its lanes, tail
+  // word and tail bytes one load each
+  const uint64_t n_all = min(n, sg.n_keys);
+  const uint64_t b0 = MODE == kKeyVar ? offs[sg.key_begin] : sg.key_begin * stride;
+  const uint64_t b1 = MODE == kKeyVar ? offs[sg.key_begin + n_all] : (sg.key_begin + n_all) * stride;
+  const VarRsrc vr = var_rsrc(keys, b0, b1, b1);
   uint32_t len;
   const uint8_t* p = key_at<MODE>(keys, offs, stride, sg.key_begin + i, len);
   uint32_t bits[8], r0, r1, r2;
-  const uint32_t blk = rec_hash_bits_any(KeyRef{p, len}, sg.n_blocks, sg.hash_count, bits);
+  uint32_t blk;
+  if (len < 32 && vr.nrec) {
+    KeyWin kw;
+    key_win_load(vr, (uint32_t)(p - keys - vr.base), kw);
+    uint64_t l[3];
+    uint32_t t4, tb;
+    key_win_parts(kw, len, l, t4, tb);
+    const XxhShort x(len, l, t4, tb);
+    const uint64_t h0 = x.finish(c_bloom.seed_p5[0]);
+    bits[0] = (uint32_t)h0 & 511u;
+#pragma unroll
+    for (uint32_t j = 1; j < 8; ++j) bits[j] = j < k ? x.finish_lo9(c_bloom.seed_p5[j]) & 511u : bits[0];
+    blk = (uint32_t)__umul64hi(h0, (uint64_t)sg.n_blocks);
+  } else {
+    blk = rec_hash_bits_any(KeyRef{p, len}, sg.n_blocks, k, bits);
+  }
   rec_pack(blk & (kTileBlocks - 1), blk >> kTileShift, bits, r0, r1, r2);
   uint3 v;
   v.x = r0;
