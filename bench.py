@@ -915,6 +915,8 @@ def bench_hash_sharded(args, torch, dist, amq, world, rank, dev, bpk, label, pg=
         path = f"route ({chunks} chunks) -> all-to-all -> part builds -> all-gather, pipelined"
     elif pg:
         path = f"route ({chunks} chunks) -> all-to-all -> part builds, pipelined"
+    elif hs._direct:
+        path = "one range build from the keys (one GPU, <= 6,400 tiles: no route)"
     else:
         path = f"route ({chunks} chunk(s)) -> part builds"
     rp = getattr(hs, "rp", None)
@@ -936,15 +938,18 @@ def bench_hash_sharded(args, torch, dist, amq, world, rank, dev, bpk, label, pg=
         "roofline": {"bound": "hbm", "achieved": round(alg / (ms_per_step * 1e-3) / 1e9, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(alg / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                     "traffic": load_profile(f"bloom12hash{'1B' if total >= 1_000_000_000 else ''}")
-                                .get("hbm_bytes_per_launch"),
+                     "traffic": (None if hs._direct else
+                                 load_profile(f"bloom12hash{'1B' if total >= 1_000_000_000 else ''}")
+                                 .get("hbm_bytes_per_launch")),
                      "alg_bytes_per_launch": alg,
                      "note": "whole step on rank 0; traffic: PMC bytes of the step's kernels"},
         "cpu_baseline": base,
         "step_breakdown_rank0_ms": {"route": round(route_ms, 4), "all_to_all": round(a2a_ms, 4),
                                     "part_builds": round(build_ms, 4),
                                     "allgather": round(gather_ms, 4),
-                                    "note": "the stages run one after another (untimed by value)"},
+                                    "note": "the routed form's stages one after another (untimed "
+                                            "by value" + ("; the timed step is the direct range "
+                                                          "build)" if hs._direct else ")")},
         "step_timeline_rank0_ms": timeline,
         "verified": check["ok"] if check else None, "verify": check,
     }

@@ -36,6 +36,7 @@
 #include <optional>
 #include <string>
 #include <string_view>
+#include <thread>
 #include <vector>
 
 #include "../tkv_amq.h"
@@ -662,9 +663,20 @@ class LeafBatcher
       lk.unlock();
       run(*b);
       lk.lock();
-      for (Req* q : b->reqs) q->done = true;
+      for (Req* q : b->reqs) {
+        q->done = true;
+        q->done_flag.store(true, std::memory_order_release);
+      }
       cv_.notify_all();
     } else {
+      // a member first polls its flag (yielding) for about a batch's device time, then sleeps:
+      // a condition-variable wake-up costs tens of microseconds on a busy host, about as long
+      // as the batch's kernel
+      lk.unlock();
+      const auto spin_until = std::chrono::steady_clock::now() + std::chrono::microseconds{kSpinUs};
+      while (!r.done_flag.load(std::memory_order_acquire) && std::chrono::steady_clock::now() < spin_until)
+        std::this_thread::yield();
+      lk.lock();
       cv_.wait(lk, [&] { return r.done; });
     }
     lk.unlock();
@@ -697,8 +709,11 @@ class LeafBatcher
     u64 page_bytes = 0;
     bool rebuilt = false;
     std::vector<u8> rebuilt_page;
-    bool done = false;
+    bool done = false;                 // under mu_
+    std::atomic<bool> done_flag{false};  // the same, for the members' polling
   };
+
+  static constexpr int kSpinUs = 400;
 
   struct Batch {
     FilterKind kind{};
@@ -873,9 +888,12 @@ class LeafBatcher
                           reinterpret_cast<const tkv_amq_segment*>(b.h_io), (u32)n_segs, max_blocks, b.d_out.get(),
                           ws_bytes ? d_ws : nullptr, ws_bytes, s);
     if (st != TKV_AMQ_OK) return Status::from(st, "tkv_amq_build_ex");
-    if (hipMemcpyAsync(h_out, b.d_out.get(), out_bytes, hipMemcpyDeviceToHost, s) != hipSuccess ||
-        hipStreamSynchronize(s) != hipSuccess)
+    if (hipMemcpyAsync(h_out, b.d_out.get(), out_bytes, hipMemcpyDeviceToHost, s) != hipSuccess)
       return Status::from(TKV_AMQ_INTERNAL, "hipMemcpyAsync pages");
+    // (polled, yielding: a blocking synchronisation sleeps until an interrupt wakes it)
+    hipError_t q;
+    while ((q = hipStreamQuery(s)) == hipErrorNotReady) std::this_thread::yield();
+    if (q != hipSuccess) return Status::from(TKV_AMQ_INTERNAL, "hipStreamQuery");
     u32 flags = 0;
     if (flags_out) {
       const u32* h_flags = reinterpret_cast<const u32*>(h_out + ws_off + TKV_AMQ_VQF_NELTS_OFFSET);

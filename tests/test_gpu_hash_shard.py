@@ -368,10 +368,10 @@ def test_pipelined_blocks_report_lost_overflow(oracle, amq, torch):
     n = 30_000_000   # 344 tiles: two parts
     keys = amq.gen_keys16(32, 0, n)
     keys[n // 2:] = keys[7]
-    hs = HashShardedBloom(n, 12, 1, 0, "cuda")
+    hs = HashShardedBloom(n, 12, 1, 0, "cuda", direct=False)
     hs.step(keys)
     assert hs.lost()
-    filt = HashShardedBloom(n, 12, 1, 0, "cuda").build(keys)
+    filt = HashShardedBloom(n, 12, 1, 0, "cuda", direct=False).build(keys)
     st, ref = oracle.bloom_build(keys.cpu().numpy(), n, 12, src_page_id=0)
     assert st == 0 and filt.cpu().numpy().tobytes() == ref.tobytes()
 

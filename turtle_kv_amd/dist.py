@@ -463,13 +463,16 @@ class HashShardedBloom:
 
     `build(keys)` returns the whole filter payload (header + bitmap), byte-identical to a one-GPU
     tkv_amq_build of the concatenated keys, on every rank.  Without a process group (one GPU)
-    the route writes the part builds' input directly.  k > 8 (bits_per_key >= 13), a rank holding
+    a filter of at most 6,400 tiles with 16-byte keys is one range build (no route: the
+    partition hashes the keys itself; `direct=False` keeps the route), and a larger one's route
+    writes the part builds' input directly.  k > 8 (bits_per_key >= 13), a rank holding
     more keys than the plan's chunks take, and a step whose blocks lost overflow entries (`lost()`;
     keys far from uniform, e.g. one key repeated) go through ExactHashShardedBloom.  The receive
     buffer holds round j's blocks at [j][chunk][sender]."""
 
     def __init__(self, n_total_keys: int, bits_per_key: int, world: int, rank: int, device,
-                 src_page_id: int = 0, group=None, chunks: int = 1, max_keys_per_rank=None):
+                 src_page_id: int = 0, group=None, chunks: int = 1, max_keys_per_rank=None,
+                 direct: bool = True):
         import ctypes
 
         import torch
@@ -523,6 +526,9 @@ class HashShardedBloom:
         self.comm = torch.cuda.Stream(device=self.dev) if self.dev.type == "cuda" else None
         self.last_lost = None
         self.timeline = None
+        self._direct = False
+        self._direct_ok = direct   # one GPU, no process group, T <= 6,400: no route
+        self._direct_ws = None
 
     @property
     def capacity(self) -> int:
@@ -668,6 +674,17 @@ class HashShardedBloom:
                 tl[name] = e
 
         mark("start", cur)
+        self._direct = (self._direct_ok and not self._collective and self.T <= KEY_RANGE_MAX_TILES
+                        and keys.dim() == 2
+                        and keys.shape[1] == 16)
+        if self._direct:
+            # one GPU, no process group, a filter one partition takes whole: no route, no
+            # blocks (the range build hashes the keys into its records itself)
+            self._direct_build(keys)
+            mark("build_direct", cur)
+            mark("end", cur)
+            self.timeline = tl
+            return
         if coll:
             self.comm.wait_stream(cur)  # the previous step's readers are done
         C, g = self.chunks, self.g
@@ -721,6 +738,24 @@ class HashShardedBloom:
         mark("end", cur)
         self.timeline = tl
 
+    def _direct_build(self, keys):
+        """The whole filter from the keys by one range build (tkv_amq_bloom_build_range)."""
+        import torch
+
+        from . import abi
+        from .filters import _ptr, _stream_handle
+        L = abi.lib()
+        n = keys.shape[0]
+        if keys.shape[0] > self.capacity:
+            raise abi.TkvAmqError(abi.INVALID_ARGUMENT, f"{n} keys: the plan routes at most {self.capacity}")
+        need = int(L.tkv_amq_bloom_build_range_ws_bytes(n, 0, self.T))
+        if self._direct_ws is None or self._direct_ws.numel() < need:
+            self._direct_ws = torch.empty(max(need, 1), dtype=torch.uint8, device=self.dev)
+        abi.check(L.tkv_amq_bloom_build_range(_ptr(keys) if n else None, n, _ptr(self.d_seg), self.n_blocks, 0,
+                                              self.T, _ptr(self.out), _ptr(self._direct_ws),
+                                              self._direct_ws.numel(), _stream_handle()),
+                  "tkv_amq_bloom_build_range")
+
     def timeline_ms(self) -> dict:
         """Milliseconds from the step's start to each recorded stage end (after a step with
         timeline=True and a synchronisation)."""
@@ -757,7 +792,7 @@ class HashShardedBloom:
 
         from . import abi
         from .filters import _ptr, _stream_handle
-        if not self.records:
+        if not self.records or self._direct:
             return False
         r = abi.lib().tkv_amq_bloom_blocks_lost(_ptr(self.recv), self.g * self.chunks * self.world,
                                                 ctypes.byref(self.rp), _stream_handle())
