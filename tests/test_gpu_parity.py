@@ -770,8 +770,8 @@ def test_bloom_oversize_leaves_among_many(oracle, amq, torch, shape):
 ])
 def test_bloom_oversize_other_key_shapes(oracle, amq, torch, shape, bpk, counts):
     """Leaves past 16 LDS windows of variable-length or other fixed-size keys, in a batch and
-    alone: the tiled build with the partition hashing each key into its bit record
-    (bloom_part_any; round 5: device atomics at 3.6 Gkeys/s), byte-equal to the oracle."""
+    alone: each key hashed into its bit record (bloom_any_records), then the tiled build (round
+    5: device atomics at 3.6 Gkeys/s), byte-equal to the oracle."""
     rng = np.random.default_rng(len(counts) * bpk)
     n = sum(counts)
     offs = None
@@ -790,6 +790,48 @@ def test_bloom_oversize_other_key_shapes(oracle, amq, torch, shape, bpk, counts)
                           offsets_t=None if offs is None else torch.from_numpy(offs).cuda())
     assert plan.max_seg_blocks > 16 * 160 * 1024 // 64
     assert_same(plan, out, ref)
+
+
+@pytest.mark.parametrize("shape", ["var", "k16"])
+def test_bloom_oversize_batch_side_stream_and_short_workspace(oracle, amq, torch, shape):
+    """A batch of small leaves around one past the window path (tkv_amq_build_ex): built on a
+    non-default caller stream and read after that stream alone is synchronised, and through
+    the C ABI with a workspace 256 bytes short of the plan's (the Python entry refuses one; the
+    library then takes whatever path still fits, down to device atomics).  Byte-equal either
+    way, on output buffers poisoned beforehand."""
+    from turtle_kv_amd import abi
+    rng = np.random.default_rng(77)
+    counts = [700, 3_000_000, 500, 16384, 0, 9000]
+    n = sum(counts)
+    if shape == "var":
+        lens = rng.integers(8, 32, n)
+        keys, stride = rng.integers(0, 256, int(lens.sum()), dtype=np.uint8), 0
+        offs = np.zeros(n + 1, np.int64)
+        offs[1:] = np.cumsum(lens)
+    else:
+        keys, stride, offs = oracle.gen_keys16(77, 0, n), 16, None
+    ref = oracle_per_segment(oracle, 0, keys, counts, 10, stride=stride,
+                             offsets=None if offs is None else offs.astype(np.uint64))
+    plan = amq.plan_filters(amq.BLOOM, counts, 10)
+    keys_t = torch.from_numpy(keys).cuda()
+    offs_t = None if offs is None else torch.from_numpy(offs).cuda()
+    kb = amq.KeyBatch.fixed(keys_t) if offs_t is None else amq.KeyBatch.variable(keys_t, offs_t)
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        out = torch.full((plan.total_out_bytes,), 0xA5, dtype=torch.uint8, device="cuda")
+        amq.build_all_filters(plan, kb, out=out, stream=s, check=False)
+    s.synchronize()
+    assert_same(plan, out.cpu().numpy(), ref)
+    ws = torch.full((plan.workspace_bytes,), 0xFF, dtype=torch.uint8, device="cuda")
+    out2 = torch.full((plan.total_out_bytes,), 0x5A, dtype=torch.uint8, device="cuda")
+    ptr = lambda t: None if t is None else t.data_ptr()
+    st = abi.lib().tkv_amq_build_ex(plan.kind, keys_t.data_ptr(), ptr(offs_t), stride, n,
+                                    plan.device_segs(keys_t.device).data_ptr(), plan.segs.ctypes.data,
+                                    plan.n_segs, plan.max_seg_blocks, out2.data_ptr(), ws.data_ptr(),
+                                    plan.workspace_bytes - 256, None)
+    abi.check(st, "tkv_amq_build_ex")
+    torch.cuda.synchronize()
+    assert_same(plan, out2.cpu().numpy(), ref)
 
 
 @pytest.mark.parametrize("shape,bpk,n_big", [("k16", 10, 35), ("k16", 16, 17), ("k24", 12, 17)])

@@ -5,6 +5,7 @@ variable-length keys of 8-31 bytes, or 20-byte keys (random bytes made on the de
 leaves past 16 windows take bloom_part_any (round 5: device atomics)."""
 import os
 import sys
+import time
 
 import numpy as np
 
@@ -57,13 +58,19 @@ def main():
         for _ in range(3):
             amq.build_all_filters(plan, kb, out=out, workspace=ws, check=False)
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(20)]
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
         for a, b in ev:
             a.record()
             amq.build_all_filters(plan, kb, out=out, workspace=ws, check=False)
             b.record()
+        host_us = (time.perf_counter() - t0) / len(ev) * 1e6
         torch.cuda.synchronize()
         ms = float(np.median([a.elapsed_time(b) for a, b in ev]))
-        print(f"{args.shape} {name}: {n} keys, {ms * 1e3:.1f} us, {n / ms / 1e6:.1f} Gkeys/s", flush=True)
+        # (host_us: the enqueue time per call; when it is above the events' time, the host and
+        # not the device sets the rate of back-to-back calls)
+        print(f"{args.shape} {name}: {n} keys, {ms * 1e3:.1f} us, {n / ms / 1e6:.1f} Gkeys/s "
+              f"(host enqueue {host_us:.1f} us per call)", flush=True)
         del kb, out, ws
         torch.cuda.empty_cache()
 

@@ -4695,10 +4695,11 @@ __global__ __launch_bounds__(1024) void bloom_compact_segs(const tkv_amq_segment
                                                            uint32_t n_segs, uint32_t max_small_blocks,
                                                            tkv_amq_segment* __restrict__ dst)
 {
+  // (256 or 1,024 threads: a short list launches narrow, a quarter of a CU's wave slots)
   __shared__ uint32_t s_w[16];
-  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6, nt = blockDim.x, nw = nt >> 6;
   uint32_t base = 0;
-  for (uint32_t c0 = 0; c0 < n_segs; c0 += 1024) {
+  for (uint32_t c0 = 0; c0 < n_segs; c0 += nt) {
     const uint32_t s = c0 + tid;
     const bool keep = s < n_segs && segs[s].n_blocks <= max_small_blocks;
     const uint64_t m = __ballot(keep);
@@ -4706,7 +4707,7 @@ __global__ __launch_bounds__(1024) void bloom_compact_segs(const tkv_amq_segment
     if (lane == 0) s_w[wave] = (uint32_t)__popcll(m);
     __syncthreads();
     uint32_t off = base, tot = 0;
-    for (uint32_t w = 0; w < 16; ++w) {
+    for (uint32_t w = 0; w < nw; ++w) {
       off += w < wave ? s_w[w] : 0u;
       tot += s_w[w];
     }
@@ -5839,8 +5840,8 @@ static int build_batch(int kind, const uint8_t* keys, const uint64_t* offs, uint
       launch_mono(mp, s, keys, mono24 ? 24u : 16u, (uint32_t)sizing_keys, d_segs, static_cast<uint8_t*>(d_ws),
                   d_out);
     } else if (mono_any) {
-      // one filter of variable-length or other fixed-size keys: the same, the partition
-      // hashing them (bloom_part_any)
+      // one filter of variable-length or other fixed-size keys: the same, from bit records
+      // (bloom_any_records)
       launch_any(any_plan(sizing_keys, max_blocks), s, keys, mode == kKeyVar ? offs : nullptr, stride,
                  (uint32_t)sizing_keys, d_segs, static_cast<uint8_t*>(d_ws), d_out);
     } else {
@@ -6097,7 +6098,8 @@ int tkv_amq_build_ex(int kind, const uint8_t* keys, const uint64_t* offs, uint32
   if (n_small) {
     tkv_amq_segment* list = reinterpret_cast<tkv_amq_segment*>(ws);
     const uint32_t small_blocks = batch_window_max(fixed) * (kBloomLeafLdsBudget / 64);
-    hipLaunchKernelGGL(bloom_compact_segs, dim3(1), dim3(1024), 0, s, d_segs, n_segs, small_blocks, list);
+    hipLaunchKernelGGL(bloom_compact_segs, dim3(1), dim3(n_segs <= 4096 ? 256 : 1024), 0, s, d_segs, n_segs,
+                       small_blocks, list);
     const int st = build_batch(kind, keys, offs, stride, n_keys, list, n_small, small_max, d_out, rest,
                                rest_bytes, stream, small_keys);
     if (st != TKV_AMQ_OK) return st;
@@ -6171,7 +6173,8 @@ int tkv_amq_build_ex(int kind, const uint8_t* keys, const uint64_t* offs, uint32
     if (mono) {
       launch_mono(mp, s, keys, mode == kKey16 ? 16u : 24u, g.n_keys, d_segs + i, rest, d_out, g.key_begin);
     } else if (any) {
-      // variable-length or other fixed-size keys: the partition hashes them (bloom_part_any)
+      // variable-length or other fixed-size keys: hashed into bit records (bloom_any_records),
+      // then the tiled build
       launch_any(any_plan(g.n_keys, g.n_blocks), s, keys, mode == kKeyVar ? offs : nullptr, stride,
                  (uint32_t)g.n_keys, d_segs + i, rest, d_out);
     } else {
