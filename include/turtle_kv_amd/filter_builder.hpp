@@ -539,11 +539,14 @@ inline Status build_filter_for_leaf_in_job(usize filter_bits_per_key, u64 leaf_p
 //   - a call reserves its leaf's place in the open batch's pinned arena (keys, offsets) and
 //     stages its keys there itself, in parallel with the other callers;
 //   - the call that opened the batch (its leader) closes it after `linger`, or as soon as
-//     `max_batch` leaves have joined or the arena is full, and the next call opens another
-//     batch, which fills while this one is on the GPU;
+//     the batch holds its share of the callers (below) or the arena is full, and the next call
+//     opens another batch, which fills while this one is on the GPU;
 //   - the leader waits for every member's keys, then builds the batch on its thread's stream:
 //     one copy of the arena in, one plan, one build, one copy of the pages out;
 //   - each caller copies its own page out of the batch's pinned output.
+// A batch's share of the callers: the callers inside build() divided by `batches_in_flight`
+// (at least 2, at most `max_batch`), so that several small batches run at once, each on its
+// own stream, rather than one large one while the next collects.
 // A batch holds leaves of one kind, bits/key, page size and key stride (0 = variable length);
 // other calls open their own batch.  A leaf larger than the arena is built on its own.  If a
 // batch's VQF build reports an insert failure, its leaves are rebuilt one by one so that only
@@ -552,17 +555,24 @@ class LeafBatcher
 {
  public:
   struct Options {
-    usize max_batch;
+    usize max_batch;  // leaves per batch at most
     std::chrono::microseconds linger;
     usize arena_bytes;  // pinned key bytes per batch (and as many bytes of offsets)
+    usize batches_in_flight = 5;  // a batch closes at (callers in build()) / this many leaves
   };
 
-  // (a batch collects callers for up to 60 us: 16 VQF callers 786-860 Mkeys/s at 60, 658-785 at
-  // 20-40, 634-757 at 80-120; profiles/r05/leaf_bench_sweep*.txt)
-  LeafBatcher() : LeafBatcher(Options{8, std::chrono::microseconds{60}, usize{8} << 20}) {}
+  // (a batch collects callers for up to 60 us.  16 callers of 16K-key leaves, median of three
+  // processes of five passes each, profiles/r06/leaf_sweep/: fixed batches of 3 leaves VQF
+  // 1,046 Mkeys/s (members spinning 300 us), 4: 979, 5: 930, 8: 750-860, 16: 650-710; Bloom
+  // 1,367-1,389 at 3, 1,259-1,279 at 4, 930-1,002 at 8.  32 callers at a fixed 3 fell to
+  // 466-912 (VQF): hence a share of the callers, 16 / 5 -> 3, 32 / 5 -> 6.  With one wake-up
+  // per batch instead of one for every waiting caller, 32 VQF callers run at 1,015-1,363
+  // instead of swinging between ~450 and ~1,200; profiles/r06/leaf_default/, leaf_spin/)
+  LeafBatcher() : LeafBatcher(Options{16, std::chrono::microseconds{60}, usize{8} << 20}) {}
   explicit LeafBatcher(Options o) : opt_{o}
   {
     if (opt_.max_batch == 0) opt_.max_batch = 1;
+    if (opt_.batches_in_flight == 0) opt_.batches_in_flight = 1;
   }
   LeafBatcher(const LeafBatcher&) = delete;
   LeafBatcher& operator=(const LeafBatcher&) = delete;
@@ -637,7 +647,7 @@ class LeafBatcher
     b->bytes += bytes;
     b->reqs.push_back(&r);
     ++b->users;
-    if (b->reqs.size() >= opt_.max_batch) close(b);
+    if (b->reqs.size() >= batch_share()) close(b);
     lk.unlock();
 
     Status staged = stage(r, *b);
@@ -652,14 +662,14 @@ class LeafBatcher
 
     lk.lock();
     ++b->staged;
-    cv_.notify_all();
+    b->cv.notify_all();
     if (leader) {
       const auto deadline = std::chrono::steady_clock::now() + opt_.linger;
       // no lingering once every caller inside build() has joined this batch (one thread alone
       // never waits)
-      cv_.wait_until(lk, deadline, [&] { return b->closed || b->reqs.size() >= active_; });
+      b->cv.wait_until(lk, deadline, [&] { return b->closed || b->reqs.size() >= active_; });
       if (!b->closed) close(b);
-      cv_.wait(lk, [&] { return b->staged == b->reqs.size(); });
+      b->cv.wait(lk, [&] { return b->staged == b->reqs.size(); });
       lk.unlock();
       run(*b);
       lk.lock();
@@ -667,17 +677,21 @@ class LeafBatcher
         q->done = true;
         q->done_flag.store(true, std::memory_order_release);
       }
-      cv_.notify_all();
+      b->cv.notify_all();
     } else {
       // a member first polls its flag (yielding) for about a batch's device time, then sleeps:
       // a condition-variable wake-up costs tens of microseconds on a busy host, about as long
-      // as the batch's kernel
+      // as the batch's kernel.  At most kMaxSpinners poll at once (more callers than CPUs:
+      // the pollers would take the CPUs the others stage their keys on)
       lk.unlock();
-      const auto spin_until = std::chrono::steady_clock::now() + std::chrono::microseconds{kSpinUs};
-      while (!r.done_flag.load(std::memory_order_acquire) && std::chrono::steady_clock::now() < spin_until)
-        std::this_thread::yield();
+      if (spinners_.fetch_add(1, std::memory_order_relaxed) < kMaxSpinners) {
+        const auto spin_until = std::chrono::steady_clock::now() + std::chrono::microseconds{kSpinUs};
+        while (!r.done_flag.load(std::memory_order_acquire) && std::chrono::steady_clock::now() < spin_until)
+          std::this_thread::yield();
+      }
+      spinners_.fetch_sub(1, std::memory_order_relaxed);
       lk.lock();
-      cv_.wait(lk, [&] { return r.done; });
+      b->cv.wait(lk, [&] { return r.done; });
     }
     lk.unlock();
 
@@ -694,7 +708,7 @@ class LeafBatcher
     lk.lock();
     if (--b->users == 0) release(b);
     --active_;
-    cv_.notify_all();
+    for (Batch* o : open_) o->cv.notify_all();  // (their leaders' linger ends at every caller joined)
     return st;
   }
 
@@ -713,7 +727,17 @@ class LeafBatcher
     std::atomic<bool> done_flag{false};  // the same, for the members' polling
   };
 
-  static constexpr int kSpinUs = 400;
+#ifndef TKV_LEAF_SPIN_US
+#define TKV_LEAF_SPIN_US 300  // (a compile-time override for tools/leaf_bench.cpp sweeps: 16 VQF
+                              // callers 1,046 at 300, 930 at 200, ~750-860 at 0-100 or 400)
+#endif
+  static constexpr int kSpinUs = TKV_LEAF_SPIN_US;
+#ifndef TKV_LEAF_MAX_SPINNERS
+#define TKV_LEAF_MAX_SPINNERS 4  // (16 / 32 VQF callers, medians of three processes: 942 / 1,272
+                                 // Mkeys/s at 4, 878 / 1,105 at 8, 977 / 1,095 at 16;
+                                 // profiles/r06/leaf_spin/)
+#endif
+  static constexpr int kMaxSpinners = TKV_LEAF_MAX_SPINNERS;
 
   struct Batch {
     FilterKind kind{};
@@ -730,9 +754,17 @@ class LeafBatcher
     usize staged = 0, users = 0;
     bool closed = false;
     std::vector<Req*> reqs;
+    std::condition_variable cv;  // this batch's leader and members wait here (under mu_)
   };
 
   usize key_cap() const { return opt_.arena_bytes / 8; }
+
+  // under mu_: the leaves a batch closes at (Options::batches_in_flight)
+  usize batch_share() const
+  {
+    const usize share = active_ / opt_.batches_in_flight;
+    return std::min(opt_.max_batch, std::max<usize>(share, 2));
+  }
 
   // under mu_
   void close(Batch* b)
@@ -743,7 +775,7 @@ class LeafBatcher
         open_.erase(open_.begin() + i);
         break;
       }
-    cv_.notify_all();
+    b->cv.notify_all();
   }
 
   // the segments after the batch's keys in the same buffers (256-byte aligned)
@@ -911,7 +943,7 @@ class LeafBatcher
 
   Options opt_;
   std::mutex mu_;
-  std::condition_variable cv_;
+  std::atomic<int> spinners_{0};
   std::vector<Batch*> open_, free_, all_;
   usize active_ = 0;  // callers inside build() past their size check
 };
