@@ -4,6 +4,7 @@
 #include <turtle_kv_amd/filter_builder.hpp>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <fstream>
 #include <iterator>
@@ -143,22 +144,31 @@ int main(int argc, char** argv)
     }
     std::vector<std::vector<std::string_view>> views(n_leaves);
     for (int l = 0; l < n_leaves; ++l) views[l].assign(leaf_keys[l].begin(), leaf_keys[l].end());
+    // (the process-wide batcher from 16 and 32 threads: batches close at 3 and 6 leaves; a
+    // batcher whose max_batch 4 caps the 32 threads' share of 16)
+    LeafBatcher capped{LeafBatcher::Options{4, std::chrono::microseconds{60}, usize{8} << 20, 2}};
     for (FilterKind kind : {FilterKind::kQuotient, FilterKind::kBloom}) {
       const usize bpk = kind == FilterKind::kBloom ? 10 : 12;
-      std::vector<std::vector<u8>> got(n_leaves), want(n_leaves);
-      std::vector<Status> got_st(n_leaves);
-      std::vector<std::thread> pool;
-      for (int t = 0; t < 16; ++t)
-        pool.emplace_back([&, t] {
-          for (int l = t; l < n_leaves; l += 16)
-            got_st[l] = build_filter_for_leaf_in_job_batched(bpk, 500 + l, views[l], got[l],
-                                                             32768 - 64, kind);
-        });
-      for (auto& th : pool) th.join();
-      for (int l = 0; l < n_leaves; ++l) {
-        EXPECT(got_st[l].ok());
+      std::vector<std::vector<u8>> want(n_leaves);
+      for (int l = 0; l < n_leaves; ++l)
         EXPECT(build_filter_for_leaf_in_job(bpk, 500 + l, views[l], want[l], 32768 - 64, kind).ok());
-        EXPECT(got[l] == want[l]);
+      for (const int threads : {16, 32, -32}) {
+        std::vector<std::vector<u8>> got(n_leaves);
+        std::vector<Status> got_st(n_leaves);
+        std::vector<std::thread> pool;
+        const int nt = threads < 0 ? -threads : threads;
+        for (int t = 0; t < nt; ++t)
+          pool.emplace_back([&, t] {
+            for (int l = t; l < n_leaves; l += nt)
+              got_st[l] = threads < 0 ? capped.build(kind, bpk, 500 + l, views[l], got[l], 32768 - 64)
+                                      : build_filter_for_leaf_in_job_batched(bpk, 500 + l, views[l], got[l],
+                                                                             32768 - 64, kind);
+          });
+        for (auto& th : pool) th.join();
+        for (int l = 0; l < n_leaves; ++l) {
+          EXPECT(got_st[l].ok());
+          EXPECT(got[l] == want[l]);
+        }
       }
       // one caller alone: its batch closes at once
       std::vector<u8> solo;
