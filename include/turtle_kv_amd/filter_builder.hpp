@@ -551,6 +551,17 @@ inline Status build_filter_for_leaf_in_job(usize filter_bits_per_key, u64 leaf_p
 // other calls open their own batch.  A leaf larger than the arena is built on its own.  If a
 // batch's VQF build reports an insert failure, its leaves are rebuilt one by one so that only
 // the failing leaf goes without a filter (filter_builder.hpp:323-325).
+// compile-time overrides for tools/leaf_bench.cpp sweeps (profiles/r06/leaf_sweep/, leaf_spin/):
+// how long a member polls before it sleeps (16 VQF callers 1,046 Mkeys/s at 300 us, 930 at
+// 200, ~750-860 at 0-100 or 400), and how many poll at once (16 / 32 VQF callers 942 / 1,272
+// at 4, 878 / 1,105 at 8, 977 / 1,095 at 16; 2-6 within noise, sweep4)
+#ifndef TKV_LEAF_SPIN_US
+#define TKV_LEAF_SPIN_US 300
+#endif
+#ifndef TKV_LEAF_MAX_SPINNERS
+#define TKV_LEAF_MAX_SPINNERS 4
+#endif
+
 class LeafBatcher
 {
  public:
@@ -727,16 +738,7 @@ class LeafBatcher
     std::atomic<bool> done_flag{false};  // the same, for the members' polling
   };
 
-#ifndef TKV_LEAF_SPIN_US
-#define TKV_LEAF_SPIN_US 300  // (a compile-time override for tools/leaf_bench.cpp sweeps: 16 VQF
-                              // callers 1,046 at 300, 930 at 200, ~750-860 at 0-100 or 400)
-#endif
   static constexpr int kSpinUs = TKV_LEAF_SPIN_US;
-#ifndef TKV_LEAF_MAX_SPINNERS
-#define TKV_LEAF_MAX_SPINNERS 4  // (16 / 32 VQF callers, medians of three processes: 942 / 1,272
-                                 // Mkeys/s at 4, 878 / 1,105 at 8, 977 / 1,095 at 16;
-                                 // profiles/r06/leaf_spin/)
-#endif
   static constexpr int kMaxSpinners = TKV_LEAF_MAX_SPINNERS;
 
   struct Batch {
