@@ -551,7 +551,8 @@ inline Status build_filter_for_leaf_in_job(usize filter_bits_per_key, u64 leaf_p
 // other calls open their own batch.  A leaf larger than the arena is built on its own.  If a
 // batch's VQF build reports an insert failure, its leaves are rebuilt one by one so that only
 // the failing leaf goes without a filter (filter_builder.hpp:323-325).
-// compile-time overrides for tools/leaf_bench.cpp sweeps (profiles/r06/leaf_sweep/, leaf_spin/):
+//
+// Compile-time overrides for tools/leaf_bench.cpp sweeps (profiles/r06/leaf_sweep/, leaf_spin/):
 // how long a member polls before it sleeps (16 VQF callers 1,046 Mkeys/s at 300 us, 930 at
 // 200, ~750-860 at 0-100 or 400), and how many poll at once (16 / 32 VQF callers 942 / 1,272
 // at 4, 878 / 1,105 at 8, 977 / 1,095 at 16; 2-6 within noise, sweep4)
