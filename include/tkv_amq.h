@@ -183,9 +183,11 @@ int tkv_amq_build(int kind, const uint8_t* keys, const uint64_t* key_offsets,
  * tkv_amq_plan filled; d_segs is their device copy).  With it a Bloom batch of 16- or 24-byte
  * keys builds its leaves of more than 5 LDS windows (images past 800 KB; tree/tree_options.hpp:
  * 177-215 sizes any leaf) through the tiled build, up to 40 of them per launch, and the other
- * leaves through the batch kernels; with other key shapes only the leaves past 16 windows (2.5
- * MB) leave the batch kernels, each setting its bits with device atomics (tkv_amq_build: device
- * atomics for the whole batch).  The workspace tkv_amq_plan sizes covers either key shape.
+ * leaves through the batch kernels; with other key shapes (variable-length, other strides) only
+ * the leaves past 16 windows (2.5 MB) leave the batch kernels, each hashed into bit records by
+ * a pass of its own and built by the tiled build (k <= 8; above, device atomics); tkv_amq_build
+ * of such a batch sets those leaves' bits with device atomics.  The workspace tkv_amq_plan
+ * sizes covers either key shape.
  * h_segs == NULL, a single leaf, or a batch without such leaves: exactly tkv_amq_build. */
 int tkv_amq_build_ex(int kind, const uint8_t* keys, const uint64_t* key_offsets, uint32_t key_stride,
                      uint64_t n_keys, const tkv_amq_segment* d_segs, const tkv_amq_segment* h_segs,
