@@ -299,6 +299,14 @@ def main():
     cap = (amq.TreeOptions(kind).set_filter_bits_per_key(bpk).filter_page_payload_size()
            if kind == amq.VQF else 0)
     from turtle_kv_amd import dist as tdist
+
+    t_start = time.perf_counter()
+
+    def progress(msg):  # multi-rank runs report their stages on stderr (rank 0)
+        if world > 1 and rank == 0:
+            print(f"bench.py {args.workload} x{world} +{time.perf_counter() - t_start:.1f}s: {msg}",
+                  file=sys.stderr, flush=True)
+
     strong = args.total_keys is not None
     leaf_keys = args.leaf_keys or LEAF_KEYS.get(args.workload, SEG_KEYS)
     if args.workload in MONOLITHIC and args.leaf_keys is None:
@@ -339,8 +347,11 @@ def main():
         # VQF inserts in leaf key order: sort each leaf's keys (memcmp order) on the device
         # (other key shapes are inserted in generation order: the same work, and the oracle
         # check below inserts them in the same order)
-        keys = sort_segments_device(torch, keys, counts)
+        progress("keys generated; sorting each leaf")
+        keys = one_rank_at_a_time(torch, dist, world, rank,
+                                  lambda: sort_segments_device(torch, keys, counts))
     kb = amq.KeyBatch.variable(keys, offsets) if offsets is not None else amq.KeyBatch.fixed(keys)
+    progress(f"{n} keys per rank generated")
     # zeroed once: the build never writes past a leaf's payload, so the slack bytes of every
     # fixed-stride slot stay 0 and the gathered array is comparable byte for byte
     out = torch.zeros(plan.total_out_bytes, dtype=torch.uint8, device=dev)
@@ -399,6 +410,7 @@ def main():
     if pg:
         wall = reduce_max(torch, dist, wall, coll_dev)
     kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    progress(f"{args.steps} timed steps: {wall / args.steps * 1e3:.3f} ms per step; verifying")
 
     units = 2 * total_keys if probe else total_keys
     ms_per_step = wall / args.steps * 1e3
@@ -460,6 +472,7 @@ def main():
     allgather_ms = None
     gather_ok = None
     if pg:
+        progress("verified; timing the all-gather")
         if not args.allgather:
             torch.cuda.synchronize()
             dist.barrier()
@@ -471,8 +484,12 @@ def main():
         else:
             tdist.allgather_filters(out, gathered)
         if rank == 0 and not args.no_verify and not probe:
+            progress("checking the gathered array against a one-process build")
             gather_ok = verify_gather(torch, amq, kind, bpk, cap, all_counts, stride, gathered,
                                       key_bytes, dev)
+        if world > n_dev:
+            dist.barrier()  # (ranks sharing rank 0's device wait for its check and sort)
+        progress("all-gather done; the pipelined figure")
 
     # the north star's whole step with the all-gather overlapped (untimed by `value`): the same
     # leaves dealt in block-cyclic rounds, round c gathered on a communication stream while
@@ -490,6 +507,7 @@ def main():
             torch.cuda.synchronize()
             dist.barrier()
 
+    progress("pipelined figure done; host legs")
     sweep = None
     if rank == 0 and world == 1 and not probe and args.sweep and \
             args.workload not in MONOLITHIC and len(counts) > SWEEP_LEAVES[0]:
@@ -630,15 +648,19 @@ def pipelined_figure(torch, dist, amq, tdist, kind, bpk, cap, all_counts, world,
     q = -(-per_rank // max(1, rounds))
     pl = tdist.PipelinedLeafGather(kind, all_counts, bpk, world, rank, stride, q, dev,
                                    payload_capacity=cap)
-    batches = []
-    for (b, e), (k0, k1) in zip(pl.rounds, pl.key_ranges()):
-        if k1 == k0:
-            batches.append(None)
-            continue
-        keys = amq.gen_keys16(42, k0, k1 - k0, device=dev)
-        if kind == 1:
-            keys = sort_segments_device(torch, keys, all_counts[b:e])
-        batches.append(amq.KeyBatch.fixed(keys))
+    def make_batches():
+        bs = []
+        for (b, e), (k0, k1) in zip(pl.rounds, pl.key_ranges()):
+            if k1 == k0:
+                bs.append(None)
+                continue
+            keys = amq.gen_keys16(42, k0, k1 - k0, device=dev)
+            if kind == 1:
+                keys = sort_segments_device(torch, keys, all_counts[b:e])
+            bs.append(amq.KeyBatch.fixed(keys))
+        return bs
+
+    batches = one_rank_at_a_time(torch, dist, world, rank, make_batches)
     pl.step(batches)
     torch.cuda.synchronize()
     dist.barrier()
@@ -688,17 +710,20 @@ def bench_pipelined_gather(args, torch, dist, amq, world, rank, dev, kind, bpk, 
     stride = tdist.leaf_stride(kind, bpk, max(all_counts), cap)
     pl = tdist.PipelinedLeafGather(kind, all_counts, bpk, world, rank, stride, q, dev,
                                    payload_capacity=cap)
-    batches = []
-    n = 0
-    for (b, e), (k0, k1) in zip(pl.rounds, pl.key_ranges()):
-        if k1 == k0:
-            batches.append(None)
-            continue
-        keys = amq.gen_keys16(42, k0, k1 - k0, device=dev)
-        if kind == 1:
-            keys = sort_segments_device(torch, keys, all_counts[b:e])
-        batches.append(amq.KeyBatch.fixed(keys))
-        n += k1 - k0
+    def make_batches():
+        bs = []
+        for (b, e), (k0, k1) in zip(pl.rounds, pl.key_ranges()):
+            if k1 == k0:
+                bs.append(None)
+                continue
+            keys = amq.gen_keys16(42, k0, k1 - k0, device=dev)
+            if kind == 1:
+                keys = sort_segments_device(torch, keys, all_counts[b:e])
+            bs.append(amq.KeyBatch.fixed(keys))
+        return bs
+
+    batches = one_rank_at_a_time(torch, dist, world, rank, make_batches)
+    n = sum(k1 - k0 for k0, k1 in pl.key_ranges())
     total_keys = sum(all_counts)
     coll_dev = dev if args.backend == "nccl" else "cpu"
 
@@ -1252,6 +1277,22 @@ def batch_sweep(torch, amq, kind, bpk, cap, counts, kb, ws, plan_all, kernel_ms_
     rows.append({"leaves": len(counts), "keys": int(sum(counts)), "ms": round(kernel_ms_all, 4),
                  "mkeys_s": round(sum(counts) / kernel_ms_all / 1e3, 1)})
     return rows
+
+
+def one_rank_at_a_time(torch, dist, world, rank, fn):
+    """fn() on every rank.  Ranks sharing one device (gloo rehearsals with more ranks than
+    GPUs) run it one after another: torch's device sort, run from several processes on one GPU
+    at once, stalled for minutes (4 and 8 ranks, round 6) while each alone takes ~0.2 s."""
+    import torch.distributed as tdist_
+    if not (tdist_.is_available() and tdist_.is_initialized()) or world <= torch.cuda.device_count():
+        return fn()
+    res = None
+    for r in range(world):
+        if r == rank:
+            res = fn()
+            torch.cuda.synchronize()
+        dist.barrier()
+    return res
 
 
 def sort_segments_device(torch, keys, counts, chunk_keys=1 << 23):
