@@ -1463,9 +1463,11 @@ __host__ __device__ inline uint64_t div_magic(uint32_t d) { return (0x100000000u
 static_assert(sizeof(tkv_amq_route_plan) == 120, "abi.RoutePlan");
 __device__ inline uint32_t div_by_magic(uint32_t x, uint64_t m) { return (uint32_t)(((uint64_t)x * m) >> 32); }
 
+// (nontemporal, as the tile kernel's record loads: the records are read once)
+typedef uint32_t u32x3_nt_t __attribute__((ext_vector_type(3)));
 __device__ inline uint4 load_rec12(const uint8_t* recs, uint32_t i)
 {
-  const uint3 r = reinterpret_cast<const uint3*>(recs)[i];
+  const u32x3_nt_t r = __builtin_nontemporal_load(reinterpret_cast<const u32x3_nt_t*>(recs + 12ull * i));
   return make_uint4(r.x, r.y, r.z, 0u);
 }
 
