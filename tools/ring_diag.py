@@ -1,5 +1,8 @@
 """Per-step cycle stamps of vqf_decide_ring's decider wave for one lone leaf (diagnostic build:
-hipcc ... -DTKV_DIAG_RING -o tools/exp/libtkv_amq_diag.so, loaded through TKV_AMQ_LIB).
+hipcc -O3 --offload-arch=gfx950 -std=c++17 -shared -fPIC -Iinclude -DTKV_DIAG_RING
+-DTKV_AMQ_EXPERIMENT_BUILD -o tools/diag/libtkv_amq_diag.so turtle_kv_amd/csrc/*.hip *.cpp,
+run with TKV_AMQ_EXPERIMENT=1 TKV_AMQ_LIB=tools/diag/libtkv_amq_diag.so: tools/gpu/plans/
+ring_diag.txt; tools/diag/ travels to the GPU box, tools/exp/ does not).
 Prints, over the leaf's 64-key steps: the wait for the slot, the count read (one LDS round trip
 after the previous step's count update), the decision, and the whole step (stamp to stamp)."""
 import ctypes
