@@ -2053,7 +2053,7 @@ __device__ void tile_body(const tkv_amq_segment& sg, const PartArgs& a, uint32_t
         // 16 bytes at the 12-byte stride (the next record's first word, or the workspace
         // after the last region, is ignored), nontemporal: the records are read once, and
         // plain loads ran 20% slower (0.351 vs 0.292 ms per 100M keys)
-        const u32x4_t e = __builtin_nontemporal_load(reinterpret_cast<const u32x4_a4_t*>(p));
+        const u32x3_nt_t e = __builtin_nontemporal_load(reinterpret_cast<const u32x3_nt_t*>(p));
         q.x[v][0] = e.x; q.x[v][1] = e.y; q.x[v][2] = e.z; q.x[v][3] = 0;
       }
     }
