@@ -83,9 +83,6 @@ __constant__ BloomSeeds c_bloom = make_bloom_seeds();
 enum KeyMode : int { kKey16 = 0, kKeyFixed = 1, kKeyVar = 2, kKey24 = 3, kKeyLoc = 4 };
 
 typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
-// the same vector at 4-byte alignment: 16-byte loads of 12-byte records at their 12-byte stride
-// (gfx950 global loads take any dword-aligned address; a u32x4_t* there would claim 16)
-typedef u32x4_t u32x4_a4_t __attribute__((aligned(4)));
 
 // streaming (non-temporal) loads/stores for data touched exactly once, so it does not
 // evict reused data (the probe's filter array) from L2 / the Infinity Cache
@@ -2050,9 +2047,9 @@ __device__ void tile_body(const tkv_amq_segment& sg, const PartArgs& a, uint32_t
         const u32x4_t e = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(p));
         q.x[v][0] = e.x; q.x[v][1] = e.y; q.x[v][2] = e.z; q.x[v][3] = e.w;
       } else {
-        // 16 bytes at the 12-byte stride (the next record's first word, or the workspace
-        // after the last region, is ignored), nontemporal: the records are read once, and
-        // plain loads ran 20% slower (0.351 vs 0.292 ms per 100M keys)
+        // one 12-byte load per record, nontemporal: the records are read once (plain loads
+        // ran 20% slower, 0.351 vs 0.292 ms per 100M keys), and 16 bytes at the 12-byte
+        // stride -- until round 6 -- took 77 instead of 68.7 us per config-5 part
         const u32x3_nt_t e = __builtin_nontemporal_load(reinterpret_cast<const u32x3_nt_t*>(p));
         q.x[v][0] = e.x; q.x[v][1] = e.y; q.x[v][2] = e.z; q.x[v][3] = 0;
       }
